@@ -1,0 +1,119 @@
+"""In-tree build of the native extension ``analyzer_amd._C`` for gfx950.
+
+Device code (``*.hip``) is compiled by ``hipcc --offload-arch=gfx950``; the
+torch binding and the C++ host mirror by ``g++``; everything is linked into
+``analyzer_amd/_C*.so`` next to this file, so the built library travels with
+the repository snapshot to the GPU box and is what the tests load.
+
+    python -m analyzer_amd.build_ext [--force] [--jobs N]
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import subprocess
+import sys
+import sysconfig
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+BUILD = PKG.parent / "build" / "analyzer_amd"
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+
+HIP_SOURCES = ["kernels.hip", "sweep.hip", "telemetry.hip"]
+CPP_SOURCES = ["host.cpp", "bindings.cpp"]
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def target_path() -> Path:
+    return PKG / ("_C" + _ext_suffix())
+
+
+def _torch_paths():
+    import torch.utils.cpp_extension as ce
+
+    return ce.include_paths(), ce.library_paths()
+
+
+def _deps_mtime(src: Path) -> float:
+    headers = [p.stat().st_mtime for p in CSRC.glob("*.h")]
+    return max([src.stat().st_mtime] + headers)
+
+
+def _compile(cmd, src: Path, obj: Path, force: bool) -> str:
+    if not force and obj.exists() and obj.stat().st_mtime >= _deps_mtime(src):
+        return "up-to-date %s" % src.name
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("compile failed: %s\n%s\n%s" % (" ".join(cmd), res.stdout, res.stderr))
+    return "built %s" % src.name
+
+
+def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
+    incs, libs = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    objs = []
+    tasks = []
+    for name in HIP_SOURCES:
+        src = CSRC / name
+        if not src.exists():
+            continue
+        obj = BUILD / (name + ".o")
+        cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
+               "-I" + str(CSRC), "-c", str(src), "-o", str(obj)]
+        tasks.append((cmd, src, obj))
+        objs.append(obj)
+    for name in CPP_SOURCES:
+        src = CSRC / name
+        obj = BUILD / (name + ".o")
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+               "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
+               "-D_GLIBCXX_USE_CXX11_ABI=1", "-I" + str(CSRC), "-I" + ROCM + "/include",
+               "-I" + py_inc] + ["-I" + p for p in incs] + ["-c", str(src), "-o", str(obj)]
+        tasks.append((cmd, src, obj))
+        objs.append(obj)
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for msg in ex.map(lambda t: _compile(t[0], t[1], t[2], force), tasks):
+            if verbose:
+                print(msg, flush=True)
+    out = target_path()
+    newest = max(o.stat().st_mtime for o in objs)
+    if force or not out.exists() or out.stat().st_mtime < newest:
+        cmd = ["g++", "-shared", "-o", str(out)] + [str(o) for o in objs]
+        for p in libs:
+            cmd += ["-L" + p, "-Wl,-rpath," + p]
+        cmd += ["-ltorch", "-ltorch_cpu", "-lc10", "-lc10_hip", "-ltorch_hip", "-ltorch_python",
+                "-L" + ROCM + "/lib", "-Wl,-rpath," + ROCM + "/lib", "-lamdhip64"]
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError("link failed:\n%s\n%s" % (res.stdout, res.stderr))
+        if verbose:
+            print("linked", out, flush=True)
+    return out
+
+
+def _abi_flag() -> str:  # pragma: no cover - informational
+    import torch
+
+    return "-D_GLIBCXX_USE_CXX11_ABI=%d" % int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--jobs", type=int, default=4)
+    args = ap.parse_args(argv)
+    path = build(force=args.force, jobs=args.jobs, verbose=True)
+    print(path)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,256 @@
+// PyTorch bindings of the engine.  Device (ROCm) tensors run the gfx950
+// kernels of kernels.hip on the current HIP stream; CPU tensors run the host
+// mirror of host.cpp.  Every shape/dtype/device assumption a kernel makes is
+// checked here, on the host, before anything is launched.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "gen_core.h"
+#include "host.h"
+#include "kernels.h"
+
+namespace {
+
+using torch::Tensor;
+
+void check_hip(int err, const char* what) {
+  TORCH_CHECK(err == 0, what, " failed: ", hipGetErrorString((hipError_t)err), " (", err, ")");
+}
+
+void check(const Tensor& t, const char* name, torch::ScalarType dt, const torch::Device& dev) {
+  TORCH_CHECK(t.defined(), name, " is undefined");
+  TORCH_CHECK(t.scalar_type() == dt, name, " must be ", c10::toString(dt), ", got ",
+              c10::toString(t.scalar_type()));
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(t.device() == dev, name, " is on ", t.device(), " but expected ", dev);
+}
+
+hipStream_t stream_of(const Tensor& t) {
+  return at::hip::getCurrentHIPStream(t.device().index()).stream();
+}
+
+uint32_t u32(int64_t v, const char* name) {
+  TORCH_CHECK(v >= 0 && v <= 0xffffffffLL, name, " must fit in uint32");
+  return (uint32_t)v;
+}
+
+// --------------------------------------------------------------------- K7
+void gen_roster(Tensor state, Tensor attrs, int64_t seed, int64_t p_tier_null, int64_t p_tier_bad,
+                int64_t p_rp_ranked, int64_t p_rp_blitz, int64_t p_rated, int64_t p_mode_rated,
+                double mu_lo, double mu_span, double sig_lo, double sig_span) {
+  const auto dev = state.device();
+  check(state, "state", torch::kFloat32, dev);
+  check(attrs, "attrs", torch::kFloat32, dev);
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == 2 * ana::kTrackStride, "state must be [P, 16]");
+  TORCH_CHECK(attrs.dim() == 2 && attrs.size(1) == 4 && attrs.size(0) == state.size(0),
+              "attrs must be [P, 4]");
+  ana::GenRosterParams g{};
+  g.seed = (uint64_t)seed;
+  g.num_players = state.size(0);
+  g.p_tier_null = u32(p_tier_null, "p_tier_null");
+  g.p_tier_bad = u32(p_tier_bad, "p_tier_bad");
+  g.p_rp_ranked = u32(p_rp_ranked, "p_rp_ranked");
+  g.p_rp_blitz = u32(p_rp_blitz, "p_rp_blitz");
+  g.p_rated = u32(p_rated, "p_rated");
+  g.p_mode_rated = u32(p_mode_rated, "p_mode_rated");
+  g.mu_lo = (float)mu_lo;
+  g.mu_span = (float)mu_span;
+  g.sig_lo = (float)sig_lo;
+  g.sig_span = (float)sig_span;
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_gen_roster(g, state.data_ptr<float>(), attrs.data_ptr<float>(),
+                                     stream_of(state)), "gen_roster");
+  } else {
+    ana::host_gen_roster(g, state.data_ptr<float>(), attrs.data_ptr<float>());
+  }
+}
+
+void gen_stream(Tensor rec, int64_t K, int64_t seed, int64_t base, int64_t num_players,
+                int64_t team_size, std::vector<int64_t> mode_cdf, int64_t p_uneven,
+                int64_t p_bad_rosters, int64_t p_tie, int64_t p_afk, int64_t p_hot,
+                int64_t hot_players) {
+  const auto dev = rec.device();
+  check(rec, "rec", torch::kInt32, dev);
+  TORCH_CHECK(K >= 1 && K <= 5, "K (players per roster slot block) must be 1..5");
+  TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  TORCH_CHECK(team_size >= 1 && team_size <= K, "team_size must be in 1..K");
+  TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
+  TORCH_CHECK(hot_players >= 1 && hot_players <= num_players, "hot_players must be 1..num_players");
+  TORCH_CHECK(mode_cdf.size() == 7, "mode_cdf must have 7 thresholds");
+  ana::GenStreamParams g{};
+  g.seed = (uint64_t)seed;
+  g.base = base;
+  g.num_players = num_players;
+  g.team_size = (int32_t)team_size;
+  for (int k = 0; k < 7; ++k) g.mode_cdf[k] = u32(mode_cdf[k], "mode_cdf");
+  g.p_uneven = u32(p_uneven, "p_uneven");
+  g.p_bad_rosters = u32(p_bad_rosters, "p_bad_rosters");
+  g.p_tie = u32(p_tie, "p_tie");
+  g.p_afk = u32(p_afk, "p_afk");
+  g.p_hot = u32(p_hot, "p_hot");
+  g.hot_players = u32(hot_players, "hot_players");
+  const int64_t M = rec.size(0);
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_gen_stream((int)K, g, rec.data_ptr<int32_t>(), M, stream_of(rec)),
+              "gen_stream");
+  } else {
+    TORCH_CHECK(ana::host_gen_stream((int)K, g, rec.data_ptr<int32_t>(), M) == 0, "bad K");
+  }
+}
+
+// --------------------------------------------------------------------- K5
+int64_t schedule_workspace_bytes(int64_t nslots, int64_t num_players) {
+  return (int64_t)ana::schedule_workspace_bytes(nslots, num_players);
+}
+
+void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor occ, Tensor workspace) {
+  const auto dev = rec.device();
+  check(rec, "rec", torch::kInt32, dev);
+  check(occ, "occ", torch::kInt32, dev);
+  TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
+  TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  const int64_t M = rec.size(0);
+  TORCH_CHECK(occ.dim() == 2 && occ.size(0) == M && occ.size(1) == 2 * K, "occ must be [M, 2K]");
+  TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
+  TORCH_CHECK(M * 2 * K < 0x7fffffffLL, "too many slots for one schedule (split the stream)");
+  if (dev.is_cuda()) {
+    check(workspace, "workspace", torch::kUInt8, dev);
+    const size_t need = ana::schedule_workspace_bytes(M * 2 * K, num_players);
+    TORCH_CHECK((size_t)workspace.numel() >= need, "workspace too small: need ", need, " bytes");
+    check_hip(ana::launch_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
+                                   reinterpret_cast<uint32_t*>(occ.data_ptr<int32_t>()),
+                                   workspace.data_ptr<uint8_t>(), (size_t)workspace.numel(),
+                                   stream_of(rec)), "schedule");
+  } else {
+    TORCH_CHECK(ana::host_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
+                                   reinterpret_cast<uint32_t*>(occ.data_ptr<int32_t>())) == 0,
+                "bad K");
+  }
+}
+
+// ------------------------------------------------------------ K1-K4, K6
+void rate(Tensor rec, int64_t K, Tensor occ, Tensor state, Tensor attrs, Tensor ver,
+          Tensor first_prior, Tensor quality, Tensor status, Tensor s_mu, Tensor s_sig,
+          Tensor delta, Tensor m_mu, Tensor m_sig, Tensor ctrl, Tensor vst, double beta2,
+          double tau2, double unknown_sigma, bool record_first_prior, int64_t max_blocks,
+          bool host_fp64) {
+  const auto dev = rec.device();
+  check(rec, "rec", torch::kInt32, dev);
+  check(state, "state", torch::kFloat32, dev);
+  check(attrs, "attrs", torch::kFloat32, dev);
+  check(quality, "quality", torch::kFloat32, dev);
+  check(status, "status", torch::kUInt8, dev);
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
+  TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  const int64_t M = rec.size(0);
+  const int64_t S = 2 * K;
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == 2 * ana::kTrackStride, "state must be [P, 16]");
+  const int64_t P = state.size(0);
+  TORCH_CHECK(P >= 1 && P < 0x7fffffffLL, "roster size out of range");
+  TORCH_CHECK(attrs.dim() == 2 && attrs.size(0) == P && attrs.size(1) == 4, "attrs must be [P, 4]");
+  TORCH_CHECK(quality.numel() == M && status.numel() == M, "quality/status must have M entries");
+  for (const Tensor* t : {&s_mu, &s_sig, &delta, &m_mu, &m_sig}) {
+    check(*t, "per-slot output", torch::kFloat32, dev);
+    TORCH_CHECK(t->numel() == M * S, "per-slot outputs must be [M, 2K]");
+  }
+  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries (tiers -1..29)");
+  float* fp = nullptr;
+  if (record_first_prior) {
+    check(first_prior, "first_prior", torch::kFloat32, dev);
+    TORCH_CHECK(first_prior.sizes() == state.sizes(), "first_prior must match state");
+    fp = first_prior.data_ptr<float>();
+  }
+  ana::RateOut out{quality.data_ptr<float>(), status.data_ptr<uint8_t>(), s_mu.data_ptr<float>(),
+                   s_sig.data_ptr<float>(), delta.data_ptr<float>(), m_mu.data_ptr<float>(),
+                   m_sig.data_ptr<float>()};
+  ana::RateParams prm{};
+  prm.beta2 = (float)beta2;
+  prm.tau2 = (float)tau2;
+  prm.unknown_sigma = (float)unknown_sigma;
+  prm.num_players = (int32_t)P;
+  prm.num_matches = M;
+  prm.record_first_prior = record_first_prior ? 1 : 0;
+  prm.vst = vst.data_ptr<float>();
+  if (dev.is_cuda()) {
+    check(occ, "occ", torch::kInt32, dev);
+    check(ver, "ver", torch::kInt32, dev);
+    check(ctrl, "ctrl", torch::kInt32, dev);
+    TORCH_CHECK(occ.numel() == M * S, "occ must be [M, 2K]");
+    TORCH_CHECK(ver.numel() >= P, "ver must have P entries");
+    TORCH_CHECK(ctrl.numel() >= 4, "ctrl must have 4 entries");
+    TORCH_CHECK(max_blocks >= 1, "max_blocks must be >= 1");
+    check_hip(ana::launch_rate((int)K, rec.data_ptr<int32_t>(),
+                               reinterpret_cast<const uint32_t*>(occ.data_ptr<int32_t>()),
+                               state.data_ptr<float>(), attrs.data_ptr<float>(),
+                               reinterpret_cast<uint32_t*>(ver.data_ptr<int32_t>()), fp, out,
+                               reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm,
+                               (int)max_blocks, stream_of(rec)), "rate");
+  } else {
+    TORCH_CHECK(ana::host_rate((int)K, host_fp64, rec.data_ptr<int32_t>(), state.data_ptr<float>(),
+                               attrs.data_ptr<float>(), fp, out, prm) == 0, "bad K");
+  }
+}
+
+// ------------------------------------------------------------- K9 / C1
+void check_rows(const Tensor& t, const char* name, int64_t P, int64_t cols, const torch::Device& dev) {
+  check(t, name, torch::kFloat32, dev);
+  TORCH_CHECK(t.dim() == 2 && t.size(0) == P && t.size(1) == cols, name, " must be [P, ", cols, "]");
+}
+
+void sweep_delta(Tensor s0, Tensor s, Tensor first_prior, Tensor buf) {
+  const auto dev = s.device();
+  const int64_t P = s.size(0);
+  check_rows(s0, "s0", P, 16, dev);
+  check_rows(s, "state", P, 16, dev);
+  check_rows(first_prior, "first_prior", P, 16, dev);
+  check_rows(buf, "buf", P, 16, dev);
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(),
+                                      first_prior.data_ptr<float>(), buf.data_ptr<float>(), P,
+                                      stream_of(s)), "sweep_delta");
+  } else {
+    ana::host_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(), first_prior.data_ptr<float>(),
+                          buf.data_ptr<float>(), P);
+  }
+}
+
+void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor vst, double unknown_sigma) {
+  const auto dev = s.device();
+  const int64_t P = s.size(0);
+  check_rows(s0, "s0", P, 16, dev);
+  check_rows(buf, "buf", P, 16, dev);
+  check_rows(attrs, "attrs", P, 4, dev);
+  check_rows(s, "state", P, 16, dev);
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(),
+                                      attrs.data_ptr<float>(), s.data_ptr<float>(),
+                                      vst.data_ptr<float>(), (float)unknown_sigma, P,
+                                      stream_of(s)), "sweep_apply");
+  } else {
+    ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
+                          s.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, P);
+  }
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "analyzer_amd native engine: gfx950 HIP kernels + C++ host mirror";
+  m.def("gen_roster", &gen_roster, "K7: synthetic roster (state [P,16], attrs [P,4])");
+  m.def("gen_stream", &gen_stream, "K7: synthetic match stream rec [M, 2K+2]");
+  m.def("schedule_workspace_bytes", &schedule_workspace_bytes);
+  m.def("schedule", &schedule, "K5: per-slot occurrence index (chronological order per player)");
+  m.def("rate", &rate, "K1-K4/K6: exact dataflow rating of a stream");
+  m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
+  m.def("sweep_apply", &sweep_apply, "K9: apply all-reduced messages to the replicated roster");
+  m.attr("TRACK_STRIDE") = ana::kTrackStride;
+  m.attr("N_TRACKS") = ana::kTracks;
+  m.attr("VST_TIERS") = ana::kVstTiers;
+}

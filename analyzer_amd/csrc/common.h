@@ -1,0 +1,105 @@
+// Shared definitions for the MI355X rating engine (device kernels + host mirror).
+//
+// Data layout:
+//  * roster state: float2 state[P][8]   -- tracks 0..6 = shared, casual, ranked,
+//    blitz, br, 5v5_casual, 5v5_ranked as (mu, sigma); slot 7 spare.  One
+//    player = one 64-B line, so a match slot touches one line for both tracks.
+//    NaN mu is the SQL NULL ("no rating yet", rater.py:115,124,150).
+//  * player attributes: float4 attrs[P] = (rank_points_ranked,
+//    rank_points_blitz, skill_tier, unused); NaN = NULL.  Only read to seed.
+//  * match stream: int32 rec[M][2K+2]: 2K player ids (-1 = empty slot; slots
+//    0..K-1 roster 0, K..2K-1 roster 1), then meta0 = mode | n0<<8 | n1<<16 |
+//    nrosters<<24 and meta1 = winner0 | winner1<<1 | afk_any<<2 | afk_mask<<8.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define ANA_HD __host__ __device__ __forceinline__
+#else
+#define ANA_HD inline
+#endif
+
+namespace ana {
+
+constexpr int kTracks = 7;        // shared + 6 modes
+constexpr int kTrackStride = 8;   // float2 slots per player record (64 B)
+constexpr int kModes = 6;
+constexpr int kModeUnsupported = 255;
+constexpr int kVstTiers = 31;     // tiers -1..29
+
+// per-match status codes (the reference's outcomes and error classes)
+enum Status : uint8_t {
+  kRated = 0,           // valid matchup, both tracks updated
+  kAfk = 1,             // any went_afk == 1 -> quality 0, all any_afk
+  kInvalidRosters = 2,  // len(rosters) != 2 -> quality 0, all any_afk
+  kUnsupportedMode = 3, // nothing written
+  kErrSeed = 4,         // KeyError: no rank points and tier outside -1..29
+  kErrSigma = 5,        // ValueError: sigma == 0 (or NULL sigma with a mu)
+  kErrEmptyRoster = 6,  // ValueError: a roster without participants
+  kErrNumeric = 7,      // FloatingPointError / non-finite result
+  kErrBadRecord = 8,    // malformed stream record (player id out of range, n > K)
+  kNotProcessed = 255,  // poison value before the kernel runs
+};
+
+struct RateParams {
+  float beta2;          // beta^2 = 1e6
+  float tau2;           // tau^2 (TAU env, default 100)
+  float unknown_sigma;  // UNKNOWN_PLAYER_SIGMA
+  int32_t num_players;
+  int64_t num_matches;
+  int32_t record_first_prior;  // sweep mode: remember priors of NULL tracks
+  int32_t pad;
+  const float* vst;            // vst_points[tier + 1], kVstTiers entries (device/host memory)
+};
+
+// Per-match outputs, structure-of-arrays.  Per-slot arrays are [M][2K]; the
+// participant record of the reference (rater.py:151-169) is
+// (s_mu, s_sig, delta) on ``participant`` and (m_mu, m_sig) on
+// ``participant_items``; any_afk follows from status.
+struct RateOut {
+  float* quality;  // [M]  match.trueskill_quality (0 for AFK/invalid, NaN = not written)
+  uint8_t* status; // [M]  Status
+  float* s_mu;
+  float* s_sig;
+  float* delta;
+  float* m_mu;
+  float* m_sig;
+};
+
+ANA_HD int meta_mode(uint32_t m0) { return (int)(m0 & 0xffu); }
+ANA_HD int meta_n0(uint32_t m0) { return (int)((m0 >> 8) & 0xffu); }
+ANA_HD int meta_n1(uint32_t m0) { return (int)((m0 >> 16) & 0xffu); }
+ANA_HD int meta_nrosters(uint32_t m0) { return (int)((m0 >> 24) & 0xffu); }
+ANA_HD bool meta_winner0(uint32_t m1) { return (m1 & 1u) != 0; }
+ANA_HD bool meta_winner1(uint32_t m1) { return (m1 & 2u) != 0; }
+ANA_HD bool meta_afk(uint32_t m1) { return (m1 & 4u) != 0; }
+ANA_HD uint32_t pack_meta0(int mode, int n0, int n1, int nrosters) {
+  return (uint32_t)(mode & 0xff) | ((uint32_t)(n0 & 0xff) << 8) |
+         ((uint32_t)(n1 & 0xff) << 16) | ((uint32_t)(nrosters & 0xff) << 24);
+}
+ANA_HD uint32_t pack_meta1(bool w0, bool w1, uint32_t afk_mask) {
+  return (w0 ? 1u : 0u) | (w1 ? 2u : 0u) | (afk_mask ? 4u : 0u) | ((afk_mask & 0xffffffu) << 8);
+}
+
+// ---------------------------------------------------------------- RNG (K7)
+// Counter-based: every random number is a pure function of (seed, index,
+// field), so device and host generators produce bit-identical streams and any
+// window/shard can be regenerated independently (checkpoint/resume needs no
+// RNG state beyond the seed and the stream offset).
+ANA_HD uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+ANA_HD uint64_t rng_u64(uint64_t seed, uint64_t index, uint32_t field) {
+  return mix64(mix64(seed ^ (0xd1b54a32d192ed03ull * (uint64_t)(field + 1))) + index);
+}
+// uniform in [0, 1) with 24 random bits (exactly representable in fp32)
+ANA_HD float rng_unit(uint64_t seed, uint64_t index, uint32_t field) {
+  return (float)(rng_u64(seed, index, field) >> 40) * (1.0f / 16777216.0f);
+}
+
+}  // namespace ana

@@ -1,0 +1,32 @@
+// Host-callable launchers of the MI355X kernels (implemented in kernels.hip).
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "common.h"
+#include "gen_core.h"
+
+namespace ana {
+
+int launch_gen_roster(const GenRosterParams& g, float* state, float* attrs, hipStream_t s);
+int launch_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M, hipStream_t s);
+
+size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
+int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* occ, void* ws,
+                    size_t ws_bytes, hipStream_t s);
+
+int launch_rate(int K, const int32_t* rec, const uint32_t* occ, float* state, const float* attrs,
+                uint32_t* ver, float* first_prior, const RateOut& out, uint32_t* ctrl,
+                const RateParams& prm, int max_blocks, hipStream_t s);
+
+}  // namespace ana
+
+namespace ana {
+int launch_sweep_delta(const float* s0, const float* s, const float* fp, float* buf, int64_t P,
+                       hipStream_t st);
+int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,
+                       const float* vst, float unknown_sigma, int64_t P, hipStream_t st);
+}  // namespace ana

@@ -1,0 +1,205 @@
+"""Batched, exact TrueSkill rating of match streams (SURVEY K1-K6, A1 batched API).
+
+``BatchRater.rate(roster, rec)`` is the tensor counterpart of calling
+``rater.rate_match`` on every match of a stream in order
+(/root/reference/worker.py:176-192 + rater.py:69-169):
+
+* on a ROCm device it runs the schedule prepass (occurrence index per slot,
+  csrc/kernels.hip ``launch_schedule``) and then the single-launch dataflow
+  kernel that rates the whole stream in per-player chronological order;
+* on the CPU it runs the C++ host mirror sequentially (fp64 by default), which
+  is the semantic oracle for the device path.
+
+The roster is updated in place.  Outputs are per match (quality, status) and
+per slot ``[M, 2K]`` (shared mu/sigma and delta for ``participant``, mode
+mu/sigma for ``participant_items``); NaN means "not written".
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from ..config import MODES, N_TRACKS, RaterConfig
+from ..models.tiers import vst_table
+from .native import native
+
+# status codes (csrc/common.h)
+RATED, AFK, INVALID_ROSTERS, UNSUPPORTED_MODE = 0, 1, 2, 3
+ERR_SEED, ERR_SIGMA, ERR_EMPTY_ROSTER, ERR_NUMERIC, ERR_BAD_RECORD = 4, 5, 6, 7, 8
+NOT_PROCESSED = 255
+STATUS_NAMES = {RATED: "rated", AFK: "afk", INVALID_ROSTERS: "invalid_rosters",
+                UNSUPPORTED_MODE: "unsupported_mode", ERR_SEED: "error_seed",
+                ERR_SIGMA: "error_sigma", ERR_EMPTY_ROSTER: "error_empty_roster",
+                ERR_NUMERIC: "error_numeric", ERR_BAD_RECORD: "error_bad_record",
+                NOT_PROCESSED: "not_processed"}
+# the reference raises (and fails the whole batch) for these classes
+ERROR_STATUSES = (ERR_SEED, ERR_SIGMA, ERR_EMPTY_ROSTER, ERR_NUMERIC, ERR_BAD_RECORD)
+
+
+class NativeRateError(RuntimeError):
+    pass
+
+
+@dataclass
+class Roster:
+    """Device-resident player table (structure of arrays, 64 B per player).
+
+    ``state[p]`` = 8 (mu, sigma) pairs: track 0 shared, 1..6 the modes of
+    ``config.MODES``, slot 7 spare; NaN mu = NULL.  ``attrs[p]`` =
+    (rank_points_ranked, rank_points_blitz, skill_tier, 0); NaN = NULL.
+    """
+
+    state: torch.Tensor
+    attrs: torch.Tensor
+
+    @property
+    def num_players(self) -> int:
+        return int(self.state.shape[0])
+
+    @property
+    def device(self) -> torch.device:
+        return self.state.device
+
+    @staticmethod
+    def empty(num_players: int, device="cpu") -> "Roster":
+        state = torch.full((num_players, 16), float("nan"), dtype=torch.float32, device=device)
+        state[:, 15] = 0.0
+        attrs = torch.full((num_players, 4), float("nan"), dtype=torch.float32, device=device)
+        attrs[:, 3] = 0.0
+        return Roster(state, attrs)
+
+    def tracks(self) -> torch.Tensor:
+        """View ``[P, 8, 2]`` of (mu, sigma) per track."""
+        return self.state.view(-1, 8, 2)
+
+    def track(self, name: str) -> torch.Tensor:
+        """``[P, 2]`` (mu, sigma) of ``trueskill`` or ``trueskill_<mode>``."""
+        idx = 0 if name in ("shared", "trueskill") else 1 + MODES.index(name.replace("trueskill_", ""))
+        return self.tracks()[:, idx]
+
+    def to(self, device) -> "Roster":
+        return Roster(self.state.to(device), self.attrs.to(device))
+
+    def clone(self) -> "Roster":
+        return Roster(self.state.clone(), self.attrs.clone())
+
+
+@dataclass
+class RateResult:
+    quality: torch.Tensor   # [M]
+    status: torch.Tensor    # [M] uint8
+    s_mu: torch.Tensor      # [M, 2K]
+    s_sig: torch.Tensor
+    delta: torch.Tensor
+    m_mu: torch.Tensor
+    m_sig: torch.Tensor
+
+    @staticmethod
+    def allocate(M: int, K: int, device) -> "RateResult":
+        f = dict(dtype=torch.float32, device=device)
+        return RateResult(torch.empty(M, **f), torch.empty(M, dtype=torch.uint8, device=device),
+                          *(torch.empty((M, 2 * K), **f) for _ in range(5)))
+
+    @property
+    def any_afk(self) -> torch.Tensor:
+        """``participant_items.any_afk`` per match (True for AFK / invalid)."""
+        return (self.status == AFK) | (self.status == INVALID_ROSTERS)
+
+    def status_counts(self) -> Dict[str, int]:
+        vals, counts = torch.unique(self.status.cpu(), return_counts=True)
+        return {STATUS_NAMES.get(int(v), str(int(v))): int(c) for v, c in zip(vals, counts)}
+
+
+class BatchRater:
+    """Stateless-per-call batched rater with cached device workspaces."""
+
+    def __init__(self, cfg: Optional[RaterConfig] = None, host_fp64: bool = True,
+                 max_blocks: int = 2048):
+        self.cfg = cfg or RaterConfig.from_env()
+        self.host_fp64 = host_fp64
+        self.max_blocks = int(max_blocks)
+        self._vst: Dict[str, torch.Tensor] = {}
+        self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
+
+    # ------------------------------------------------------------- buffers
+    def vst(self, device) -> torch.Tensor:
+        key = str(device)
+        if key not in self._vst:
+            self._vst[key] = torch.tensor(vst_table(), dtype=torch.float32, device=device)
+        return self._vst[key]
+
+    def _buffer(self, device, name: str, numel: int, dtype) -> torch.Tensor:
+        key = (str(device), name)
+        buf = self._ws.get(key)
+        if buf is None or buf.numel() < numel or buf.dtype != dtype:
+            buf = torch.empty(int(numel), dtype=dtype, device=device)
+            self._ws[key] = buf
+        return buf[:numel]
+
+    # ------------------------------------------------------------- schedule
+    def schedule(self, rec: torch.Tensor, K: int, num_players: int,
+                 occ: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Occurrence index of each slot's player among earlier rated matches."""
+        M = rec.shape[0]
+        if occ is None:
+            occ = self._buffer(rec.device, "occ", M * 2 * K, torch.int32).view(M, 2 * K)
+        if rec.is_cuda:
+            nbytes = native().schedule_workspace_bytes(M * 2 * K, num_players)
+            ws = self._buffer(rec.device, "sched_ws", nbytes, torch.uint8)
+        else:
+            ws = torch.empty(0, dtype=torch.uint8)
+        native().schedule(rec, K, num_players, occ, ws)
+        return occ
+
+    # ----------------------------------------------------------------- rate
+    def rate(self, roster: Roster, rec: torch.Tensor, K: Optional[int] = None,
+             out: Optional[RateResult] = None, first_prior: Optional[torch.Tensor] = None,
+             check: bool = True, occ: Optional[torch.Tensor] = None) -> RateResult:
+        """Rate every match of ``rec`` in order, updating ``roster`` in place."""
+        K = int(K or (rec.shape[1] - 2) // 2)
+        M = int(rec.shape[0])
+        dev = rec.device
+        if roster.device != dev:
+            raise ValueError("roster is on %s but the stream is on %s" % (roster.device, dev))
+        if out is None:
+            out = RateResult.allocate(M, K, dev)
+        P = roster.num_players
+        cfg = self.cfg
+        record = first_prior is not None
+        fp = first_prior if record else torch.empty(0, dtype=torch.float32, device=dev)
+        if dev.type == "cuda":
+            if occ is None:
+                occ = self.schedule(rec, K, P)
+            ver = self._buffer(dev, "ver", P, torch.int32)
+            ctrl = self._buffer(dev, "ctrl", 4, torch.int32)
+        else:
+            occ = ver = ctrl = torch.empty(0, dtype=torch.int32)
+        native().rate(rec, K, occ, roster.state, roster.attrs, ver, fp, out.quality, out.status,
+                      out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
+                      float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
+                      record, self.max_blocks, self.host_fp64)
+        if check and dev.type == "cuda":
+            self.check_errors(dev)
+        return out
+
+    def error_flags(self, device) -> torch.Tensor:
+        """Device tensor [timeout, protocol] of the last launch (no sync)."""
+        return self._buffer(device, "ctrl", 4, torch.int32)[1:3]
+
+    def check_errors(self, device) -> None:
+        flags = self.error_flags(device).cpu()
+        if int(flags[0]):
+            raise NativeRateError("dataflow rating timed out (a dependency never resolved)")
+        if int(flags[1]):
+            raise NativeRateError("dataflow protocol violation (version counter overtook a slot)")
+
+
+def rate_stream(roster: Roster, rec: torch.Tensor, K: Optional[int] = None,
+                cfg: Optional[RaterConfig] = None) -> RateResult:
+    """Convenience wrapper: ``BatchRater(cfg).rate(roster, rec, K)``."""
+    return BatchRater(cfg).rate(roster, rec, K)
+
+
+__all__ = ["Roster", "RateResult", "BatchRater", "rate_stream", "STATUS_NAMES", "N_TRACKS"]

@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Headline benchmark: matches/sec rated (whole node), 3v3 TrueSkill, 1M-player roster.
+
+Metric/config from BASELINE.json.  One step = every rank rates its own window of
+``--matches-per-gpu`` synthetic 3v3 matches (10M by default, BASELINE config 2)
+against the replicated 1M-player roster, in exact per-player chronological
+order (schedule prepass + one dataflow launch, both tracks, full output
+records), then -- for N > 1 -- merges the per-player posteriors of all ranks
+with an RCCL all-reduce of natural-parameter deltas (sweep DP, BASELINE
+config 3 / north star).  Weak scaling: per-GPU work is fixed as N grows.
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N bench.py --gpus N ...   (driver launches N>1)
+
+Synthetic data: roster and streams come from the on-device counter RNG
+(random-init ratings), generated before the timed region like a prefetched
+data loader; the timed region contains all rating work of every step.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+# reference rate: ~354 3v3 matches/s per CPU core for rater.rate_match
+# (measured); the whole-node bound is 8 cores x 354 = 2832/s.
+BASELINE_MATCHES_PER_S = 2832.0
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--players", type=int, default=1_000_000)
+    ap.add_argument("--matches-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--team-size", type=int, default=3)
+    ap.add_argument("--ring", type=int, default=4, help="distinct pre-generated windows per rank")
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--check", action="store_true", help="also validate statuses after timing")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world),
+              file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from analyzer_amd.ops.rate import BatchRater, RateResult, NOT_PROCESSED
+    from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
+    from analyzer_amd.parallel.sweep import SweepMerger
+
+    P, M, K = args.players, args.matches_per_gpu, args.team_size
+    roster = make_roster(RosterSpec(num_players=P, seed=args.seed), device=dev)
+    spec = StreamSpec(team_size=K, seed=args.seed + 1)
+    n_windows = max(1, min(args.ring, args.steps + args.warmup))
+    total_windows = args.steps + args.warmup
+    windows = [make_stream(spec, M, P, K=K, base=(w * world + rank) * M, device=dev)
+               for w in range(n_windows)]
+    rater = BatchRater()
+    out = RateResult.allocate(M, K, dev)
+    merger = SweepMerger(P, dev) if world > 1 else None
+    err = torch.zeros(2, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def step(i):
+        rec = windows[i % n_windows]
+        if merger is not None:
+            merger.begin(roster)
+            rater.rate(roster, rec, K, out=out, first_prior=merger.first_prior, check=False)
+            merger.merge(roster)
+        else:
+            rater.rate(roster, rec, K, out=out, check=False)
+        err.bitwise_or_(rater.error_flags(dev))
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, total_windows):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ms = elapsed * 1000.0 / args.steps
+    t = torch.tensor([ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms = float(t.item())
+    flags = err.cpu()
+    if int(flags.sum()):
+        raise RuntimeError("dataflow error flags set during the benchmark: %s" % flags.tolist())
+    if args.check:
+        counts = out.status_counts()
+        assert NOT_PROCESSED not in out.status.unique().tolist(), counts
+        if rank == 0:
+            print("status counts (last window):", counts, file=sys.stderr)
+    value = world * M / (ms / 1000.0)
+    if rank == 0:
+        print(json.dumps({
+            "metric": "matches/sec rated (whole node), 3v3 TrueSkill, 1M-player roster",
+            "value": value,
+            "unit": "matches/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": value / BASELINE_MATCHES_PER_S,
+            "dtype": "fp32",
+            "data": "synthetic (on-device counter RNG stream, random-init 1M-player roster)",
+            "config": {
+                "model": "TrueSkill 2-team EP (beta=1000, tau=10, draw_probability=0), "
+                         "shared + per-mode tracks",
+                "global_batch": world * M,
+                "seq_len": 2 * K,
+                "players": P,
+                "matches_per_gpu": M,
+                "team_size": K,
+                "parallelism": "dp%d" % world,
+                "mode": "exact" if world == 1 else "sweep (exact per rank + RCCL posterior merge)",
+            },
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

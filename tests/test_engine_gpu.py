@@ -1,0 +1,87 @@
+"""MI355X kernels vs the C++ host mirror / object rater (numerics tests, ``-m gpu``)."""
+import numpy as np
+import pytest
+import torch
+
+from analyzer_amd.config import RaterConfig
+from analyzer_amd.ops import rate as R
+from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
+
+from engine_parity import assert_engine_matches, object_run
+from test_engine_host import SPECS
+
+pytestmark = pytest.mark.gpu
+
+
+def test_native_module_is_loaded(gpu_device):
+    from analyzer_amd.ops.native import native
+
+    mod = native()
+    assert mod.__file__.startswith(__import__("os").path.dirname(__import__("analyzer_amd").__file__))
+
+
+def test_generators_bit_identical(gpu_device):
+    rs = RosterSpec(num_players=5000, seed=21, p_tier_null=0.1, p_tier_bad=0.1)
+    a, b = make_roster(rs), make_roster(rs, device=gpu_device)
+    assert torch.equal(a.state.view(torch.int32), b.state.cpu().view(torch.int32))
+    assert torch.equal(a.attrs.view(torch.int32), b.attrs.cpu().view(torch.int32))
+    for K in (1, 3, 5):
+        ss = StreamSpec(team_size=K, seed=33, p_afk=0.1, p_tie=0.1, p_hot=0.3, p_uneven=0.1)
+        ra = make_stream(ss, 20000, 5000, base=123)
+        rb = make_stream(ss, 20000, 5000, base=123, device=gpu_device)
+        assert torch.equal(ra, rb.cpu())
+
+
+@pytest.mark.parametrize("P,M,K", [(20, 3000, 3), (5000, 100000, 3), (300, 20000, 5)])
+def test_schedule_matches_host(gpu_device, P, M, K):
+    ss = StreamSpec(team_size=K, seed=P, p_afk=0.05, p_unsupported=0.05)
+    rec = make_stream(ss, M, P, K=K)
+    br = R.BatchRater()
+    occ_h = br.schedule(rec, K, P).clone()
+    occ_d = br.schedule(rec.to(gpu_device), K, P)
+    # only slots of rated matches carry an occurrence index
+    res = R.BatchRater().rate(make_roster(RosterSpec(num_players=P)), rec, K)
+    mask = (res.status != R.AFK) & (res.status != R.UNSUPPORTED_MODE)
+    np.testing.assert_array_equal(occ_d.cpu()[mask].numpy(), occ_h[mask].numpy())
+
+
+@pytest.mark.parametrize("name", sorted(SPECS))
+def test_device_matches_object_rater(gpu_device, name):
+    rspec, sspec, K = SPECS[name]
+    roster = make_roster(rspec)
+    rec = make_stream(sspec, 400, rspec.num_players, K=K)
+    ref = object_run(roster, rec, K)
+    work = roster.to(gpu_device)
+    res = R.BatchRater(RaterConfig()).rate(work, rec.to(gpu_device), K)
+    assert_engine_matches(res, work, ref, rtol=2e-4, atol_mu=5e-2, atol_delta=5e-2)
+
+
+@pytest.mark.parametrize("P,M,hot", [(16, 4000, 0.0), (2000, 300000, 0.3), (100000, 1000000, 0.0)])
+def test_device_matches_host_under_contention(gpu_device, P, M, hot):
+    """Heavy per-player chains (P=16: every match depends on the previous ones) and
+    hot-set skew exercise the cross-workgroup hand-off; any stale read shows up here."""
+    rs = RosterSpec(num_players=P, seed=P + 1)
+    ss = StreamSpec(team_size=3, seed=M, p_hot=hot, hot_fraction=0.01)
+    roster = make_roster(rs)
+    rec = make_stream(ss, M, P)
+    host = roster.clone()
+    rh = R.BatchRater(host_fp64=False).rate(host, rec, 3)
+    dev = roster.to(gpu_device)
+    rd = R.BatchRater().rate(dev, rec.to(gpu_device), 3)
+    np.testing.assert_array_equal(rd.status.cpu().numpy(), rh.status.numpy())
+    np.testing.assert_allclose(rd.s_mu.cpu().numpy(), rh.s_mu.numpy(), rtol=1e-3, atol=0.5,
+                               equal_nan=True)
+    np.testing.assert_allclose(dev.state.cpu().numpy(), host.state.numpy(), rtol=1e-3, atol=0.5,
+                               equal_nan=True)
+
+
+def test_device_repeat_launch_deterministic(gpu_device):
+    rs = RosterSpec(num_players=1000, seed=4)
+    rec = make_stream(StreamSpec(seed=5), 50000, 1000, device=gpu_device)
+    outs = []
+    for _ in range(2):
+        ro = make_roster(rs, device=gpu_device)
+        res = R.BatchRater().rate(ro, rec)
+        outs.append((ro.state.cpu(), res.s_mu.cpu()))
+    assert torch.equal(outs[0][0].view(torch.int32), outs[1][0].view(torch.int32))
+    assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32))

@@ -1,0 +1,92 @@
+"""Batched engine (C++ host mirror) == per-object reference-semantics rater."""
+import numpy as np
+import pytest
+import torch
+
+from analyzer_amd.config import RaterConfig
+from analyzer_amd.ops import rate as R
+from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
+
+from engine_parity import assert_engine_matches, object_run
+
+SPECS = {
+    "3v3": (RosterSpec(num_players=64, seed=5), StreamSpec(team_size=3, seed=11), 3),
+    "5v5_edge": (RosterSpec(num_players=40, seed=6, p_tier_null=0.05, p_tier_bad=0.05,
+                            p_rated=0.3),
+                 StreamSpec(team_size=5, seed=12, p_tie=0.1, p_afk=0.05, p_uneven=0.2,
+                            p_bad_rosters=0.03, p_unsupported=0.05,
+                            modes={"5v5_casual": 0.5, "5v5_ranked": 0.5}), 5),
+    "1v1_empty": (RosterSpec(num_players=12, seed=7),
+                  StreamSpec(team_size=1, seed=13, p_uneven=0.2, p_tie=0.2), 1),
+    "uneven_K4": (RosterSpec(num_players=30, seed=8, p_rated=0.0),
+                  StreamSpec(team_size=4, seed=14, p_uneven=0.5), 4),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SPECS))
+def test_host_engine_matches_object_rater(name):
+    rspec, sspec, K = SPECS[name]
+    roster = make_roster(rspec)
+    rec = make_stream(sspec, 400, rspec.num_players, K=K)
+    ref = object_run(roster, rec, K)
+    work = roster.clone()
+    res = R.BatchRater(RaterConfig(), host_fp64=True).rate(work, rec, K)
+    assert_engine_matches(res, work, ref, rtol=2e-6, atol_mu=2e-3, atol_delta=2e-3)
+
+
+def test_host_engine_fp32_close_to_fp64():
+    rspec, sspec, K = SPECS["3v3"]
+    roster = make_roster(rspec)
+    rec = make_stream(sspec, 400, rspec.num_players, K=K)
+    a, b = roster.clone(), roster.clone()
+    r64 = R.BatchRater(host_fp64=True).rate(a, rec, K)
+    r32 = R.BatchRater(host_fp64=False).rate(b, rec, K)
+    np.testing.assert_array_equal(r64.status.numpy(), r32.status.numpy())
+    np.testing.assert_allclose(r32.s_mu.numpy(), r64.s_mu.numpy(), rtol=1e-4, equal_nan=True)
+
+
+def test_stream_generator_properties():
+    rec = make_stream(StreamSpec(team_size=3, seed=3, p_afk=0.0, p_tie=0.0), 5000, 1000)
+    assert rec.shape == (5000, 8)
+    ids = rec[:, :6]
+    assert int(ids.min()) >= 0 and int(ids.max()) < 1000
+    meta0 = rec[:, 6]
+    assert bool(((meta0 >> 8) & 0xFF).eq(3).all())
+    modes = (meta0 & 0xFF)
+    counts = torch.bincount(modes, minlength=6)
+    assert counts[1] > counts[2] > 0  # ranked 40% > blitz 15%
+    w = rec[:, 7] & 3
+    assert bool(((w == 1) | (w == 2)).all())
+    # same seed -> same stream, different base -> different stream
+    assert torch.equal(rec, make_stream(StreamSpec(team_size=3, seed=3, p_afk=0.0, p_tie=0.0), 5000, 1000))
+    other = make_stream(StreamSpec(team_size=3, seed=3, p_afk=0.0, p_tie=0.0), 5000, 1000, base=5000)
+    assert not torch.equal(rec, other)
+
+
+def test_schedule_occurrence_index_host():
+    from analyzer_amd.ops.rate import BatchRater
+
+    rec = make_stream(StreamSpec(team_size=3, seed=9, p_afk=0.1), 300, 20)
+    occ = BatchRater().schedule(rec, 3, 20).numpy()
+    seen = {}
+    for m in range(rec.shape[0]):
+        meta1 = int(rec[m, 7])
+        afk = bool(meta1 & 4)
+        for j in range(6):
+            pid = int(rec[m, j])
+            if afk:
+                continue
+            assert occ[m, j] == seen.get(pid, 0)
+            seen[pid] = seen.get(pid, 0) + 1
+
+
+def test_status_counts_and_any_afk():
+    rspec, sspec, K = SPECS["5v5_edge"]
+    roster = make_roster(rspec)
+    rec = make_stream(sspec, 300, rspec.num_players, K=K)
+    res = R.BatchRater().rate(roster, rec, K)
+    counts = res.status_counts()
+    assert counts.get("rated", 0) > 0 and counts.get("afk", 0) > 0
+    assert bool(res.any_afk[res.status == R.AFK].all())
+    assert torch.isnan(res.quality[res.status == R.UNSUPPORTED_MODE]).all()
+    assert (res.quality[res.status == R.AFK] == 0).all()
