@@ -45,7 +45,7 @@ void gen_roster(Tensor state, Tensor attrs, int64_t seed, int64_t p_tier_null, i
   const auto dev = state.device();
   check(state, "state", torch::kFloat32, dev);
   check(attrs, "attrs", torch::kFloat32, dev);
-  TORCH_CHECK(state.dim() == 2 && state.size(1) == 2 * ana::kTrackStride, "state must be [P, 16]");
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == ana::kRowFloats, "state must be [P, 32]");
   TORCH_CHECK(attrs.dim() == 2 && attrs.size(1) == 4 && attrs.size(0) == state.size(0),
               "attrs must be [P, 4]");
   ana::GenRosterParams g{};
@@ -107,37 +107,46 @@ int64_t schedule_workspace_bytes(int64_t nslots, int64_t num_players) {
   return (int64_t)ana::schedule_workspace_bytes(nslots, num_players);
 }
 
-void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor occ, Tensor workspace) {
+void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
+              Tensor workspace, Tensor ctrl) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
-  check(occ, "occ", torch::kInt32, dev);
+  check(link, "link", torch::kInt32, dev);
+  check(deps, "deps", torch::kInt32, dev);
   TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
   TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
   const int64_t M = rec.size(0);
-  TORCH_CHECK(occ.dim() == 2 && occ.size(0) == M && occ.size(1) == 2 * K, "occ must be [M, 2K]");
+  TORCH_CHECK(link.dim() == 3 && link.size(0) == M && link.size(1) == 2 * K && link.size(2) == 2,
+              "link must be [M, 2K, 2]");
+  TORCH_CHECK(deps.numel() == M, "deps must have M entries");
   TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
   TORCH_CHECK(M * 2 * K < 0x7fffffffLL, "too many slots for one schedule (split the stream)");
   if (dev.is_cuda()) {
     check(workspace, "workspace", torch::kUInt8, dev);
+    check(ctrl, "ctrl", torch::kInt32, dev);
+    TORCH_CHECK(ctrl.numel() >= 16, "ctrl must have 16 entries");
     const size_t need = ana::schedule_workspace_bytes(M * 2 * K, num_players);
     TORCH_CHECK((size_t)workspace.numel() >= need, "workspace too small: need ", need, " bytes");
     check_hip(ana::launch_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
-                                   reinterpret_cast<uint32_t*>(occ.data_ptr<int32_t>()),
-                                   workspace.data_ptr<uint8_t>(), (size_t)workspace.numel(),
+                                   reinterpret_cast<uint32_t*>(link.data_ptr<int32_t>()),
+                                   deps.data_ptr<int32_t>(), workspace.data_ptr<uint8_t>(),
+                                   (size_t)workspace.numel(),
+                                   reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()),
                                    stream_of(rec)), "schedule");
   } else {
     TORCH_CHECK(ana::host_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
-                                   reinterpret_cast<uint32_t*>(occ.data_ptr<int32_t>())) == 0,
+                                   reinterpret_cast<uint32_t*>(link.data_ptr<int32_t>()),
+                                   deps.data_ptr<int32_t>()) == 0,
                 "bad K");
   }
 }
 
 // ------------------------------------------------------------ K1-K4, K6
-void rate(Tensor rec, int64_t K, Tensor occ, Tensor state, Tensor attrs, Tensor ver,
+void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor attrs,
           Tensor first_prior, Tensor quality, Tensor status, Tensor s_mu, Tensor s_sig,
           Tensor delta, Tensor m_mu, Tensor m_sig, Tensor ctrl, Tensor vst, double beta2,
-          double tau2, double unknown_sigma, bool record_first_prior, int64_t max_blocks,
-          bool host_fp64) {
+          double tau2, double unknown_sigma, bool record_first_prior, int64_t blocks,
+          int64_t epoch, bool host_fp64) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
@@ -149,9 +158,10 @@ void rate(Tensor rec, int64_t K, Tensor occ, Tensor state, Tensor attrs, Tensor 
   TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
   const int64_t M = rec.size(0);
   const int64_t S = 2 * K;
-  TORCH_CHECK(state.dim() == 2 && state.size(1) == 2 * ana::kTrackStride, "state must be [P, 16]");
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == ana::kRowFloats, "state must be [P, 32]");
   const int64_t P = state.size(0);
-  TORCH_CHECK(P >= 1 && P < 0x7fffffffLL, "roster size out of range");
+  TORCH_CHECK(P >= 1 && P * ana::kRowFloats * 4 < 0x7fffffffLL,
+              "roster size out of range (<= 16.7M players per device roster)");
   TORCH_CHECK(attrs.dim() == 2 && attrs.size(0) == P && attrs.size(1) == 4, "attrs must be [P, 4]");
   TORCH_CHECK(quality.numel() == M && status.numel() == M, "quality/status must have M entries");
   for (const Tensor* t : {&s_mu, &s_sig, &delta, &m_mu, &m_sig}) {
@@ -175,21 +185,23 @@ void rate(Tensor rec, int64_t K, Tensor occ, Tensor state, Tensor attrs, Tensor 
   prm.num_players = (int32_t)P;
   prm.num_matches = M;
   prm.record_first_prior = record_first_prior ? 1 : 0;
+  TORCH_CHECK(epoch >= 1 && epoch <= 255, "epoch must be 1..255");
+  prm.epoch = (int32_t)epoch;
   prm.vst = vst.data_ptr<float>();
   if (dev.is_cuda()) {
-    check(occ, "occ", torch::kInt32, dev);
-    check(ver, "ver", torch::kInt32, dev);
+    check(link, "link", torch::kInt32, dev);
+    check(deps, "deps", torch::kInt32, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
-    TORCH_CHECK(occ.numel() == M * S, "occ must be [M, 2K]");
-    TORCH_CHECK(ver.numel() >= P, "ver must have P entries");
-    TORCH_CHECK(ctrl.numel() >= 4, "ctrl must have 4 entries");
-    TORCH_CHECK(max_blocks >= 1, "max_blocks must be >= 1");
+    TORCH_CHECK(link.numel() == M * S * 2, "link must be [M, 2K, 2]");
+    TORCH_CHECK(deps.numel() == M, "deps must have M entries");
+    TORCH_CHECK(ctrl.numel() >= 16, "ctrl must have 16 entries");
+    TORCH_CHECK(blocks >= 1 && blocks <= 65535, "blocks must be 1..65535");
     check_hip(ana::launch_rate((int)K, rec.data_ptr<int32_t>(),
-                               reinterpret_cast<const uint32_t*>(occ.data_ptr<int32_t>()),
-                               state.data_ptr<float>(), attrs.data_ptr<float>(),
-                               reinterpret_cast<uint32_t*>(ver.data_ptr<int32_t>()), fp, out,
+                               reinterpret_cast<const uint32_t*>(link.data_ptr<int32_t>()),
+                               deps.data_ptr<int32_t>(), state.data_ptr<float>(),
+                               attrs.data_ptr<float>(), fp, out,
                                reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm,
-                               (int)max_blocks, stream_of(rec)), "rate");
+                               (int)blocks, stream_of(rec)), "rate");
   } else {
     TORCH_CHECK(ana::host_rate((int)K, host_fp64, rec.data_ptr<int32_t>(), state.data_ptr<float>(),
                                attrs.data_ptr<float>(), fp, out, prm) == 0, "bad K");
@@ -205,9 +217,9 @@ void check_rows(const Tensor& t, const char* name, int64_t P, int64_t cols, cons
 void sweep_delta(Tensor s0, Tensor s, Tensor first_prior, Tensor buf) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
-  check_rows(s0, "s0", P, 16, dev);
-  check_rows(s, "state", P, 16, dev);
-  check_rows(first_prior, "first_prior", P, 16, dev);
+  check_rows(s0, "s0", P, ana::kRowFloats, dev);
+  check_rows(s, "state", P, ana::kRowFloats, dev);
+  check_rows(first_prior, "first_prior", P, ana::kRowFloats, dev);
   check_rows(buf, "buf", P, 16, dev);
   if (dev.is_cuda()) {
     check_hip(ana::launch_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(),
@@ -222,10 +234,10 @@ void sweep_delta(Tensor s0, Tensor s, Tensor first_prior, Tensor buf) {
 void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor vst, double unknown_sigma) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
-  check_rows(s0, "s0", P, 16, dev);
+  check_rows(s0, "s0", P, ana::kRowFloats, dev);
   check_rows(buf, "buf", P, 16, dev);
   check_rows(attrs, "attrs", P, 4, dev);
-  check_rows(s, "state", P, 16, dev);
+  check_rows(s, "state", P, ana::kRowFloats, dev);
   check(vst, "vst", torch::kFloat32, dev);
   TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
   if (dev.is_cuda()) {
@@ -236,6 +248,19 @@ void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor vst, doub
   } else {
     ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
                           s.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, P);
+  }
+}
+
+void reset_tags(Tensor state) {
+  const auto dev = state.device();
+  check(state, "state", torch::kFloat32, dev);
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == ana::kRowFloats, "state must be [P, 32]");
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_reset_tags(state.data_ptr<float>(), state.size(0), stream_of(state)),
+              "reset_tags");
+  } else {
+    float* p = state.data_ptr<float>();
+    for (int64_t i = 0; i < state.numel(); i += 2) p[i + 1] = 0.f;
   }
 }
 
@@ -250,7 +275,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rate", &rate, "K1-K4/K6: exact dataflow rating of a stream");
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
   m.def("sweep_apply", &sweep_apply, "K9: apply all-reduced messages to the replicated roster");
-  m.attr("TRACK_STRIDE") = ana::kTrackStride;
+  m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
+  m.attr("ROW_FLOATS") = ana::kRowFloats;
   m.attr("N_TRACKS") = ana::kTracks;
   m.attr("VST_TIERS") = ana::kVstTiers;
 }

@@ -1,15 +1,21 @@
 // Shared definitions for the MI355X rating engine (device kernels + host mirror).
 //
 // Data layout:
-//  * roster state: float2 state[P][8]   -- tracks 0..6 = shared, casual, ranked,
-//    blitz, br, 5v5_casual, 5v5_ranked as (mu, sigma); slot 7 spare.  One
-//    player = one 64-B line, so a match slot touches one line for both tracks.
-//    NaN mu is the SQL NULL ("no rating yet", rater.py:115,124,150).
+//  * roster state: float state[P][32] = 8 granules of 16 B, one per track:
+//    {mu, tag, sigma, tag}.  Tracks 0..6 = shared, casual, ranked, blitz, br,
+//    5v5_casual, 5v5_ranked; granule 7 spare.  One player = one 128-B line.
+//    NaN mu is the SQL NULL ("no rating yet", rater.py:115,124,150).  The two
+//    tag words make every 8-B half of a granule self-validating, so a granule
+//    is its own ready flag in the dataflow executor (kernels.hip); host code
+//    and the generator write tag 0, which never matches a live tag.
 //  * player attributes: float4 attrs[P] = (rank_points_ranked,
 //    rank_points_blitz, skill_tier, unused); NaN = NULL.  Only read to seed.
 //  * match stream: int32 rec[M][2K+2]: 2K player ids (-1 = empty slot; slots
 //    0..K-1 roster 0, K..2K-1 roster 1), then meta0 = mode | n0<<8 | n1<<16 |
 //    nrosters<<24 and meta1 = winner0 | winner1<<1 | afk_any<<2 | afk_mask<<8.
+//  * schedule: uint32 occ[M][2K][2] = (occurrence index of the slot's player
+//    among earlier stateful matches of the window, same but counting only
+//    matches of the same game mode).
 #pragma once
 
 #include <stdint.h>
@@ -24,7 +30,10 @@
 namespace ana {
 
 constexpr int kTracks = 7;        // shared + 6 modes
-constexpr int kTrackStride = 8;   // float2 slots per player record (64 B)
+constexpr int kGranules = 8;      // 16-B granules per player row
+constexpr int kRowFloats = 32;    // floats per player row (128 B)
+constexpr int kTagBits = 24;      // low bits of a tag = occurrence count + 1
+constexpr uint32_t kMaxOcc = (1u << kTagBits) - 2;
 constexpr int kModes = 6;
 constexpr int kModeUnsupported = 255;
 constexpr int kVstTiers = 31;     // tiers -1..29
@@ -50,7 +59,7 @@ struct RateParams {
   int32_t num_players;
   int64_t num_matches;
   int32_t record_first_prior;  // sweep mode: remember priors of NULL tracks
-  int32_t pad;
+  int32_t epoch;               // 1..255: high byte of every tag written by this launch
   const float* vst;            // vst_points[tier + 1], kVstTiers entries (device/host memory)
 };
 

@@ -46,7 +46,7 @@ ANA_HD uint32_t rng_u32(uint64_t seed, uint64_t index, uint32_t field) {
 // floor(u * n) for u uniform in [0, 2^32): exact integer mapping
 ANA_HD uint32_t mulhi_range(uint32_t u, uint64_t n) { return (uint32_t)(((uint64_t)u * n) >> 32); }
 
-ANA_HD void gen_player(const GenRosterParams& g, int64_t p, float* st /*16*/, float* at /*4*/) {
+ANA_HD void gen_player(const GenRosterParams& g, int64_t p, float* st /*32*/, float* at /*4*/) {
   const uint64_t s = g.seed;
   const uint32_t ut = rng_u32(s, p, 0);
   float tier;
@@ -61,16 +61,15 @@ ANA_HD void gen_player(const GenRosterParams& g, int64_t p, float* st /*16*/, fl
   at[1] = rng_u32(s, p, 4) < g.p_rp_blitz ? fmaf(2600.f, rng_unit(s, p, 5), 400.f) : NAN;
   at[2] = tier;
   at[3] = 0.f;
-  for (int k = 0; k < 16; ++k) st[k] = NAN;
-  st[15] = 0.f;
+  for (int k = 0; k < kRowFloats; ++k) st[k] = (k & 1) ? 0.f : NAN;  // tags 0, values NULL
   if (rng_u32(s, p, 6) < g.p_rated) {
     const float mu = fmaf(g.mu_span, rng_unit(s, p, 7), g.mu_lo);
     st[0] = mu;
-    st[1] = fmaf(g.sig_span, rng_unit(s, p, 8), g.sig_lo);
+    st[2] = fmaf(g.sig_span, rng_unit(s, p, 8), g.sig_lo);
     for (int t = 1; t < kTracks; ++t) {
       if (rng_u32(s, p, 8 + 3 * t) < g.p_mode_rated) {
-        st[2 * t] = mu + fmaf(300.f, rng_unit(s, p, 9 + 3 * t), -150.f);
-        st[2 * t + 1] = fmaf(g.sig_span, rng_unit(s, p, 10 + 3 * t), g.sig_lo);
+        st[4 * t] = mu + fmaf(300.f, rng_unit(s, p, 9 + 3 * t), -150.f);
+        st[4 * t + 2] = fmaf(g.sig_span, rng_unit(s, p, 10 + 3 * t), g.sig_lo);
       }
     }
   }

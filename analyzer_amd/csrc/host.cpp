@@ -16,7 +16,7 @@
 namespace ana {
 
 void host_gen_roster(const GenRosterParams& g, float* state, float* attrs) {
-  for (int64_t p = 0; p < g.num_players; ++p) gen_player(g, p, state + p * 16, attrs + p * 4);
+  for (int64_t p = 0; p < g.num_players; ++p) gen_player(g, p, state + p * kRowFloats, attrs + p * 4);
 }
 
 template <int K>
@@ -35,27 +35,38 @@ int host_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M) {
   }
 }
 
+// Same outputs as the device schedule: link[slot] = (occurrence index, next slot
+// of the same player or ~0u) for slots of stateful matches; deps[m].
 template <int K>
-static void schedule_k(const int32_t* rec, int64_t M, int64_t P, uint32_t* occ) {
+static void schedule_k(const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps) {
   constexpr int S = 2 * K;
   std::vector<uint32_t> cnt((size_t)P, 0u);
+  std::vector<uint32_t> last((size_t)P, 0xffffffffu);
   for (int64_t m = 0; m < M; ++m) {
     MatchWork<float, K> w;
     decode_record<float, K>(rec + m * (S + 2), P, w);
+    deps[m] = 0;
     for (int j = 0; j < S; ++j) {
-      occ[m * S + j] = 0;
-      if (w.status == kRated && w.id[j] >= 0) occ[m * S + j] = cnt[(size_t)w.id[j]]++;
+      uint32_t* l = link + (m * S + j) * 2;
+      l[0] = 0;
+      l[1] = 0xffffffffu;
+      if (w.status != kRated || w.id[j] < 0) continue;
+      const size_t p = (size_t)w.id[j];
+      l[0] = cnt[p]++;
+      if (last[p] != 0xffffffffu) link[(size_t)last[p] * 2 + 1] = (uint32_t)(m * S + j);
+      last[p] = (uint32_t)(m * S + j);
+      if (w.first[j] == j && l[0] > 0) ++deps[m];
     }
   }
 }
 
-int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* occ) {
+int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps) {
   switch (K) {
-    case 1: schedule_k<1>(rec, M, P, occ); return 0;
-    case 2: schedule_k<2>(rec, M, P, occ); return 0;
-    case 3: schedule_k<3>(rec, M, P, occ); return 0;
-    case 4: schedule_k<4>(rec, M, P, occ); return 0;
-    case 5: schedule_k<5>(rec, M, P, occ); return 0;
+    case 1: schedule_k<1>(rec, M, P, link, deps); return 0;
+    case 2: schedule_k<2>(rec, M, P, link, deps); return 0;
+    case 3: schedule_k<3>(rec, M, P, link, deps); return 0;
+    case 4: schedule_k<4>(rec, M, P, link, deps); return 0;
+    case 5: schedule_k<5>(rec, M, P, link, deps); return 0;
     default: return -1;
   }
 }
@@ -73,10 +84,10 @@ static void rate_k(const int32_t* rec, float* state, const float* attrs, float* 
       uint8_t st = kRated;
       for (int j = 0; j < S && st == kRated; ++j) {
         if (w.first[j] != j) continue;
-        const float* row = state + (int64_t)w.id[j] * 2 * kTrackStride;
-        st = make_prior<T, K>(w, j, (T)row[0], (T)row[1], (T)row[2 + 2 * w.mode],
-                              (T)row[3 + 2 * w.mode], attrs + (int64_t)w.id[j] * 4, us, prm.vst,
-                              nulls);
+        const float* row = state + (int64_t)w.id[j] * kRowFloats;
+        const float* gm = row + 4 * (1 + w.mode);
+        st = make_prior<T, K>(w, j, (T)row[0], (T)row[2], (T)gm[0], (T)gm[2],
+                              attrs + (int64_t)w.id[j] * 4, us, prm.vst, nulls);
       }
       w.status = st;
       if (st == kRated) {
@@ -88,19 +99,21 @@ static void rate_k(const int32_t* rec, float* state, const float* attrs, float* 
     if (rated) {
       for (int j = 0; j < S; ++j) {
         if (w.id[j] < 0) continue;
-        float* row = state + (int64_t)w.id[j] * 2 * kTrackStride;
-        if ((w.last >> j) & 1u) {
+        float* row = state + (int64_t)w.id[j] * kRowFloats;
+        float* gm = row + 4 * (1 + w.mode);
+        if ((w.last >> j) & 1u) {  // host mirror writes tag 0 (never a live device tag)
           row[0] = (float)w.ns_mu[j];
-          row[1] = (float)w.ns_sig[j];
-          row[2 + 2 * w.mode] = (float)w.nm_mu[j];
-          row[3 + 2 * w.mode] = (float)w.nm_sig[j];
+          row[2] = (float)w.ns_sig[j];
+          gm[0] = (float)w.nm_mu[j];
+          gm[2] = (float)w.nm_sig[j];
+          row[1] = row[3] = gm[1] = gm[3] = 0.f;
         }
         if (prm.record_first_prior && first_prior && w.first[j] == j) {
-          float* fp = first_prior + (int64_t)w.id[j] * 2 * kTrackStride;
-          if ((nulls >> (2 * j)) & 1u) { fp[0] = (float)w.ms[j]; fp[1] = (float)w.ss[j]; }
+          float* fp = first_prior + (int64_t)w.id[j] * kRowFloats;
+          if ((nulls >> (2 * j)) & 1u) { fp[0] = (float)w.ms[j]; fp[2] = (float)w.ss[j]; }
           if ((nulls >> (2 * j + 1)) & 1u) {
-            fp[2 + 2 * w.mode] = (float)w.mm[j];
-            fp[3 + 2 * w.mode] = (float)w.sm[j];
+            fp[4 * (1 + w.mode)] = (float)w.mm[j];
+            fp[4 * (1 + w.mode) + 2] = (float)w.sm[j];
           }
         }
       }
@@ -145,13 +158,15 @@ int host_rate(int K, bool fp64, const int32_t* rec, float* state, const float* a
 namespace ana {
 
 void host_sweep_delta(const float* s0, const float* s, const float* fp, float* buf, int64_t P) {
-  for (int64_t p = 0; p < P; ++p) sweep_delta_player(s0 + p * 16, s + p * 16, fp + p * 16, buf + p * 16);
+  for (int64_t p = 0; p < P; ++p)
+    sweep_delta_player(s0 + p * kRowFloats, s + p * kRowFloats, fp + p * kRowFloats, buf + p * 16);
 }
 
 void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,
                       const float* vst, float unknown_sigma, int64_t P) {
   for (int64_t p = 0; p < P; ++p)
-    sweep_apply_player(s0 + p * 16, buf + p * 16, attrs + p * 4, vst, unknown_sigma, s + p * 16);
+    sweep_apply_player(s0 + p * kRowFloats, buf + p * 16, attrs + p * 4, vst, unknown_sigma,
+                       s + p * kRowFloats);
 }
 
 }  // namespace ana

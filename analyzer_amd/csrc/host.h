@@ -10,7 +10,7 @@ namespace ana {
 
 void host_gen_roster(const GenRosterParams& g, float* state, float* attrs);
 int host_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M);
-int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* occ);
+int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps);
 int host_rate(int K, bool fp64, const int32_t* rec, float* state, const float* attrs,
               float* first_prior, const RateOut& out, const RateParams& prm);
 

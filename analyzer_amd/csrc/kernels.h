@@ -14,13 +14,17 @@ namespace ana {
 int launch_gen_roster(const GenRosterParams& g, float* state, float* attrs, hipStream_t s);
 int launch_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M, hipStream_t s);
 
-size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
-int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* occ, void* ws,
-                    size_t ws_bytes, hipStream_t s);
+int launch_reset_tags(float* state, int64_t P, hipStream_t s);
 
-int launch_rate(int K, const int32_t* rec, const uint32_t* occ, float* state, const float* attrs,
-                uint32_t* ver, float* first_prior, const RateOut& out, uint32_t* ctrl,
-                const RateParams& prm, int max_blocks, hipStream_t s);
+size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
+// link: uint32 [M][2K][2] = (occurrence index, next slot of the same player or ~0u)
+// deps: int32 [M] = distinct players with an earlier occurrence in the window
+int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
+                    int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s);
+
+int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, float* state,
+                const float* attrs, float* first_prior, const RateOut& out, uint32_t* ctrl,
+                const RateParams& prm, int blocks, hipStream_t s);
 
 }  // namespace ana
 

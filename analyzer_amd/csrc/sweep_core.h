@@ -14,12 +14,13 @@ ANA_HD void nat_params(float mu, float sig, float& pi, float& tau) {
   tau = mu * pi;
 }
 
-// s0: window-start row (16 floats), s: row after the local window, fp: priors the
-// rate kernel recorded for tracks it found NULL.  o: 16 floats of message.
+// a: window-start row, b: row after the local window, f: priors the rate kernel
+// recorded for tracks it found NULL (all kRowFloats-float rows, mu at 4t, sigma
+// at 4t+2).  o: 16 floats of message = (d_pi, d_tau) per track + touch fields.
 ANA_HD void sweep_delta_player(const float* a, const float* b, const float* f, float* o) {
   float touch_lo = 0.f, touch_hi = 0.f;
   for (int t = 0; t < kTracks; ++t) {
-    const float mu0 = a[2 * t], sg0 = a[2 * t + 1], mu = b[2 * t], sg = b[2 * t + 1];
+    const float mu0 = a[4 * t], sg0 = a[4 * t + 2], mu = b[4 * t], sg = b[4 * t + 2];
     float dp = 0.f, dt = 0.f;
     if (mu0 == mu0) {
       if (mu != mu0 || sg != sg0) {
@@ -32,7 +33,7 @@ ANA_HD void sweep_delta_player(const float* a, const float* b, const float* f, f
     } else if (mu == mu) {
       float p1, t1, pf, tf;
       nat_params(mu, sg, p1, t1);
-      nat_params(f[2 * t], f[2 * t + 1], pf, tf);
+      nat_params(f[4 * t], f[4 * t + 2], pf, tf);
       dp = p1 - pf;
       dt = t1 - tf;
       if (t < 4) touch_lo += (float)(1 << (4 * t));
@@ -46,19 +47,19 @@ ANA_HD void sweep_delta_player(const float* a, const float* b, const float* f, f
 }
 
 // a: window-start row, d: all-reduced messages, attr: player attributes,
-// o: merged row.
+// o: merged row (tags reset to 0).
 ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr,
                                const float* vst, float unknown_sigma, float* o) {
   float seed_mu = NAN, seed_sig = NAN;
   const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
-  float base_mu = a[0], base_sig = a[1];
+  float base_mu = a[0], base_sig = a[2];
   if (base_mu != base_mu) {
     base_mu = seed_mu;
     base_sig = seed_sig;
   }
   const unsigned lo = (unsigned)d[14], hi = (unsigned)d[15];
   for (int t = 0; t < kTracks; ++t) {
-    const float mu0 = a[2 * t], sg0 = a[2 * t + 1];
+    const float mu0 = a[4 * t], sg0 = a[4 * t + 2];
     const unsigned touched = t < 4 ? (lo >> (4 * t)) & 15u : (hi >> (4 * (t - 4))) & 15u;
     float mu = mu0, sg = sg0, pb = 0.f, tb = 0.f;
     bool have = false;
@@ -77,11 +78,12 @@ ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr
       mu = tau / pi;
       sg = 1.f / sqrtf(pi);
     }
-    o[2 * t] = mu;
-    o[2 * t + 1] = sg;
+    o[4 * t] = mu;
+    o[4 * t + 1] = 0.f;
+    o[4 * t + 2] = sg;
+    o[4 * t + 3] = 0.f;
   }
-  o[14] = a[14];
-  o[15] = a[15];
+  for (int k = 4 * kTracks; k < kRowFloats; ++k) o[k] = (k & 1) ? 0.f : a[k];
 }
 
 }  // namespace ana

@@ -16,8 +16,9 @@ mu/sigma for ``participant_items``); NaN means "not written".
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
-from typing import Dict, Optional, Tuple
+from typing import Dict, NamedTuple, Optional, Tuple
 
 import torch
 
@@ -42,17 +43,28 @@ class NativeRateError(RuntimeError):
     pass
 
 
+class Schedule(NamedTuple):
+    link: torch.Tensor  # [M, 2K, 2] int32: (occurrence index, next slot of the player or -1)
+    deps: torch.Tensor  # [M] int32: players with an earlier occurrence in the window
+
+
 @dataclass
 class Roster:
-    """Device-resident player table (structure of arrays, 64 B per player).
+    """Device-resident player table (structure of arrays, 128 B per player).
 
-    ``state[p]`` = 8 (mu, sigma) pairs: track 0 shared, 1..6 the modes of
-    ``config.MODES``, slot 7 spare; NaN mu = NULL.  ``attrs[p]`` =
-    (rank_points_ranked, rank_points_blitz, skill_tier, 0); NaN = NULL.
+    ``state[p]`` = 8 granules of (mu, tag, sigma, tag): granule 0 the shared
+    track, 1..6 the modes of ``config.MODES``, 7 spare; NaN mu = NULL.  Tags
+    are owned by the dataflow kernel (csrc/kernels.hip); everything else writes
+    0.  ``attrs[p]`` = (rank_points_ranked, rank_points_blitz, skill_tier, 0);
+    NaN = NULL.  ``epoch`` numbers the device launches since the last tag reset
+    (``None`` = tags of unknown origin, reset before the next device launch).
     """
 
     state: torch.Tensor
     attrs: torch.Tensor
+    epoch: Optional[int] = None
+
+    ROW = 32
 
     @property
     def num_players(self) -> int:
@@ -64,26 +76,40 @@ class Roster:
 
     @staticmethod
     def empty(num_players: int, device="cpu") -> "Roster":
-        state = torch.full((num_players, 16), float("nan"), dtype=torch.float32, device=device)
-        state[:, 15] = 0.0
+        state = torch.zeros((num_players, 32), dtype=torch.float32, device=device)
+        state[:, 0::2] = float("nan")
         attrs = torch.full((num_players, 4), float("nan"), dtype=torch.float32, device=device)
         attrs[:, 3] = 0.0
-        return Roster(state, attrs)
+        return Roster(state, attrs, epoch=0)
 
     def tracks(self) -> torch.Tensor:
-        """View ``[P, 8, 2]`` of (mu, sigma) per track."""
-        return self.state.view(-1, 8, 2)
+        """``[P, 8, 2]`` copy of (mu, sigma) per track."""
+        return self.state.view(-1, 8, 4)[:, :, 0::2]
+
+    def mu(self) -> torch.Tensor:
+        return self.state[:, 0::4]
+
+    def sigma(self) -> torch.Tensor:
+        return self.state[:, 2::4]
 
     def track(self, name: str) -> torch.Tensor:
         """``[P, 2]`` (mu, sigma) of ``trueskill`` or ``trueskill_<mode>``."""
         idx = 0 if name in ("shared", "trueskill") else 1 + MODES.index(name.replace("trueskill_", ""))
-        return self.tracks()[:, idx]
+        return self.state[:, 4 * idx:4 * idx + 3:2]
 
     def to(self, device) -> "Roster":
-        return Roster(self.state.to(device), self.attrs.to(device))
+        return Roster(self.state.to(device), self.attrs.to(device), self.epoch)
 
     def clone(self) -> "Roster":
-        return Roster(self.state.clone(), self.attrs.clone())
+        return Roster(self.state.clone(), self.attrs.clone(), self.epoch)
+
+    def next_epoch(self) -> int:
+        """Epoch for the next device launch, resetting the tags when needed."""
+        if self.epoch is None or self.epoch >= 255:
+            native().reset_tags(self.state)
+            self.epoch = 0
+        self.epoch += 1
+        return self.epoch
 
 
 @dataclass
@@ -116,10 +142,11 @@ class BatchRater:
     """Stateless-per-call batched rater with cached device workspaces."""
 
     def __init__(self, cfg: Optional[RaterConfig] = None, host_fp64: bool = True,
-                 max_blocks: int = 2048):
+                 blocks: Optional[int] = None):
         self.cfg = cfg or RaterConfig.from_env()
         self.host_fp64 = host_fp64
-        self.max_blocks = int(max_blocks)
+        # persistent-grid size of the dataflow launch (4 waves per block)
+        self.blocks = int(blocks or os.environ.get("ANA_RATE_BLOCKS", 512))
         self._vst: Dict[str, torch.Tensor] = {}
         self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
 
@@ -140,23 +167,31 @@ class BatchRater:
 
     # ------------------------------------------------------------- schedule
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
-                 occ: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Occurrence index of each slot's player among earlier rated matches."""
+                 tag: str = "") -> Schedule:
+        """Dependency structure of a window (K5): per slot (occurrence index of its
+        player, next slot of that player or -1) and per match the number of
+        distinct players with an earlier occurrence.  ``deps`` is consumed (counted
+        down to 0) by the device rate launch, so a schedule is single-use there.
+        ``tag`` selects a separate buffer set (to prepare the next window while the
+        current one is being rated)."""
         M = rec.shape[0]
-        if occ is None:
-            occ = self._buffer(rec.device, "occ", M * 2 * K, torch.int32).view(M, 2 * K)
+        dev = rec.device
+        link = self._buffer(dev, "link" + tag, M * 4 * K, torch.int32).view(M, 2 * K, 2)
+        deps = self._buffer(dev, "deps" + tag, M, torch.int32)
         if rec.is_cuda:
             nbytes = native().schedule_workspace_bytes(M * 2 * K, num_players)
-            ws = self._buffer(rec.device, "sched_ws", nbytes, torch.uint8)
+            ws = self._buffer(dev, "sched_ws", nbytes, torch.uint8)
+            ctrl = self._buffer(dev, "ctrl", 16, torch.int32)
         else:
             ws = torch.empty(0, dtype=torch.uint8)
-        native().schedule(rec, K, num_players, occ, ws)
-        return occ
+            ctrl = torch.empty(0, dtype=torch.int32)
+        native().schedule(rec, K, num_players, link, deps, ws, ctrl)
+        return Schedule(link, deps)
 
     # ----------------------------------------------------------------- rate
     def rate(self, roster: Roster, rec: torch.Tensor, K: Optional[int] = None,
              out: Optional[RateResult] = None, first_prior: Optional[torch.Tensor] = None,
-             check: bool = True, occ: Optional[torch.Tensor] = None) -> RateResult:
+             check: bool = True, schedule: Optional[Schedule] = None) -> RateResult:
         """Rate every match of ``rec`` in order, updating ``roster`` in place."""
         K = int(K or (rec.shape[1] - 2) // 2)
         M = int(rec.shape[0])
@@ -170,30 +205,35 @@ class BatchRater:
         record = first_prior is not None
         fp = first_prior if record else torch.empty(0, dtype=torch.float32, device=dev)
         if dev.type == "cuda":
-            if occ is None:
-                occ = self.schedule(rec, K, P)
-            ver = self._buffer(dev, "ver", P, torch.int32)
-            ctrl = self._buffer(dev, "ctrl", 4, torch.int32)
+            if schedule is None:
+                schedule = self.schedule(rec, K, P)
+            link, deps = schedule
+            ctrl = self._buffer(dev, "ctrl", 16, torch.int32)
+            epoch = roster.next_epoch()
         else:
-            occ = ver = ctrl = torch.empty(0, dtype=torch.int32)
-        native().rate(rec, K, occ, roster.state, roster.attrs, ver, fp, out.quality, out.status,
+            link = deps = ctrl = torch.empty(0, dtype=torch.int32)
+            epoch = 1
+        native().rate(rec, K, link, deps, roster.state, roster.attrs, fp, out.quality, out.status,
                       out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
                       float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
-                      record, self.max_blocks, self.host_fp64)
+                      record, self.blocks, epoch, self.host_fp64)
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out
 
     def error_flags(self, device) -> torch.Tensor:
-        """Device tensor [timeout, protocol] of the last launch (no sync)."""
-        return self._buffer(device, "ctrl", 4, torch.int32)[1:3]
+        """Device tensor [schedule overflow, timeout, protocol] of the last launch (no sync)."""
+        return self._buffer(device, "ctrl", 16, torch.int32)[0:3]
 
     def check_errors(self, device) -> None:
         flags = self.error_flags(device).cpu()
         if int(flags[0]):
-            raise NativeRateError("dataflow rating timed out (a dependency never resolved)")
+            raise NativeRateError("a player occurs more than 16.7M times in one window; "
+                                  "split the stream into smaller windows")
         if int(flags[1]):
-            raise NativeRateError("dataflow protocol violation (version counter overtook a slot)")
+            raise NativeRateError("dataflow rating timed out (a dependency never resolved)")
+        if int(flags[2]):
+            raise NativeRateError("dataflow protocol violation (a tag overtook its slot)")
 
 
 def rate_stream(roster: Roster, rec: torch.Tensor, K: Optional[int] = None,

@@ -68,18 +68,18 @@ class StreamSpec:
 
 
 def make_roster(spec: RosterSpec, device="cpu"):
-    """Return (state [P,16] f32, attrs [P,4] f32) for ``spec``."""
+    """Return a :class:`Roster` (state [P,32] f32, attrs [P,4] f32) for ``spec``."""
     from .rate import Roster
 
     P = int(spec.num_players)
-    state = torch.empty((P, 16), dtype=torch.float32, device=device)
+    state = torch.empty((P, 32), dtype=torch.float32, device=device)
     attrs = torch.empty((P, 4), dtype=torch.float32, device=device)
     native().gen_roster(state, attrs, int(spec.seed), prob_u32(spec.p_tier_null),
                         prob_u32(spec.p_tier_bad), prob_u32(spec.p_rp_ranked),
                         prob_u32(spec.p_rp_blitz), prob_u32(spec.p_rated),
                         prob_u32(spec.p_mode_rated), spec.mu_lo, spec.mu_span, spec.sig_lo,
                         spec.sig_span)
-    return Roster(state, attrs)
+    return Roster(state, attrs, epoch=0)
 
 
 def make_stream(spec: StreamSpec, num_matches: int, num_players: int, K: Optional[int] = None,

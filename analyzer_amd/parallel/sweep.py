@@ -1,6 +1,6 @@
 """Data-parallel rating with per-window posterior merge.
 
-Each rank holds a replica of the roster (64 B/player: 1M players = 64 MB, so
+Each rank holds a replica of the roster (128 B/player: 1M players = 128 MB, so
 replication is the right call on 288 GB devices), rates its shard of every
 window exactly and in order, and then all ranks merge what they learned with
 ONE dense all-reduce of natural-parameter messages (csrc/sweep.hip):
@@ -42,8 +42,8 @@ class SweepMerger:
             raise ValueError("only fp32 merge messages are supported (touch counts are exact "
                              "integers in the message buffer)")
         f = dict(dtype=torch.float32, device=self.device)
-        self.start = torch.empty((self.P, 16), **f)
-        self.first_prior = torch.full((self.P, 16), float("nan"), **f)
+        self.start = torch.empty((self.P, 32), **f)
+        self.first_prior = torch.full((self.P, 32), float("nan"), **f)
         self.buf = torch.empty((self.P, 16), **f)
         self.vst = torch.tensor(vst_table(), **f)
         self.comm_bytes = self.buf.numel() * 4
@@ -63,6 +63,7 @@ class SweepMerger:
     def apply(self, roster) -> None:
         native().sweep_apply(self.start, self.buf, roster.attrs, roster.state, self.vst,
                              float(self.cfg.unknown_player_sigma))
+        roster.epoch = roster.epoch if roster.epoch is not None else 0  # apply wrote tag 0
 
     def merge(self, roster) -> None:
         """Combine every rank's window into the replicated roster (in place)."""

@@ -87,8 +87,8 @@ def players_from_roster(state: torch.Tensor, attrs: torch.Tensor) -> List[Player
     for p in range(st.shape[0]):
         kw = {}
         for t, col in enumerate(TRACK_COLUMNS):
-            kw[col + "_mu"] = _none_if_nan(float(st[p, 2 * t]))
-            kw[col + "_sigma"] = _none_if_nan(float(st[p, 2 * t + 1])) if kw[col + "_mu"] is not None else None
+            kw[col + "_mu"] = _none_if_nan(float(st[p, 4 * t]))
+            kw[col + "_sigma"] = _none_if_nan(float(st[p, 4 * t + 2])) if kw[col + "_mu"] is not None else None
         tier = _none_if_nan(float(at[p, 2]))
         players.append(Player("p%d" % p, None if tier is None else int(tier),
                               _none_if_nan(float(at[p, 0])), _none_if_nan(float(at[p, 1])), **kw))
@@ -130,22 +130,22 @@ def roster_from_players(players: Sequence[Player], device="cpu"):
     from ..ops.rate import Roster as TRoster
 
     P = len(players)
-    state = torch.full((P, 16), float("nan"), dtype=torch.float64)
-    state[:, 15] = 0
+    state = torch.zeros((P, 32), dtype=torch.float64)
+    state[:, 0::2] = float("nan")
     attrs = torch.full((P, 4), float("nan"), dtype=torch.float64)
     attrs[:, 3] = 0
     for p, pl in enumerate(players):
         for t, col in enumerate(TRACK_COLUMNS):
             mu = getattr(pl, col + "_mu", None)
             if mu is not None:
-                state[p, 2 * t] = float(mu)
+                state[p, 4 * t] = float(mu)
                 sig = getattr(pl, col + "_sigma", None)
-                state[p, 2 * t + 1] = float(sig) if sig is not None else float("nan")
+                state[p, 4 * t + 2] = float(sig) if sig is not None else float("nan")
         for c, name in enumerate(("rank_points_ranked", "rank_points_blitz", "skill_tier")):
             v = getattr(pl, name, None)
             if v is not None:
                 attrs[p, c] = float(v)
-    return TRoster(state.float().to(device), attrs.float().to(device))
+    return TRoster(state.float().to(device), attrs.float().to(device), epoch=0)
 
 
 def encode_matches(matches: Sequence[Match], player_index: Dict[int, int], K: int,

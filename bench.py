@@ -73,7 +73,7 @@ def main(argv=None) -> int:
     rater = BatchRater()
     out = RateResult.allocate(M, K, dev)
     merger = SweepMerger(P, dev) if world > 1 else None
-    err = torch.zeros(2, dtype=torch.int32, device=dev)
+    err = torch.zeros(3, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
 
     def step(i):

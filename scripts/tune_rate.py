@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Time the schedule prepass and the dataflow launch separately for several
+persistent-grid sizes, interleaved in one process (guide §5.4 rule 24)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from analyzer_amd.ops.rate import BatchRater, RateResult  # noqa: E402
+from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--players", type=int, default=1_000_000)
+    ap.add_argument("--matches", type=int, default=10_000_000)
+    ap.add_argument("--team-size", type=int, default=3)
+    ap.add_argument("--blocks", default="128,256,512,1024,2048")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--hot", type=float, default=0.0)
+    ap.add_argument("--pattern", default="random", choices=["random", "serial", "disjoint"])
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    P, M, K = args.players, args.matches, args.team_size
+    rec = make_stream(StreamSpec(team_size=K, seed=5, p_hot=args.hot, p_afk=0.0), M, P, device=dev)
+    if args.pattern == "serial":      # every match has the same 2K players: chain depth = M
+        rec[:, :2 * K] = torch.arange(2 * K, dtype=torch.int32, device=dev)
+    elif args.pattern == "disjoint":  # no player repeats: nothing ever waits
+        assert P >= 2 * K * M, "disjoint pattern needs players >= 2K * matches"
+        rec[:, :2 * K] = (torch.arange(M, dtype=torch.int32, device=dev)[:, None] * (2 * K)
+                          + torch.arange(2 * K, dtype=torch.int32, device=dev)[None, :])
+    out = RateResult.allocate(M, K, dev)
+    results = {}
+    for rnd in range(args.rounds):
+        for b in [int(x) for x in args.blocks.split(",")]:
+            roster = make_roster(RosterSpec(num_players=P, seed=1), device=dev)
+            br = BatchRater(blocks=b)
+            br.schedule(rec, K, P)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sched = br.schedule(rec, K, P)
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            br.rate(roster, rec, K, out=out, schedule=sched, check=False)
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            br.check_errors(dev)
+            results.setdefault(b, []).append(((t1 - t0) * 1e3, (t2 - t1) * 1e3))
+            print("round %d blocks %5d schedule %7.2f ms rate %8.2f ms" % (rnd, b, (t1 - t0) * 1e3,
+                                                                          (t2 - t1) * 1e3), flush=True)
+    summary = {b: {"schedule_ms_min": min(x[0] for x in v), "rate_ms_min": min(x[1] for x in v),
+                   "rate_ms_median": sorted(x[1] for x in v)[len(v) // 2]} for b, v in results.items()}
+    print(json.dumps({"pattern": args.pattern, "players": P, "matches": M, "team_size": K, "hot": args.hot,
+                      "by_blocks": summary}))
+
+
+if __name__ == "__main__":
+    main()

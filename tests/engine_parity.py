@@ -64,13 +64,13 @@ def object_run(roster, rec, K, cfg=None):
             for c in TRACK_COLUMNS:
                 setattr(pl, c + "_mu", _f32(getattr(pl, c + "_mu")))
                 setattr(pl, c + "_sigma", _f32(getattr(pl, c + "_sigma")))
-    state = np.full((len(players), 16), np.nan)
+    state = np.full((len(players), 8, 2), np.nan)
     for p, pl in enumerate(players):
         for t, c in enumerate(TRACK_COLUMNS):
             mu = getattr(pl, c + "_mu")
             if mu is not None:
-                state[p, 2 * t] = mu
-                state[p, 2 * t + 1] = getattr(pl, c + "_sigma")
+                state[p, t, 0] = mu
+                state[p, t, 1] = getattr(pl, c + "_sigma")
     return dict(quality=quality, status=status, state=state, **outs)
 
 
@@ -84,10 +84,9 @@ def assert_engine_matches(res: "R.RateResult", roster_after, ref, *, rtol, atol_
                                    atol=atol_mu, equal_nan=True, err_msg=k)
     np.testing.assert_allclose(res.delta.cpu().numpy(), ref["delta"], rtol=0, atol=atol_delta,
                                equal_nan=True)
-    got = roster_after.state.cpu().numpy().astype(np.float64)
-    got[:, 14:] = np.nan  # spare slot
+    got = roster_after.tracks().cpu().numpy().astype(np.float64)
+    got[:, 7] = np.nan  # spare granule
     exp = ref["state"].copy()
-    exp[:, 14:] = np.nan
     np.testing.assert_allclose(got, exp, rtol=rtol, atol=atol_mu, equal_nan=True)
 
 

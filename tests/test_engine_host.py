@@ -67,17 +67,28 @@ def test_schedule_occurrence_index_host():
     from analyzer_amd.ops.rate import BatchRater
 
     rec = make_stream(StreamSpec(team_size=3, seed=9, p_afk=0.1), 300, 20)
-    occ = BatchRater().schedule(rec, 3, 20).numpy()
-    seen = {}
+    link, deps = BatchRater().schedule(rec, 3, 20)
+    link, deps = link.numpy(), deps.numpy()
+    seen, last = {}, {}
+    expect_deps = np.zeros(rec.shape[0], dtype=np.int64)
     for m in range(rec.shape[0]):
-        meta1 = int(rec[m, 7])
-        afk = bool(meta1 & 4)
+        if int(rec[m, 7]) & 4:  # AFK: no state, not scheduled
+            assert deps[m] == 0
+            continue
+        firsts = set()
         for j in range(6):
             pid = int(rec[m, j])
-            if afk:
-                continue
-            assert occ[m, j] == seen.get(pid, 0)
+            assert link[m, j, 0] == seen.get(pid, 0)
+            if pid not in firsts:
+                firsts.add(pid)
+                expect_deps[m] += seen.get(pid, 0) > 0
+            if pid in last:
+                assert link.reshape(-1, 2)[last[pid], 1] == m * 6 + j  # successor link
             seen[pid] = seen.get(pid, 0) + 1
+            last[pid] = m * 6 + j
+    assert (deps == expect_deps).all()
+    for pid, slot in last.items():  # last occurrences have no successor
+        assert link.reshape(-1, 2)[slot, 1] == -1
 
 
 def test_status_counts_and_any_afk():
