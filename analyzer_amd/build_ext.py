@@ -23,7 +23,7 @@ BUILD = PKG.parent / "build" / "analyzer_amd"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-HIP_SOURCES = ["kernels.hip", "sweep.hip", "telemetry.hip"]
+HIP_SOURCES = ["kernels.hip", "radix_sort.hip", "dataflow.hip", "sweep.hip", "telemetry.hip"]
 CPP_SOURCES = ["host.cpp", "bindings.cpp"]
 
 

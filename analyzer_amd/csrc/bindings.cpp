@@ -3,6 +3,8 @@
 // mirror of host.cpp.  Every shape/dtype/device assumption a kernel makes is
 // checked here, on the host, before anything is launched.
 #include <torch/extension.h>
+
+#include <cstdlib>
 #include <ATen/hip/HIPContext.h>
 
 #include <string>
@@ -107,6 +109,28 @@ int64_t schedule_workspace_bytes(int64_t nslots, int64_t num_players) {
   return (int64_t)ana::schedule_workspace_bytes(nslots, num_players);
 }
 
+// Stable sort of int32 (key, value) pairs by the low ``bits`` key bits on the
+// device (the K5 radix sort, exposed for tests and tools).  Returns new tensors.
+std::vector<Tensor> sort_pairs(Tensor keys, Tensor vals, int64_t bits) {
+  const auto dev = keys.device();
+  TORCH_CHECK(dev.is_cuda(), "sort_pairs runs on the device");
+  check(keys, "keys", torch::kInt32, dev);
+  check(vals, "vals", torch::kInt32, dev);
+  const int64_t n = keys.numel();
+  TORCH_CHECK(vals.numel() == n, "keys and vals must have the same length");
+  TORCH_CHECK(bits >= 1 && bits <= 32, "bits must be 1..32");
+  auto ka = keys.clone(), va = vals.clone();
+  auto kb = torch::empty_like(ka), vb = torch::empty_like(va);
+  auto ws = torch::empty({(int64_t)ana::radix_sort_workspace_bytes(n)},
+                         keys.options().dtype(torch::kUInt8));
+  int in_alt = 0;
+  auto u = [](Tensor& t) { return reinterpret_cast<uint32_t*>(t.data_ptr<int32_t>()); };
+  check_hip(ana::launch_radix_sort_pairs(u(ka), u(va), u(kb), u(vb), n, (int)bits,
+                                         ws.data_ptr<uint8_t>(), &in_alt, stream_of(keys)),
+            "sort_pairs");
+  return in_alt ? std::vector<Tensor>{kb, vb} : std::vector<Tensor>{ka, va};
+}
+
 void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
               Tensor workspace, Tensor ctrl) {
   const auto dev = rec.device();
@@ -116,11 +140,12 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
   TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
   const int64_t M = rec.size(0);
-  TORCH_CHECK(link.dim() == 3 && link.size(0) == M && link.size(1) == 2 * K && link.size(2) == 2,
+  TORCH_CHECK(link.dim() == 3 && link.size(0) == M && link.size(1) == 2 * K &&
+                  link.size(2) == ana::kLinkWords,
               "link must be [M, 2K, 2]");
   TORCH_CHECK(deps.numel() == M, "deps must have M entries");
   TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
-  TORCH_CHECK(M * 2 * K < 0x7fffffffLL, "too many slots for one schedule (split the stream)");
+  TORCH_CHECK(M * 2 * K <= ana::kMaxSlots, "more than 2^28 slots in one window (split the stream)");
   if (dev.is_cuda()) {
     check(workspace, "workspace", torch::kUInt8, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
@@ -188,11 +213,12 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   TORCH_CHECK(epoch >= 1 && epoch <= 255, "epoch must be 1..255");
   prm.epoch = (int32_t)epoch;
   prm.vst = vst.data_ptr<float>();
+  if (const char* e = std::getenv("ANA_RATE_IDLE")) prm.idle_spins = std::atoi(e);  // tuning knob
   if (dev.is_cuda()) {
     check(link, "link", torch::kInt32, dev);
     check(deps, "deps", torch::kInt32, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
-    TORCH_CHECK(link.numel() == M * S * 2, "link must be [M, 2K, 2]");
+    TORCH_CHECK(link.numel() == M * S * ana::kLinkWords, "link must be [M, 2K, 2]");
     TORCH_CHECK(deps.numel() == M, "deps must have M entries");
     TORCH_CHECK(ctrl.numel() >= 16, "ctrl must have 16 entries");
     TORCH_CHECK(blocks >= 1 && blocks <= 65535, "blocks must be 1..65535");
@@ -271,6 +297,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gen_roster", &gen_roster, "K7: synthetic roster (state [P,16], attrs [P,4])");
   m.def("gen_stream", &gen_stream, "K7: synthetic match stream rec [M, 2K+2]");
   m.def("schedule_workspace_bytes", &schedule_workspace_bytes);
+  m.def("sort_pairs", &sort_pairs, "stable LSD radix sort of int32 (key, value) pairs (device)");
   m.def("schedule", &schedule, "K5: per-slot occurrence index (chronological order per player)");
   m.def("rate", &rate, "K1-K4/K6: exact dataflow rating of a stream");
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");

@@ -32,8 +32,20 @@ namespace ana {
 constexpr int kTracks = 7;        // shared + 6 modes
 constexpr int kGranules = 8;      // 16-B granules per player row
 constexpr int kRowFloats = 32;    // floats per player row (128 B)
-constexpr int kTagBits = 24;      // low bits of a tag = occurrence count + 1
-constexpr uint32_t kMaxOcc = (1u << kTagBits) - 2;
+// Schedule link of a slot (K5), 8 bytes: word 0 = match of the player's next
+// occurrence (kNoMatch: none) | kLinkHasPred | kLinkHasPredMode, word 1 = match
+// of its next occurrence in the same game mode.  A match publishes each
+// player's shared granule tagged with word 0 and the mode granule tagged with
+// word 1, so the reader of a granule recognises the write it waits for by its
+// own match index (csrc/dataflow.hip).
+constexpr int kLinkWords = 2;
+constexpr uint32_t kNoMatch = 0x0fffffffu;
+constexpr uint32_t kMatchMask = 0x0fffffffu;
+constexpr uint32_t kLinkHasPred = 1u << 30;      // the player occurred earlier in the window
+constexpr uint32_t kLinkHasPredMode = 1u << 31;  // ... earlier in a match of the same mode
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr int kSlotBits = 28;     // sort values carry slot | mode << kSlotBits
+constexpr int64_t kMaxSlots = 1ll << kSlotBits;
 constexpr int kModes = 6;
 constexpr int kModeUnsupported = 255;
 constexpr int kVstTiers = 31;     // tiers -1..29
@@ -59,8 +71,9 @@ struct RateParams {
   int32_t num_players;
   int64_t num_matches;
   int32_t record_first_prior;  // sweep mode: remember priors of NULL tracks
-  int32_t epoch;               // 1..255: high byte of every tag written by this launch
+  int32_t epoch;               // 1..255: granule tag word 1 of this launch (word 3 = match)
   const float* vst;            // vst_points[tier + 1], kVstTiers entries (device/host memory)
+  int32_t idle_spins;          // dataflow: max s_sleep(2) rounds of an idle wave (0 = default)
 };
 
 // Per-match outputs, structure-of-arrays.  Per-slot arrays are [M][2K]; the

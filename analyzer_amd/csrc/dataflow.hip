@@ -1,0 +1,475 @@
+// K1-K4, K3, K6: the dataflow rating executor for MI355X (gfx950).
+//
+// ONE persistent launch rates a whole window of matches in exact per-player
+// chronological order -- the order the reference gets from
+// ORDER BY created_at + a sequential loop (/root/reference/worker.py:176-192)
+// -- without rounds or grid barriers (Kahn's algorithm over per-player chains):
+//
+//  * The schedule prepass (kernels.hip) gives every slot the slot of its
+//    player's next occurrence (link) and every match the number of distinct
+//    players with an earlier occurrence (deps).
+//  * 8 sharded tickets (MICROARCH "dequeue") hand out chunks of 64
+//    consecutive matches.  A wave holds up to 4 chunks (256 matches; records
+//    cached in LDS), so ~1M matches wait in flight GPU-wide: per-player
+//    dependency levels of a random stream spread over hundreds of thousands of
+//    matches, and a narrower window starves the machine.  Waiting costs nothing
+//    per match: the wave polls its chunks' deps counters with one coalesced
+//    4-B sc1 load per lane.
+//  * The oldest ready matches go to the wave's lane groups (G lanes = one
+//    match, one roster slot per lane).  A group gathers its players' 16-B
+//    granules {mu, epoch, sigma, reader match} (sc1 buffer loads), seeds,
+//    rates both tracks (rate_core.h), publishes the granules (sc1 stores) and
+//    at once decrements the deps counter of each player's next match.  The
+//    notification does not wait for the stores: each granule is tagged with
+//    the match that will read it next (the player's next match for the shared
+//    granule, its next same-mode match for the mode granule: schedule link
+//    words), a reader with an in-window predecessor checks for its own match
+//    index and retries the match otherwise, so a dependency hop costs no
+//    store round trip.
+//  * Software pipeline, one memory round trip per iteration: this iteration's
+//    granule/link/attribute loads, the next iteration's counter polls and the
+//    next chunk ticket retire in ONE vmcnt(0) wait.
+//
+// Claims are monotone per ticket shard and every claimed match is held by a
+// running wave, so the oldest unfinished match is always ready: no deadlock
+// whatever the residency.  Spins back off and give up after 5 s.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "kernels.h"
+#include "rate_core.h"
+
+namespace ana {
+
+typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr uint64_t kTimeoutTicks = 500000000ull;  // 5 s of the 100 MHz s_memrealtime clock
+constexpr int kHeads = 8;                          // ticket shards
+constexpr int kChunk = 64;                         // matches per ticket = one per lane
+constexpr int kHeld = 4;                           // chunks a wave keeps in flight
+constexpr int kWavesPerBlock = 4;
+
+template <int G>
+__device__ __forceinline__ float group_sum(float x) {
+#pragma unroll
+  for (int off = G / 2; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+  return x;
+}
+
+// {mu, epoch, sigma, writer match}: the tag words let a reader verify that the
+// write it depends on has landed
+__device__ __forceinline__ v4i granule(float mu, int epoch, float sig, uint32_t m) {
+  v4i v;
+  v.x = __float_as_int(mu);
+  v.y = epoch;
+  v.z = __float_as_int(sig);
+  v.w = (int)m;
+  return v;
+}
+
+// position of the k-th (0-based) set bit of x (x has more than k bits set)
+__device__ __forceinline__ int nth_set_bit(uint64_t x, int k) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t low = x & ((1ull << w) - 1ull);
+    const int c = __popcll(low);
+    if (k >= c) {
+      k -= c;
+      x >>= w;
+      pos += w;
+    } else {
+      x = low;
+    }
+  }
+  return pos;
+}
+
+// early outcome of a match that touches no state (decided when its chunk arrives)
+template <int K>
+__device__ __forceinline__ uint8_t early_status(const int32_t* r, int64_t P) {
+  constexpr int S = 2 * K;
+  const uint32_t m0 = (uint32_t)r[S], m1 = (uint32_t)r[S + 1];
+  const int n0 = meta_n0(m0), n1 = meta_n1(m0);
+  bool bad = n0 > K || n1 > K;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int pos = j < K ? j : j - K;
+    if (pos < (j < K ? n0 : n1) && (r[j] < 0 || (int64_t)r[j] >= P)) bad = true;
+  }
+  if (meta_mode(m0) >= kModes) return kUnsupportedMode;
+  if (bad) return kErrBadRecord;
+  if (meta_nrosters(m0) != 2) return kInvalidRosters;
+  if (meta_afk(m1)) return kAfk;
+  return kRated;
+}
+
+template <int K>
+__global__ void __launch_bounds__(256)
+rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
+                     int32_t* deps, float* state, const float* __restrict__ attrs,
+                     float* __restrict__ first_prior, RateOut out, uint32_t* ctrl,
+                     RateParams prm) {
+  constexpr int S = 2 * K;
+  constexpr int R = S + 2;
+  constexpr int G = S <= 2 ? 2 : (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
+  constexpr int NG = 64 / G;
+  __shared__ int32_t lrec[kWavesPerBlock][kHeld][kChunk * R];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int j = lane % G;
+  const int g = lane / G;
+  const int gbase = lane - j;
+  const uint64_t gmask = (((1ull << G) - 1ull) << gbase);
+  const bool r0 = j < K;
+  const int rpos = r0 ? j : j - K;
+  const int64_t M = prm.num_matches;
+  const int64_t P = prm.num_players;
+  const float beta2 = prm.beta2, tau2 = prm.tau2, us = prm.unknown_sigma;
+  const int epoch = prm.epoch;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(state, 0, (int)(P * kRowFloats * 4), 0x00020000);
+  const int head = blockIdx.x % kHeads;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+
+  int64_t cbase[kHeld];   // wave-uniform: first match of each held chunk, -1 = free slot
+  uint64_t pend[kHeld];   // wave-uniform: stateful matches not yet handed to a group
+  uint32_t dval[kHeld];   // per lane: deps counter of match cbase+lane, as last polled
+#pragma unroll
+  for (int h = 0; h < kHeld; ++h) {
+    cbase[h] = -1;
+    pend[h] = 0ull;
+    dval[h] = 1u;
+  }
+  bool exhausted = false, tk_pending = false;
+  unsigned tk = 0;                 // ticket returned to lane 0
+  uint32_t spins = 0;
+  const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : 8u;
+
+  for (;;) {
+    // ---------------------------------------------- (1) a ticket came back: stage its chunk
+    int staging = -1;
+    int32_t r[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) r[k] = -1;
+    if (tk_pending) {
+      const unsigned t = __shfl(tk, 0);
+      tk_pending = false;
+      const int64_t c = (int64_t)t * kHeads + head;
+      if (c * kChunk >= M) {
+        exhausted = true;
+      } else {
+#pragma unroll
+        for (int h = kHeld - 1; h >= 0; --h)
+          if (cbase[h] < 0) staging = h;
+#pragma unroll
+        for (int h = 0; h < kHeld; ++h)
+          if (h == staging) cbase[h] = c * kChunk;
+        const int64_t m = c * kChunk + lane;
+        if (m < M) {
+          const int32_t* src = rec + m * R;
+          if constexpr (R % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < R / 4; ++k) {
+              const int4 v = reinterpret_cast<const int4*>(src)[k];
+              r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < R; ++k) r[k] = src[k];
+          }
+        }
+      }
+    }
+
+    // ---------------------------------------------- (2) readiness from the last poll
+    uint64_t ready[kHeld];
+#pragma unroll
+    for (int h = 0; h < kHeld; ++h) ready[h] = __ballot(dval[h] == 0u) & pend[h];
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
+
+    // ---------------------------------------------- (3) oldest ready matches -> groups
+    int my_h = -1, my_bit = 0, nassigned = 0;
+#pragma unroll
+    for (int pass = 0; pass < kHeld; ++pass) {
+      int best = -1;
+      int64_t bb = 0;
+#pragma unroll
+      for (int h = 0; h < kHeld; ++h)
+        if (ready[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
+      if (best < 0 || nassigned >= NG) break;
+      uint64_t rdy = 0;
+#pragma unroll
+      for (int h = 0; h < kHeld; ++h) if (h == best) rdy = ready[h];
+      const int cnt = __popcll(rdy);
+      const int take = cnt < NG - nassigned ? cnt : NG - nassigned;
+      if (g >= nassigned && g < nassigned + take) {
+        my_h = best;
+        my_bit = nth_set_bit(rdy, g - nassigned);
+      }
+      uint64_t taken = rdy;
+      if (take < cnt) taken &= (1ull << nth_set_bit(rdy, take)) - 1ull;
+#pragma unroll
+      for (int h = 0; h < kHeld; ++h)
+        if (h == best) { pend[h] &= ~taken; ready[h] = 0ull; }
+      nassigned += take;
+    }
+    const bool worked = nassigned > 0;
+
+    // ---------------------------------------------- (4) this group's loads
+    int64_t m = 0;
+    int mode = 0, n0 = 0, n1 = 0, rank0 = 1, rank1 = 1, first = j, prevdup = -1;
+    int32_t id = -1;
+    bool inr = false, islast = false, own = false;
+    uint32_t lk0 = kNoMatch, lk1 = kNoMatch;  // schedule link words (common.h)
+    v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
+    float4 at4 = make_float4(NAN, NAN, NAN, 0.f);
+    if (my_h >= 0) {
+      int64_t cb = 0;
+#pragma unroll
+      for (int h = 0; h < kHeld; ++h) if (h == my_h) cb = cbase[h];
+      m = cb + my_bit;
+      const int32_t* lr = &lrec[wv][my_h][my_bit * R];
+      const uint32_t m0 = (uint32_t)lr[S], m1 = (uint32_t)lr[S + 1];
+      mode = meta_mode(m0);
+      n0 = meta_n0(m0);
+      n1 = meta_n1(m0);
+      rank0 = meta_winner0(m1) ? 0 : 1;
+      rank1 = meta_winner1(m1) ? 0 : 1;
+      inr = j < S && rpos < (r0 ? n0 : n1);
+      id = inr ? lr[j] : -1;
+      islast = true;
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        const int32_t oid = __shfl(id, gbase + q);
+        if (id >= 0 && oid == id) {
+          if (q < j) {
+            if (first == j) first = q;
+            prevdup = q;
+          }
+          if (q > j) islast = false;
+        }
+      }
+      own = inr && first == j;
+      if (inr) {
+        const uint2 lk = reinterpret_cast<const uint2*>(link)[m * S + j];
+        lk0 = lk.x;
+        lk1 = lk.y;
+      }
+      if (own) {  // state and seed attributes in the same round trip
+        const int off = id * (kRowFloats * 4);
+        gs = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+        gm = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * (1 + mode), 0, 16);
+        at4 = reinterpret_cast<const float4*>(attrs)[id];
+      }
+    }
+
+    // ---------------------------------------------- (5) next iteration's counter polls
+#pragma unroll
+    for (int h = 0; h < kHeld; ++h)
+      if ((pend[h] >> lane) & 1ull)
+        dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+
+    // ---------------------------------------------- (6) next ticket if a ring slot is free
+    {
+      bool free_slot = false;
+#pragma unroll
+      for (int h = 0; h < kHeld; ++h) free_slot |= cbase[h] < 0;
+      if (free_slot && !exhausted) {
+        if (lane == 0)
+          tk = __hip_atomic_fetch_add((gu32*)&ctrl[4 + head], 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+        tk_pending = true;
+      }
+    }
+
+    // ---------------------------------------------- (7) the one wait of the iteration
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---------------------------------------------- (9) install the staged chunk
+    if (staging >= 0) {
+      int64_t cb = 0;
+#pragma unroll
+      for (int h = 0; h < kHeld; ++h) if (h == staging) cb = cbase[h];
+      const int64_t mm = cb + lane;
+#pragma unroll
+      for (int k = 0; k < R; ++k) lrec[wv][staging][lane * R + k] = r[k];
+      const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
+      if (mm < M && est != kRated) {  // no state, no dependencies: finish it now
+#pragma unroll
+        for (int q = 0; q < S; ++q) {
+          out.s_mu[mm * S + q] = NAN;
+          out.s_sig[mm * S + q] = NAN;
+          out.delta[mm * S + q] = NAN;
+          out.m_mu[mm * S + q] = NAN;
+          out.m_sig[mm * S + q] = NAN;
+        }
+        out.quality[mm] = (est == kAfk || est == kInvalidRosters) ? 0.f : NAN;
+        out.status[mm] = est;
+      }
+      const uint64_t pm = __ballot(mm < M && est == kRated);
+#pragma unroll
+      for (int h = 0; h < kHeld; ++h)
+        if (h == staging) {
+          pend[h] = pm;
+          dval[h] = 1u;  // first poll next iteration
+          if (pm == 0ull) cbase[h] = -1;
+        }
+    }
+
+    // ---------------------------------------------- (10) rate this batch
+    // A deps counter can reach 0 before the writes it announces have landed
+    // (notifications do not wait for store acknowledgements): a group whose
+    // granules do not carry the tags of their last writers retries next iteration.
+    const bool fresh =
+        !own || ((!(lk0 & kLinkHasPred) || (gs.y == epoch && (uint32_t)gs.w == (uint32_t)m)) &&
+                 (!(lk0 & kLinkHasPredMode) || (gm.y == epoch && (uint32_t)gm.w == (uint32_t)m)));
+    const uint64_t stale_lanes = __ballot(!fresh);
+    if (stale_lanes) {
+      const bool gstale = (stale_lanes & gmask) != 0ull;
+#pragma unroll
+      for (int h = 0; h < kHeld; ++h) {
+        uint64_t back = 0ull;
+        for (int q = 0; q < NG; ++q) {
+          const int bq = __shfl(gstale && my_h == h ? my_bit : -1, q * G);
+          if (bq >= 0) back |= 1ull << bq;
+        }
+        pend[h] |= back;
+      }
+      if (gstale) my_h = -1;
+    }
+    if (my_h >= 0) {
+      const float smu = __int_as_float(gs.x), ssg = __int_as_float(gs.z);
+      const float mmu = __int_as_float(gm.x), msg = __int_as_float(gm.z);
+      const float attr[4] = {at4.x, at4.y, at4.z, at4.w};
+      float pms = 0.f, pss = 1.f, pmm = 0.f, psm = 1.f;
+      uint32_t pflags = 0;
+      uint8_t lst = kRated;
+      if (own)
+        lst = player_prior<float>(smu, ssg, mmu, msg, attr, us, prm.vst, pms, pss, pmm, psm,
+                                  pflags);
+      const uint64_t eb = __ballot(lst != kRated) & gmask;
+      uint8_t gst = kRated;
+      if (eb) gst = (uint8_t)__shfl((int)lst, (int)__builtin_ctzll(eb));
+      // duplicates see the pre-match values of their first occurrence
+      const int src = gbase + first;
+      pms = __shfl(pms, src);
+      pss = __shfl(pss, src);
+      pmm = __shfl(pmm, src);
+      psm = __shfl(psm, src);
+      pflags = (uint32_t)__shfl((int)pflags, src);
+      const float rsmu = __shfl(smu, src), rssg = __shfl(ssg, src);
+      const float rmmu = __shfl(mmu, src), rmsg = __shfl(msg, src);
+      if (gst == kRated && (n0 == 0 || n1 == 0)) gst = kErrEmptyRoster;
+      float nsm = NAN, nss = NAN, nmm = NAN, nms = NAN, dl = NAN, q = NAN;
+      if (gst == kRated) {
+        const float sgn = r0 ? 1.f : -1.f;
+        const float s_c2 = group_sum<G>(inr ? pss * pss + tau2 : 0.f);
+        const float s_d = group_sum<G>(inr ? sgn * pms : 0.f);
+        const float m_c2 = group_sum<G>(inr ? psm * psm + tau2 : 0.f);
+        const float m_d = group_sum<G>(inr ? sgn * pmm : 0.f);
+        const float m_q = group_sum<G>(inr ? psm * psm : 0.f);
+        const int n = n0 + n1;
+        const float nb2 = (float)n * beta2;
+        q = quality_from_sums<float>(n, m_q, m_d, beta2);
+        const UpdCoef<float> ks = update_coef<float>(s_d, nb2 + s_c2, rank0, rank1);
+        const UpdCoef<float> km = update_coef<float>(m_d, nb2 + m_c2, rank0, rank1);
+        apply_coef<float>(ks, r0, pms, pss, tau2, nsm, nss);
+        apply_coef<float>(km, r0, pmm, psm, tau2, nmm, nms);
+        const bool bad_num = inr && !(isfinite(nsm) && isfinite(nss) && isfinite(nmm) &&
+                                      isfinite(nms) && isfinite(q));
+        if ((__ballot(bad_num) & gmask) != 0ull) gst = kErrNumeric;
+        // conservative-skill delta (rater.py:150-153), in slot (= write) order
+        const float cur = nsm - nss;
+        const float prevw = __shfl(cur, gbase + (prevdup >= 0 ? prevdup : j));
+        if (prevdup >= 0) dl = cur - prevw;
+        else if (pflags & 1u) dl = cur - (pms - pss);
+        else dl = 0.f;
+      }
+      const bool ok = gst == kRated && inr;
+      if (inr && islast) {  // publish: new values, or the untouched ones on error
+        const int off = id * (kRowFloats * 4);
+        // tagged with the match that will read them next (link words 0 and 1)
+        const uint32_t succ = lk0 & kMatchMask;
+        __builtin_amdgcn_raw_buffer_store_b128(
+            ok ? granule(nmm, epoch, nms, lk1) : granule(rmmu, epoch, rmsg, lk1),
+            rs, off + 16 * (1 + mode), 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(
+            ok ? granule(nsm, epoch, nss, succ) : granule(rsmu, epoch, rssg, succ),
+            rs, off, 0, 16);
+        if (succ != kNoMatch)  // the successor verifies the tags, so no store wait
+          __hip_atomic_fetch_add((gu32*)(deps + succ), 0xffffffffu, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (ok && prm.record_first_prior && own) {
+        float* fp = first_prior + (int64_t)id * kRowFloats;
+        if (pflags & 2u) { fp[0] = pms; fp[2] = pss; }
+        if (pflags & 4u) { fp[4 * (1 + mode)] = pmm; fp[4 * (1 + mode) + 2] = psm; }
+      }
+      if (j < S) {
+        out.s_mu[m * S + j] = ok ? nsm : NAN;
+        out.s_sig[m * S + j] = ok ? nss : NAN;
+        out.delta[m * S + j] = ok ? dl : NAN;
+        out.m_mu[m * S + j] = ok ? nmm : NAN;
+        out.m_sig[m * S + j] = ok ? nms : NAN;
+      }
+      if (j == 0) {
+        out.quality[m] = gst == kRated ? q : NAN;
+        out.status[m] = gst;
+      }
+    }
+
+    // ---------------------------------------------- (11) retire finished chunks
+#pragma unroll
+    for (int h = 0; h < kHeld; ++h)
+      if (cbase[h] >= 0 && pend[h] == 0ull) cbase[h] = -1;
+
+    // ---------------------------------------------- (12) done?
+    bool held = false;
+#pragma unroll
+    for (int h = 0; h < kHeld; ++h) held |= cbase[h] >= 0;
+    if (exhausted && !held && !tk_pending) break;
+
+    // ---------------------------------------------- (13) idle: back off, bounded
+    if (worked || staging >= 0) {
+      spins = 0;
+    } else {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
+        if (lane == 0) atomicOr(&ctrl[1], 1u);
+#pragma unroll
+        for (int h = 0; h < kHeld; ++h)
+          if (cbase[h] >= 0 && ((pend[h] >> lane) & 1ull)) out.status[cbase[h] + lane] = kNotProcessed;
+        return;  // give up: the host sees ctrl[1] and raises
+      }
+      spins = spins < max_spins ? spins + 1u : max_spins;
+      for (uint32_t k = 0; k < spins; ++k) __builtin_amdgcn_s_sleep(2);
+    }
+  }
+}
+
+int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, float* state,
+                const float* attrs, float* first_prior, const RateOut& out, uint32_t* ctrl,
+                const RateParams& prm, int blocks, hipStream_t s) {
+  const int64_t M = prm.num_matches;
+  // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] spare, [4..11] tickets
+  if (hipMemsetAsync(ctrl + 1, 0, 11 * 4, s) != hipSuccess) return (int)hipGetLastError();
+  if (M <= 0) return 0;
+  if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  if (prm.epoch < 1 || prm.epoch > 255) return (int)hipErrorInvalidValue;
+  if (blocks < kHeads) blocks = kHeads;
+  switch (K) {
+#define ANA_RATE_CASE(k)                                                                      \
+  case k:                                                                                     \
+    hipLaunchKernelGGL(rate_dataflow_kernel<k>, dim3((unsigned)blocks), dim3(256), 0, s, rec,  \
+                       link, deps, state, attrs, first_prior, out, ctrl, prm);                \
+    break;
+    ANA_RATE_CASE(1) ANA_RATE_CASE(2) ANA_RATE_CASE(3) ANA_RATE_CASE(4) ANA_RATE_CASE(5)
+#undef ANA_RATE_CASE
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace ana

@@ -17,8 +17,17 @@ int launch_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M, 
 int launch_reset_tags(float* state, int64_t P, hipStream_t s);
 
 size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
-// link: uint32 [M][2K][2] = (occurrence index, next slot of the same player or ~0u)
+
+// Stable LSD radix sort of (key, value) pairs on the low ``bits`` key bits
+// (radix_sort.hip).  Ping-pongs between the two buffer pairs; *result_in_alt
+// says which holds the result.  ws: radix_sort_workspace_bytes(n) bytes.
+size_t radix_sort_workspace_bytes(int64_t n);
+int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                            int64_t n, int bits, void* ws, int* result_in_alt, hipStream_t s);
+// link: uint32 [M][2K] = next slot of the same player (0x7fffffff: none)
+//       | 0x80000000 if the player has an earlier occurrence in the window
 // deps: int32 [M] = distinct players with an earlier occurrence in the window
+// overflow: zeroed (reserved for schedule error reporting)
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s);
 

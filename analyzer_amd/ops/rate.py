@@ -44,8 +44,15 @@ class NativeRateError(RuntimeError):
 
 
 class Schedule(NamedTuple):
-    link: torch.Tensor  # [M, 2K, 2] int32: (occurrence index, next slot of the player or -1)
+    # [M, 2K, 2] int32 per slot: next match of the player (NO_MATCH: none)
+    # | HAS_PRED | HAS_PRED_MODE, next match of the player in the same mode
+    link: torch.Tensor
     deps: torch.Tensor  # [M] int32: players with an earlier occurrence in the window
+
+    NO_MATCH = 0x0FFFFFFF
+    MATCH_MASK = 0x0FFFFFFF
+    HAS_PRED = 1 << 30
+    HAS_PRED_MODE = 1 << 31
 
 
 @dataclass
@@ -168,15 +175,16 @@ class BatchRater:
     # ------------------------------------------------------------- schedule
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
                  tag: str = "") -> Schedule:
-        """Dependency structure of a window (K5): per slot (occurrence index of its
-        player, next slot of that player or -1) and per match the number of
-        distinct players with an earlier occurrence.  ``deps`` is consumed (counted
+        """Dependency structure of a window (K5): per slot the matches of its
+        player's next occurrence (any mode / same mode) and whether it occurred
+        earlier, and per match the number of distinct players with an earlier
+        occurrence.  ``deps`` is consumed (counted
         down to 0) by the device rate launch, so a schedule is single-use there.
         ``tag`` selects a separate buffer set (to prepare the next window while the
         current one is being rated)."""
         M = rec.shape[0]
         dev = rec.device
-        link = self._buffer(dev, "link" + tag, M * 4 * K, torch.int32).view(M, 2 * K, 2)
+        link = self._buffer(dev, "link" + tag, M * 2 * K * 2, torch.int32).view(M, 2 * K, 2)
         deps = self._buffer(dev, "deps" + tag, M, torch.int32)
         if rec.is_cuda:
             nbytes = native().schedule_workspace_bytes(M * 2 * K, num_players)
@@ -228,8 +236,7 @@ class BatchRater:
     def check_errors(self, device) -> None:
         flags = self.error_flags(device).cpu()
         if int(flags[0]):
-            raise NativeRateError("a player occurs more than 16.7M times in one window; "
-                                  "split the stream into smaller windows")
+            raise NativeRateError("schedule prepass failed (flag %d)" % int(flags[0]))
         if int(flags[1]):
             raise NativeRateError("dataflow rating timed out (a dependency never resolved)")
         if int(flags[2]):

@@ -62,6 +62,7 @@ def main(argv=None) -> int:
     from analyzer_amd.ops.rate import BatchRater, RateResult, NOT_PROCESSED
     from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
     from analyzer_amd.parallel.sweep import SweepMerger
+    from analyzer_amd.runtime.engine import WindowPipeline
 
     P, M, K = args.players, args.matches_per_gpu, args.team_size
     roster = make_roster(RosterSpec(num_players=P, seed=args.seed), device=dev)
@@ -73,17 +74,16 @@ def main(argv=None) -> int:
     rater = BatchRater()
     out = RateResult.allocate(M, K, dev)
     merger = SweepMerger(P, dev) if world > 1 else None
+    pipe = WindowPipeline(rater, roster, K, merger=merger)
     err = torch.zeros(3, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
+    prepared = {0: pipe.prepare(windows[0])}
 
     def step(i):
-        rec = windows[i % n_windows]
-        if merger is not None:
-            merger.begin(roster)
-            rater.rate(roster, rec, K, out=out, first_prior=merger.first_prior, check=False)
-            merger.merge(roster)
-        else:
-            rater.rate(roster, rec, K, out=out, check=False)
+        # the prepass of window i+1 runs on the side stream while window i is rated
+        # (every timed step carries exactly one prepass and one rating)
+        prepared[i + 1] = pipe.prepare(windows[(i + 1) % n_windows])
+        pipe.rate(prepared.pop(i), out=out)
         err.bitwise_or_(rater.error_flags(dev))
 
     for i in range(args.warmup):

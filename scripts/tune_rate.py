@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--team-size", type=int, default=3)
     ap.add_argument("--blocks", default="128,256,512,1024,2048")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--idle", default="8", help="ANA_RATE_IDLE values (max idle sleep rounds)")
     ap.add_argument("--hot", type=float, default=0.0)
     ap.add_argument("--pattern", default="random", choices=["random", "serial", "disjoint"])
     args = ap.parse_args()
@@ -37,7 +38,9 @@ def main():
     out = RateResult.allocate(M, K, dev)
     results = {}
     for rnd in range(args.rounds):
-        for b in [int(x) for x in args.blocks.split(",")]:
+        for b, idle in [(int(x), int(y)) for x in args.blocks.split(",") for y in args.idle.split(",")]:
+            os.environ["ANA_RATE_IDLE"] = str(idle)
+            key = "%d/%d" % (b, idle)
             roster = make_roster(RosterSpec(num_players=P, seed=1), device=dev)
             br = BatchRater(blocks=b)
             br.schedule(rec, K, P)
@@ -50,8 +53,8 @@ def main():
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             br.check_errors(dev)
-            results.setdefault(b, []).append(((t1 - t0) * 1e3, (t2 - t1) * 1e3))
-            print("round %d blocks %5d schedule %7.2f ms rate %8.2f ms" % (rnd, b, (t1 - t0) * 1e3,
+            results.setdefault(key, []).append(((t1 - t0) * 1e3, (t2 - t1) * 1e3))
+            print("round %d blocks/idle %9s schedule %7.2f ms rate %8.2f ms" % (rnd, key, (t1 - t0) * 1e3,
                                                                           (t2 - t1) * 1e3), flush=True)
     summary = {b: {"schedule_ms_min": min(x[0] for x in v), "rate_ms_min": min(x[1] for x in v),
                    "rate_ms_median": sorted(x[1] for x in v)[len(v) // 2]} for b, v in results.items()}

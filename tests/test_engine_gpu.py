@@ -87,3 +87,23 @@ def test_device_repeat_launch_deterministic(gpu_device):
     assert torch.equal(outs[0][0][:, 0::2].contiguous().view(torch.int32),
                        outs[1][0][:, 0::2].contiguous().view(torch.int32))
     assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32))
+
+
+@pytest.mark.parametrize("n,bits", [(1, 8), (4095, 20), (4097, 12), (1_000_003, 20), (300_000, 32)])
+def test_radix_sort_pairs_stable(gpu_device, n, bits):
+    from analyzer_amd.ops.native import native
+
+    g = torch.Generator().manual_seed(n)
+    hi = 1 << min(bits, 31)
+    keys = torch.randint(0, hi, (n,), generator=g, dtype=torch.int64)
+    if bits == 32:
+        keys = keys * 2 - hi  # negative int32 = high unsigned keys
+    keys = keys.to(torch.int32)
+    if n > 1000:
+        keys[: n // 3] = keys[0]  # long equal runs exercise stability
+    vals = torch.arange(n, dtype=torch.int32)
+    ks, vs = native().sort_pairs(keys.to(gpu_device), vals.to(gpu_device), bits)
+    ukeys = keys.to(torch.int64) & 0xFFFFFFFF
+    order = torch.sort(ukeys, stable=True).indices
+    assert torch.equal(ks.cpu(), keys[order])
+    assert torch.equal(vs.cpu(), vals[order])

@@ -63,32 +63,36 @@ def test_stream_generator_properties():
     assert not torch.equal(rec, other)
 
 
-def test_schedule_occurrence_index_host():
-    from analyzer_amd.ops.rate import BatchRater
+def test_schedule_links_host():
+    from analyzer_amd.ops.rate import BatchRater, Schedule
 
     rec = make_stream(StreamSpec(team_size=3, seed=9, p_afk=0.1), 300, 20)
     link, deps = BatchRater().schedule(rec, 3, 20)
-    link, deps = link.numpy(), deps.numpy()
-    seen, last = {}, {}
+    link = link.numpy().reshape(-1, 2).astype(np.int64) & 0xFFFFFFFF
+    deps = deps.numpy()
+    occ = {}  # player -> [(match, mode, slot)] in stream order
     expect_deps = np.zeros(rec.shape[0], dtype=np.int64)
     for m in range(rec.shape[0]):
         if int(rec[m, 7]) & 4:  # AFK: no state, not scheduled
             assert deps[m] == 0
             continue
-        firsts = set()
+        seen_here = set()
         for j in range(6):
             pid = int(rec[m, j])
-            assert link[m, j, 0] == seen.get(pid, 0)
-            if pid not in firsts:
-                firsts.add(pid)
-                expect_deps[m] += seen.get(pid, 0) > 0
-            if pid in last:
-                assert link.reshape(-1, 2)[last[pid], 1] == m * 6 + j  # successor link
-            seen[pid] = seen.get(pid, 0) + 1
-            last[pid] = m * 6 + j
+            if pid not in seen_here:
+                seen_here.add(pid)
+                expect_deps[m] += pid in occ
+            occ.setdefault(pid, []).append((m, int(rec[m, 6]) & 0xFF, m * 6 + j))
     assert (deps == expect_deps).all()
-    for pid, slot in last.items():  # last occurrences have no successor
-        assert link.reshape(-1, 2)[slot, 1] == -1
+    for pid, lst in occ.items():
+        for i, (m, mode, slot) in enumerate(lst):
+            w0, w1 = int(link[slot, 0]), int(link[slot, 1])
+            nxt = lst[i + 1][0] if i + 1 < len(lst) else Schedule.NO_MATCH
+            nxt_mode = next((x[0] for x in lst[i + 1:] if x[1] == mode), Schedule.NO_MATCH)
+            assert w0 & Schedule.MATCH_MASK == nxt
+            assert w1 == nxt_mode
+            assert bool(w0 & Schedule.HAS_PRED) == (i > 0)
+            assert bool(w0 & Schedule.HAS_PRED_MODE) == any(x[1] == mode for x in lst[:i])
 
 
 def test_status_counts_and_any_afk():
