@@ -95,12 +95,15 @@ def players_from_roster(state: torch.Tensor, attrs: torch.Tensor) -> List[Player
     return players
 
 
-def matches_from_stream(rec: torch.Tensor, K: int, players: Sequence[Player]) -> List[Match]:
-    """Decode stream records into objects (invalid records -> nrosters padding)."""
+def matches_from_stream(rec: torch.Tensor, K: int, players: Sequence[Player], base: int = 0,
+                        prefix: str = "m") -> List[Match]:
+    """Decode stream records into objects (invalid records -> nrosters padding).
+    Match ``i`` gets api id ``<prefix><base+i>`` and ``created_at = base + i``."""
     r = rec.detach().cpu().numpy()
     S = 2 * K
     out = []
     for m in range(r.shape[0]):
+        g = base + m
         m0, m1 = int(r[m, S]) & 0xffffffff, int(r[m, S + 1]) & 0xffffffff
         mode = m0 & 0xff
         n0, n1, nrost = (m0 >> 8) & 0xff, (m0 >> 16) & 0xff, (m0 >> 24) & 0xff
@@ -112,16 +115,16 @@ def matches_from_stream(rec: torch.Tensor, K: int, players: Sequence[Player]) ->
             for pos in range(n):
                 pid = int(r[m, ri * K + pos])
                 afk = 1 if (afk_mask >> k) & 1 else 0
-                parts.append(Participant(players[pid], "m%dp%d" % (m, k), went_afk=afk))
+                parts.append(Participant(players[pid], "%s%dp%d" % (prefix, g, k), went_afk=afk))
                 k += 1
             winner = bool(m1 & (1 << ri))
-            rosters.append(Roster(parts, winner=winner, api_id="m%dr%d" % (m, ri)))
+            rosters.append(Roster(parts, winner=winner, api_id="%s%dr%d" % (prefix, g, ri)))
         for extra in range(max(0, nrost - 2)):
-            rosters.append(Roster([], winner=False, api_id="m%dx%d" % (m, extra)))
+            rosters.append(Roster([], winner=False, api_id="%s%dx%d" % (prefix, g, extra)))
         if nrost < 2:
             rosters = rosters[:nrost]
         game_mode = MODES[mode] if mode < len(MODES) else "private"
-        out.append(Match(game_mode, rosters, api_id="m%d" % m, created_at=float(m)))
+        out.append(Match(game_mode, rosters, api_id="%s%d" % (prefix, g), created_at=float(g)))
     return out
 
 

@@ -1,0 +1,369 @@
+"""State store of the worker: the reference's MySQL tables.
+
+The reference reflects ``match, roster, participant, participant_items,
+participant_stats, player, asset`` with SQLAlchemy automap and wires list-valued
+relationships on the ``api_id`` foreign keys (/root/reference/worker.py:38-83).
+Neither SQLAlchemy nor a MySQL driver exists in this image, so the
+store is pluggable behind one small session interface:
+
+    with store.session() as s:
+        for match in s.load_matches(ids, chunksize):   # ORDER BY created_at ASC
+            ...mutate objects...
+        s.commit()       # or s.rollback()
+        s.assets(match_api_id)
+
+* ``MemoryStore`` keeps the object graph in process (tests, config 1, bench
+  plumbing);
+* ``SqliteStore`` (``DATABASE_URI=sqlite:///path``) stores the same tables and
+  columns in SQLite through the standard library, with an identity map per
+  session so one player that appears in several matches of a batch is ONE
+  object -- exactly what the sequential rating semantics need
+  (worker.py:191-192).
+
+Both snapshot the writable fields of every loaded object so ``rollback()``
+restores them (and ``restore(match)`` undoes a single quarantined match).
+"""
+from __future__ import annotations
+
+import sqlite3
+from dataclasses import dataclass
+from typing import Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
+
+from ..config import TRACK_COLUMNS
+from .objects import Match, Participant, ParticipantItems, Player, Roster
+
+PLAYER_RATING_COLS = tuple(c + s for c in TRACK_COLUMNS for s in ("_mu", "_sigma"))
+ITEM_RATING_COLS = tuple(c + s for c in TRACK_COLUMNS[1:] for s in ("_mu", "_sigma"))
+PARTICIPANT_WRITE_COLS = ("trueskill_mu", "trueskill_sigma", "trueskill_delta")
+ITEM_WRITE_COLS = ("any_afk",) + ITEM_RATING_COLS
+
+
+@dataclass
+class Asset:
+    url: str
+    match_api_id: str
+
+
+def _q(col: str) -> str:
+    return '"%s"' % col  # 5v5_* columns start with a digit
+
+
+SCHEMA = [
+    "CREATE TABLE IF NOT EXISTS player (api_id TEXT PRIMARY KEY, skill_tier INTEGER, "
+    "rank_points_ranked REAL, rank_points_blitz REAL, %s)"
+    % ", ".join("%s REAL" % _q(c) for c in PLAYER_RATING_COLS),
+    "CREATE TABLE IF NOT EXISTS match (api_id TEXT PRIMARY KEY, game_mode TEXT, "
+    "created_at REAL, trueskill_quality REAL)",
+    "CREATE INDEX IF NOT EXISTS match_created ON match(created_at)",
+    "CREATE TABLE IF NOT EXISTS roster (api_id TEXT PRIMARY KEY, match_api_id TEXT, winner INTEGER)",
+    "CREATE INDEX IF NOT EXISTS roster_match ON roster(match_api_id)",
+    "CREATE TABLE IF NOT EXISTS participant (api_id TEXT PRIMARY KEY, match_api_id TEXT, "
+    "roster_api_id TEXT, player_api_id TEXT, skill_tier INTEGER, went_afk INTEGER, "
+    "trueskill_mu REAL, trueskill_sigma REAL, trueskill_delta REAL)",
+    "CREATE INDEX IF NOT EXISTS participant_match ON participant(match_api_id)",
+    "CREATE TABLE IF NOT EXISTS participant_items (api_id TEXT PRIMARY KEY, "
+    "participant_api_id TEXT, any_afk INTEGER, %s)" % ", ".join("%s REAL" % _q(c) for c in ITEM_RATING_COLS),
+    "CREATE INDEX IF NOT EXISTS items_participant ON participant_items(participant_api_id)",
+    "CREATE TABLE IF NOT EXISTS participant_stats (api_id TEXT PRIMARY KEY, "
+    "participant_api_id TEXT, kills INTEGER, deaths INTEGER, assists INTEGER, "
+    "farm REAL, gold REAL, damage REAL, events INTEGER)",
+    "CREATE TABLE IF NOT EXISTS asset (api_id TEXT PRIMARY KEY, match_api_id TEXT, url TEXT)",
+    "CREATE INDEX IF NOT EXISTS asset_match ON asset(match_api_id)",
+]
+
+
+# ---------------------------------------------------------------- snapshots
+def _snap_match(m: Match) -> tuple:
+    return (m.trueskill_quality,
+            [tuple(getattr(p, c) for c in PARTICIPANT_WRITE_COLS) for p in m.participants],
+            [tuple(getattr(p.participant_items[0], c) for c in ITEM_WRITE_COLS) for p in m.participants])
+
+
+def _restore_match(m: Match, snap: tuple) -> None:
+    q, parts, items = snap
+    m.trueskill_quality = q
+    for p, vals in zip(m.participants, parts):
+        for c, v in zip(PARTICIPANT_WRITE_COLS, vals):
+            setattr(p, c, v)
+    for p, vals in zip(m.participants, items):
+        for c, v in zip(ITEM_WRITE_COLS, vals):
+            setattr(p.participant_items[0], c, v)
+
+
+def _snap_player(pl: Player) -> tuple:
+    return tuple(getattr(pl, c) for c in PLAYER_RATING_COLS)
+
+
+def _restore_player(pl: Player, snap: tuple) -> None:
+    for c, v in zip(PLAYER_RATING_COLS, snap):
+        setattr(pl, c, v)
+
+
+class _SessionBase:
+    """Snapshot bookkeeping shared by both stores."""
+
+    def __init__(self):
+        self._match_snaps: Dict[int, Tuple[Match, tuple]] = {}
+        self._player_snaps: Dict[int, Tuple[Player, tuple]] = {}
+        self.closed = False
+
+    def _track(self, m: Match) -> None:
+        self._match_snaps.setdefault(id(m), (m, _snap_match(m)))
+        for p in m.participants:
+            pl = p.player[0]
+            self._player_snaps.setdefault(id(pl), (pl, _snap_player(pl)))
+
+    def savepoint(self, m: Match) -> tuple:
+        """Snapshot of one match and its players (for per-match quarantine)."""
+        return (_snap_match(m), [(p.player[0], _snap_player(p.player[0])) for p in m.participants])
+
+    def restore(self, m: Match, sp: tuple) -> None:
+        _restore_match(m, sp[0])
+        for pl, snap in sp[1]:
+            _restore_player(pl, snap)
+
+    def rollback(self) -> None:
+        for m, snap in self._match_snaps.values():
+            _restore_match(m, snap)
+        for pl, snap in self._player_snaps.values():
+            _restore_player(pl, snap)
+
+    def loaded_matches(self) -> List[Match]:
+        return [m for m, _ in self._match_snaps.values()]
+
+    def close(self) -> None:
+        self.closed = True
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
+# ---------------------------------------------------------------- in-memory
+class MemorySession(_SessionBase):
+    def __init__(self, store: "MemoryStore"):
+        super().__init__()
+        self.store = store
+
+    def load_matches(self, ids: Iterable[str], chunksize: int = 100) -> Iterator[Match]:
+        found = [self.store.matches[i] for i in set(ids) if i in self.store.matches]
+        found.sort(key=lambda m: m.created_at)
+        for m in found:
+            self._track(m)
+            yield m
+
+    def commit(self) -> None:
+        self.store.commits += 1
+        self._match_snaps.clear()
+        self._player_snaps.clear()
+
+    def assets(self, match_api_id: str) -> List[Asset]:
+        return list(self.store.assets.get(match_api_id, ()))
+
+
+class MemoryStore:
+    def __init__(self):
+        self.matches: Dict[str, Match] = {}
+        self.players: Dict[str, Player] = {}
+        self.assets: Dict[str, List[Asset]] = {}
+        self.commits = 0
+
+    def add_players(self, players: Iterable[Player]) -> None:
+        for p in players:
+            self.players[p.api_id] = p
+
+    def add_matches(self, matches: Iterable[Match]) -> None:
+        for m in matches:
+            self.matches[m.api_id] = m
+
+    def add_asset(self, match_api_id: str, url: str) -> None:
+        self.assets.setdefault(match_api_id, []).append(Asset(url, match_api_id))
+
+    def session(self) -> MemorySession:
+        return MemorySession(self)
+
+    def close(self) -> None:
+        pass
+
+
+# ---------------------------------------------------------------- sqlite
+class SqliteSession(_SessionBase):
+    def __init__(self, store: "SqliteStore"):
+        super().__init__()
+        self.store = store
+        self.conn = store.conn
+        self._players: Dict[str, Player] = {}  # identity map
+
+    def _load_players(self, api_ids: Sequence[str]) -> None:
+        need = [a for a in set(api_ids) if a not in self._players]
+        cols = ("api_id", "skill_tier", "rank_points_ranked", "rank_points_blitz") + PLAYER_RATING_COLS
+        for chunk in _chunks(need, 500):
+            rows = self.conn.execute(
+                "SELECT %s FROM player WHERE api_id IN (%s)" % (", ".join(_q(c) for c in cols),
+                                                                ", ".join("?" * len(chunk))), chunk)
+            for row in rows:
+                kw = dict(zip(cols, row))
+                api = kw.pop("api_id")
+                tier = kw.pop("skill_tier")
+                rr = kw.pop("rank_points_ranked")
+                rb = kw.pop("rank_points_blitz")
+                self._players[api] = Player(api, tier, rr, rb, **kw)
+
+    def load_matches(self, ids: Iterable[str], chunksize: int = 100) -> Iterator[Match]:
+        ids = list(set(ids))
+        heads: List[tuple] = []
+        for chunk in _chunks(ids, 500):
+            heads += self.conn.execute(
+                "SELECT api_id, game_mode, created_at, trueskill_quality FROM match "
+                "WHERE api_id IN (%s)" % ", ".join("?" * len(chunk)), chunk).fetchall()
+        heads.sort(key=lambda r: (r[2] is None, r[2]))
+        # yield_per(chunksize): relationships are loaded one chunk of matches at a time
+        for chunk in _chunks(heads, max(1, int(chunksize))):
+            for m in self._build(chunk):
+                self._track(m)
+                yield m
+
+    def _build(self, heads: Sequence[tuple]) -> List[Match]:
+        mids = [h[0] for h in heads]
+        ph = ", ".join("?" * len(mids))
+        rosters: Dict[str, List[tuple]] = {}
+        for r in self.conn.execute("SELECT api_id, match_api_id, winner FROM roster WHERE "
+                                   "match_api_id IN (%s) ORDER BY rowid" % ph, mids):
+            rosters.setdefault(r[1], []).append(r)
+        parts = self.conn.execute(
+            "SELECT api_id, match_api_id, roster_api_id, player_api_id, skill_tier, went_afk, "
+            "trueskill_mu, trueskill_sigma, trueskill_delta FROM participant WHERE match_api_id "
+            "IN (%s) ORDER BY rowid" % ph, mids).fetchall()
+        self._load_players([p[3] for p in parts])
+        pids = [p[0] for p in parts]
+        items: Dict[str, ParticipantItems] = {}
+        icols = ("api_id", "participant_api_id") + ITEM_WRITE_COLS
+        for chunk in _chunks(pids, 500):
+            for row in self.conn.execute(
+                    "SELECT %s FROM participant_items WHERE participant_api_id IN (%s) ORDER BY rowid"
+                    % (", ".join(_q(c) for c in icols), ", ".join("?" * len(chunk))), chunk):
+                it = ParticipantItems(row[0])
+                for c, v in zip(ITEM_WRITE_COLS, row[2:]):
+                    setattr(it, c, bool(v) if c == "any_afk" and v is not None else v)
+                items.setdefault(row[1], it)
+        by_roster: Dict[str, List[Participant]] = {}
+        by_match: Dict[str, List[Participant]] = {}
+        for api, mid, rid, plid, tier, afk, mu, sig, dl in parts:
+            pl = self._players.get(plid) or Player(plid)
+            self._players.setdefault(plid, pl)
+            p = Participant(pl, api, went_afk=afk, skill_tier=tier,
+                            items=items.get(api) or ParticipantItems(api))
+            p.trueskill_mu, p.trueskill_sigma, p.trueskill_delta = mu, sig, dl
+            by_roster.setdefault(rid, []).append(p)
+            by_match.setdefault(mid, []).append(p)
+        out = []
+        for api, mode, created, quality in heads:
+            rs = [Roster(by_roster.get(r[0], []), winner=None if r[2] is None else bool(r[2]),
+                         api_id=r[0]) for r in rosters.get(api, [])]
+            m = Match(mode, rs, api_id=api, created_at=created)
+            m.participants = by_match.get(api, [])
+            m.trueskill_quality = quality
+            out.append(m)
+        return out
+
+    def commit(self) -> None:
+        c = self.conn
+        for m, _ in self._match_snaps.values():
+            c.execute("UPDATE match SET trueskill_quality=? WHERE api_id=?", (m.trueskill_quality, m.api_id))
+            for p in m.participants:
+                c.execute("UPDATE participant SET trueskill_mu=?, trueskill_sigma=?, trueskill_delta=? "
+                          "WHERE api_id=?", (p.trueskill_mu, p.trueskill_sigma, p.trueskill_delta, p.api_id))
+                it = p.participant_items[0]
+                vals = [getattr(it, col) for col in ITEM_WRITE_COLS]
+                vals[0] = None if vals[0] is None else int(bool(vals[0]))
+                c.execute("UPDATE participant_items SET %s WHERE participant_api_id=?"
+                          % ", ".join("%s=?" % _q(col) for col in ITEM_WRITE_COLS), vals + [p.api_id])
+        for pl, _ in self._player_snaps.values():
+            c.execute("UPDATE player SET %s WHERE api_id=?" % ", ".join("%s=?" % _q(col) for col in PLAYER_RATING_COLS),
+                      [getattr(pl, col) for col in PLAYER_RATING_COLS] + [pl.api_id])
+        c.commit()
+        self.store.commits += 1
+        self._match_snaps.clear()
+        self._player_snaps.clear()
+
+    def rollback(self) -> None:
+        super().rollback()
+        self.conn.rollback()
+
+    def assets(self, match_api_id: str) -> List[Asset]:
+        return [Asset(u, m) for u, m in self.conn.execute(
+            "SELECT url, match_api_id FROM asset WHERE match_api_id=? ORDER BY rowid", (match_api_id,))]
+
+
+class SqliteStore:
+    def __init__(self, path: str = ":memory:"):
+        self.path = path
+        self.conn = sqlite3.connect(path)
+        for ddl in SCHEMA:
+            self.conn.execute(ddl)
+        self.conn.commit()
+        self.commits = 0
+
+    def session(self) -> SqliteSession:
+        return SqliteSession(self)
+
+    # ------------------------------------------------------------- loading
+    def add_players(self, players: Iterable[Player]) -> None:
+        cols = ("api_id", "skill_tier", "rank_points_ranked", "rank_points_blitz") + PLAYER_RATING_COLS
+        self.conn.executemany(
+            "INSERT OR REPLACE INTO player (%s) VALUES (%s)" % (", ".join(_q(c) for c in cols),
+                                                               ", ".join("?" * len(cols))),
+            [[getattr(p, c) for c in cols] for p in players])
+        self.conn.commit()
+
+    def add_matches(self, matches: Iterable[Match]) -> None:
+        c = self.conn
+        icols = ("api_id", "participant_api_id") + ITEM_WRITE_COLS
+        for m in matches:
+            c.execute("INSERT OR REPLACE INTO match VALUES (?, ?, ?, ?)",
+                      (m.api_id, m.game_mode, m.created_at, m.trueskill_quality))
+            for r in m.rosters:
+                c.execute("INSERT OR REPLACE INTO roster VALUES (?, ?, ?)",
+                          (r.api_id, m.api_id, None if r.winner is None else int(bool(r.winner))))
+                for p in r.participants:
+                    c.execute("INSERT OR REPLACE INTO participant VALUES (?, ?, ?, ?, ?, ?, ?, ?, ?)",
+                              (p.api_id, m.api_id, r.api_id, p.player[0].api_id, p.skill_tier,
+                               p.went_afk, p.trueskill_mu, p.trueskill_sigma, p.trueskill_delta))
+                    it = p.participant_items[0]
+                    vals = [it.api_id or p.api_id, p.api_id] + [getattr(it, col) for col in ITEM_WRITE_COLS]
+                    vals[2] = None if vals[2] is None else int(bool(vals[2]))
+                    c.execute("INSERT OR REPLACE INTO participant_items (%s) VALUES (%s)"
+                              % (", ".join(_q(x) for x in icols), ", ".join("?" * len(icols))), vals)
+        c.commit()
+
+    def add_asset(self, match_api_id: str, url: str) -> None:
+        n = self.conn.execute("SELECT COUNT(*) FROM asset").fetchone()[0]
+        self.conn.execute("INSERT INTO asset VALUES (?, ?, ?)", ("a%d" % n, match_api_id, url))
+        self.conn.commit()
+
+    def close(self) -> None:
+        self.conn.close()
+
+
+def _chunks(seq: Sequence, n: int):
+    seq = list(seq)
+    for i in range(0, len(seq), n):
+        yield seq[i:i + n]
+
+
+def open_store(uri: Optional[str]):
+    """Store for a ``DATABASE_URI``: None / ``memory://`` -> MemoryStore,
+    ``sqlite:///path`` (or ``sqlite://`` for an in-memory database) -> SqliteStore."""
+    if not uri or uri.startswith("memory:"):
+        return MemoryStore()
+    if uri.startswith("sqlite://"):
+        path = uri[len("sqlite://"):]
+        path = path[1:] if path.startswith("/") else path
+        return SqliteStore(path or ":memory:")
+    if uri.startswith("mysql"):
+        raise RuntimeError("DATABASE_URI=%s needs a MySQL driver (cymysql/SQLAlchemy), which this "
+                           "image does not ship; use sqlite:///path or memory://" % uri)
+    raise ValueError("unsupported DATABASE_URI %r" % uri)

@@ -1,0 +1,248 @@
+"""The rating worker: ingest -> micro-batch -> rate -> commit -> ack -> fan-out
+(/root/reference/worker.py).
+
+Same observable protocol as the reference:
+
+* ``connect()`` opens the store and the broker, declares ``QUEUE``,
+  ``QUEUE_failed``, ``CRUNCH_QUEUE`` and ``TELESUCK_QUEUE`` (durable), sets
+  ``prefetch_count=BATCHSIZE`` and consumes ``QUEUE`` (worker.py:85-92);
+* ``newjob`` appends the delivery and arms ONE ``IDLE_TIMEOUT`` timer on the
+  first message of a batch -- a max-latency bound, not reset by later
+  messages -- and flushes at ``BATCHSIZE`` (worker.py:95-101);
+* ``process`` dedups the bodies (match api ids), loads the matches ordered by
+  ``created_at`` in chunks of ``CHUNKSIZE``, rates them in order and commits
+  once (worker.py:169-199);
+* ``try_process`` acks every delivery on success and fans out: ``notify``
+  header -> ``"analyze_update"`` on ``amq.topic``; ``DOCRUNCHMATCH`` /
+  ``DOSEWMATCH`` forward the body; ``DOTELESUCKMATCH`` publishes every asset
+  url of the match with a ``match_api_id`` header (worker.py:103-166).  On
+  failure every body goes to ``QUEUE_failed`` with its properties and is
+  nacked without requeue (worker.py:108-120).
+
+Deliberate, documented differences:
+
+* ``ENGINE=native`` rates the whole batch with one launch of the batched
+  engine (runtime/batch.py) instead of per-object Python;
+* ``QUARANTINE=true`` (default) isolates the matches the reference would raise
+  on (tier None/30, sigma 0, empty roster, non-finite result): only their
+  deliveries go to ``QUEUE_failed``; the rest of the batch commits.
+  ``QUARANTINE=false`` restores the all-or-nothing batch of the reference;
+* a delivery without headers is simply not notified (the reference raises
+  AttributeError there and kills the consumer, worker.py:132);
+* ``SEW_QUEUE`` is declared when ``DOSEWMATCH`` is on (the reference forwards to
+  a queue it never declares, which a broker silently drops).
+
+Per-batch counters (matches rated/afk/invalid/unsupported/quarantined, timing)
+are kept in ``stats`` and logged as one JSON line per batch (SURVEY §5 metrics).
+"""
+from __future__ import annotations
+
+import json
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Tuple
+
+from ..config import RaterConfig, WorkerConfig
+from ..models.match_rater import MatchRater
+from ..utils.log import get_logger
+from . import broker as B
+from .store import open_store
+
+logger = get_logger()
+
+
+@dataclass
+class WorkerStats:
+    batches: int = 0
+    failed_batches: int = 0
+    messages: int = 0
+    matches: int = 0
+    quarantined: int = 0
+    acked: int = 0
+    nacked: int = 0
+    published: Dict[str, int] = field(default_factory=dict)
+    seconds: float = 0.0
+
+    def bump(self, key: str, n: int = 1) -> None:
+        self.published[key] = self.published.get(key, 0) + n
+
+
+class MatchError(Exception):
+    """A match the reference rater would raise on."""
+
+
+class Worker:
+    def __init__(self, cfg: Optional[WorkerConfig] = None, store=None, broker=None,
+                 rater_cfg: Optional[RaterConfig] = None, clock: Optional[Callable[[], float]] = None,
+                 object_rater=None):
+        self.cfg = cfg or WorkerConfig.from_env()
+        self.rater_cfg = rater_cfg or RaterConfig.from_env()
+        self.store = store
+        self.rabbit = broker
+        self.clock = clock
+        self.channel = None
+        self.queue: List[Tuple[B.Method, B.BasicProperties, bytes]] = []
+        self.timer = None
+        self.stats = WorkerStats()
+        self.failed_ids: List[str] = []
+        self._python_rater = MatchRater(self.rater_cfg)
+        self._object_rater = object_rater  # runtime.batch.ObjectBatchRater, built lazily
+
+    # ------------------------------------------------------------ connect (W3/W4)
+    def connect(self) -> "Worker":
+        if self.store is None:
+            self.store = open_store(self.cfg.database_uri)
+        if self.rabbit is None:
+            self.rabbit = B.connect(self.cfg.rabbitmq_uri, clock=self.clock)
+        ch = self.rabbit.channel()
+        for q in (self.cfg.queue, self.cfg.failed_queue, self.cfg.crunch_queue, self.cfg.telesuck_queue):
+            ch.queue_declare(queue=q, durable=True)
+        if self.cfg.dosewmatch:
+            ch.queue_declare(queue=self.cfg.sew_queue, durable=True)
+        ch.basic_qos(prefetch_count=self.cfg.batchsize)
+        ch.basic_consume(self.newjob, queue=self.cfg.queue)
+        self.channel = ch
+        return self
+
+    # ------------------------------------------------------------ batcher (W5)
+    def newjob(self, _ch, method, properties, body) -> None:
+        self.queue.append((method, properties, body))
+        if self.timer is None:
+            self.timer = self.rabbit.add_timeout(self.cfg.idle_timeout, self.try_process)
+        if len(self.queue) == self.cfg.batchsize:
+            self.try_process()
+
+    # ------------------------------------------------------------ ack / fan-out (W6)
+    def try_process(self) -> None:
+        if self.timer is not None:
+            self.rabbit.remove_timeout(self.timer)
+            self.timer = None
+        batch, self.queue = self.queue, []
+        if not batch:
+            return
+        t0 = time.perf_counter()
+        try:
+            failed = set(self.process(batch))
+        except Exception as e:  # the whole batch goes to the failed queue (worker.py:110-120)
+            logger.error(e)
+            for meth, prop, body in batch:
+                self._publish("", self.cfg.failed_queue, body, prop)
+                self.channel.basic_nack(meth.delivery_tag, requeue=False)
+                self.stats.nacked += 1
+            self.stats.failed_batches += 1
+            self.stats.seconds += time.perf_counter() - t0
+            return
+
+        logger.info("acking batch")
+        session = self.store.session() if self.cfg.dotelesuckmatch else None
+        try:
+            for meth, prop, body in batch:
+                mid = _decode(body)
+                if mid in failed:  # quarantined match
+                    self._publish("", self.cfg.failed_queue, body, prop)
+                    self.channel.basic_nack(meth.delivery_tag, requeue=False)
+                    self.stats.nacked += 1
+                    continue
+                self.channel.basic_ack(meth.delivery_tag)
+                self.stats.acked += 1
+                headers = (prop.headers if prop is not None else None) or {}
+                if headers.get("notify"):
+                    self._publish("amq.topic", headers.get("notify"), b"analyze_update", None)
+                if self.cfg.docrunchmatch:
+                    self._publish("", self.cfg.crunch_queue, body, prop)
+                if self.cfg.dosewmatch:
+                    self._publish("", self.cfg.sew_queue, body, prop)
+                if self.cfg.dotelesuckmatch:
+                    for asset in session.assets(mid):
+                        self._publish("", self.cfg.telesuck_queue, asset.url,
+                                      B.BasicProperties(headers={"match_api_id": asset.match_api_id}))
+        finally:
+            if session is not None:
+                session.close()
+        self.stats.batches += 1
+        self.stats.seconds += time.perf_counter() - t0
+
+    def _publish(self, exchange: str, key: str, body, props) -> None:
+        self.channel.basic_publish(exchange=exchange, routing_key=key, body=body, properties=props)
+        self.stats.bump(key if exchange == "" else exchange)
+
+    # ------------------------------------------------------------ process (W7)
+    def process(self, batch=None) -> List[str]:
+        """Rate one batch; returns the api ids of quarantined matches.  Raises
+        (after rolling back) when the batch must fail as a whole."""
+        batch = self.queue if batch is None else batch
+        logger.info("analyzing batch %s", str(len(batch)))
+        ids = list(set(_decode(body) for _, _, body in batch))
+        self.stats.messages += len(batch)
+        session = self.store.session()
+        quarantined: List[str] = []
+        counts: Dict[str, int] = {}
+        try:
+            matches = list(session.load_matches(ids, self.cfg.chunksize))
+            if self.cfg.engine == "native" and self._batched().supports(matches):
+                quarantined = self._rate_native(session, matches, counts)
+            else:
+                quarantined = self._rate_python(session, matches, counts)
+            session.commit()
+        except Exception:
+            session.rollback()
+            raise
+        finally:
+            session.close()
+        self.stats.matches += len(matches)
+        self.stats.quarantined += len(quarantined)
+        self.failed_ids += quarantined
+        logger.info(json.dumps({"batch": self.stats.batches, "messages": len(batch),
+                                "matches": len(matches), "engine": self.cfg.engine,
+                                "quarantined": len(quarantined), **counts}))
+        return quarantined
+
+    def _rate_python(self, session, matches, counts) -> List[str]:
+        bad = []
+        for match in matches:
+            sp = session.savepoint(match) if self.cfg.quarantine else None
+            try:
+                self._python_rater.rate_match(match)
+                counts["rated"] = counts.get("rated", 0) + 1
+            except (KeyError, ValueError, FloatingPointError, ZeroDivisionError, IndexError,
+                    TypeError) as e:
+                if not self.cfg.quarantine:
+                    raise
+                session.restore(match, sp)
+                logger.error("quarantined match %s: %r", match.api_id, e)
+                bad.append(match.api_id)
+        return bad
+
+    def _batched(self):
+        if self._object_rater is None:
+            from .batch import ObjectBatchRater
+
+            from ..ops.rate import BatchRater
+            self._object_rater = ObjectBatchRater(BatchRater(self.rater_cfg))
+        return self._object_rater
+
+    def _rate_native(self, session, matches, counts) -> List[str]:
+        from ..ops import rate as R
+
+        status = self._batched().rate(matches)
+        bad = []
+        for m, s in zip(matches, status):
+            name = R.STATUS_NAMES.get(s, str(s))
+            counts[name] = counts.get(name, 0) + 1
+            if s in R.ERROR_STATUSES or s == R.NOT_PROCESSED:
+                bad.append(m.api_id)
+        if bad and not self.cfg.quarantine:
+            raise MatchError("%d match(es) failed to rate (first: %s)" % (len(bad), bad[0]))
+        return bad
+
+    # ------------------------------------------------------------ entry point (W9)
+    def start_consuming(self, until: Optional[Callable[[], bool]] = None) -> None:
+        self.rabbit.run(until=until)
+
+    def run(self) -> None:
+        self.connect()
+        self.start_consuming()
+
+
+def _decode(body) -> str:
+    return str(body, "utf-8") if isinstance(body, (bytes, bytearray)) else str(body)

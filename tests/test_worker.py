@@ -1,0 +1,254 @@
+"""Worker runtime: batcher, ack/nack, fan-out, quarantine,
+stores, engines.  Everything runs on the CPU with the in-process broker and a
+manual clock, so batching is deterministic."""
+import copy
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from analyzer_amd.config import RaterConfig, WorkerConfig
+from analyzer_amd.models.match_rater import MatchRater
+from analyzer_amd.ops.synth import RosterSpec, StreamSpec
+from analyzer_amd.runtime import broker as B
+from analyzer_amd.runtime.source import populate, publish, synth_objects
+from analyzer_amd.runtime.store import MemoryStore, SqliteStore, open_store
+from analyzer_amd.runtime.objects import Player
+from analyzer_amd.runtime.worker import Worker
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def make_worker(n=20, players=30, batch=4, engine="python", quarantine=True, store=None, seed=3,
+                **flags):
+    clock = B.ManualClock()
+    cfg = WorkerConfig(batchsize=batch, chunksize=3, idle_timeout=1.0, engine=engine,
+                       quarantine=quarantine, **flags)
+    store = store if store is not None else MemoryStore()
+    matches = populate(store, n, players, team_size=3, seed=seed)
+    w = Worker(cfg, store=store, broker=B.MemoryBroker(clock), rater_cfg=RaterConfig(), clock=clock)
+    w.connect()
+    return w, matches, clock
+
+
+def ratings(store_matches):
+    out = {}
+    for m in store_matches:
+        for p in m.participants:
+            pl = p.player[0]
+            out[pl.api_id] = (pl.trueskill_mu, pl.trueskill_sigma, pl.trueskill_ranked_mu,
+                              pl.trueskill_casual_mu)
+    return out
+
+
+def test_size_flush_and_max_latency_timer():
+    w, matches, clock = make_worker(n=10, batch=4)
+    publish(w.channel, "analyze", [m.api_id for m in matches])
+    w.rabbit.process_data_events()
+    # two full batches flushed by size; the remaining 2 wait for the timer
+    assert w.stats.batches == 2 and len(w.queue) == 2
+    assert w.channel.acked == 8
+    clock.advance(0.5)
+    w.rabbit.process_data_events()
+    assert w.stats.batches == 2  # timer armed by the 9th message, 1 s max latency
+    clock.advance(0.6)
+    w.rabbit.process_data_events()
+    assert w.stats.batches == 3 and w.channel.acked == 10 and not w.queue
+    assert w.rabbit.depth("analyze") == 0
+
+
+def test_timer_not_reset_by_later_messages():
+    w, matches, clock = make_worker(n=3, batch=100)
+    publish(w.channel, "analyze", [matches[0].api_id])
+    w.rabbit.process_data_events()
+    clock.advance(0.9)
+    publish(w.channel, "analyze", [matches[1].api_id])
+    w.rabbit.process_data_events()
+    clock.advance(0.2)  # 1.1 s after the FIRST message
+    w.rabbit.process_data_events()
+    assert w.stats.batches == 1 and w.channel.acked == 2
+
+
+def test_prefetch_bounds_unacked():
+    w, matches, clock = make_worker(n=10, batch=4)
+    seen = []
+    orig = w.try_process
+
+    def spy():
+        seen.append(len(w.channel.unacked))
+        orig()
+
+    w.newjob.__func__  # bound method exists
+    w.rabbit.remove_timeout(w.timer) if w.timer else None
+    w.try_process = spy
+    publish(w.channel, "analyze", [m.api_id for m in matches])
+    w.rabbit.process_data_events()
+    assert seen and max(seen) <= 4
+
+
+def test_results_equal_sequential_reference_order():
+    """Out-of-order delivery + duplicates inside one batch: the worker dedups and
+    rates in created_at order (order only holds within a batch, as in the reference)."""
+    store = MemoryStore()
+    w, matches, clock = make_worker(n=24, players=12, batch=30, store=store)
+    ref_players, ref_matches = synth_objects(24, 12, team_size=3, seed=3)
+    r = MatchRater(RaterConfig())
+    for m in ref_matches:
+        r.rate_match(m)
+    ids = [m.api_id for m in matches]
+    ids = ids[::-1] + ids[:3]  # reversed, with duplicates
+    publish(w.channel, "analyze", ids)
+    w.start_consuming()
+    assert w.stats.acked == len(ids) and w.stats.batches == 1 and w.stats.matches == 24
+    got, exp = ratings(matches), ratings(ref_matches)
+    for k in exp:
+        for a, b in zip(got[k], exp[k]):
+            assert (a is None and b is None) or abs(a - b) < 1e-9
+
+
+def test_whole_batch_fails_without_quarantine():
+    w, matches, clock = make_worker(n=8, batch=8, quarantine=False)
+    bad = matches[3]
+    p = bad.rosters[0].participants[0].player[0]
+    p.trueskill_mu, p.skill_tier, p.rank_points_ranked, p.rank_points_blitz = None, None, None, None
+    before = ratings(matches)
+    publish(w.channel, "analyze", [m.api_id for m in matches])
+    w.start_consuming()
+    assert w.stats.failed_batches == 1 and w.channel.nacked == 8
+    failed = w.rabbit.drain("analyze_failed")
+    assert sorted(m.body for m in failed) == sorted(m.api_id.encode() for m in matches)
+    assert ratings(matches) == before  # rolled back
+
+
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_quarantine_isolates_bad_match(engine):
+    w, matches, clock = make_worker(n=8, batch=8, engine=engine)
+    bad = matches[3]
+    bad.rosters[0].participants[0].player[0] = Player("newcomer", skill_tier=30)  # KeyError in the reference
+    publish(w.channel, "analyze", [m.api_id for m in matches])
+    w.start_consuming()
+    failed = w.rabbit.drain("analyze_failed")
+    assert [m.body for m in failed] == [bad.api_id.encode()]
+    assert w.channel.acked == 7 and w.channel.nacked == 1
+    assert bad.trueskill_quality is None
+    assert all(m.trueskill_quality is not None for m in matches if m is not bad
+               and m.game_mode in ("casual", "ranked", "blitz", "br", "5v5_casual", "5v5_ranked"))
+
+
+def test_fanout_notify_crunch_sew_telesuck():
+    w, matches, clock = make_worker(n=3, batch=3, docrunchmatch=True, dosewmatch=True,
+                                    dotelesuckmatch=True)
+    w.channel.queue_bind("web", "amq.topic", "user.*")
+    ids = [m.api_id for m in matches]
+    publish(w.channel, "analyze", ids[:2], notify="user.42")
+    publish(w.channel, "analyze", ids[2:])
+    w.start_consuming()
+    assert [m.body for m in w.rabbit.drain("web")] == [b"analyze_update"] * 2
+    assert [m.body for m in w.rabbit.drain("crunch_global")] == [i.encode() for i in ids]
+    assert [m.body for m in w.rabbit.drain("sew")] == [i.encode() for i in ids]
+    tele = w.rabbit.drain("telesuck")
+    assert len(tele) == 3
+    assert [m.properties.headers["match_api_id"] for m in tele] == ids
+    assert all(m.body.startswith(b"https://telemetry.invalid/") for m in tele)
+
+
+def test_sew_dropped_when_not_declared_like_reference_broker():
+    b = B.MemoryBroker()
+    ch = b.channel()
+    ch.basic_publish(exchange="", routing_key="nowhere", body=b"x")
+    assert len(b.dropped) == 1
+
+
+def test_channel_death_redelivers_unacked():
+    b = B.MemoryBroker(B.ManualClock())
+    ch = b.channel()
+    ch.queue_declare("q")
+    got = []
+    ch.basic_consume(lambda c, m, p, body: got.append((m.delivery_tag, m.redelivered, body)), queue="q")
+    for i in range(3):
+        ch.basic_publish("", "q", b"%d" % i)
+    b.process_data_events()
+    ch.basic_ack(got[0][0])
+    ch.close()  # consumer dies with 2 unacked
+    ch2 = b.channel()
+    got2 = []
+    ch2.basic_consume(lambda c, m, p, body: got2.append((m.redelivered, body)), queue="q")
+    b.process_data_events()
+    assert got2 == [(True, b"1"), (True, b"2")]
+
+
+def test_native_engine_matches_python_engine():
+    wp, mp, _ = make_worker(n=60, players=25, batch=16, engine="python", seed=7)
+    wn, mn, _ = make_worker(n=60, players=25, batch=16, engine="native", seed=7)
+    for w, ms in ((wp, mp), (wn, mn)):
+        publish(w.channel, "analyze", [m.api_id for m in ms])
+        w.start_consuming()
+    a, b = ratings(mp), ratings(mn)
+    for k in a:
+        for x, y in zip(a[k], b[k]):
+            assert (x is None) == (y is None)
+            if x is not None:
+                assert abs(x - y) < 2e-3
+    for x, y in zip(mp, mn):
+        assert (x.trueskill_quality is None) == (y.trueskill_quality is None)
+        if x.trueskill_quality is not None:
+            assert abs(x.trueskill_quality - y.trueskill_quality) < 1e-5
+        for p, q in zip(x.participants, y.participants):
+            assert p.participant_items[0].any_afk == q.participant_items[0].any_afk
+            if p.trueskill_delta is not None:
+                assert abs(p.trueskill_delta - q.trueskill_delta) < 2e-3
+
+
+def test_sqlite_store_roundtrip(tmp_path):
+    path = str(tmp_path / "ana.db")
+    store = open_store("sqlite:///" + path)
+    assert isinstance(store, SqliteStore)
+    w, matches, clock = make_worker(n=12, players=10, batch=5, store=store)
+    publish(w.channel, "analyze", [m.api_id for m in matches])
+    w.start_consuming()
+    assert w.stats.acked == 12 and store.commits >= 3
+    # the same data rated in memory gives the same persisted values
+    mem = MemoryStore()
+    w2, m2, _ = make_worker(n=12, players=10, batch=5, store=mem)
+    publish(w2.channel, "analyze", [m.api_id for m in m2])
+    w2.start_consuming()
+    reopened = SqliteStore(path)
+    with reopened.session() as s:
+        loaded = list(s.load_matches([m.api_id for m in m2]))
+    assert [m.api_id for m in loaded] == [m.api_id for m in sorted(m2, key=lambda m: m.created_at)]
+    exp = {m.api_id: m for m in m2}
+    for m in loaded:
+        e = exp[m.api_id]
+        assert (m.trueskill_quality is None) == (e.trueskill_quality is None)
+        if e.trueskill_quality is not None:
+            assert abs(m.trueskill_quality - e.trueskill_quality) < 1e-12
+        for p, q in zip(m.participants, e.participants):
+            assert p.trueskill_mu == pytest.approx(q.trueskill_mu) if q.trueskill_mu is not None \
+                else p.trueskill_mu is None
+            assert bool(p.participant_items[0].any_afk) == bool(q.participant_items[0].any_afk)
+    reopened.close()
+
+
+def test_env_config_names_and_defaults():
+    cfg = WorkerConfig.from_env({})
+    assert (cfg.batchsize, cfg.chunksize, cfg.idle_timeout, cfg.queue) == (500, 100, 1.0, "analyze")
+    assert (cfg.crunch_queue, cfg.telesuck_queue, cfg.sew_queue) == ("crunch_global", "telesuck", "sew")
+    assert not (cfg.docrunchmatch or cfg.dotelesuckmatch or cfg.dosewmatch)
+    cfg = WorkerConfig.from_env({"DOCRUNCHMATCH": "true", "DOSEWMATCH": "True", "BATCHSIZE": "7"})
+    assert cfg.docrunchmatch and not cfg.dosewmatch and cfg.batchsize == 7  # only literal "true"
+    assert cfg.failed_queue == "analyze_failed"
+
+
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_config1_worker_cli_1k_matches(engine):
+    """BASELINE config 1: 1k synthetic 3v3 matches through worker.py on the CPU."""
+    env = dict(os.environ, ENGINE=engine, BATCHSIZE="500", IDLE_TIMEOUT="0.01")
+    env.pop("DATABASE_URI", None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "worker.py"), "--synthetic", "1000"],
+                         env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [l for l in out.stdout.splitlines() if l.startswith("{\"matches\"")][-1]
+    res = json.loads(line)
+    assert res["matches"] == 1000 and res["acked"] == 1000 and res["failed_batches"] == 0
