@@ -8,6 +8,7 @@
 #include <ATen/hip/HIPContext.h>
 
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "common.h"
@@ -131,6 +132,18 @@ std::vector<Tensor> sort_pairs(Tensor keys, Tensor vals, int64_t bits) {
   return in_alt ? std::vector<Tensor>{kb, vb} : std::vector<Tensor>{ka, va};
 }
 
+// K5 host levelizer (conflict-free rounds for the exact DP mode).
+std::tuple<Tensor, int64_t> levels(Tensor rec, int64_t K, int64_t num_players) {
+  TORCH_CHECK(!rec.is_cuda(), "levels runs on the host (pass a CPU stream)");
+  check(rec, "rec", torch::kInt32, rec.device());
+  TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
+  TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  auto level = torch::empty({rec.size(0)}, rec.options());
+  const int64_t depth = ana::host_levels((int)K, rec.data_ptr<int32_t>(), rec.size(0), num_players,
+                                         level.data_ptr<int32_t>());
+  return {level, depth};
+}
+
 void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
               Tensor workspace, Tensor ctrl) {
   const auto dev = rec.device();
@@ -240,20 +253,23 @@ void check_rows(const Tensor& t, const char* name, int64_t P, int64_t cols, cons
   TORCH_CHECK(t.dim() == 2 && t.size(0) == P && t.size(1) == cols, name, " must be [P, ", cols, "]");
 }
 
-void sweep_delta(Tensor s0, Tensor s, Tensor first_prior, Tensor buf) {
+void sweep_delta(Tensor s0, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma, Tensor buf) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
   check_rows(s0, "s0", P, ana::kRowFloats, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
-  check_rows(first_prior, "first_prior", P, ana::kRowFloats, dev);
+  check_rows(attrs, "attrs", P, 4, dev);
   check_rows(buf, "buf", P, 16, dev);
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
   if (dev.is_cuda()) {
     check_hip(ana::launch_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(),
-                                      first_prior.data_ptr<float>(), buf.data_ptr<float>(), P,
-                                      stream_of(s)), "sweep_delta");
+                                      attrs.data_ptr<float>(), vst.data_ptr<float>(),
+                                      (float)unknown_sigma, buf.data_ptr<float>(), P, stream_of(s)),
+              "sweep_delta");
   } else {
-    ana::host_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(), first_prior.data_ptr<float>(),
-                          buf.data_ptr<float>(), P);
+    ana::host_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(), attrs.data_ptr<float>(),
+                          vst.data_ptr<float>(), (float)unknown_sigma, buf.data_ptr<float>(), P);
   }
 }
 
@@ -298,6 +314,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gen_stream", &gen_stream, "K7: synthetic match stream rec [M, 2K+2]");
   m.def("schedule_workspace_bytes", &schedule_workspace_bytes);
   m.def("sort_pairs", &sort_pairs, "stable LSD radix sort of int32 (key, value) pairs (device)");
+  m.def("levels", &levels, "K5 host levelizer: per-match conflict-free round (0 = stateless)");
   m.def("schedule", &schedule, "K5: per-slot occurrence index (chronological order per player)");
   m.def("rate", &rate, "K1-K4/K6: exact dataflow rating of a stream");
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");

@@ -72,6 +72,39 @@ static void schedule_k(const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
   }
 }
 
+template <int K>
+static int64_t levels_k(const int32_t* rec, int64_t M, int64_t P, int32_t* level) {
+  constexpr int S = 2 * K;
+  std::vector<int32_t> last((size_t)P, 0);
+  int64_t depth = 0;
+  for (int64_t m = 0; m < M; ++m) {
+    MatchWork<float, K> w;
+    decode_record<float, K>(rec + m * (S + 2), P, w);
+    level[m] = 0;
+    if (w.status != kRated) continue;
+    int32_t l = 0;
+    for (int j = 0; j < S; ++j)
+      if (w.id[j] >= 0 && last[(size_t)w.id[j]] > l) l = last[(size_t)w.id[j]];
+    ++l;
+    for (int j = 0; j < S; ++j)
+      if (w.id[j] >= 0) last[(size_t)w.id[j]] = l;
+    level[m] = l;
+    if (l > depth) depth = l;
+  }
+  return depth;
+}
+
+int64_t host_levels(int K, const int32_t* rec, int64_t M, int64_t P, int32_t* level) {
+  switch (K) {
+    case 1: return levels_k<1>(rec, M, P, level);
+    case 2: return levels_k<2>(rec, M, P, level);
+    case 3: return levels_k<3>(rec, M, P, level);
+    case 4: return levels_k<4>(rec, M, P, level);
+    case 5: return levels_k<5>(rec, M, P, level);
+    default: return -1;
+  }
+}
+
 int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps) {
   switch (K) {
     case 1: schedule_k<1>(rec, M, P, link, deps); return 0;
@@ -169,9 +202,11 @@ int host_rate(int K, bool fp64, const int32_t* rec, float* state, const float* a
 
 namespace ana {
 
-void host_sweep_delta(const float* s0, const float* s, const float* fp, float* buf, int64_t P) {
+void host_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
+                      float unknown_sigma, float* buf, int64_t P) {
   for (int64_t p = 0; p < P; ++p)
-    sweep_delta_player(s0 + p * kRowFloats, s + p * kRowFloats, fp + p * kRowFloats, buf + p * 16);
+    sweep_delta_player(s0 + p * kRowFloats, s + p * kRowFloats, attrs + p * 4, vst, unknown_sigma,
+                       buf + p * 16);
 }
 
 void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,

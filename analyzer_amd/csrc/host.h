@@ -11,13 +11,18 @@ namespace ana {
 void host_gen_roster(const GenRosterParams& g, float* state, float* attrs);
 int host_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M);
 int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps);
+// K5 levelizer: level[m] = 1 + max level of the previous matches of m's players
+// (1 for a player's first match), 0 for matches that touch no state.  Returns
+// the number of levels (conflict-free rounds).
+int64_t host_levels(int K, const int32_t* rec, int64_t M, int64_t P, int32_t* level);
 int host_rate(int K, bool fp64, const int32_t* rec, float* state, const float* attrs,
               float* first_prior, const RateOut& out, const RateParams& prm);
 
 }  // namespace ana
 
 namespace ana {
-void host_sweep_delta(const float* s0, const float* s, const float* fp, float* buf, int64_t P);
+void host_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
+                      float unknown_sigma, float* buf, int64_t P);
 void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,
                       const float* vst, float unknown_sigma, int64_t P);
 }  // namespace ana

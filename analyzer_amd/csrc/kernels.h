@@ -38,8 +38,8 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
 }  // namespace ana
 
 namespace ana {
-int launch_sweep_delta(const float* s0, const float* s, const float* fp, float* buf, int64_t P,
-                       hipStream_t st);
+int launch_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
+                       float unknown_sigma, float* buf, int64_t P, hipStream_t st);
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,
                        const float* vst, float unknown_sigma, int64_t P, hipStream_t st);
 }  // namespace ana

@@ -1,6 +1,6 @@
 // Data-parallel posterior merge (SURVEY K9 + C1; BASELINE config 3 / north star).
 //
-// Every rank holds the full roster (64 B/player), rates its own shard of the
+// Every rank holds the full roster (128 B/player), rates its own shard of the
 // window exactly (kernels.hip), then the ranks combine what they learned:
 // in natural parameters (pi = 1/sigma^2, tau = mu/sigma^2) a Gaussian posterior
 // is prior x likelihood messages, so the per-rank message is
@@ -8,15 +8,14 @@
 // and the merged posterior is  nat(prior) + sum_g delta_g  -- one dense
 // all-reduce (SUM) of a [P][8][2] fp32 buffer over RCCL/xGMI.
 //
-//  * tracks rated before the window: prior = window-start value (same on all ranks)
-//  * shared track NULL at window start: prior = the seed (deterministic, same everywhere)
-//  * mode track NULL at window start: each rank's message is taken against the
-//    prior it actually used (recorded by the rate kernel in first_prior); the
-//    merged base is the window-start shared rating (or the seed) -- the one
-//    approximation beyond treating concurrent shards as independent.
-// Slot 7 of each player's buffer row carries touch counts for NULL-start
-// tracks (base-16 fields, exact in fp32 for <= 15 ranks) so a track touched on
-// any rank becomes non-NULL everywhere.
+// Every rank measures its message against the SAME base (sweep_core.h
+// track_base): the window-start value, or for a track NULL at window start the
+// prior the reference would assign (seed / window-start shared).  A track only
+// one rank touched therefore merges to exactly that rank's posterior; tracks
+// several ranks touched combine as independent evidence (the sweep-mode
+// approximation of concurrent shards).  Slot 7 of each player's buffer row
+// carries touch counts for NULL-start tracks (base-16 fields, exact in fp32
+// for <= 15 ranks) so a track touched on any rank becomes non-NULL everywhere.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -26,21 +25,28 @@
 
 namespace ana {
 
-// one thread per player, 16-B vector accesses (rows are 64 B)
+// one thread per player, 16-B vector accesses (rows are kRowFloats = 32 floats)
+constexpr int kRowVec = kRowFloats / 4;
+
+__device__ __forceinline__ void load_row(const float4* __restrict__ src, int64_t p, float* r) {
+#pragma unroll
+  for (int k = 0; k < kRowVec; ++k) {
+    const float4 x = src[p * kRowVec + k];
+    r[4 * k] = x.x; r[4 * k + 1] = x.y; r[4 * k + 2] = x.z; r[4 * k + 3] = x.w;
+  }
+}
+
 __global__ void sweep_delta_kernel(const float4* __restrict__ s0, const float4* __restrict__ s,
-                                   const float4* __restrict__ fp, float4* __restrict__ buf,
-                                   int64_t P) {
+                                   const float4* __restrict__ attrs, const float* __restrict__ vst,
+                                   float unknown_sigma, float4* __restrict__ buf, int64_t P) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  float a[16], b[16], f[16], o[16];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float4 x = s0[p * 4 + k], y = s[p * 4 + k], z = fp[p * 4 + k];
-    a[4 * k] = x.x; a[4 * k + 1] = x.y; a[4 * k + 2] = x.z; a[4 * k + 3] = x.w;
-    b[4 * k] = y.x; b[4 * k + 1] = y.y; b[4 * k + 2] = y.z; b[4 * k + 3] = y.w;
-    f[4 * k] = z.x; f[4 * k + 1] = z.y; f[4 * k + 2] = z.z; f[4 * k + 3] = z.w;
-  }
-  sweep_delta_player(a, b, f, o);
+  float a[kRowFloats], b[kRowFloats], o[16];
+  load_row(s0, p, a);
+  load_row(s, p, b);
+  const float4 at = attrs[p];
+  const float attr[4] = {at.x, at.y, at.z, at.w};
+  sweep_delta_player(a, b, attr, vst, unknown_sigma, o);
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     buf[p * 4 + k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
@@ -51,27 +57,28 @@ __global__ void sweep_apply_kernel(const float4* __restrict__ s0, const float4* 
                                    const float* __restrict__ vst, float unknown_sigma, int64_t P) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  float a[16], d[16], o[16];
+  float a[kRowFloats], d[16], o[kRowFloats];
+  load_row(s0, p, a);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const float4 x = s0[p * 4 + k], y = buf[p * 4 + k];
-    a[4 * k] = x.x; a[4 * k + 1] = x.y; a[4 * k + 2] = x.z; a[4 * k + 3] = x.w;
+    const float4 y = buf[p * 4 + k];
     d[4 * k] = y.x; d[4 * k + 1] = y.y; d[4 * k + 2] = y.z; d[4 * k + 3] = y.w;
   }
   const float4 at = attrs[p];
   const float attr[4] = {at.x, at.y, at.z, at.w};
   sweep_apply_player(a, d, attr, vst, unknown_sigma, o);
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-    s[p * 4 + k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+  for (int k = 0; k < kRowVec; ++k)
+    s[p * kRowVec + k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
 }
 
-int launch_sweep_delta(const float* s0, const float* s, const float* fp, float* buf, int64_t P,
-                       hipStream_t st) {
+int launch_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
+                       float unknown_sigma, float* buf, int64_t P, hipStream_t st) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(sweep_delta_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(s0), reinterpret_cast<const float4*>(s),
-                     reinterpret_cast<const float4*>(fp), reinterpret_cast<float4*>(buf), P);
+                     reinterpret_cast<const float4*>(attrs), vst, unknown_sigma,
+                     reinterpret_cast<float4*>(buf), P);
   return (int)hipGetLastError();
 }
 

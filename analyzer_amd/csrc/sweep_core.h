@@ -1,5 +1,6 @@
 // Per-player math of the data-parallel posterior merge (see sweep.hip for the
-// protocol); shared by the gfx950 kernels and the host mirror.
+// protocol); shared by the gfx950 kernels and the host mirror.  Rows are
+// kRowFloats floats: track t at mu = 4t, sigma = 4t + 2 (NaN mu = NULL).
 #pragma once
 
 #include <math.h>
@@ -14,28 +15,50 @@ ANA_HD void nat_params(float mu, float sig, float& pi, float& tau) {
   tau = mu * pi;
 }
 
-// a: window-start row, b: row after the local window, f: priors the rate kernel
-// recorded for tracks it found NULL (all kRowFloats-float rows, mu at 4t, sigma
-// at 4t+2).  o: 16 floats of message = (d_pi, d_tau) per track + touch fields.
-ANA_HD void sweep_delta_player(const float* a, const float* b, const float* f, float* o) {
+// The common base every rank measures its message against, for each track:
+// the window-start value; for a track NULL at window start the prior the
+// reference would give it -- the seed for the shared track, the window-start
+// shared rating (else the seed) for a mode track (rater.py:115-136).  Returns
+// false when the track has no base (NULL and the player cannot be seeded).
+ANA_HD bool track_base(const float* a, int t, bool seeded, float seed_mu, float seed_sig,
+                       float& mu, float& sig) {
+  if (a[4 * t] == a[4 * t]) {
+    mu = a[4 * t];
+    sig = a[4 * t + 2];
+    return true;
+  }
+  if (t > 0 && a[0] == a[0]) {
+    mu = a[0];
+    sig = a[2];
+    return true;
+  }
+  mu = seed_mu;
+  sig = seed_sig;
+  return seeded;
+}
+
+// a: window-start row, b: row after the local window, attr/vst/unknown_sigma:
+// seed inputs.  o: 16 floats = (d_pi, d_tau) per track + touch fields for
+// tracks that were NULL at window start and are rated now (base-16 counters,
+// exact in fp32 for <= 15 ranks).
+ANA_HD void sweep_delta_player(const float* a, const float* b, const float* attr, const float* vst,
+                               float unknown_sigma, float* o) {
+  float seed_mu = NAN, seed_sig = NAN;
+  const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
   float touch_lo = 0.f, touch_hi = 0.f;
   for (int t = 0; t < kTracks; ++t) {
     const float mu0 = a[4 * t], sg0 = a[4 * t + 2], mu = b[4 * t], sg = b[4 * t + 2];
     float dp = 0.f, dt = 0.f;
-    if (mu0 == mu0) {
-      if (mu != mu0 || sg != sg0) {
-        float p1, t1, p0, t0;
-        nat_params(mu, sg, p1, t1);
-        nat_params(mu0, sg0, p0, t0);
-        dp = p1 - p0;
-        dt = t1 - t0;
-      }
-    } else if (mu == mu) {
-      float p1, t1, pf, tf;
+    const bool changed = mu0 == mu0 ? (mu != mu0 || sg != sg0) : mu == mu;
+    float bm, bs;
+    if (changed && track_base(a, t, seeded, seed_mu, seed_sig, bm, bs)) {
+      float p1, t1, p0, t0;
       nat_params(mu, sg, p1, t1);
-      nat_params(f[4 * t], f[4 * t + 2], pf, tf);
-      dp = p1 - pf;
-      dt = t1 - tf;
+      nat_params(bm, bs, p0, t0);
+      dp = p1 - p0;
+      dt = t1 - t0;
+    }
+    if (mu0 != mu0 && mu == mu) {
       if (t < 4) touch_lo += (float)(1 << (4 * t));
       else touch_hi += (float)(1 << (4 * (t - 4)));
     }
@@ -47,31 +70,20 @@ ANA_HD void sweep_delta_player(const float* a, const float* b, const float* f, f
 }
 
 // a: window-start row, d: all-reduced messages, attr: player attributes,
-// o: merged row (tags reset to 0).
+// o: merged row (tags reset to 0; spare floats copied).
 ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr,
                                const float* vst, float unknown_sigma, float* o) {
   float seed_mu = NAN, seed_sig = NAN;
   const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
-  float base_mu = a[0], base_sig = a[2];
-  if (base_mu != base_mu) {
-    base_mu = seed_mu;
-    base_sig = seed_sig;
-  }
   const unsigned lo = (unsigned)d[14], hi = (unsigned)d[15];
   for (int t = 0; t < kTracks; ++t) {
     const float mu0 = a[4 * t], sg0 = a[4 * t + 2];
     const unsigned touched = t < 4 ? (lo >> (4 * t)) & 15u : (hi >> (4 * (t - 4))) & 15u;
-    float mu = mu0, sg = sg0, pb = 0.f, tb = 0.f;
-    bool have = false;
-    if (mu0 == mu0) {
-      nat_params(mu0, sg0, pb, tb);
-      have = d[2 * t] != 0.f || d[2 * t + 1] != 0.f;
-    } else if (touched && seeded) {
-      if (t == 0) nat_params(seed_mu, seed_sig, pb, tb);
-      else nat_params(base_mu, base_sig, pb, tb);
-      have = true;
-    }
-    if (have) {
+    float mu = mu0, sg = sg0, bm, bs;
+    const bool live = mu0 == mu0 ? (d[2 * t] != 0.f || d[2 * t + 1] != 0.f) : touched != 0u;
+    if (live && track_base(a, t, seeded, seed_mu, seed_sig, bm, bs)) {
+      float pb, tb;
+      nat_params(bm, bs, pb, tb);
       float pi = pb + d[2 * t];
       const float tau = tb + d[2 * t + 1];
       pi = pi > 1e-12f ? pi : 1e-12f;  // merged precision never below "no information"

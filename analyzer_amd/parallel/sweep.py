@@ -6,8 +6,9 @@ window exactly and in order, and then all ranks merge what they learned with
 ONE dense all-reduce of natural-parameter messages (csrc/sweep.hip):
 
     begin(roster)   -> snapshot the window-start roster
-    <rate the local shard with first_prior recording>
-    merge(roster)   -> messages -> all_reduce(SUM) over RCCL/xGMI -> apply
+    <rate the local shard exactly>
+    merge(roster)   -> messages against a common base -> all_reduce(SUM) over
+                       RCCL/xGMI -> apply (csrc/sweep_core.h)
 
 With one rank the merge is skipped (the exact single-GPU result stands).
 Backend: ``nccl`` (RCCL on ROCm) for device tensors, ``gloo`` for CPU tests.
@@ -43,7 +44,6 @@ class SweepMerger:
                              "integers in the message buffer)")
         f = dict(dtype=torch.float32, device=self.device)
         self.start = torch.empty((self.P, 32), **f)
-        self.first_prior = torch.full((self.P, 32), float("nan"), **f)
         self.buf = torch.empty((self.P, 16), **f)
         self.vst = torch.tensor(vst_table(), **f)
         self.comm_bytes = self.buf.numel() * 4
@@ -53,7 +53,8 @@ class SweepMerger:
         self.start.copy_(roster.state)
 
     def messages(self, roster) -> torch.Tensor:
-        native().sweep_delta(self.start, roster.state, self.first_prior, self.buf)
+        native().sweep_delta(self.start, roster.state, roster.attrs, self.vst,
+                             float(self.cfg.unknown_player_sigma), self.buf)
         return self.buf
 
     def reduce(self) -> None:
@@ -79,6 +80,6 @@ class SweepMerger:
 def rate_window_dp(rater, merger: SweepMerger, roster, rec, K=None, out=None, check=True):
     """One DP step: exact local rating of this rank's shard + posterior merge."""
     merger.begin(roster)
-    res = rater.rate(roster, rec, K, out=out, first_prior=merger.first_prior, check=check)
+    res = rater.rate(roster, rec, K, out=out, check=check)
     merger.merge(roster)
     return res

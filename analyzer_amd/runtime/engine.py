@@ -70,12 +70,10 @@ class WindowPipeline:
         main = torch.cuda.current_stream(self.device) if self.cuda else None
         if prep.ready is not None:
             main.wait_event(prep.ready)
-        fp = None
         if self.merger is not None:
             self.merger.begin(self.roster)
-            fp = self.merger.first_prior
-        res = self.rater.rate(self.roster, prep.rec, self.K, out=out, first_prior=fp,
-                              check=check, schedule=prep.schedule)
+        res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
+                              schedule=prep.schedule)
         if self.cuda:
             done = torch.cuda.Event()
             done.record(main)

@@ -1,0 +1,170 @@
+"""Full-history re-rate driver (SURVEY P4 + C5 + C4; BASELINE configs 3 and 5).
+
+The reference is online-only: batches of <= 500 matches in arrival order, no
+way to re-rate a history (/root/reference/worker.py:18,176).  This driver
+streams a long synthetic history through the engine window by window:
+
+* the history is a counter-RNG stream, so window ``g`` of rank ``r`` is
+  generated on the device from its global offset -- no host I/O, and any window
+  can be regenerated after a crash;
+* one rank: windows are rated exactly, in order (dataflow engine, prepass of
+  window g+1 overlapped with rating g -- runtime/engine.py);
+* N ranks (one per GPU): time-axis sharding -- global window g is N
+  consecutive blocks of ``window`` matches, rank r rates block r exactly from
+  the window-start roster, then one RCCL all-reduce of natural-parameter
+  messages merges the blocks (sweep mode, parallel/sweep.py);
+* every ``checkpoint_every`` windows the replicated roster and the stream
+  position are checkpointed atomically; a restarted run resumes from there and
+  produces the same roster as an uninterrupted run (exactly-once);
+* status counters are accumulated on the device and reduced over ranks (C4).
+
+    python -m analyzer_amd.runtime.rerate --matches 1000000000 --players 10000000 \\
+        --window 16000000 --team-size 3 --checkpoint-dir /tmp/ck
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from dataclasses import asdict, dataclass
+from typing import Callable, Dict, Optional
+
+import torch
+
+from ..config import RaterConfig
+from ..ops import rate as R
+from ..ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
+from ..parallel.comm import broadcast_roster, init_from_env, reduce_counts, world
+from ..parallel.sweep import SweepMerger
+from .checkpoint import CheckpointManager
+from .engine import WindowPipeline
+
+
+class InjectedFault(SystemExit):
+    """Raised by ``fault_kill_after`` to simulate a crash (exit code 17)."""
+
+
+@dataclass
+class RerateSpec:
+    total_matches: int
+    players: int
+    team_size: int = 3
+    window: int = 1_000_000          # matches per rank per window
+    seed: int = 2024
+    p_afk: float = 0.02
+    p_rated: float = 0.0             # fraction of players with a stored rating at start
+
+    def roster_spec(self) -> RosterSpec:
+        return RosterSpec(num_players=self.players, seed=self.seed, p_rated=self.p_rated)
+
+    def stream_spec(self) -> StreamSpec:
+        return StreamSpec(team_size=self.team_size, seed=self.seed + 1, p_afk=self.p_afk)
+
+
+def n_windows(spec: RerateSpec, size: int) -> int:
+    per = spec.window * size
+    return (spec.total_matches + per - 1) // per
+
+
+def window_slice(spec: RerateSpec, g: int, rank: int, size: int):
+    """[lo, hi) global match offsets of rank's block of window g."""
+    lo = g * spec.window * size + rank * spec.window
+    hi = min(lo + spec.window, spec.total_matches)
+    return lo, max(lo, hi)
+
+
+def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
+        checkpoint_every: int = 1, fault_kill_after: Optional[int] = None,
+        on_window: Optional[Callable[[int, R.RateResult], None]] = None,
+        rater: Optional[R.BatchRater] = None):
+    """Rate the whole history; returns (metrics reduced over ranks, final roster)."""
+    rank, size = world()
+    dev = torch.device(device) if device is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+    rater = rater or R.BatchRater(RaterConfig())
+    K = spec.team_size
+    ck = CheckpointManager(checkpoint_dir, checkpoint_every, rank=0)
+    start_window = 0
+    restored = ck.latest(dev)
+    if restored is not None:
+        roster, meta = restored
+        if meta.get("spec") != asdict(spec) or meta.get("world") != size:
+            raise ValueError("checkpoint in %s belongs to a different run" % checkpoint_dir)
+        start_window = int(meta["windows_done"])
+    else:
+        roster = make_roster(spec.roster_spec(), device=dev)
+        broadcast_roster(roster)  # C3 (identical by construction; keeps replicas honest)
+    merger = SweepMerger(spec.players, dev, rater.cfg) if size > 1 else None
+    pipe = WindowPipeline(rater, roster, K, merger=merger)
+    total = n_windows(spec, size)
+    counts = torch.zeros(256, dtype=torch.int64, device=dev)
+    sspec = spec.stream_spec()
+    out = None
+
+    def window_rec(g):
+        lo, hi = window_slice(spec, g, rank, size)
+        return make_stream(sspec, hi - lo, spec.players, K=K, base=lo, device=dev)
+
+    t0 = time.perf_counter()
+    rated = 0
+    nxt = pipe.prepare(window_rec(start_window)) if start_window < total else None
+    for g in range(start_window, total):
+        cur = nxt
+        nxt = pipe.prepare(window_rec(g + 1)) if g + 1 < total else None
+        M = cur.rec.shape[0]
+        if out is None or out.quality.shape[0] != M:
+            out = R.RateResult.allocate(M, K, dev)
+        res = pipe.rate(cur, out=out)
+        counts += torch.bincount(res.status.to(torch.int64), minlength=256)
+        rated += M
+        if on_window is not None:
+            on_window(g, res)
+        if rank == 0:
+            ck.maybe_save(g + 1, roster, {"spec": asdict(spec), "world": size,
+                                          "next_offset": window_slice(spec, g + 1, 0, size)[0]})
+        if fault_kill_after is not None and g + 1 >= fault_kill_after:
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            raise InjectedFault(17)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    rater.check_errors(dev) if dev.type == "cuda" else None
+    c = counts.cpu()
+    local = {R.STATUS_NAMES.get(i, str(i)): float(c[i]) for i in range(256) if int(c[i])}
+    local["matches"] = float(rated)
+    summed = reduce_counts(local, dev)
+    summed["seconds"] = reduce_counts({"seconds": dt}, dev, op="max")["seconds"]
+    summed["windows"] = float(total - start_window)
+    summed["resumed_from_window"] = float(start_window)
+    summed["matches_per_s"] = summed["matches"] / summed["seconds"] if summed["seconds"] > 0 else 0.0
+    return summed, roster
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--matches", type=float, required=True)
+    ap.add_argument("--players", type=float, required=True)
+    ap.add_argument("--team-size", type=int, default=3)
+    ap.add_argument("--window", type=float, default=1e6)
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--checkpoint-dir", default=os.environ.get("CHECKPOINT_DIR"))
+    ap.add_argument("--checkpoint-every", type=int, default=int(os.environ.get("CHECKPOINT_EVERY") or 1))
+    ap.add_argument("--fault-kill-after", type=int, default=None,
+                    help="fault injection: exit(17) after this many windows")
+    ap.add_argument("--device", default=None)
+    args = ap.parse_args(argv)
+    rank, size, dev = init_from_env()
+    spec = RerateSpec(total_matches=int(args.matches), players=int(args.players),
+                      team_size=args.team_size, window=int(args.window), seed=args.seed)
+    res, _ = run(spec, args.device or dev, args.checkpoint_dir, args.checkpoint_every,
+                 args.fault_kill_after)
+    if rank == 0:
+        print(json.dumps(dict(res, n_ranks=size, spec=asdict(spec))), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,165 @@
+"""Multi-process tests of the comm layer on the CPU (gloo, world size 2-4):
+C1 sweep merge, C2 exact DP, C3 broadcast, C4 metric reduce.
+Each test spawns ranks that write their results to a temp dir; the parent checks."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _entry(rank, size, port, fn, outdir, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(size), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=size)
+    try:
+        res = fn(rank, size, *args)
+        torch.save(res, os.path.join(outdir, "r%d.pt" % rank))
+    finally:
+        dist.destroy_process_group()
+
+
+def run_ranks(fn, size, tmp_path, *args):
+    mp.spawn(_entry, args=(size, _free_port(), fn, str(tmp_path), args), nprocs=size, join=True)
+    return [torch.load(os.path.join(str(tmp_path), "r%d.pt" % r), weights_only=True) for r in range(size)]
+
+
+# ------------------------------------------------------------------ C3 / C4
+def _bcast_and_counts(rank, size):
+    from analyzer_amd.ops.rate import Roster
+    from analyzer_amd.parallel.comm import broadcast_roster, reduce_counts
+
+    roster = make_roster(RosterSpec(num_players=50, seed=4)) if rank == 0 else Roster.empty(50)
+    broadcast_roster(roster)
+    c = reduce_counts({"rated": 10.0 * (rank + 1), "only_r%d" % rank: 1.0}, "cpu")
+    m = reduce_counts({"ms": float(rank)}, "cpu", op="max")
+    return {"state": roster.state, "attrs": roster.attrs, "counts": c, "max": m}
+
+
+def test_broadcast_roster_and_reduce_counts(tmp_path):
+    res = run_ranks(_bcast_and_counts, 3, tmp_path)
+    ref = make_roster(RosterSpec(num_players=50, seed=4))
+    for r in res:
+        assert torch.equal(r["state"].nan_to_num(-7), ref.state.nan_to_num(-7))
+        assert torch.equal(r["attrs"].nan_to_num(-7), ref.attrs.nan_to_num(-7))
+        assert r["counts"] == {"rated": 60.0, "only_r0": 1.0, "only_r1": 1.0, "only_r2": 1.0}
+        assert r["max"] == {"ms": 2.0}
+
+
+# ------------------------------------------------------------------ C2 exact DP
+def _exact(rank, size, P, M, K, seed):
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.parallel.exact_dp import rate_exact_dp
+
+    roster = make_roster(RosterSpec(num_players=P, seed=seed))
+    rec = make_stream(StreamSpec(team_size=K, seed=seed + 1, p_afk=0.05, p_unsupported=0.05), M, P, K=K)
+    out = rate_exact_dp(BatchRater(), roster, rec, K)
+    return {"state": roster.state, "status": out.status, "s_mu": out.s_mu, "delta": out.delta,
+            "m_mu": out.m_mu, "quality": out.quality}
+
+
+@pytest.mark.parametrize("size", [2, 3])
+def test_exact_dp_bit_identical_to_sequential(tmp_path, size):
+    from analyzer_amd.ops.rate import BatchRater
+
+    P, M, K, seed = 40, 300, 3, 9
+    res = run_ranks(_exact, size, tmp_path, P, M, K, seed)
+    roster = make_roster(RosterSpec(num_players=P, seed=seed))
+    rec = make_stream(StreamSpec(team_size=K, seed=seed + 1, p_afk=0.05, p_unsupported=0.05), M, P, K=K)
+    ref = BatchRater().rate(roster, rec, K)
+    for r in res:  # replicas agree with the sequential run, bit for bit
+        assert torch.equal(r["state"].nan_to_num(-7), roster.state.nan_to_num(-7))
+    # outputs are sharded: every match rated by exactly one rank, identical values
+    owner = torch.stack([r["status"] != 255 for r in res]).sum(0)
+    assert bool((owner == 1).all())
+    for key, ref_t in (("s_mu", ref.s_mu), ("delta", ref.delta), ("m_mu", ref.m_mu)):
+        merged = torch.full_like(ref_t, float("nan"))
+        for r in res:
+            mine = r["status"] != 255
+            merged[mine] = r[key][mine]
+        assert torch.equal(merged.nan_to_num(-7), ref_t.nan_to_num(-7)), key
+
+
+def test_levels_host():
+    from analyzer_amd.ops.native import native
+
+    rec = make_stream(StreamSpec(team_size=3, seed=2, p_afk=0.0), 200, 15)
+    level, depth = native().levels(rec, 3, 15)
+    last = {}
+    for m in range(200):
+        ids = [int(x) for x in rec[m, :6]]
+        exp = 1 + max(last.get(p, 0) for p in ids)
+        assert int(level[m]) == exp
+        for p in ids:
+            last[p] = exp
+    assert depth == int(level.max())
+
+
+# ------------------------------------------------------------------ C1 sweep merge
+def _sweep(rank, size, P, M, K, seed, disjoint):
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.parallel.sweep import SweepMerger
+
+    roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.5))
+    rec = make_stream(StreamSpec(team_size=K, seed=seed + 1 + rank, p_afk=0.0), M, P, K=K)
+    if disjoint:  # rank r only sees players r, r+size, ...
+        rec[:, :2 * K] = rec[:, :2 * K] - rec[:, :2 * K] % size + rank
+    merger = SweepMerger(P, "cpu")
+    merger.begin(roster)
+    local = roster.clone()
+    BatchRater().rate(local, rec, K)
+    merger.messages(local)
+    msg = merger.buf.clone()
+    merger.reduce()
+    merged = local.clone()
+    merger.apply(merged)
+    return {"local": local.state, "msg": msg, "merged": merged.state, "rec": rec}
+
+
+def test_sweep_merge_disjoint_equals_union(tmp_path):
+    """Players partitioned across ranks: the merge reproduces every rank's exact
+    result (up to the natural-parameter round trip in fp32)."""
+    P, M, K, seed, size = 60, 200, 3, 5, 2
+    res = run_ranks(_sweep, size, tmp_path, P, M, K, seed, True)
+    for rank, r in enumerate(res):
+        mine = torch.arange(P) % size == rank
+        a, b = r["merged"][mine], r["local"][mine]
+        mu_a, mu_b = a[:, 0::4], b[:, 0::4]
+        assert torch.equal(torch.isnan(mu_a), torch.isnan(mu_b))
+        ok = ~torch.isnan(mu_b)
+        assert torch.allclose(mu_a[ok], mu_b[ok], rtol=1e-5, atol=2e-3)
+        sg_a, sg_b = a[:, 2::4][ok], b[:, 2::4][ok]
+        assert torch.allclose(sg_a, sg_b, rtol=1e-4)
+    assert torch.equal(res[0]["merged"].nan_to_num(-7), res[1]["merged"].nan_to_num(-7))
+
+
+def test_sweep_merge_overlapping_sums_messages(tmp_path):
+    """Overlapping players: merged natural parameters = start + sum of every
+    rank's (posterior - start) message (EP product of the rank posteriors)."""
+    P, M, K, seed, size = 30, 150, 3, 6, 3
+    res = run_ranks(_sweep, size, tmp_path, P, M, K, seed, False)
+    total = sum(r["msg"] for r in res)
+    start = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.5)).state
+    merged = res[0]["merged"]
+    for t in range(7):
+        mu0, sg0 = start[:, 4 * t], start[:, 4 * t + 2]
+        have = ~torch.isnan(mu0) & ((total[:, 2 * t] != 0) | (total[:, 2 * t + 1] != 0))
+        pi = 1 / sg0[have].double() ** 2 + total[have, 2 * t].double()
+        tau = mu0[have].double() / sg0[have].double() ** 2 + total[have, 2 * t + 1].double()
+        assert torch.allclose(merged[have, 4 * t].double(), tau / pi, rtol=1e-5, atol=1e-2)
+        assert torch.allclose(merged[have, 4 * t + 2].double(), pi.rsqrt(), rtol=1e-4)
+    for r in res[1:]:
+        assert torch.equal(r["merged"].nan_to_num(-7), merged.nan_to_num(-7))
