@@ -131,4 +131,5 @@ def test_sweep_kernels_match_host(gpu_device):
     sd = start.state.to(gpu_device).clone()
     native().sweep_apply(start.state.to(gpu_device), (bh * 2).to(gpu_device),
                          start.attrs.to(gpu_device), sd, vst.to(gpu_device), 500.0)
-    np.testing.assert_allclose(sd.cpu().numpy(), sh.numpy(), rtol=1e-6, atol=1e-6, equal_nan=True)
+    # fp32 (tau / pi, 1 / sqrt(pi)): device fma contraction vs host rounding
+    np.testing.assert_allclose(sd.cpu().numpy(), sh.numpy(), rtol=5e-5, atol=1e-6, equal_nan=True)
