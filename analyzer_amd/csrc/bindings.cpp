@@ -179,12 +179,29 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   }
 }
 
+static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& events,
+                                             const Tensor& stats, int64_t M, int64_t K,
+                                             const torch::Device& dev) {
+  ana::TelemetryParams tp{nullptr, nullptr, nullptr, M};
+  if (evoff.numel() == 0) return tp;
+  check(evoff, "evoff", torch::kInt64, dev);
+  check(events, "events", torch::kInt32, dev);
+  check(stats, "stats", torch::kFloat32, dev);
+  TORCH_CHECK(evoff.numel() == M + 1, "evoff must have M + 1 entries");
+  TORCH_CHECK(events.dim() == 2 && events.size(1) == 4, "events must be [E, 4]");
+  TORCH_CHECK(stats.numel() == M * 2 * K * ana::kStatFeatures, "stats must be [M, 2K, 8]");
+  tp.evoff = evoff.data_ptr<int64_t>();
+  tp.events = events.data_ptr<int32_t>();
+  tp.stats = stats.data_ptr<float>();
+  return tp;
+}
+
 // ------------------------------------------------------------ K1-K4, K6
 void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor attrs,
           Tensor first_prior, Tensor quality, Tensor status, Tensor s_mu, Tensor s_sig,
           Tensor delta, Tensor m_mu, Tensor m_sig, Tensor ctrl, Tensor vst, double beta2,
           double tau2, double unknown_sigma, bool record_first_prior, int64_t blocks,
-          int64_t epoch, bool host_fp64) {
+          int64_t epoch, bool host_fp64, Tensor tele_evoff, Tensor tele_events, Tensor tele_stats) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
@@ -227,6 +244,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   prm.epoch = (int32_t)epoch;
   prm.vst = vst.data_ptr<float>();
   if (const char* e = std::getenv("ANA_RATE_IDLE")) prm.idle_spins = std::atoi(e);  // tuning knob
+  const ana::TelemetryParams tp = telemetry_params(tele_evoff, tele_events, tele_stats, M, K, dev);
   if (dev.is_cuda()) {
     check(link, "link", torch::kInt32, dev);
     check(deps, "deps", torch::kInt32, dev);
@@ -239,12 +257,67 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
                                reinterpret_cast<const uint32_t*>(link.data_ptr<int32_t>()),
                                deps.data_ptr<int32_t>(), state.data_ptr<float>(),
                                attrs.data_ptr<float>(), fp, out,
-                               reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm,
+                               reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm, tp,
                                (int)blocks, stream_of(rec)), "rate");
   } else {
     TORCH_CHECK(ana::host_rate((int)K, host_fp64, rec.data_ptr<int32_t>(), state.data_ptr<float>(),
                                attrs.data_ptr<float>(), fp, out, prm) == 0, "bad K");
+    if (tp.evoff) ana::host_telemetry((int)K, tp);
   }
+}
+
+// ------------------------------------------------------------------ K8
+Tensor gen_event_counts(int64_t M, int64_t seed, int64_t min_events, int64_t max_events,
+                        int64_t base, torch::Device device) {
+  TORCH_CHECK(min_events >= 0 && max_events >= min_events, "need 0 <= min_events <= max_events");
+  ana::GenEventParams g{(uint64_t)seed, (int32_t)min_events, (int32_t)max_events};
+  auto counts = torch::empty({M}, torch::TensorOptions().dtype(torch::kInt64).device(device));
+  if (device.is_cuda())
+    check_hip(ana::launch_gen_event_counts(g, base, M, counts.data_ptr<int64_t>(),
+                                           at::hip::getCurrentHIPStream(device.index()).stream()),
+              "gen_event_counts");
+  else
+    ana::host_gen_event_counts(g, base, M, counts.data_ptr<int64_t>());
+  return counts;
+}
+
+void gen_events(Tensor rec, int64_t K, Tensor evoff, int64_t seed, int64_t min_events,
+                int64_t max_events, int64_t base, Tensor events) {
+  const auto dev = rec.device();
+  check(rec, "rec", torch::kInt32, dev);
+  check(evoff, "evoff", torch::kInt64, dev);
+  check(events, "events", torch::kInt32, dev);
+  TORCH_CHECK(K >= 1 && K <= 5 && rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  const int64_t M = rec.size(0);
+  TORCH_CHECK(evoff.numel() == M + 1, "evoff must have M + 1 entries");
+  TORCH_CHECK(events.dim() == 2 && events.size(1) == 4, "events must be [E, 4]");
+  ana::GenEventParams g{(uint64_t)seed, (int32_t)min_events, (int32_t)max_events};
+  if (dev.is_cuda())
+    check_hip(ana::launch_gen_events((int)K, g, base, rec.data_ptr<int32_t>(),
+                                     evoff.data_ptr<int64_t>(), M, events.data_ptr<int32_t>(),
+                                     stream_of(rec)), "gen_events");
+  else
+    TORCH_CHECK(ana::host_gen_events((int)K, g, base, rec.data_ptr<int32_t>(),
+                                     evoff.data_ptr<int64_t>(), M, events.data_ptr<int32_t>()) == 0,
+                "bad K");
+}
+
+// standalone aggregation; bad (device: int32[>=1] counter, host: ignored) counts malformed events
+int64_t telemetry(Tensor evoff, Tensor events, int64_t K, Tensor stats, Tensor bad) {
+  const auto dev = events.device();
+  TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
+  const int64_t M = evoff.numel() - 1;
+  TORCH_CHECK(M >= 0, "evoff must have M + 1 entries");
+  const ana::TelemetryParams tp = telemetry_params(evoff, events, stats, M, K, dev);
+  if (!tp.evoff) return 0;
+  if (dev.is_cuda()) {
+    check(bad, "bad", torch::kInt32, dev);
+    TORCH_CHECK(bad.numel() >= 1, "bad must have an entry");
+    check_hip(ana::launch_telemetry((int)K, tp, reinterpret_cast<uint32_t*>(bad.data_ptr<int32_t>()),
+                                    stream_of(events)), "telemetry");
+    return -1;
+  }
+  return ana::host_telemetry((int)K, tp);
 }
 
 // ------------------------------------------------------------- K9 / C1
@@ -317,6 +390,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("levels", &levels, "K5 host levelizer: per-match conflict-free round (0 = stateless)");
   m.def("schedule", &schedule, "K5: per-slot occurrence index (chronological order per player)");
   m.def("rate", &rate, "K1-K4/K6: exact dataflow rating of a stream");
+  m.def("gen_event_counts", &gen_event_counts, "K8/K7: synthetic telemetry events per match");
+  m.def("gen_events", &gen_events, "K8/K7: synthetic telemetry events (CSR by match)");
+  m.def("telemetry", &telemetry, "K8: per-participant telemetry aggregation [M, 2K, 8]");
+  m.attr("STAT_FEATURES") = ana::kStatFeatures;
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
   m.def("sweep_apply", &sweep_apply, "K9: apply all-reduced messages to the replicated roster");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");

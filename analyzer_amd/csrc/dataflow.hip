@@ -38,6 +38,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "rate_core.h"
+#include "telemetry_dev.h"
 
 namespace ana {
 
@@ -110,12 +111,13 @@ __global__ void __launch_bounds__(256)
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
                      float* __restrict__ first_prior, RateOut out, uint32_t* ctrl,
-                     RateParams prm) {
+                     RateParams prm, TelemetryParams tp) {
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
   constexpr int G = S <= 2 ? 2 : (S <= 4 ? 4 : (S <= 8 ? 8 : 16));
   constexpr int NG = 64 / G;
   __shared__ int32_t lrec[kWavesPerBlock][kHeld][kChunk * R];
+  __shared__ float tele[kWavesPerBlock][kTeleTile * S * (kStatFeatures + 1)];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int j = lane % G;
@@ -145,6 +147,16 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   bool exhausted = false, tk_pending = false;
   unsigned tk = 0;                 // ticket returned to lane 0
   uint32_t spins = 0;
+  // K8 fused mode: telemetry tiles fill the time a wave would spend waiting
+  const int64_t tele_tiles = tp.evoff ? (tp.num_matches + kTeleTile - 1) / kTeleTile : 0;
+  bool tele_done = tele_tiles == 0;
+  auto tele_claim = [&]() -> int64_t {
+    unsigned t = 0;
+    if (lane == 0)
+      t = __hip_atomic_fetch_add((gu32*)&ctrl[12], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __shfl(t, 0);
+    return (int64_t)t < tele_tiles ? (int64_t)t : -1;
+  };
   const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : 8u;
 
   for (;;) {
@@ -430,7 +442,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     bool held = false;
 #pragma unroll
     for (int h = 0; h < kHeld; ++h) held |= cbase[h] >= 0;
-    if (exhausted && !held && !tk_pending) break;
+    if (exhausted && !held && !tk_pending) {
+      while (!tele_done) {  // leftover telemetry tiles
+        const int64_t t = tele_claim();
+        if (t < 0) tele_done = true;
+        else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+      }
+      break;
+    }
 
     // ---------------------------------------------- (13) idle: back off, bounded
     if (worked || staging >= 0) {
@@ -443,6 +462,15 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           if (cbase[h] >= 0 && ((pend[h] >> lane) & 1ull)) out.status[cbase[h] + lane] = kNotProcessed;
         return;  // give up: the host sees ctrl[1] and raises
       }
+      if (!tele_done) {  // nothing ready: aggregate a telemetry tile instead of sleeping
+        const int64_t t = tele_claim();
+        if (t >= 0) {
+          telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+          spins = 0;
+          continue;
+        }
+        tele_done = true;
+      }
       spins = spins < max_spins ? spins + 1u : max_spins;
       for (uint32_t k = 0; k < spins; ++k) __builtin_amdgcn_s_sleep(2);
     }
@@ -451,10 +479,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 
 int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, float* state,
                 const float* attrs, float* first_prior, const RateOut& out, uint32_t* ctrl,
-                const RateParams& prm, int blocks, hipStream_t s) {
+                const RateParams& prm, const TelemetryParams& tp, int blocks, hipStream_t s) {
   const int64_t M = prm.num_matches;
-  // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] spare, [4..11] tickets
-  if (hipMemsetAsync(ctrl + 1, 0, 11 * 4, s) != hipSuccess) return (int)hipGetLastError();
+  // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] spare, [4..11] tickets,
+  // [12] telemetry tile ticket, [13] malformed telemetry events
+  if (hipMemsetAsync(ctrl + 1, 0, 13 * 4, s) != hipSuccess) return (int)hipGetLastError();
   if (M <= 0) return 0;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
   if (prm.epoch < 1 || prm.epoch > 255) return (int)hipErrorInvalidValue;
@@ -463,7 +492,7 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
 #define ANA_RATE_CASE(k)                                                                      \
   case k:                                                                                     \
     hipLaunchKernelGGL(rate_dataflow_kernel<k>, dim3((unsigned)blocks), dim3(256), 0, s, rec,  \
-                       link, deps, state, attrs, first_prior, out, ctrl, prm);                \
+                       link, deps, state, attrs, first_prior, out, ctrl, prm, tp);            \
     break;
     ANA_RATE_CASE(1) ANA_RATE_CASE(2) ANA_RATE_CASE(3) ANA_RATE_CASE(4) ANA_RATE_CASE(5)
 #undef ANA_RATE_CASE

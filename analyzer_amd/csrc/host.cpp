@@ -72,6 +72,50 @@ static void schedule_k(const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
   }
 }
 
+void host_gen_event_counts(const GenEventParams& g, int64_t base, int64_t M, int64_t* counts) {
+  for (int64_t m = 0; m < M; ++m) counts[m] = gen_event_count(g, (uint64_t)(base + m));
+}
+
+int host_gen_events(int K, const GenEventParams& g, int64_t base, const int32_t* rec,
+                    const int64_t* evoff, int64_t M, int32_t* events) {
+  if (K < 1 || K > 5) return -1;
+  const int S = 2 * K;
+  for (int64_t m = 0; m < M; ++m) {
+    const uint32_t m0 = (uint32_t)rec[m * (S + 2) + S];
+    const int n0 = meta_n0(m0) < K ? meta_n0(m0) : K, n1 = meta_n1(m0) < K ? meta_n1(m0) : K;
+    for (int64_t e = evoff[m]; e < evoff[m + 1]; ++e) {
+      int32_t* ev = events + e * 4;
+      gen_event(g, (uint64_t)(base + m), e - evoff[m], (int32_t)m, n0 + n1, ev);
+      const int r = event_slot(ev[1]);
+      ev[1] = (ev[1] & ~0xff) | (r < n0 ? r : K + (r - n0));
+    }
+  }
+  return 0;
+}
+
+int64_t host_telemetry(int K, const TelemetryParams& tp) {
+  const int S = 2 * K;
+  const int64_t M = tp.num_matches;
+  int64_t bad = 0;
+  for (int64_t i = 0; i < M * S * kStatFeatures; ++i) tp.stats[i] = 0.f;
+  for (int64_t m = 0; m < M; ++m)
+    for (int64_t e = tp.evoff[m]; e < tp.evoff[m + 1]; ++e) {
+      const int32_t* ev = tp.events + e * 4;
+      const int slot = event_slot(ev[1]);
+      if (ev[0] < 0 || (int64_t)ev[0] / kTeleTile != m / kTeleTile || ev[0] >= M || slot >= S) {
+        ++bad;
+        continue;
+      }
+      float value, add;
+      memcpy(&value, ev + 2, 4);
+      const int f = event_feature(event_type(ev[1]), value, add);
+      float* row = tp.stats + ((int64_t)ev[0] * S + slot) * kStatFeatures;
+      if (f >= 0) row[f] += add;
+      row[kStatEvents] += 1.f;
+    }
+  return bad;
+}
+
 template <int K>
 static int64_t levels_k(const int32_t* rec, int64_t M, int64_t P, int32_t* level) {
   constexpr int S = 2 * K;

@@ -5,6 +5,7 @@
 
 #include "common.h"
 #include "gen_core.h"
+#include "telemetry_core.h"
 
 namespace ana {
 
@@ -14,6 +15,12 @@ int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* lin
 // K5 levelizer: level[m] = 1 + max level of the previous matches of m's players
 // (1 for a player's first match), 0 for matches that touch no state.  Returns
 // the number of levels (conflict-free rounds).
+// K8 host mirror: generation (counts per match, then events given the CSR
+// offsets) and aggregation into stats [M][2K][kStatFeatures].
+void host_gen_event_counts(const GenEventParams& g, int64_t base, int64_t M, int64_t* counts);
+int host_gen_events(int K, const GenEventParams& g, int64_t base, const int32_t* rec,
+                    const int64_t* evoff, int64_t M, int32_t* events);
+int64_t host_telemetry(int K, const TelemetryParams& tp);
 int64_t host_levels(int K, const int32_t* rec, int64_t M, int64_t P, int32_t* level);
 int host_rate(int K, bool fp64, const int32_t* rec, float* state, const float* attrs,
               float* first_prior, const RateOut& out, const RateParams& prm);

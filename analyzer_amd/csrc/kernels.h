@@ -8,6 +8,7 @@
 
 #include "common.h"
 #include "gen_core.h"
+#include "telemetry_core.h"
 
 namespace ana {
 
@@ -31,9 +32,19 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s);
 
+// tp.evoff == nullptr: no telemetry; otherwise idle waves aggregate telemetry
+// tiles (K8 fused streaming mode).  ctrl[12] = telemetry tile ticket,
+// ctrl[13] = malformed events.
 int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, float* state,
                 const float* attrs, float* first_prior, const RateOut& out, uint32_t* ctrl,
-                const RateParams& prm, int blocks, hipStream_t s);
+                const RateParams& prm, const TelemetryParams& tp, int blocks, hipStream_t s);
+
+// K8 (telemetry.hip)
+int launch_gen_event_counts(const GenEventParams& g, int64_t base, int64_t M, int64_t* counts,
+                            hipStream_t s);
+int launch_gen_events(int K, const GenEventParams& g, int64_t base, const int32_t* rec,
+                      const int64_t* evoff, int64_t M, int32_t* events, hipStream_t s);
+int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_t s);
 
 }  // namespace ana
 

@@ -199,8 +199,13 @@ class BatchRater:
     # ----------------------------------------------------------------- rate
     def rate(self, roster: Roster, rec: torch.Tensor, K: Optional[int] = None,
              out: Optional[RateResult] = None, first_prior: Optional[torch.Tensor] = None,
-             check: bool = True, schedule: Optional[Schedule] = None) -> RateResult:
-        """Rate every match of ``rec`` in order, updating ``roster`` in place."""
+             check: bool = True, schedule: Optional[Schedule] = None,
+             telemetry=None) -> RateResult:
+        """Rate every match of ``rec`` in order, updating ``roster`` in place.
+
+        ``telemetry`` = (evoff [M+1] int64, events [E,4] int32, stats [M,2K,8] f32):
+        per-participant telemetry is aggregated into ``stats`` in the same launch
+        (K8 fused streaming mode: idle dataflow waves take telemetry tiles)."""
         K = int(K or (rec.shape[1] - 2) // 2)
         M = int(rec.shape[0])
         dev = rec.device
@@ -221,13 +226,20 @@ class BatchRater:
         else:
             link = deps = ctrl = torch.empty(0, dtype=torch.int32)
             epoch = 1
+        if telemetry is None:
+            none = torch.empty(0, dtype=torch.int64, device=dev)
+            telemetry = (none, none.to(torch.int32), none.to(torch.float32))
         native().rate(rec, K, link, deps, roster.state, roster.attrs, fp, out.quality, out.status,
                       out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
                       float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
-                      record, self.blocks, epoch, self.host_fp64)
+                      record, self.blocks, epoch, self.host_fp64, *telemetry)
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out
+
+    def telemetry_errors(self, device) -> int:
+        """Malformed telemetry events seen by the last fused launch (syncs)."""
+        return int(self._buffer(device, "ctrl", 16, torch.int32)[13].item())
 
     def error_flags(self, device) -> torch.Tensor:
         """Device tensor [schedule overflow, timeout, protocol] of the last launch (no sync)."""

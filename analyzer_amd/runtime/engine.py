@@ -65,15 +65,17 @@ class WindowPipeline:
         self._set ^= 1
         return Prepared(rec, sched, ready, used)
 
-    def rate(self, prep: Prepared, out: Optional[RateResult] = None, check: bool = False) -> RateResult:
-        """Rate a prepared window on the main stream (+ DP merge if configured)."""
+    def rate(self, prep: Prepared, out: Optional[RateResult] = None, check: bool = False,
+             telemetry=None) -> RateResult:
+        """Rate a prepared window on the main stream (+ DP merge if configured);
+        ``telemetry`` = (evoff, events, stats) aggregates K8 stats in the same launch."""
         main = torch.cuda.current_stream(self.device) if self.cuda else None
         if prep.ready is not None:
             main.wait_event(prep.ready)
         if self.merger is not None:
             self.merger.begin(self.roster)
         res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
-                              schedule=prep.schedule)
+                              schedule=prep.schedule, telemetry=telemetry)
         if self.cuda:
             done = torch.cuda.Event()
             done.record(main)

@@ -30,6 +30,8 @@ import torch.distributed as dist
 # reference rate: ~354 3v3 matches/s per CPU core for rater.rate_match
 # (measured); the whole-node bound is 8 cores x 354 = 2832/s.
 BASELINE_MATCHES_PER_S = 2832.0
+# 5v5 (config 3): ~264 matches/s per core x 8 cores
+BASELINE_5V5_MATCHES_PER_S = 2112.0
 
 
 def parse(argv=None):
@@ -43,7 +45,19 @@ def parse(argv=None):
     ap.add_argument("--ring", type=int, default=4, help="distinct pre-generated windows per rank")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--check", action="store_true", help="also validate statuses after timing")
-    return ap.parse_args(argv)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4],
+                    help="BASELINE config: 2 = 10M 3v3/GPU (headline), 3 = 12.5M 5v5/GPU (100M at DP=8), "
+                         "4 = streaming: rating + per-event telemetry aggregation")
+    ap.add_argument("--events", default="20,60", help="config 4: min,max telemetry events per match")
+    ap.add_argument("--telemetry-mode", default="fused", choices=["fused", "separate"])
+    args = ap.parse_args(argv)
+    if args.config == 3:
+        args.team_size = 5
+        if args.matches_per_gpu == 10_000_000:
+            args.matches_per_gpu = 12_500_000
+    if args.config == 4:
+        args.ring = min(args.ring, 2)
+    return args
 
 
 def main(argv=None) -> int:
@@ -73,6 +87,14 @@ def main(argv=None) -> int:
                for w in range(n_windows)]
     rater = BatchRater()
     out = RateResult.allocate(M, K, dev)
+    tele = stats = None
+    if args.config == 4:
+        from analyzer_amd.ops.telemetry import TelemetrySpec, aggregate, allocate_stats, make_telemetry
+        lo, hi = (int(x) for x in args.events.split(","))
+        tspec = TelemetrySpec(seed=args.seed + 7, min_events=lo, max_events=hi)
+        tele = [make_telemetry(tspec, windows[w], K, base=(w * world + rank) * M) for w in range(n_windows)]
+        stats = allocate_stats(M, K, dev)
+        n_events = sum(t.num_events for t in tele) / n_windows
     merger = SweepMerger(P, dev) if world > 1 else None
     pipe = WindowPipeline(rater, roster, K, merger=merger)
     err = torch.zeros(3, dtype=torch.int32, device=dev)
@@ -83,7 +105,14 @@ def main(argv=None) -> int:
         # the prepass of window i+1 runs on the side stream while window i is rated
         # (every timed step carries exactly one prepass and one rating)
         prepared[i + 1] = pipe.prepare(windows[(i + 1) % n_windows])
-        pipe.rate(prepared.pop(i), out=out)
+        if tele is None:
+            pipe.rate(prepared.pop(i), out=out)
+        elif args.telemetry_mode == "fused":
+            t = tele[i % n_windows]
+            pipe.rate(prepared.pop(i), out=out, telemetry=(t.evoff, t.events, stats))
+        else:
+            pipe.rate(prepared.pop(i), out=out)
+            aggregate(tele[i % n_windows], K, stats)
         err.bitwise_or_(rater.error_flags(dev))
 
     for i in range(args.warmup):
@@ -114,9 +143,18 @@ def main(argv=None) -> int:
         if rank == 0:
             print("status counts (last window):", counts, file=sys.stderr)
     value = world * M / (ms / 1000.0)
+    metric = "matches/sec rated (whole node), 3v3 TrueSkill, 1M-player roster"
+    extra = {}
+    if args.config == 3:
+        metric = "matches/sec rated (whole node), 5v5 TrueSkill, 1M-player roster, DP sweep merge"
+    if args.config == 4:
+        metric = ("matches/sec rated + telemetry aggregated (whole node), 3v3 TrueSkill, "
+                  "1M-player roster, streaming")
+        extra = {"events_per_match": n_events / M, "events_per_s": world * n_events / (ms / 1000.0),
+                 "telemetry_mode": args.telemetry_mode}
     if rank == 0:
         print(json.dumps({
-            "metric": "matches/sec rated (whole node), 3v3 TrueSkill, 1M-player roster",
+            "metric": metric,
             "value": value,
             "unit": "matches/s",
             "n_gpus": world,
@@ -125,7 +163,8 @@ def main(argv=None) -> int:
             "ms_per_step": ms,
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": value / BASELINE_MATCHES_PER_S,
+            "vs_baseline": value / (BASELINE_5V5_MATCHES_PER_S if args.config == 3
+                                    else BASELINE_MATCHES_PER_S),
             "dtype": "fp32",
             "data": "synthetic (on-device counter RNG stream, random-init 1M-player roster)",
             "config": {
@@ -138,6 +177,8 @@ def main(argv=None) -> int:
                 "team_size": K,
                 "parallelism": "dp%d" % world,
                 "mode": "exact" if world == 1 else "sweep (exact per rank + RCCL posterior merge)",
+                "bench_config": args.config,
+                **extra,
             },
         }), flush=True)
     if world > 1:

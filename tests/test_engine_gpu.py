@@ -133,3 +133,36 @@ def test_sweep_kernels_match_host(gpu_device):
                          start.attrs.to(gpu_device), sd, vst.to(gpu_device), 500.0)
     # fp32 (tau / pi, 1 / sqrt(pi)): device fma contraction vs host rounding
     np.testing.assert_allclose(sd.cpu().numpy(), sh.numpy(), rtol=5e-5, atol=1e-6, equal_nan=True)
+
+
+def test_telemetry_device_generator_and_aggregation(gpu_device):
+    from analyzer_amd.ops.telemetry import TelemetrySpec, aggregate, aggregate_reference, make_telemetry
+
+    K = 3
+    rec = make_stream(StreamSpec(team_size=K, seed=21, p_uneven=0.2), 50000, 4000, K=K)
+    spec = TelemetrySpec(seed=4, min_events=20, max_events=120)
+    th = make_telemetry(spec, rec, K)
+    td = make_telemetry(spec, rec.to(gpu_device), K)
+    assert torch.equal(td.evoff.cpu(), th.evoff) and torch.equal(td.events.cpu(), th.events)
+    sd = aggregate(td, K)
+    np.testing.assert_allclose(sd.cpu().numpy(), aggregate_reference(th, K), rtol=2e-5, atol=0.05)
+
+
+def test_fused_rate_telemetry_on_device(gpu_device):
+    from analyzer_amd.ops.telemetry import (TelemetrySpec, aggregate_reference, allocate_stats,
+                                            make_telemetry)
+
+    K, P, M = 3, 20000, 400000
+    roster = make_roster(RosterSpec(num_players=P, seed=5), device=gpu_device)
+    rec = make_stream(StreamSpec(team_size=K, seed=6), M, P, K=K, device=gpu_device)
+    tel = make_telemetry(TelemetrySpec(seed=8, min_events=10, max_events=60), rec, K)
+    stats = allocate_stats(M, K, gpu_device)
+    a, b = roster.clone(), roster.clone()
+    br = R.BatchRater()
+    ra = br.rate(a, rec, K, telemetry=(tel.evoff, tel.events, stats))
+    assert br.telemetry_errors(gpu_device) == 0
+    rb = R.BatchRater().rate(b, rec, K)
+    assert torch.equal(a.state.nan_to_num(-7), b.state.nan_to_num(-7))
+    assert torch.equal(ra.s_mu.nan_to_num(-7), rb.s_mu.nan_to_num(-7))
+    ref = aggregate_reference(type(tel)(tel.evoff.cpu(), tel.events.cpu()), K)
+    np.testing.assert_allclose(stats.cpu().numpy(), ref, rtol=2e-5, atol=0.05)
