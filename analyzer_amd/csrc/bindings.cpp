@@ -244,6 +244,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   prm.epoch = (int32_t)epoch;
   prm.vst = vst.data_ptr<float>();
   if (const char* e = std::getenv("ANA_RATE_IDLE")) prm.idle_spins = std::atoi(e);  // tuning knob
+  if (const char* e = std::getenv("ANA_RATE_DEBUG")) prm.debug_flags = std::atoi(e);  // experiments
   const ana::TelemetryParams tp = telemetry_params(tele_evoff, tele_events, tele_stats, M, K, dev);
   if (dev.is_cuda()) {
     check(link, "link", torch::kInt32, dev);

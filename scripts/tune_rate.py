@@ -23,7 +23,10 @@ def main():
     ap.add_argument("--blocks", default="128,256,512,1024,2048")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--idle", default="8", help="ANA_RATE_IDLE values (max idle sleep rounds)")
+    ap.add_argument("--debug", default="0", help="ANA_RATE_DEBUG values (experiments)")
     ap.add_argument("--hot", type=float, default=0.0)
+    ap.add_argument("--rated", type=float, default=1.0,
+                    help="fraction of players with stored ratings (1.0 = steady state, no seeding)")
     ap.add_argument("--pattern", default="random", choices=["random", "serial", "disjoint"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
@@ -38,10 +41,13 @@ def main():
     out = RateResult.allocate(M, K, dev)
     results = {}
     for rnd in range(args.rounds):
-        for b, idle in [(int(x), int(y)) for x in args.blocks.split(",") for y in args.idle.split(",")]:
+        for b, idle, dbg in [(int(x), int(y), int(z)) for x in args.blocks.split(",")
+                             for y in args.idle.split(",") for z in args.debug.split(",")]:
             os.environ["ANA_RATE_IDLE"] = str(idle)
-            key = "%d/%d" % (b, idle)
-            roster = make_roster(RosterSpec(num_players=P, seed=1), device=dev)
+            os.environ["ANA_RATE_DEBUG"] = str(dbg)
+            key = "%d/%d/%d" % (b, idle, dbg)
+            roster = make_roster(RosterSpec(num_players=P, seed=1, p_rated=args.rated,
+                                            p_mode_rated=args.rated), device=dev)
             br = BatchRater(blocks=b)
             br.schedule(rec, K, P)
             torch.cuda.synchronize()
