@@ -74,7 +74,8 @@ struct RateParams {
   int32_t epoch;               // 1..255: granule tag word 1 of this launch (word 3 = match)
   const float* vst;            // vst_points[tier + 1], kVstTiers entries (device/host memory)
   int32_t idle_spins;          // dataflow: max s_sleep(2) rounds of an idle wave (0 = default)
-  int32_t debug_flags;         // experiments only (ANA_RATE_DEBUG): 1 skip attrs, 2 skip slot outputs
+  int32_t debug_flags;         // experiments only (ANA_RATE_DEBUG): 2 skip slot outputs
+  int32_t spec;                // dataflow: speculative one-dependency matches per wave iteration
 };
 
 // Per-match outputs, structure-of-arrays.  Per-slot arrays are [M][2K]; the

@@ -202,30 +202,43 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
 
     // ---------------------------------------------- (3) oldest ready matches -> groups
+    // then, in spare groups, up to prm.spec matches still waiting on ONE
+    // predecessor: their loads race the predecessor's stores and the tag check
+    // accepts them if the stores won (saves the poll round trip on the hop)
     int my_h = -1, my_bit = 0, nassigned = 0;
+    auto assign = [&](uint64_t (&sets)[kHeld], int limit) {
 #pragma unroll
-    for (int pass = 0; pass < kHeld; ++pass) {
-      int best = -1;
-      int64_t bb = 0;
+      for (int pass = 0; pass < kHeld; ++pass) {
+        int best = -1;
+        int64_t bb = 0;
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h)
-        if (ready[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
-      if (best < 0 || nassigned >= NG) break;
-      uint64_t rdy = 0;
+        for (int h = 0; h < kHeld; ++h)
+          if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
+        if (best < 0 || nassigned >= limit) break;
+        uint64_t rdy = 0;
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h) if (h == best) rdy = ready[h];
-      const int cnt = __popcll(rdy);
-      const int take = cnt < NG - nassigned ? cnt : NG - nassigned;
-      if (g >= nassigned && g < nassigned + take) {
-        my_h = best;
-        my_bit = nth_set_bit(rdy, g - nassigned);
+        for (int h = 0; h < kHeld; ++h) if (h == best) rdy = sets[h];
+        const int cnt = __popcll(rdy);
+        const int take = cnt < limit - nassigned ? cnt : limit - nassigned;
+        if (g >= nassigned && g < nassigned + take) {
+          my_h = best;
+          my_bit = nth_set_bit(rdy, g - nassigned);
+        }
+        uint64_t taken = rdy;
+        if (take < cnt) taken &= (1ull << nth_set_bit(rdy, take)) - 1ull;
+#pragma unroll
+        for (int h = 0; h < kHeld; ++h)
+          if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
+        nassigned += take;
       }
-      uint64_t taken = rdy;
-      if (take < cnt) taken &= (1ull << nth_set_bit(rdy, take)) - 1ull;
+    };
+    assign(ready, NG);
+    if (prm.spec > 0 && nassigned < NG) {
+      uint64_t cand[kHeld];
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h)
-        if (h == best) { pend[h] &= ~taken; ready[h] = 0ull; }
-      nassigned += take;
+      for (int h = 0; h < kHeld; ++h) cand[h] = __ballot(dval[h] == 1u) & pend[h];
+      const int lim = nassigned + prm.spec < NG ? nassigned + prm.spec : NG;
+      assign(cand, lim);
     }
     const bool worked = nassigned > 0;
 

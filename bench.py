@@ -68,10 +68,18 @@ def main(argv=None) -> int:
     if world != args.gpus:
         print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world),
               file=sys.stderr)
+    # one rank per GPU; ANA_DIST_BACKEND=gloo lets several ranks share one GPU to
+    # rehearse the multi-process path on a 1-GPU box (production: nccl = RCCL)
+    backend = os.environ.get("ANA_DIST_BACKEND", "nccl")
+    ngpu = torch.cuda.device_count()
+    local = local % ngpu if backend != "nccl" and ngpu else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from analyzer_amd.ops.rate import BatchRater, RateResult, NOT_PROCESSED
     from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--idle", default="8", help="ANA_RATE_IDLE values (max idle sleep rounds)")
     ap.add_argument("--debug", default="0", help="ANA_RATE_DEBUG values (experiments)")
+    ap.add_argument("--spec", default="0", help="ANA_RATE_SPEC values (speculative matches/iteration)")
     ap.add_argument("--hot", type=float, default=0.0)
     ap.add_argument("--rated", type=float, default=1.0,
                     help="fraction of players with stored ratings (1.0 = steady state, no seeding)")
@@ -41,11 +42,13 @@ def main():
     out = RateResult.allocate(M, K, dev)
     results = {}
     for rnd in range(args.rounds):
-        for b, idle, dbg in [(int(x), int(y), int(z)) for x in args.blocks.split(",")
-                             for y in args.idle.split(",") for z in args.debug.split(",")]:
+        for b, idle, dbg, sp in [(int(x), int(y), int(z), int(w)) for x in args.blocks.split(",")
+                                 for y in args.idle.split(",") for z in args.debug.split(",")
+                                 for w in args.spec.split(",")]:
             os.environ["ANA_RATE_IDLE"] = str(idle)
             os.environ["ANA_RATE_DEBUG"] = str(dbg)
-            key = "%d/%d/%d" % (b, idle, dbg)
+            os.environ["ANA_RATE_SPEC"] = str(sp)
+            key = "b%d/i%d/d%d/s%d" % (b, idle, dbg, sp)
             roster = make_roster(RosterSpec(num_players=P, seed=1, p_rated=args.rated,
                                             p_mode_rated=args.rated), device=dev)
             br = BatchRater(blocks=b)
