@@ -69,8 +69,11 @@ class WorkerConfig:
     sew_queue: str = "sew"
     # new: which rating path processes a batch (python | native)
     engine: str = "python"
-    # new: max matches quarantined per batch before the whole batch is failed
+    # new: quarantine only the failing matches of a batch (false: fail the whole batch)
     quarantine: bool = True
+    # new: aggregate per-participant telemetry (participant_stats) in the rating launch
+    dotelemetry: bool = False
+    telemetry_events: str = "100,300"
 
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "WorkerConfig":
@@ -89,6 +92,8 @@ class WorkerConfig:
             sew_queue=_env(env, "SEW_QUEUE") or "sew",
             engine=_env(env, "ENGINE") or "python",
             quarantine=(env.get("QUARANTINE") or "true") == "true",
+            dotelemetry=env.get("DOTELEMETRY") == "true",
+            telemetry_events=_env(env, "TELEMETRY_EVENTS") or "100,300",
         )
 
     @property

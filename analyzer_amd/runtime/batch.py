@@ -26,7 +26,8 @@ import torch
 
 from ..config import MODES, TRACK_COLUMNS
 from ..ops import rate as R
-from .objects import Match, Player, encode_matches, roster_from_players
+from .objects import (STAT_COLUMNS, Match, ParticipantStats, Player, encode_matches,
+                      roster_from_players)
 
 MAX_TEAM = 5  # kernel instantiations: K = 1..5
 
@@ -56,8 +57,12 @@ class ObjectBatchRater:
     def supports(self, matches: Sequence[Match]) -> bool:
         return team_size(matches) <= MAX_TEAM
 
-    def rate(self, matches: Sequence[Match]) -> List[int]:
-        """Rate ``matches`` (already in chronological order); returns the status per match."""
+    def rate(self, matches: Sequence[Match], telemetry=None) -> List[int]:
+        """Rate ``matches`` (already in chronological order); returns the status per match.
+
+        ``telemetry``: a ``TelemetrySpec`` -- synthetic per-event telemetry of the
+        batch is aggregated in the same launch (K8 fused streaming mode) and
+        written to ``participant.participant_stats[0]``."""
         if not matches:
             return []
         K = team_size(matches)
@@ -74,9 +79,26 @@ class ObjectBatchRater:
         # (a batch without participants still needs one roster row to launch)
         roster = roster_from_players(players or [Player("")], device=self.device)
         rec = encode_matches(matches, index, K, device=self.device)
-        res = self.rater.rate(roster, rec, K)
+        tele = stats = None
+        if telemetry is not None:
+            from ..ops.telemetry import allocate_stats, make_telemetry
+            tel = make_telemetry(telemetry, rec, K)
+            stats = allocate_stats(len(matches), K, self.device)
+            tele = (tel.evoff, tel.events, stats)
+        res = self.rater.rate(roster, rec, K, telemetry=tele)
         self._write_back(matches, res, roster, players, K)
+        if stats is not None:
+            self._write_stats(matches, stats, K)
         return [int(s) for s in res.status.cpu().tolist()]
+
+    @staticmethod
+    def _write_stats(matches, stats: torch.Tensor, K: int) -> None:
+        st = stats.cpu().double().numpy()
+        for i, m in enumerate(matches):
+            for ri, r in enumerate(list(m.rosters)[:2]):
+                for pos, p in enumerate(r.participants[:K]):
+                    vals = dict(zip(STAT_COLUMNS, (float(v) for v in st[i, ri * K + pos])))
+                    p.participant_stats = [ParticipantStats(p.api_id, **vals)]
 
     def _write_back(self, matches, res: R.RateResult, roster, players, K: int) -> None:
         st = res.status.cpu().numpy()

@@ -47,6 +47,19 @@ class ParticipantItems:
             setattr(self, col + "_sigma", None)
 
 
+STAT_COLUMNS = ("kills", "deaths", "assists", "damage", "gold", "farm", "healing", "events")
+
+
+class ParticipantStats:
+    """``participant_stats`` row (mapped but never filled by the reference,
+    worker.py:75-78; here filled by the K8 telemetry aggregation)."""
+
+    def __init__(self, api_id: str = "", **values):
+        self.api_id = api_id
+        for c in STAT_COLUMNS:
+            setattr(self, c, values.get(c))
+
+
 class Participant:
     def __init__(self, player: Player, api_id: str = "", went_afk=0, skill_tier=None,
                  items: Optional[ParticipantItems] = None):
@@ -59,6 +72,7 @@ class Participant:
         self.trueskill_delta = None
         self.player = [player]
         self.participant_items = [items or ParticipantItems(api_id)]
+        self.participant_stats: List[ParticipantStats] = []
 
 
 class Roster:

@@ -30,7 +30,7 @@ from dataclasses import dataclass
 from typing import Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 from ..config import TRACK_COLUMNS
-from .objects import Match, Participant, ParticipantItems, Player, Roster
+from .objects import STAT_COLUMNS, Match, Participant, ParticipantItems, Player, Roster
 
 PLAYER_RATING_COLS = tuple(c + s for c in TRACK_COLUMNS for s in ("_mu", "_sigma"))
 ITEM_RATING_COLS = tuple(c + s for c in TRACK_COLUMNS[1:] for s in ("_mu", "_sigma"))
@@ -65,8 +65,8 @@ SCHEMA = [
     "participant_api_id TEXT, any_afk INTEGER, %s)" % ", ".join("%s REAL" % _q(c) for c in ITEM_RATING_COLS),
     "CREATE INDEX IF NOT EXISTS items_participant ON participant_items(participant_api_id)",
     "CREATE TABLE IF NOT EXISTS participant_stats (api_id TEXT PRIMARY KEY, "
-    "participant_api_id TEXT, kills INTEGER, deaths INTEGER, assists INTEGER, "
-    "farm REAL, gold REAL, damage REAL, events INTEGER)",
+    "participant_api_id TEXT, kills REAL, deaths REAL, assists REAL, damage REAL, "
+    "gold REAL, farm REAL, healing REAL, events REAL)",
     "CREATE TABLE IF NOT EXISTS asset (api_id TEXT PRIMARY KEY, match_api_id TEXT, url TEXT)",
     "CREATE INDEX IF NOT EXISTS asset_match ON asset(match_api_id)",
 ]
@@ -162,6 +162,14 @@ class MemorySession(_SessionBase):
 
     def assets(self, match_api_id: str) -> List[Asset]:
         return list(self.store.assets.get(match_api_id, ()))
+
+    def participant_stats(self, participant_api_id: str):
+        for m in self.store.matches.values():
+            for p in m.participants:
+                if p.api_id == participant_api_id and p.participant_stats:
+                    ps = p.participant_stats[0]
+                    return {c: getattr(ps, c) for c in STAT_COLUMNS}
+        return None
 
 
 class MemoryStore:
@@ -274,6 +282,10 @@ class SqliteSession(_SessionBase):
         for m, _ in self._match_snaps.values():
             c.execute("UPDATE match SET trueskill_quality=? WHERE api_id=?", (m.trueskill_quality, m.api_id))
             for p in m.participants:
+                for ps in getattr(p, "participant_stats", None) or []:
+                    c.execute("INSERT OR REPLACE INTO participant_stats VALUES (?, ?, %s)"
+                              % ", ".join("?" * len(STAT_COLUMNS)),
+                              [ps.api_id or p.api_id, p.api_id] + [getattr(ps, x) for x in STAT_COLUMNS])
                 c.execute("UPDATE participant SET trueskill_mu=?, trueskill_sigma=?, trueskill_delta=? "
                           "WHERE api_id=?", (p.trueskill_mu, p.trueskill_sigma, p.trueskill_delta, p.api_id))
                 it = p.participant_items[0]
@@ -292,6 +304,11 @@ class SqliteSession(_SessionBase):
     def rollback(self) -> None:
         super().rollback()
         self.conn.rollback()
+
+    def participant_stats(self, participant_api_id: str):
+        row = self.conn.execute("SELECT %s FROM participant_stats WHERE participant_api_id=?"
+                                % ", ".join(STAT_COLUMNS), (participant_api_id,)).fetchone()
+        return None if row is None else dict(zip(STAT_COLUMNS, row))
 
     def assets(self, match_api_id: str) -> List[Asset]:
         return [Asset(u, m) for u, m in self.conn.execute(

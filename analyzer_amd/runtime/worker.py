@@ -30,7 +30,11 @@ Deliberate, documented differences:
 * a delivery without headers is simply not notified (the reference raises
   AttributeError there and kills the consumer, worker.py:132);
 * ``SEW_QUEUE`` is declared when ``DOSEWMATCH`` is on (the reference forwards to
-  a queue it never declares, which a broker silently drops).
+  a queue it never declares, which a broker silently drops);
+* ``DOTELEMETRY=true`` (with ``ENGINE=native``) aggregates per-event telemetry
+  into ``participant_stats`` in the same launch as the rating (K8 fused mode,
+  BASELINE config 4).  Telemetry is synthetic here: the reference only forwards
+  asset URLs (worker.py:148-161) and this image has no network to fetch them.
 
 Per-batch counters (matches rated/afk/invalid/unsupported/quarantined, timing)
 are kept in ``stats`` and logged as one JSON line per batch (SURVEY §5 metrics).
@@ -224,7 +228,12 @@ class Worker:
     def _rate_native(self, session, matches, counts) -> List[str]:
         from ..ops import rate as R
 
-        status = self._batched().rate(matches)
+        spec = None
+        if self.cfg.dotelemetry:
+            from ..ops.telemetry import TelemetrySpec
+            lo, hi = (int(x) for x in self.cfg.telemetry_events.split(","))
+            spec = TelemetrySpec(seed=self.stats.batches + 1, min_events=lo, max_events=hi)
+        status = self._batched().rate(matches, telemetry=spec)
         bad = []
         for m, s in zip(matches, status):
             name = R.STATUS_NAMES.get(s, str(s))

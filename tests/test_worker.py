@@ -252,3 +252,24 @@ def test_config1_worker_cli_1k_matches(engine):
     line = [l for l in out.stdout.splitlines() if l.startswith("{\"matches\"")][-1]
     res = json.loads(line)
     assert res["matches"] == 1000 and res["acked"] == 1000 and res["failed_batches"] == 0
+
+
+def test_streaming_worker_telemetry_into_participant_stats(tmp_path):
+    """BASELINE config 4 on the worker path: ENGINE=native + DOTELEMETRY fills
+    participant_stats in the rating launch and persists it."""
+    store = open_store("sqlite:///" + str(tmp_path / "t.db"))
+    w, matches, clock = make_worker(n=10, players=20, batch=10, engine="native", store=store,
+                                    dotelemetry=True, telemetry_events="5,9")
+    publish(w.channel, "analyze", [m.api_id for m in matches])
+    w.start_consuming()
+    assert w.stats.acked == 10
+    with store.session() as s:
+        part = next(iter(s.load_matches([matches[0].api_id]))).participants[0]
+        row = s.participant_stats(part.api_id)
+    assert row is not None and row["events"] >= 0
+    total = 0.0
+    with store.session() as s:
+        for m in s.load_matches([x.api_id for x in matches]):
+            for p in m.participants:
+                total += s.participant_stats(p.api_id)["events"]
+    assert 5 * 10 <= total <= 9 * 10  # every event lands on exactly one participant
