@@ -32,7 +32,8 @@
 //
 // Claims are monotone per ticket shard and every claimed match is held by a
 // running wave, so the oldest unfinished match is always ready: no deadlock
-// whatever the residency.  Spins back off and give up after 5 s.
+// whatever the residency.  Spins back off; the watchdog gives up after 5 s
+// without any chunk retiring anywhere on the GPU.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -46,6 +47,7 @@ typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 constexpr uint64_t kTimeoutTicks = 500000000ull;  // 5 s of the 100 MHz s_memrealtime clock
+constexpr uint64_t kProgressTicks = 50000000ull;  // re-read the progress counter every 0.5 s
 constexpr int kHeads = 8;                          // ticket shards
 constexpr int kChunk = 64;                         // matches per ticket = one per lane
 constexpr int kHeld = 4;                           // chunks a wave keeps in flight
@@ -133,7 +135,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(state, 0, (int)(P * kRowFloats * 4), 0x00020000);
   const int head = blockIdx.x % kHeads;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  // watchdog: give up only after kTimeoutTicks without ANY chunk retiring GPU-wide
+  // (ctrl[3] counts retired chunks), so long dependency chains never trip it
+  uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint32_t seen_progress = 0;
 
   int64_t cbase[kHeld];   // wave-uniform: first match of each held chunk, -1 = free slot
   uint64_t pend[kHeld];   // wave-uniform: stateful matches not yet handed to a group
@@ -350,8 +355,19 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     const bool fresh =
         !own || ((!(lk0 & kLinkHasPred) || (gs.y == epoch && (uint32_t)gs.w == (uint32_t)m)) &&
                  (!(lk0 & kLinkHasPredMode) || (gm.y == epoch && (uint32_t)gm.w == (uint32_t)m)));
+    // race detector: a granule of this launch tagged for a LATER reader means a
+    // successor wrote before this match read -- the ordering protocol broke
+    const bool overtaken =
+        own && (((lk0 & kLinkHasPred) && gs.y == epoch && (uint32_t)gs.w != kNoMatch &&
+                 (uint32_t)gs.w > (uint32_t)m) ||
+                ((lk0 & kLinkHasPredMode) && gm.y == epoch && (uint32_t)gm.w != kNoMatch &&
+                 (uint32_t)gm.w > (uint32_t)m));
+    if (__ballot(overtaken) != 0ull && lane == 0) atomicOr(&ctrl[2], 1u);
     const uint64_t stale_lanes = __ballot(!fresh);
     if (stale_lanes) {
+      if (lane == 0)  // diagnostics: stale reads retried (ctrl[14])
+        __hip_atomic_fetch_add((gu32*)&ctrl[14], (unsigned)__popcll(stale_lanes), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
       const bool gstale = (stale_lanes & gmask) != 0ull;
 #pragma unroll
       for (int h = 0; h < kHeld; ++h) {
@@ -451,9 +467,17 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
 
     // ---------------------------------------------- (11) retire finished chunks
+    {
+      uint32_t retired = 0;
 #pragma unroll
-    for (int h = 0; h < kHeld; ++h)
-      if (cbase[h] >= 0 && pend[h] == 0ull) cbase[h] = -1;
+      for (int h = 0; h < kHeld; ++h)
+        if (cbase[h] >= 0 && pend[h] == 0ull) {
+          cbase[h] = -1;
+          ++retired;
+        }
+      if (retired && lane == 0)
+        __hip_atomic_fetch_add((gu32*)&ctrl[3], retired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 
     // ---------------------------------------------- (12) done?
     bool held = false;
@@ -472,7 +496,15 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     if (worked || staging >= 0) {
       spins = 0;
     } else {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (now - t0 > kProgressTicks) {
+        const uint32_t p = __hip_atomic_load((gu32*)&ctrl[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (p != seen_progress) {
+          seen_progress = p;
+          t0 = now;
+        }
+      }
+      if (now - t0 > kTimeoutTicks) {
         if (lane == 0) atomicOr(&ctrl[1], 1u);
 #pragma unroll
         for (int h = 0; h < kHeld; ++h)
@@ -498,9 +530,9 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
                 const float* attrs, float* first_prior, const RateOut& out, uint32_t* ctrl,
                 const RateParams& prm, const TelemetryParams& tp, int blocks, hipStream_t s) {
   const int64_t M = prm.num_matches;
-  // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] spare, [4..11] tickets,
-  // [12] telemetry tile ticket, [13] malformed telemetry events
-  if (hipMemsetAsync(ctrl + 1, 0, 13 * 4, s) != hipSuccess) return (int)hipGetLastError();
+  // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] retired chunks, [4..11] tickets,
+  // [12] telemetry tile ticket, [13] malformed telemetry events, [14] stale reads retried
+  if (hipMemsetAsync(ctrl + 1, 0, 14 * 4, s) != hipSuccess) return (int)hipGetLastError();
   if (M <= 0) return 0;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
   if (prm.epoch < 1 || prm.epoch > 255) return (int)hipErrorInvalidValue;

@@ -237,6 +237,11 @@ class BatchRater:
             self.check_errors(dev)
         return out
 
+    def stale_retries(self, device) -> int:
+        """Granule reads of the last launch that found their predecessor's write not
+        yet landed and were retried (diagnostics; syncs)."""
+        return int(self._buffer(device, "ctrl", 16, torch.int32)[14].item())
+
     def telemetry_errors(self, device) -> int:
         """Malformed telemetry events seen by the last fused launch (syncs)."""
         return int(self._buffer(device, "ctrl", 16, torch.int32)[13].item())
@@ -252,7 +257,8 @@ class BatchRater:
         if int(flags[1]):
             raise NativeRateError("dataflow rating timed out (a dependency never resolved)")
         if int(flags[2]):
-            raise NativeRateError("dataflow protocol violation (a tag overtook its slot)")
+            raise NativeRateError("dataflow race detected: a player's granule was written by a "
+                                  "later match before an earlier one read it")
 
 
 def rate_stream(roster: Roster, rec: torch.Tensor, K: Optional[int] = None,

@@ -62,9 +62,10 @@ def main():
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             br.check_errors(dev)
+            stale = br.stale_retries(dev)
             results.setdefault(key, []).append(((t1 - t0) * 1e3, (t2 - t1) * 1e3))
-            print("round %d blocks/idle %9s schedule %7.2f ms rate %8.2f ms" % (rnd, key, (t1 - t0) * 1e3,
-                                                                          (t2 - t1) * 1e3), flush=True)
+            print("round %d %s schedule %7.2f ms rate %8.2f ms stale retries %d"
+                  % (rnd, key, (t1 - t0) * 1e3, (t2 - t1) * 1e3, stale), flush=True)
     summary = {b: {"schedule_ms_min": min(x[0] for x in v), "rate_ms_min": min(x[1] for x in v),
                    "rate_ms_median": sorted(x[1] for x in v)[len(v) // 2]} for b, v in results.items()}
     print(json.dumps({"pattern": args.pattern, "players": P, "matches": M, "team_size": K, "hot": args.hot,
