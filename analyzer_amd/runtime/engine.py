@@ -21,6 +21,7 @@ from typing import Callable, Iterable, Iterator, List, Optional
 import torch
 
 from ..ops.rate import BatchRater, RateResult, Roster, Schedule
+from ..utils.trace import trace_range
 
 
 @dataclass
@@ -54,7 +55,7 @@ class WindowPipeline:
         main = torch.cuda.current_stream(self.device)
         produced = torch.cuda.Event()
         produced.record(main)  # rec was produced on the main stream
-        with torch.cuda.stream(self.side):
+        with torch.cuda.stream(self.side), trace_range("schedule", window=self.windows_rated + 1):
             self.side.wait_event(produced)
             if self._free[self._set] is not None:  # previous user of this buffer set is done
                 self.side.wait_event(self._free[self._set])
@@ -74,15 +75,17 @@ class WindowPipeline:
             main.wait_event(prep.ready)
         if self.merger is not None:
             self.merger.begin(self.roster)
-        res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
-                              schedule=prep.schedule, telemetry=telemetry)
+        with trace_range("rate", window=self.windows_rated, matches=int(prep.rec.shape[0])):
+            res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
+                                  schedule=prep.schedule, telemetry=telemetry)
         if self.cuda:
             done = torch.cuda.Event()
             done.record(main)
             # the buffer set of this schedule is free once this launch finished
             self._free[prep.buffer_set] = done
         if self.merger is not None:
-            self.merger.merge(self.roster)
+            with trace_range("merge", window=self.windows_rated):
+                self.merger.merge(self.roster)
         self.windows_rated += 1
         return res
 

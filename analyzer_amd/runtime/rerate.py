@@ -38,6 +38,7 @@ from ..ops import rate as R
 from ..ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
 from ..parallel.comm import broadcast_roster, init_from_env, reduce_counts, world
 from ..parallel.sweep import SweepMerger
+from ..utils.trace import trace_range
 from .checkpoint import CheckpointManager
 from .engine import WindowPipeline
 
@@ -121,9 +122,10 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
         rated += M
         if on_window is not None:
             on_window(g, res)
-        if rank == 0:
-            ck.maybe_save(g + 1, roster, {"spec": asdict(spec), "world": size,
-                                          "next_offset": window_slice(spec, g + 1, 0, size)[0]})
+        if rank == 0 and ck.due(g + 1):
+            with trace_range("checkpoint", window=g + 1):
+                ck.maybe_save(g + 1, roster, {"spec": asdict(spec), "world": size,
+                                              "next_offset": window_slice(spec, g + 1, 0, size)[0]})
         if fault_kill_after is not None and g + 1 >= fault_kill_after:
             if dev.type == "cuda":
                 torch.cuda.synchronize()

@@ -49,6 +49,7 @@ from typing import Callable, Dict, List, Optional, Tuple
 from ..config import RaterConfig, WorkerConfig
 from ..models.match_rater import MatchRater
 from ..utils.log import get_logger
+from ..utils.trace import trace_range
 from . import broker as B
 from .store import open_store
 
@@ -182,12 +183,15 @@ class Worker:
         quarantined: List[str] = []
         counts: Dict[str, int] = {}
         try:
-            matches = list(session.load_matches(ids, self.cfg.chunksize))
-            if self.cfg.engine == "native" and self._batched().supports(matches):
-                quarantined = self._rate_native(session, matches, counts)
-            else:
-                quarantined = self._rate_python(session, matches, counts)
-            session.commit()
+            with trace_range("load", ids=len(ids)):
+                matches = list(session.load_matches(ids, self.cfg.chunksize))
+            with trace_range("rate", matches=len(matches), engine=self.cfg.engine):
+                if self.cfg.engine == "native" and self._batched().supports(matches):
+                    quarantined = self._rate_native(session, matches, counts)
+                else:
+                    quarantined = self._rate_python(session, matches, counts)
+            with trace_range("commit"):
+                session.commit()
         except Exception:
             session.rollback()
             raise
