@@ -329,7 +329,8 @@ void check_rows(const Tensor& t, const char* name, int64_t P, int64_t cols, cons
   TORCH_CHECK(t.dim() == 2 && t.size(0) == P && t.size(1) == cols, name, " must be [P, ", cols, "]");
 }
 
-void sweep_delta(Tensor s0, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma, Tensor buf) {
+void sweep_delta(Tensor s0, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma, bool scaled,
+                 Tensor buf) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
   check_rows(s0, "s0", P, ana::kRowFloats, dev);
@@ -341,15 +342,16 @@ void sweep_delta(Tensor s0, Tensor s, Tensor attrs, Tensor vst, double unknown_s
   if (dev.is_cuda()) {
     check_hip(ana::launch_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(),
                                       attrs.data_ptr<float>(), vst.data_ptr<float>(),
-                                      (float)unknown_sigma, buf.data_ptr<float>(), P, stream_of(s)),
-              "sweep_delta");
+                                      (float)unknown_sigma, scaled ? 1 : 0, buf.data_ptr<float>(), P,
+                                      stream_of(s)), "sweep_delta");
   } else {
     ana::host_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(), attrs.data_ptr<float>(),
-                          vst.data_ptr<float>(), (float)unknown_sigma, buf.data_ptr<float>(), P);
+                          vst.data_ptr<float>(), (float)unknown_sigma, scaled, buf.data_ptr<float>(), P);
   }
 }
 
-void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor vst, double unknown_sigma) {
+void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor vst, double unknown_sigma,
+                 bool scaled) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
   check_rows(s0, "s0", P, ana::kRowFloats, dev);
@@ -361,11 +363,11 @@ void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor vst, doub
   if (dev.is_cuda()) {
     check_hip(ana::launch_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(),
                                       attrs.data_ptr<float>(), s.data_ptr<float>(),
-                                      vst.data_ptr<float>(), (float)unknown_sigma, P,
+                                      vst.data_ptr<float>(), (float)unknown_sigma, scaled ? 1 : 0, P,
                                       stream_of(s)), "sweep_apply");
   } else {
     ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
-                          s.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, P);
+                          s.data_ptr<float>(), scaled, vst.data_ptr<float>(), (float)unknown_sigma, P);
   }
 }
 

@@ -50,7 +50,7 @@ int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_
 
 namespace ana {
 int launch_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
-                       float unknown_sigma, float* buf, int64_t P, hipStream_t st);
+                       float unknown_sigma, int scaled, float* buf, int64_t P, hipStream_t st);
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,
-                       const float* vst, float unknown_sigma, int64_t P, hipStream_t st);
+                       const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st);
 }  // namespace ana

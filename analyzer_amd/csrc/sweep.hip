@@ -38,7 +38,8 @@ __device__ __forceinline__ void load_row(const float4* __restrict__ src, int64_t
 
 __global__ void sweep_delta_kernel(const float4* __restrict__ s0, const float4* __restrict__ s,
                                    const float4* __restrict__ attrs, const float* __restrict__ vst,
-                                   float unknown_sigma, float4* __restrict__ buf, int64_t P) {
+                                   float unknown_sigma, int scaled, float4* __restrict__ buf,
+                                   int64_t P) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   float a[kRowFloats], b[kRowFloats], o[16];
@@ -46,7 +47,7 @@ __global__ void sweep_delta_kernel(const float4* __restrict__ s0, const float4* 
   load_row(s, p, b);
   const float4 at = attrs[p];
   const float attr[4] = {at.x, at.y, at.z, at.w};
-  sweep_delta_player(a, b, attr, vst, unknown_sigma, o);
+  sweep_delta_player(a, b, attr, vst, unknown_sigma, scaled != 0, o);
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     buf[p * 4 + k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
@@ -54,7 +55,8 @@ __global__ void sweep_delta_kernel(const float4* __restrict__ s0, const float4* 
 
 __global__ void sweep_apply_kernel(const float4* __restrict__ s0, const float4* __restrict__ buf,
                                    const float4* __restrict__ attrs, float4* __restrict__ s,
-                                   const float* __restrict__ vst, float unknown_sigma, int64_t P) {
+                                   const float* __restrict__ vst, float unknown_sigma, int scaled,
+                                   int64_t P) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
   float a[kRowFloats], d[16], o[kRowFloats];
@@ -66,29 +68,29 @@ __global__ void sweep_apply_kernel(const float4* __restrict__ s0, const float4* 
   }
   const float4 at = attrs[p];
   const float attr[4] = {at.x, at.y, at.z, at.w};
-  sweep_apply_player(a, d, attr, vst, unknown_sigma, o);
+  sweep_apply_player(a, d, attr, vst, unknown_sigma, scaled != 0, o);
 #pragma unroll
   for (int k = 0; k < kRowVec; ++k)
     s[p * kRowVec + k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
 }
 
 int launch_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
-                       float unknown_sigma, float* buf, int64_t P, hipStream_t st) {
+                       float unknown_sigma, int scaled, float* buf, int64_t P, hipStream_t st) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(sweep_delta_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(s0), reinterpret_cast<const float4*>(s),
-                     reinterpret_cast<const float4*>(attrs), vst, unknown_sigma,
+                     reinterpret_cast<const float4*>(attrs), vst, unknown_sigma, scaled,
                      reinterpret_cast<float4*>(buf), P);
   return (int)hipGetLastError();
 }
 
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,
-                       const float* vst, float unknown_sigma, int64_t P, hipStream_t st) {
+                       const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(sweep_apply_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(s0), reinterpret_cast<const float4*>(buf),
                      reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s), vst,
-                     unknown_sigma, P);
+                     unknown_sigma, scaled, P);
   return (int)hipGetLastError();
 }
 

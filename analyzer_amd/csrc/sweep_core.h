@@ -37,12 +37,18 @@ ANA_HD bool track_base(const float* a, int t, bool seeded, float seed_mu, float 
   return seeded;
 }
 
+// Message encodings (both linear, so the all-reduce SUM stays exact in algebra):
+//  raw    (d_pi, d_tau)
+//  scaled (d_pi / pi_b, (d_tau - mu_b d_pi) / pi_b): dimensionless precision ratio and
+//         a rating-point-sized mean shift -- small, well-conditioned numbers that
+//         survive an fp16 / bf16 all-reduce (COMM_DTYPE), decoded against the same base.
+//
 // a: window-start row, b: row after the local window, attr/vst/unknown_sigma:
-// seed inputs.  o: 16 floats = (d_pi, d_tau) per track + touch fields for
-// tracks that were NULL at window start and are rated now (base-16 counters,
-// exact in fp32 for <= 15 ranks).
+// seed inputs.  o: 16 floats = message per track + touch fields for tracks
+// that were NULL at window start and are rated now (base-16 counters, exact in
+// fp32 for <= 15 ranks).
 ANA_HD void sweep_delta_player(const float* a, const float* b, const float* attr, const float* vst,
-                               float unknown_sigma, float* o) {
+                               float unknown_sigma, bool scaled, float* o) {
   float seed_mu = NAN, seed_sig = NAN;
   const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
   float touch_lo = 0.f, touch_hi = 0.f;
@@ -57,6 +63,10 @@ ANA_HD void sweep_delta_player(const float* a, const float* b, const float* attr
       nat_params(bm, bs, p0, t0);
       dp = p1 - p0;
       dt = t1 - t0;
+      if (scaled) {
+        dt = (dt - bm * dp) / p0;
+        dp = dp / p0;
+      }
     }
     if (mu0 != mu0 && mu == mu) {
       if (t < 4) touch_lo += (float)(1 << (4 * t));
@@ -72,7 +82,7 @@ ANA_HD void sweep_delta_player(const float* a, const float* b, const float* attr
 // a: window-start row, d: all-reduced messages, attr: player attributes,
 // o: merged row (tags reset to 0; spare floats copied).
 ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr,
-                               const float* vst, float unknown_sigma, float* o) {
+                               const float* vst, float unknown_sigma, bool scaled, float* o) {
   float seed_mu = NAN, seed_sig = NAN;
   const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
   const unsigned lo = (unsigned)d[14], hi = (unsigned)d[15];
@@ -82,13 +92,20 @@ ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr
     float mu = mu0, sg = sg0, bm, bs;
     const bool live = mu0 == mu0 ? (d[2 * t] != 0.f || d[2 * t + 1] != 0.f) : touched != 0u;
     if (live && track_base(a, t, seeded, seed_mu, seed_sig, bm, bs)) {
-      float pb, tb;
-      nat_params(bm, bs, pb, tb);
-      float pi = pb + d[2 * t];
-      const float tau = tb + d[2 * t + 1];
-      pi = pi > 1e-12f ? pi : 1e-12f;  // merged precision never below "no information"
-      mu = tau / pi;
-      sg = 1.f / sqrtf(pi);
+      if (scaled) {  // pi = pi_b (1 + sum r_pi), mu = mu_b + sum r_tau / (1 + sum r_pi)
+        float ratio = 1.f + d[2 * t];
+        ratio = ratio > 1e-6f ? ratio : 1e-6f;
+        mu = bm + d[2 * t + 1] / ratio;
+        sg = bs / sqrtf(ratio);
+      } else {
+        float pb, tb;
+        nat_params(bm, bs, pb, tb);
+        float pi = pb + d[2 * t];
+        const float tau = tb + d[2 * t + 1];
+        pi = pi > 1e-12f ? pi : 1e-12f;  // merged precision never below "no information"
+        mu = tau / pi;
+        sg = 1.f / sqrtf(pi);
+      }
     }
     o[4 * t] = mu;
     o[4 * t + 1] = 0.f;

@@ -27,6 +27,7 @@ from ..models.tiers import vst_table
 from ..ops.native import native
 
 MAX_RANKS = 15  # touch counts are base-16 fields in fp32 (see csrc/sweep_core.h)
+COMM_DTYPES = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
 
 
 class SweepMerger:
@@ -39,14 +40,18 @@ class SweepMerger:
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         if self.world > MAX_RANKS:
             raise ValueError("sweep merge supports at most %d ranks per group" % MAX_RANKS)
-        if comm_dtype != "fp32":
-            raise ValueError("only fp32 merge messages are supported (touch counts are exact "
-                             "integers in the message buffer)")
+        if comm_dtype not in COMM_DTYPES:
+            raise ValueError("comm_dtype must be one of %s" % sorted(COMM_DTYPES))
+        # fp16/bf16: messages use the base-relative encoding (sweep_core.h) and
+        # travel compressed; the touch counters travel separately as int32
+        self.comm_dtype = comm_dtype
+        self.scaled = comm_dtype != "fp32"
         f = dict(dtype=torch.float32, device=self.device)
         self.start = torch.empty((self.P, 32), **f)
         self.buf = torch.empty((self.P, 16), **f)
         self.vst = torch.tensor(vst_table(), **f)
-        self.comm_bytes = self.buf.numel() * 4
+        self.comm_bytes = self.P * (16 * 4 if not self.scaled else
+                                    14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4)
         self.windows = 0
 
     def begin(self, roster) -> None:
@@ -54,16 +59,25 @@ class SweepMerger:
 
     def messages(self, roster) -> torch.Tensor:
         native().sweep_delta(self.start, roster.state, roster.attrs, self.vst,
-                             float(self.cfg.unknown_player_sigma), self.buf)
+                             float(self.cfg.unknown_player_sigma), self.scaled, self.buf)
         return self.buf
 
     def reduce(self) -> None:
-        if self.world > 1:
+        if self.world <= 1:
+            return
+        if not self.scaled:
             dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group)
+            return
+        msg = self.buf[:, :14].to(COMM_DTYPES[self.comm_dtype])
+        touch = self.buf[:, 14:].to(torch.int32)
+        dist.all_reduce(msg, op=dist.ReduceOp.SUM, group=self.group)
+        dist.all_reduce(touch, op=dist.ReduceOp.SUM, group=self.group)
+        self.buf[:, :14].copy_(msg)
+        self.buf[:, 14:].copy_(touch)
 
     def apply(self, roster) -> None:
         native().sweep_apply(self.start, self.buf, roster.attrs, roster.state, self.vst,
-                             float(self.cfg.unknown_player_sigma))
+                             float(self.cfg.unknown_player_sigma), self.scaled)
         roster.epoch = roster.epoch if roster.epoch is not None else 0  # apply wrote tag 0
 
     def merge(self, roster) -> None:

@@ -79,7 +79,7 @@ def window_slice(spec: RerateSpec, g: int, rank: int, size: int):
 def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
         checkpoint_every: int = 1, fault_kill_after: Optional[int] = None,
         on_window: Optional[Callable[[int, R.RateResult], None]] = None,
-        rater: Optional[R.BatchRater] = None):
+        rater: Optional[R.BatchRater] = None, comm_dtype: str = "fp32"):
     """Rate the whole history; returns (metrics reduced over ranks, final roster)."""
     rank, size = world()
     dev = torch.device(device) if device is not None else (
@@ -97,7 +97,7 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
     else:
         roster = make_roster(spec.roster_spec(), device=dev)
         broadcast_roster(roster)  # C3 (identical by construction; keeps replicas honest)
-    merger = SweepMerger(spec.players, dev, rater.cfg) if size > 1 else None
+    merger = SweepMerger(spec.players, dev, rater.cfg, comm_dtype=comm_dtype) if size > 1 else None
     pipe = WindowPipeline(rater, roster, K, merger=merger)
     total = n_windows(spec, size)
     counts = torch.zeros(256, dtype=torch.int64, device=dev)
@@ -157,12 +157,14 @@ def main(argv=None) -> int:
     ap.add_argument("--fault-kill-after", type=int, default=None,
                     help="fault injection: exit(17) after this many windows")
     ap.add_argument("--device", default=None)
+    ap.add_argument("--comm-dtype", default=os.environ.get("COMM_DTYPE") or "fp32",
+                    choices=["fp32", "fp16", "bf16"], help="sweep-merge message precision")
     args = ap.parse_args(argv)
     rank, size, dev = init_from_env()
     spec = RerateSpec(total_matches=int(args.matches), players=int(args.players),
                       team_size=args.team_size, window=int(args.window), seed=args.seed)
     res, _ = run(spec, args.device or dev, args.checkpoint_dir, args.checkpoint_every,
-                 args.fault_kill_after)
+                 args.fault_kill_after, comm_dtype=args.comm_dtype)
     if rank == 0:
         print(json.dumps(dict(res, n_ranks=size, spec=asdict(spec))), flush=True)
     return 0

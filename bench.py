@@ -50,6 +50,8 @@ def parse(argv=None):
                          "4 = streaming: rating + per-event telemetry aggregation")
     ap.add_argument("--events", default="20,60", help="config 4: min,max telemetry events per match")
     ap.add_argument("--telemetry-mode", default="fused", choices=["fused", "separate"])
+    ap.add_argument("--comm-dtype", default=os.environ.get("COMM_DTYPE") or "fp32",
+                    choices=["fp32", "fp16", "bf16"], help="sweep-merge message precision (N > 1)")
     args = ap.parse_args(argv)
     if args.config == 3:
         args.team_size = 5
@@ -103,7 +105,7 @@ def main(argv=None) -> int:
         tele = [make_telemetry(tspec, windows[w], K, base=(w * world + rank) * M) for w in range(n_windows)]
         stats = allocate_stats(M, K, dev)
         n_events = sum(t.num_events for t in tele) / n_windows
-    merger = SweepMerger(P, dev) if world > 1 else None
+    merger = SweepMerger(P, dev, comm_dtype=args.comm_dtype) if world > 1 else None
     pipe = WindowPipeline(rater, roster, K, merger=merger)
     err = torch.zeros(3, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
@@ -186,6 +188,7 @@ def main(argv=None) -> int:
                 "parallelism": "dp%d" % world,
                 "mode": "exact" if world == 1 else "sweep (exact per rank + RCCL posterior merge)",
                 "bench_config": args.config,
+                "comm_dtype": args.comm_dtype if world > 1 else None,
                 **extra,
             },
         }), flush=True)

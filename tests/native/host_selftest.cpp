@@ -96,16 +96,19 @@ static void run(int K, int64_t P, int64_t M, uint64_t seed) {
     if (!isnan(st64[i])) maxd = fmax(maxd, fabs((double)st64[i] - st32[i]));
   CHECK(maxd < 5.0);
 
-  // DP merge round trip: messages of "after" against "before", then apply
-  std::vector<float> buf((size_t)P * 16), merged(state.size());
-  host_sweep_delta(state.data(), st64.data(), attrs.data(), vst.data(), 500.f, buf.data(), P);
-  host_sweep_apply(state.data(), buf.data(), attrs.data(), merged.data(), vst.data(), 500.f, P);
-  for (int64_t p = 0; p < P; ++p)
-    for (int t = 0; t < kTracks; ++t) {
-      const float a = st64[p * kRowFloats + 4 * t], b = merged[p * kRowFloats + 4 * t];
-      CHECK(isnan(a) == isnan(b));
-      if (!isnan(a)) CHECK(fabs(a - b) < 0.05f + 1e-4f * fabs(a));
-    }
+  // DP merge round trip (raw and base-relative encodings): messages of "after"
+  // against "before", then apply, reproduces "after"
+  for (int scaled = 0; scaled < 2; ++scaled) {
+    std::vector<float> buf((size_t)P * 16), merged(state.size());
+    host_sweep_delta(state.data(), st64.data(), attrs.data(), vst.data(), 500.f, scaled, buf.data(), P);
+    host_sweep_apply(state.data(), buf.data(), attrs.data(), merged.data(), scaled, vst.data(), 500.f, P);
+    for (int64_t p = 0; p < P; ++p)
+      for (int t = 0; t < kTracks; ++t) {
+        const float a = st64[p * kRowFloats + 4 * t], b = merged[p * kRowFloats + 4 * t];
+        CHECK(isnan(a) == isnan(b));
+        if (!isnan(a)) CHECK(fabs(a - b) < 0.05f + 1e-4f * fabs(a));
+      }
+  }
 
   // telemetry
   GenEventParams ge{seed + 2, 0, 12};

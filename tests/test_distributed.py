@@ -33,6 +33,7 @@ def _entry(rank, size, port, fn, outdir, args):
 
 
 def run_ranks(fn, size, tmp_path, *args):
+    os.makedirs(str(tmp_path), exist_ok=True)
     mp.spawn(_entry, args=(size, _free_port(), fn, str(tmp_path), args), nprocs=size, join=True)
     return [torch.load(os.path.join(str(tmp_path), "r%d.pt" % r), weights_only=True) for r in range(size)]
 
@@ -109,7 +110,7 @@ def test_levels_host():
 
 
 # ------------------------------------------------------------------ C1 sweep merge
-def _sweep(rank, size, P, M, K, seed, disjoint):
+def _sweep(rank, size, P, M, K, seed, disjoint, comm_dtype="fp32"):
     from analyzer_amd.ops.rate import BatchRater
     from analyzer_amd.parallel.sweep import SweepMerger
 
@@ -117,7 +118,7 @@ def _sweep(rank, size, P, M, K, seed, disjoint):
     rec = make_stream(StreamSpec(team_size=K, seed=seed + 1 + rank, p_afk=0.0), M, P, K=K)
     if disjoint:  # rank r only sees players r, r+size, ...
         rec[:, :2 * K] = rec[:, :2 * K] - rec[:, :2 * K] % size + rank
-    merger = SweepMerger(P, "cpu")
+    merger = SweepMerger(P, "cpu", comm_dtype=comm_dtype)
     merger.begin(roster)
     local = roster.clone()
     BatchRater().rate(local, rec, K)
@@ -163,3 +164,22 @@ def test_sweep_merge_overlapping_sums_messages(tmp_path):
         assert torch.allclose(merged[have, 4 * t + 2].double(), pi.rsqrt(), rtol=1e-4)
     for r in res[1:]:
         assert torch.equal(r["merged"].nan_to_num(-7), merged.nan_to_num(-7))
+
+
+@pytest.mark.parametrize("dtype,tol_mu", [("fp16", 1.0), ("bf16", 8.0)])
+def test_sweep_merge_compressed_messages(tmp_path, dtype, tol_mu):
+    """COMM_DTYPE fp16/bf16: base-relative messages survive the compressed
+    all-reduce (config 5 "fp16 moments"); merged ratings stay close to fp32."""
+    P, M, K, seed, size = 200, 600, 3, 7, 2
+    ref = run_ranks(_sweep, size, tmp_path / "a", P, M, K, seed, False, "fp32")
+    got = run_ranks(_sweep, size, tmp_path / "b", P, M, K, seed, False, dtype)
+    a, b = ref[0]["merged"], got[0]["merged"]
+    mu_a, mu_b = a[:, 0::4], b[:, 0::4]
+    assert torch.equal(torch.isnan(mu_a), torch.isnan(mu_b))
+    ok = ~torch.isnan(mu_a)
+    err = (mu_a[ok] - mu_b[ok]).abs()
+    # rating shifts of hundreds of points per window: fp16 keeps ~5e-4 of them, bf16 ~4e-3
+    assert float(err.max()) < tol_mu and float(err.median()) < tol_mu / 10
+    sg_a, sg_b = a[:, 2::4][ok], b[:, 2::4][ok]
+    assert float(((sg_a - sg_b).abs() / sg_a).max()) < 2e-2
+    assert torch.equal(got[0]["merged"].nan_to_num(-7), got[1]["merged"].nan_to_num(-7))

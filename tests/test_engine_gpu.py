@@ -109,7 +109,8 @@ def test_radix_sort_pairs_stable(gpu_device, n, bits):
     assert torch.equal(vs.cpu(), vals[order])
 
 
-def test_sweep_kernels_match_host(gpu_device):
+@pytest.mark.parametrize("scaled", [False, True])
+def test_sweep_kernels_match_host(gpu_device, scaled):
     """K9 device kernels (messages + apply) == C++ host mirror on 128-B rows."""
     from analyzer_amd.ops.native import native
     from analyzer_amd.models.tiers import vst_table
@@ -121,16 +122,16 @@ def test_sweep_kernels_match_host(gpu_device):
     R.BatchRater().rate(after, rec, 3)
     vst = torch.tensor(vst_table(), dtype=torch.float32)
     bh = torch.empty((P, 16))
-    native().sweep_delta(start.state, after.state, start.attrs, vst, 500.0, bh)
+    native().sweep_delta(start.state, after.state, start.attrs, vst, 500.0, scaled, bh)
     bd = torch.empty((P, 16), device=gpu_device)
     native().sweep_delta(start.state.to(gpu_device), after.state.to(gpu_device),
-                         start.attrs.to(gpu_device), vst.to(gpu_device), 500.0, bd)
+                         start.attrs.to(gpu_device), vst.to(gpu_device), 500.0, scaled, bd)
     np.testing.assert_allclose(bd.cpu().numpy(), bh.numpy(), rtol=1e-6, atol=1e-9)
     sh = start.state.clone()
-    native().sweep_apply(start.state, bh * 2, start.attrs, sh, vst, 500.0)
+    native().sweep_apply(start.state, bh * 2, start.attrs, sh, vst, 500.0, scaled)
     sd = start.state.to(gpu_device).clone()
     native().sweep_apply(start.state.to(gpu_device), (bh * 2).to(gpu_device),
-                         start.attrs.to(gpu_device), sd, vst.to(gpu_device), 500.0)
+                         start.attrs.to(gpu_device), sd, vst.to(gpu_device), 500.0, scaled)
     # fp32 (tau / pi, 1 / sqrt(pi)): device fma contraction vs host rounding
     np.testing.assert_allclose(sd.cpu().numpy(), sh.numpy(), rtol=5e-5, atol=1e-6, equal_nan=True)
 
