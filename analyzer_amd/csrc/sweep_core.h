@@ -58,14 +58,16 @@ ANA_HD void sweep_delta_player(const float* a, const float* b, const float* attr
     const bool changed = mu0 == mu0 ? (mu != mu0 || sg != sg0) : mu == mu;
     float bm, bs;
     if (changed && track_base(a, t, seeded, seed_mu, seed_sig, bm, bs)) {
-      float p1, t1, p0, t0;
-      nat_params(mu, sg, p1, t1);
-      nat_params(bm, bs, p0, t0);
-      dp = p1 - p0;
-      dt = t1 - t0;
-      if (scaled) {
-        dt = (dt - bm * dp) / p0;
-        dp = dp / p0;
+      if (scaled) {  // (pi/pi_b - 1, (pi/pi_b)(mu - mu_b)): no cancellation
+        const float r = bs / sg;
+        dp = r * r - 1.f;
+        dt = r * r * (mu - bm);
+      } else {
+        float p1, t1, p0, t0;
+        nat_params(mu, sg, p1, t1);
+        nat_params(bm, bs, p0, t0);
+        dp = p1 - p0;
+        dt = t1 - t0;
       }
     }
     if (mu0 != mu0 && mu == mu) {

@@ -126,7 +126,10 @@ def test_sweep_kernels_match_host(gpu_device, scaled):
     bd = torch.empty((P, 16), device=gpu_device)
     native().sweep_delta(start.state.to(gpu_device), after.state.to(gpu_device),
                          start.attrs.to(gpu_device), vst.to(gpu_device), 500.0, scaled, bd)
-    np.testing.assert_allclose(bd.cpu().numpy(), bh.numpy(), rtol=1e-6, atol=1e-9)
+    # scaled messages are (pi/pi_b - 1, ...): a 1-ulp difference in pi/pi_b near 1 is a
+    # large relative one in the message (they travel as fp16/bf16 anyway)
+    np.testing.assert_allclose(bd.cpu().numpy(), bh.numpy(), rtol=1e-3 if scaled else 1e-6,
+                               atol=1e-5 if scaled else 1e-9)
     sh = start.state.clone()
     native().sweep_apply(start.state, bh * 2, start.attrs, sh, vst, 500.0, scaled)
     sd = start.state.to(gpu_device).clone()
