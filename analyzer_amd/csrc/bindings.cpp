@@ -371,6 +371,31 @@ void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor vst, doub
   }
 }
 
+// A HIP stream restricted to ``num_cus`` compute units, spread evenly over the
+// device's CUs (and so over its XCDs).  Used for the schedule prepass so its
+// bandwidth-bound kernels trickle alongside the latency-bound executor instead
+// of bursting.  Returns the raw handle for torch.cuda.ExternalStream; the
+// stream lives until process exit (one per pipeline).
+int64_t cu_masked_stream(int64_t device, int64_t num_cus) {
+  hipDeviceProp_t prop;
+  check_hip((int)hipGetDeviceProperties(&prop, (int)device), "hipGetDeviceProperties");
+  const int total = prop.multiProcessorCount;
+  TORCH_CHECK(num_cus >= 1 && num_cus <= total, "num_cus must be 1..", total);
+  std::vector<uint32_t> mask((total + 31) / 32, 0u);
+  for (int64_t i = 0; i < num_cus; ++i) {
+    const int cu = (int)(i * total / num_cus);
+    mask[cu / 32] |= 1u << (cu % 32);
+  }
+  int prev = 0;
+  check_hip((int)hipGetDevice(&prev), "hipGetDevice");
+  check_hip((int)hipSetDevice((int)device), "hipSetDevice");
+  hipStream_t st = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data());
+  check_hip((int)hipSetDevice(prev), "hipSetDevice");
+  check_hip((int)e, "hipExtStreamCreateWithCUMask");
+  return (int64_t)reinterpret_cast<intptr_t>(st);
+}
+
 void reset_tags(Tensor state) {
   const auto dev = state.device();
   check(state, "state", torch::kFloat32, dev);
@@ -401,6 +426,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("STAT_FEATURES") = ana::kStatFeatures;
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
   m.def("sweep_apply", &sweep_apply, "K9: apply all-reduced messages to the replicated roster");
+  m.def("cu_masked_stream", &cu_masked_stream, "HIP stream limited to N CUs (spread over XCDs)");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
   m.attr("ROW_FLOATS") = ana::kRowFloats;
   m.attr("N_TRACKS") = ana::kTracks;

@@ -151,7 +151,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   }
   bool exhausted = false, tk_pending = false;
   unsigned tk = 0;                 // ticket returned to lane 0
-  uint32_t spins = 0;
+  uint32_t spins = 0, iter = 0;
   // K8 fused mode: telemetry tiles fill the time a wave would spend waiting
   const int64_t tele_tiles = tp.evoff ? (tp.num_matches + kTeleTile - 1) / kTeleTile : 0;
   bool tele_done = tele_tiles == 0;
@@ -295,9 +295,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
 
     // ---------------------------------------------- (5) next iteration's counter polls
+    ++iter;
 #pragma unroll
     for (int h = 0; h < kHeld; ++h)
-      if ((pend[h] >> lane) & 1ull)
+      if (((pend[h] >> lane) & 1ull) && (!(prm.debug_flags & 4) || (iter & 1u)))
         dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
 

@@ -42,10 +42,23 @@ class WindowPipeline:
         self.merger = merger
         self.device = roster.device
         self.cuda = self.device.type == "cuda"
-        self.side = torch.cuda.Stream(self.device) if self.cuda else None
+        self.side = self._side_stream() if self.cuda else None
         self._set = 0
         self._free: List[Optional[torch.cuda.Event]] = [None, None]
         self.windows_rated = 0
+
+    def _side_stream(self):
+        """Side stream of the prepass; ``ANA_PREPASS_CUS=n`` confines it to n CUs
+        (HIP CU mask) so it trickles alongside the executor instead of bursting."""
+        import os
+
+        n = int(os.environ.get("ANA_PREPASS_CUS", "0") or 0)
+        if n > 0:
+            from ..ops.native import native
+
+            handle = native().cu_masked_stream(self.device.index or 0, n)
+            return torch.cuda.ExternalStream(handle, device=self.device)
+        return torch.cuda.Stream(self.device)
 
     def prepare(self, rec: torch.Tensor) -> Prepared:
         """Enqueue the schedule prepass of ``rec`` on the side stream."""
