@@ -29,7 +29,7 @@ HIP_SOURCES = ["kernels.hip", "radix_sort.hip", "dataflow.hip", "sweep.hip", "te
 # static instructions); NaN/Inf semantics are untouched (no -ffinite-math-only),
 # which the NULL = NaN convention relies on.
 HIP_FLAGS = {"dataflow.hip": ["-fapprox-func", "-freciprocal-math", "-fno-signed-zeros"]}
-CPP_SOURCES = ["host.cpp", "bindings.cpp"]
+CPP_SOURCES = ["host.cpp", "ingest.cpp", "bindings.cpp"]
 
 
 def _ext_suffix() -> str:
@@ -78,7 +78,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
     for name in CPP_SOURCES:
         src = CSRC / name
         obj = BUILD / (name + ".o")
-        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-pthread", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                "-D_GLIBCXX_USE_CXX11_ABI=1", "-I" + str(CSRC), "-I" + ROCM + "/include",
                "-I" + py_inc] + ["-I" + p for p in incs] + ["-c", str(src), "-o", str(obj)]

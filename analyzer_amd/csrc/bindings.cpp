@@ -14,6 +14,7 @@
 #include "common.h"
 #include "gen_core.h"
 #include "host.h"
+#include "ingest.h"
 #include "kernels.h"
 
 namespace {
@@ -396,6 +397,27 @@ int64_t cu_masked_stream(int64_t device, int64_t num_cus) {
   return (int64_t)reinterpret_cast<intptr_t>(st);
 }
 
+// ------------------------------------------------------------------ ingest (P3)
+void write_record_file(const std::string& path, Tensor rec, int64_t K) {
+  check(rec, "rec", torch::kInt32, torch::Device(torch::kCPU));
+  TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  ana::write_record_file(path, rec.data_ptr<int32_t>(), rec.size(0), (int)K);
+}
+
+static py::object reader_acquire(ana::RecordReader& r) {
+  int slot = 0;
+  int64_t base = 0, n = 0;
+  bool ok;
+  {
+    py::gil_scoped_release nogil;  // the producer thread may still be reading
+    ok = r.acquire(&slot, &base, &n);
+  }
+  if (!ok) return py::none();
+  auto t = torch::from_blob(r.slot_data(slot), {n, 2 * (int64_t)r.K() + 2},
+                            torch::TensorOptions().dtype(torch::kInt32));
+  return py::make_tuple(slot, base, t);
+}
+
 void reset_tags(Tensor state) {
   const auto dev = state.device();
   check(state, "state", torch::kFloat32, dev);
@@ -426,6 +448,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("STAT_FEATURES") = ana::kStatFeatures;
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
   m.def("sweep_apply", &sweep_apply, "K9: apply all-reduced messages to the replicated roster");
+  m.def("write_record_file", &write_record_file, "P3: write a match-record file (ANAREC01)");
+  py::class_<ana::RecordReader>(m, "RecordReader")
+      .def(py::init<const std::string&, int64_t, int, bool>(), py::arg("path"), py::arg("window"),
+           py::arg("slots") = 3, py::arg("pinned") = true)
+      .def_property_readonly("K", &ana::RecordReader::K)
+      .def_property_readonly("num_matches", &ana::RecordReader::num_matches)
+      .def_property_readonly("window", &ana::RecordReader::window)
+      .def_property_readonly("num_windows", &ana::RecordReader::num_windows)
+      .def_property_readonly("pinned", &ana::RecordReader::pinned)
+      .def("acquire", &reader_acquire,
+           "next filled window as (slot, base, tensor view of pinned memory) or None at EOF")
+      .def("release", &ana::RecordReader::release, "return the oldest acquired slot");
   m.def("cu_masked_stream", &cu_masked_stream, "HIP stream limited to N CUs (spread over XCDs)");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
   m.attr("ROW_FLOATS") = ana::kRowFloats;

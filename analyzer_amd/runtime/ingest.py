@@ -1,0 +1,152 @@
+"""Host ingest and egress around the device pipeline.
+
+* ``write_records`` / ``FileSource``: match records on disk (ANAREC01 files)
+  are read by the native ``RecordReader`` (csrc/ingest.cpp) on a background
+  thread into a ring of pinned host windows; each window is copied to the GPU on
+  a dedicated copy stream (non-blocking H2D) and its pinned slot is recycled as
+  soon as that copy completes -- ingest overlaps the rating of earlier windows.
+* ``OutputSink``: per-window results are copied back D2H on a second copy
+  stream into pinned buffers and handed to a callback once they land, so output
+  egress also overlaps the next window's rating.
+
+On the CPU the same classes run synchronously (the host mirror path).
+"""
+from __future__ import annotations
+
+import collections
+from typing import Callable, Deque, Iterator, Optional, Tuple
+
+import torch
+
+from ..ops.native import native
+from ..ops.rate import RateResult
+
+
+def write_records(path: str, rec: torch.Tensor, K: int) -> None:
+    native().write_record_file(path, rec.detach().cpu().contiguous(), int(K))
+
+
+class FileSource:
+    """Iterate ``(base, rec)`` windows of a record file as device tensors."""
+
+    def __init__(self, path: str, window: int, device="cpu", slots: int = 3):
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.reader = native().RecordReader(path, int(window), int(slots), self.cuda)
+        self.K = int(self.reader.K)
+        self.copy_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self._inflight: Deque[Tuple[int, torch.cuda.Event]] = collections.deque()
+
+    @property
+    def num_windows(self) -> int:
+        return int(self.reader.num_windows)
+
+    def _recycle(self, block: bool) -> None:
+        while self._inflight:
+            slot, ev = self._inflight[0]
+            if not block and not ev.query():
+                return
+            ev.synchronize()
+            self.reader.release(slot)
+            self._inflight.popleft()
+            block = False
+
+    def __iter__(self) -> Iterator[Tuple[int, torch.Tensor]]:
+        while True:
+            if self.cuda and len(self._inflight) >= 2:
+                self._recycle(block=True)  # keep a free slot for the reader thread
+            got = self.reader.acquire()
+            if got is None:
+                break
+            slot, base, host = got
+            if not self.cuda:
+                rec = host.clone()
+                self.reader.release(slot)
+            else:
+                main = torch.cuda.current_stream(self.device)
+                with torch.cuda.stream(self.copy_stream):
+                    rec = torch.empty(host.shape, dtype=host.dtype, device=self.device)
+                    rec.copy_(host, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.copy_stream)
+                main.wait_event(ev)              # consumers on the main stream see the data
+                rec.record_stream(main)
+                self._inflight.append((slot, ev))
+                self._recycle(block=False)
+            yield int(base), rec
+        if self.cuda:
+            while self._inflight:
+                self._recycle(block=True)
+
+
+class OutputSink:
+    """Asynchronous D2H of per-window results into pinned host memory."""
+
+    FIELDS = ("quality", "status", "s_mu", "s_sig", "delta", "m_mu", "m_sig")
+
+    def __init__(self, device, on_ready: Callable[[int, dict], None]):
+        self.device = torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.on_ready = on_ready
+        self.copy_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self._pending: Deque[Tuple[int, dict, Optional[torch.cuda.Event]]] = collections.deque()
+
+    def push(self, base: int, res: RateResult) -> None:
+        if not self.cuda:
+            self.on_ready(base, {f: getattr(res, f).clone() for f in self.FIELDS})
+            return
+        main = torch.cuda.current_stream(self.device)
+        done = torch.cuda.Event()
+        done.record(main)
+        host = {}
+        with torch.cuda.stream(self.copy_stream):
+            self.copy_stream.wait_event(done)
+            for f in self.FIELDS:
+                src = getattr(res, f)
+                dst = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+                dst.copy_(src, non_blocking=True)
+                src.record_stream(self.copy_stream)
+                host[f] = dst
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+        self._pending.append((base, host, ev))
+        self.poll()
+
+    def poll(self, block: bool = False) -> None:
+        while self._pending:
+            base, host, ev = self._pending[0]
+            if not block and ev is not None and not ev.query():
+                return
+            if ev is not None:
+                ev.synchronize()
+            self.on_ready(base, host)
+            self._pending.popleft()
+
+    def flush(self) -> None:
+        self.poll(block=True)
+
+
+def rate_file(path: str, roster, window: int, rater=None, on_result=None) -> int:
+    """Rate every window of a record file in order (ingest, prepass, rating and
+    egress overlapped on a GPU); ``on_result(base, host_dict)`` receives outputs."""
+    from ..ops.rate import BatchRater
+    from .engine import WindowPipeline
+
+    src = FileSource(path, window, roster.device)
+    pipe = WindowPipeline(rater or BatchRater(), roster, src.K)
+    sink = OutputSink(roster.device, on_result) if on_result is not None else None
+    bases = []
+
+    def windows():
+        for base, rec in src:
+            bases.append(base)
+            yield rec
+
+    def done(i, res):
+        if sink is not None:
+            sink.push(bases[i], res)
+
+    n = pipe.run(windows(), on_result=done)
+    if sink is not None:
+        sink.flush()
+    return n

@@ -170,3 +170,23 @@ def test_fused_rate_telemetry_on_device(gpu_device):
     assert torch.equal(ra.s_mu.nan_to_num(-7), rb.s_mu.nan_to_num(-7))
     ref = aggregate_reference(type(tel)(tel.evoff.cpu(), tel.events.cpu()), K)
     np.testing.assert_allclose(stats.cpu().numpy(), ref, rtol=2e-5, atol=0.05)
+
+
+def test_file_ingest_pipeline_on_device(gpu_device, tmp_path):
+    """P3 on the GPU: native reader thread -> pinned ring -> H2D copy stream ->
+    prepass/rate -> D2H copy stream; equals rating the stream in one launch."""
+    from analyzer_amd.runtime.ingest import rate_file, write_records
+
+    K, P, M = 3, 50000, 600000
+    rec = make_stream(StreamSpec(team_size=K, seed=31), M, P, K=K)
+    path = str(tmp_path / "s.rec")
+    write_records(path, rec, K)
+    roster = make_roster(RosterSpec(num_players=P, seed=32), device=gpu_device)
+    direct = roster.clone()
+    ref = R.BatchRater().rate(direct, rec.to(gpu_device), K)
+    got = {}
+    n = rate_file(path, roster, 100000, on_result=lambda b, h: got.__setitem__(b, h))
+    assert n == 6
+    s_mu = torch.cat([got[b]["s_mu"] for b in sorted(got)])
+    torch.testing.assert_close(s_mu, ref.s_mu.cpu(), rtol=0, atol=0, equal_nan=True)
+    torch.testing.assert_close(roster.tracks(), direct.tracks(), rtol=0, atol=0, equal_nan=True)
