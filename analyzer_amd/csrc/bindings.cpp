@@ -248,6 +248,8 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   if (const char* e = std::getenv("ANA_RATE_DEBUG")) prm.debug_flags = std::atoi(e);  // experiments
   prm.spec = 0;
   if (const char* e = std::getenv("ANA_RATE_SPEC")) prm.spec = std::atoi(e);
+  prm.tight_groups = -1;
+  if (const char* e = std::getenv("ANA_RATE_TIGHT")) prm.tight_groups = std::atoi(e);
   const ana::TelemetryParams tp = telemetry_params(tele_evoff, tele_events, tele_stats, M, K, dev);
   if (dev.is_cuda()) {
     check(link, "link", torch::kInt32, dev);

@@ -76,6 +76,8 @@ struct RateParams {
   int32_t idle_spins;          // dataflow: max s_sleep(2) rounds of an idle wave (0 = default)
   int32_t debug_flags;         // experiments only (ANA_RATE_DEBUG): 2 skip slot outputs
   int32_t spec;                // dataflow: speculative one-dependency matches per wave iteration
+  int32_t tight_groups;        // dataflow: 2K lanes per match instead of the next power of two
+                               // (-1 auto, 0 off, 1 on)
 };
 
 // Per-match outputs, structure-of-arrays.  Per-slot arrays are [M][2K]; the
