@@ -52,6 +52,8 @@ class WindowPipeline:
         (HIP CU mask) so it trickles alongside the executor instead of bursting."""
         import os
 
+        if os.environ.get("ANA_PREPASS_SERIAL", "") not in ("", "0"):
+            return torch.cuda.current_stream(self.device)  # no overlap (A/B)
         n = int(os.environ.get("ANA_PREPASS_CUS", "0") or 0)
         if n > 0:
             from ..ops.native import native

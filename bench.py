@@ -45,9 +45,11 @@ def parse(argv=None):
     ap.add_argument("--ring", type=int, default=4, help="distinct pre-generated windows per rank")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--check", action="store_true", help="also validate statuses after timing")
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4],
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
                     help="BASELINE config: 2 = 10M 3v3/GPU (headline), 3 = 12.5M 5v5/GPU (100M at DP=8), "
-                         "4 = streaming: rating + per-event telemetry aggregation")
+                         "4 = streaming: rating + per-event telemetry aggregation, "
+                         "5 = full-history re-rate windows: 16M 3v3/GPU over a 10M-player roster, "
+                         "fp16 merge messages")
     ap.add_argument("--events", default="20,60", help="config 4: min,max telemetry events per match")
     ap.add_argument("--telemetry-mode", default="fused", choices=["fused", "separate"])
     ap.add_argument("--comm-dtype", default=os.environ.get("COMM_DTYPE") or "fp32",
@@ -58,6 +60,14 @@ def parse(argv=None):
         if args.matches_per_gpu == 10_000_000:
             args.matches_per_gpu = 12_500_000
     if args.config == 4:
+        args.ring = min(args.ring, 2)
+    if args.config == 5:
+        if args.players == 1_000_000:
+            args.players = 10_000_000
+        if args.matches_per_gpu == 10_000_000:
+            args.matches_per_gpu = 16_000_000
+        if "COMM_DTYPE" not in os.environ and "--comm-dtype" not in (argv or sys.argv):
+            args.comm_dtype = "fp16"
         args.ring = min(args.ring, 2)
     return args
 
@@ -157,6 +167,9 @@ def main(argv=None) -> int:
     extra = {}
     if args.config == 3:
         metric = "matches/sec rated (whole node), 5v5 TrueSkill, 1M-player roster, DP sweep merge"
+    if args.config == 5:
+        metric = ("matches/sec re-rated (whole node), full-history windows, 3v3 TrueSkill, "
+                  "10M-player roster")
     if args.config == 4:
         metric = ("matches/sec rated + telemetry aggregated (whole node), 3v3 TrueSkill, "
                   "1M-player roster, streaming")
@@ -176,7 +189,7 @@ def main(argv=None) -> int:
             "vs_baseline": value / (BASELINE_5V5_MATCHES_PER_S if args.config == 3
                                     else BASELINE_MATCHES_PER_S),
             "dtype": "fp32",
-            "data": "synthetic (on-device counter RNG stream, random-init 1M-player roster)",
+            "data": "synthetic (on-device counter RNG stream, random-init %d-player roster)" % P,
             "config": {
                 "model": "TrueSkill 2-team EP (beta=1000, tau=10, draw_probability=0), "
                          "shared + per-mode tracks",
