@@ -190,3 +190,38 @@ def test_file_ingest_pipeline_on_device(gpu_device, tmp_path):
     s_mu = torch.cat([got[b]["s_mu"] for b in sorted(got)])
     torch.testing.assert_close(s_mu, ref.s_mu.cpu(), rtol=0, atol=0, equal_nan=True)
     torch.testing.assert_close(roster.tracks(), direct.tracks(), rtol=0, atol=0, equal_nan=True)
+
+
+@pytest.mark.parametrize("case", ["empty", "one", "one_player", "all_afk", "all_unsupported",
+                                  "all_bad_tier", "k5_uneven_ties"])
+def test_edge_windows_device_vs_host(gpu_device, case):
+    """Degenerate windows: the device executor terminates and matches the host mirror."""
+    K, P, M = 3, 50, 400
+    rspec = RosterSpec(num_players=P, seed=3)
+    sspec = StreamSpec(team_size=K, seed=4)
+    if case == "empty":
+        M = 0
+    elif case == "one":
+        M = 1
+    elif case == "one_player":
+        P, rspec = 1, RosterSpec(num_players=1, seed=3)
+    elif case == "all_afk":
+        sspec = StreamSpec(team_size=K, seed=4, p_afk=1.0)
+    elif case == "all_unsupported":
+        sspec = StreamSpec(team_size=K, seed=4, p_unsupported=1.0)
+    elif case == "all_bad_tier":
+        rspec = RosterSpec(num_players=P, seed=3, p_rated=0.0, p_rp_ranked=0.0, p_rp_blitz=0.0,
+                           p_tier_bad=1.0)
+    elif case == "k5_uneven_ties":
+        K = 5
+        sspec = StreamSpec(team_size=K, seed=4, p_uneven=0.5, p_tie=0.5)
+    rec = make_stream(sspec, M, P, K=K)
+    host = make_roster(rspec)
+    dev = make_roster(rspec, device=gpu_device)
+    rh = R.BatchRater(host_fp64=False).rate(host, rec, K)
+    rd = R.BatchRater().rate(dev, rec.to(gpu_device), K)
+    assert torch.equal(rd.status.cpu(), rh.status)
+    np.testing.assert_allclose(rd.s_mu.cpu().numpy(), rh.s_mu.numpy(), rtol=1e-3, atol=0.5,
+                               equal_nan=True)
+    np.testing.assert_allclose(dev.tracks().cpu().numpy(), host.tracks().numpy(), rtol=1e-3,
+                               atol=0.5, equal_nan=True)
