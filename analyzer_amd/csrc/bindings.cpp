@@ -33,6 +33,23 @@ void check(const Tensor& t, const char* name, torch::ScalarType dt, const torch:
   TORCH_CHECK(t.device() == dev, name, " is on ", t.device(), " but expected ", dev);
 }
 
+// strided output views: rows of `inner` contiguous elements, any row stride
+int64_t check_rows_view(const Tensor& t, const char* name, torch::ScalarType dt,
+                        const torch::Device& dev, int64_t rows, int64_t inner) {
+  TORCH_CHECK(t.defined(), name, " is undefined");
+  TORCH_CHECK(t.scalar_type() == dt, name, " must be ", c10::toString(dt));
+  TORCH_CHECK(t.device() == dev, name, " is on ", t.device(), " but expected ", dev);
+  if (inner == 1) {
+    TORCH_CHECK(t.dim() == 1 && t.size(0) == rows, name, " must have ", rows, " entries");
+    return rows > 1 ? t.stride(0) : 1;
+  }
+  TORCH_CHECK(t.dim() == 2 && t.size(0) == rows && t.size(1) == inner, name, " must be [", rows,
+              ", ", inner, "]");
+  TORCH_CHECK(t.stride(1) == 1 && (rows <= 1 || t.stride(0) >= inner), name,
+              " rows must be contiguous and non-overlapping");
+  return rows > 1 ? t.stride(0) : inner;
+}
+
 hipStream_t stream_of(const Tensor& t) {
   return at::hip::getCurrentHIPStream(t.device().index()).stream();
 }
@@ -207,8 +224,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
   check(attrs, "attrs", torch::kFloat32, dev);
-  check(quality, "quality", torch::kFloat32, dev);
-  check(status, "status", torch::kUInt8, dev);
+
   check(vst, "vst", torch::kFloat32, dev);
   TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
   TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
@@ -219,11 +235,12 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   TORCH_CHECK(P >= 1 && P * ana::kRowFloats * 4 < 0x7fffffffLL,
               "roster size out of range (<= 16.7M players per device roster)");
   TORCH_CHECK(attrs.dim() == 2 && attrs.size(0) == P && attrs.size(1) == 4, "attrs must be [P, 4]");
-  TORCH_CHECK(quality.numel() == M && status.numel() == M, "quality/status must have M entries");
-  for (const Tensor* t : {&s_mu, &s_sig, &delta, &m_mu, &m_sig}) {
-    check(*t, "per-slot output", torch::kFloat32, dev);
-    TORCH_CHECK(t->numel() == M * S, "per-slot outputs must be [M, 2K]");
-  }
+  const int64_t qrow = check_rows_view(quality, "quality", torch::kFloat32, dev, M, 1);
+  const int64_t srow = check_rows_view(status, "status", torch::kUInt8, dev, M, 1);
+  const int64_t row = check_rows_view(s_mu, "s_mu", torch::kFloat32, dev, M, S);
+  for (const Tensor* t : {&s_sig, &delta, &m_mu, &m_sig})
+    TORCH_CHECK(check_rows_view(*t, "per-slot output", torch::kFloat32, dev, M, S) == row,
+                "per-slot outputs must share one row stride");
   TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries (tiers -1..29)");
   float* fp = nullptr;
   if (record_first_prior) {
@@ -233,7 +250,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   }
   ana::RateOut out{quality.data_ptr<float>(), status.data_ptr<uint8_t>(), s_mu.data_ptr<float>(),
                    s_sig.data_ptr<float>(), delta.data_ptr<float>(), m_mu.data_ptr<float>(),
-                   m_sig.data_ptr<float>()};
+                   m_sig.data_ptr<float>(), row, qrow, srow};
   ana::RateParams prm{};
   prm.beta2 = (float)beta2;
   prm.tau2 = (float)tau2;

@@ -80,18 +80,24 @@ struct RateParams {
                                // (-1 auto, 0 off, 1 on)
 };
 
-// Per-match outputs, structure-of-arrays.  Per-slot arrays are [M][2K]; the
-// participant record of the reference (rater.py:151-169) is
-// (s_mu, s_sig, delta) on ``participant`` and (m_mu, m_sig) on
-// ``participant_items``; any_afk follows from status.
+// Per-match outputs.  The participant record of the reference
+// (rater.py:151-169) is (s_mu, s_sig, delta) on ``participant`` and
+// (m_mu, m_sig) on ``participant_items``; any_afk follows from status.
+// Slot j of match m lives at field[m * row + j]; quality at quality[m * qrow],
+// status at status[m * srow].  The default layout (ops/rate.py) packs one
+// match per 128-B-aligned row -- [s_mu | s_sig | delta | m_mu | m_sig][2K],
+// quality, status byte -- so a match's outputs are one full-line write.
 struct RateOut {
-  float* quality;  // [M]  match.trueskill_quality (0 for AFK/invalid, NaN = not written)
-  uint8_t* status; // [M]  Status
+  float* quality;  // match.trueskill_quality (0 for AFK/invalid, NaN = not written)
+  uint8_t* status; // Status
   float* s_mu;
   float* s_sig;
   float* delta;
   float* m_mu;
   float* m_sig;
+  int64_t row;     // floats between consecutive matches in the slot fields
+  int64_t qrow;    // ... in quality
+  int64_t srow;    // bytes between consecutive matches in status
 };
 
 ANA_HD int meta_mode(uint32_t m0) { return (int)(m0 & 0xffu); }

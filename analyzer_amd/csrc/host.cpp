@@ -208,15 +208,15 @@ static void rate_k(const int32_t* rec, float* state, const float* attrs, float* 
       }
     }
     const bool afkish = w.status == kAfk || w.status == kInvalidRosters;
-    out.quality[m] = rated ? (float)w.quality : (afkish ? 0.f : NAN);
-    out.status[m] = w.status;
+    out.quality[m * out.qrow] = rated ? (float)w.quality : (afkish ? 0.f : NAN);
+    out.status[m * out.srow] = w.status;
     for (int j = 0; j < S; ++j) {
       const bool on = rated && w.id[j] >= 0;
-      out.s_mu[m * S + j] = on ? (float)w.ns_mu[j] : NAN;
-      out.s_sig[m * S + j] = on ? (float)w.ns_sig[j] : NAN;
-      out.delta[m * S + j] = on ? (float)w.delta[j] : NAN;
-      out.m_mu[m * S + j] = on ? (float)w.nm_mu[j] : NAN;
-      out.m_sig[m * S + j] = on ? (float)w.nm_sig[j] : NAN;
+      out.s_mu[m * out.row + j] = on ? (float)w.ns_mu[j] : NAN;
+      out.s_sig[m * out.row + j] = on ? (float)w.ns_sig[j] : NAN;
+      out.delta[m * out.row + j] = on ? (float)w.delta[j] : NAN;
+      out.m_mu[m * out.row + j] = on ? (float)w.nm_mu[j] : NAN;
+      out.m_sig[m * out.row + j] = on ? (float)w.nm_sig[j] : NAN;
     }
   }
 }

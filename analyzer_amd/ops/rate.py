@@ -121,6 +121,11 @@ class Roster:
 
 @dataclass
 class RateResult:
+    """Per-match outputs.  ``allocate`` packs every match into one 128-B aligned
+    row of ``packed`` -- [s_mu | s_sig | delta | m_mu | m_sig][2K], quality, status
+    byte -- so the executor writes each match with one full cache line; the fields
+    below are strided views of it (csrc/common.h RateOut)."""
+
     quality: torch.Tensor   # [M]
     status: torch.Tensor    # [M] uint8
     s_mu: torch.Tensor      # [M, 2K]
@@ -128,12 +133,26 @@ class RateResult:
     delta: torch.Tensor
     m_mu: torch.Tensor
     m_sig: torch.Tensor
+    packed: Optional[torch.Tensor] = None  # [M, row] backing storage (None: separate arrays)
+
+    FIELDS = ("quality", "status", "s_mu", "s_sig", "delta", "m_mu", "m_sig")
 
     @staticmethod
-    def allocate(M: int, K: int, device) -> "RateResult":
-        f = dict(dtype=torch.float32, device=device)
-        return RateResult(torch.empty(M, **f), torch.empty(M, dtype=torch.uint8, device=device),
-                          *(torch.empty((M, 2 * K), **f) for _ in range(5)))
+    def row_floats(K: int) -> int:
+        return -(-(5 * 2 * K + 2) // 32) * 32
+
+    @staticmethod
+    def allocate(M: int, K: int, device, packed: bool = True) -> "RateResult":
+        S = 2 * K
+        if not packed:
+            f = dict(dtype=torch.float32, device=device)
+            return RateResult(torch.empty(M, **f), torch.empty(M, dtype=torch.uint8, device=device),
+                              *(torch.empty((M, S), **f) for _ in range(5)))
+        W = RateResult.row_floats(K)
+        buf = torch.empty((M, W), dtype=torch.float32, device=device)
+        slots = [buf[:, f * S:(f + 1) * S] for f in range(5)]
+        status = buf.view(torch.uint8)[:, 4 * (5 * S + 1)]
+        return RateResult(buf[:, 5 * S], status, *slots, packed=buf)
 
     @property
     def any_afk(self) -> torch.Tensor:

@@ -101,12 +101,21 @@ class OutputSink:
         host = {}
         with torch.cuda.stream(self.copy_stream):
             self.copy_stream.wait_event(done)
-            for f in self.FIELDS:
-                src = getattr(res, f)
-                dst = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
-                dst.copy_(src, non_blocking=True)
-                src.record_stream(self.copy_stream)
-                host[f] = dst
+            if res.packed is not None:  # one DMA of the packed rows, host views rebuilt
+                buf = torch.empty(res.packed.shape, dtype=torch.float32, pin_memory=True)
+                buf.copy_(res.packed, non_blocking=True)
+                res.packed.record_stream(self.copy_stream)
+                S = res.s_mu.shape[1]
+                host = {"quality": buf[:, 5 * S], "status": buf.view(torch.uint8)[:, 4 * (5 * S + 1)]}
+                for i, f in enumerate(("s_mu", "s_sig", "delta", "m_mu", "m_sig")):
+                    host[f] = buf[:, i * S:(i + 1) * S]
+            else:
+                for f in self.FIELDS:
+                    src = getattr(res, f)
+                    dst = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+                    dst.copy_(src, non_blocking=True)
+                    src.record_stream(self.copy_stream)
+                    host[f] = dst
             ev = torch.cuda.Event()
             ev.record(self.copy_stream)
         self._pending.append((base, host, ev))

@@ -71,7 +71,8 @@ static void run(int K, int64_t P, int64_t M, uint64_t seed) {
   std::vector<float> st64 = state, st32 = state, fp(state.size(), NAN);
   std::vector<float> q(M), smu(M * S), ssg(M * S), dl(M * S), mmu(M * S), msg(M * S);
   std::vector<uint8_t> status(M);
-  RateOut out{q.data(), status.data(), smu.data(), ssg.data(), dl.data(), mmu.data(), msg.data()};
+  RateOut out{q.data(), status.data(), smu.data(), ssg.data(), dl.data(), mmu.data(), msg.data(),
+              S, 1, 1};
   std::vector<float> vst(kVstTiers);
   for (int t = 0; t < kVstTiers; ++t) vst[t] = 500.f + 70.f * t;
   RateParams prm{};

@@ -68,8 +68,8 @@ def _exact(rank, size, P, M, K, seed):
     roster = make_roster(RosterSpec(num_players=P, seed=seed))
     rec = make_stream(StreamSpec(team_size=K, seed=seed + 1, p_afk=0.05, p_unsupported=0.05), M, P, K=K)
     out = rate_exact_dp(BatchRater(), roster, rec, K)
-    return {"state": roster.state, "status": out.status, "s_mu": out.s_mu, "delta": out.delta,
-            "m_mu": out.m_mu, "quality": out.quality}
+    return {"state": roster.state, "status": out.status.clone(), "s_mu": out.s_mu.clone(),
+            "delta": out.delta.clone(), "m_mu": out.m_mu.clone(), "quality": out.quality.clone()}
 
 
 @pytest.mark.parametrize("size", [2, 3])
