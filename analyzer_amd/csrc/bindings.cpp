@@ -171,9 +171,7 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
   TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
   const int64_t M = rec.size(0);
-  TORCH_CHECK(link.dim() == 3 && link.size(0) == M && link.size(1) == 2 * K &&
-                  link.size(2) == ana::kLinkWords,
-              "link must be [M, 2K, 2]");
+  TORCH_CHECK(link.dim() == 2 && link.size(0) == M && link.size(1) == 2 * K, "link must be [M, 2K]");
   TORCH_CHECK(deps.numel() == M, "deps must have M entries");
   TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
   TORCH_CHECK(M * 2 * K <= ana::kMaxSlots, "more than 2^28 slots in one window (split the stream)");
@@ -272,7 +270,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
     check(link, "link", torch::kInt32, dev);
     check(deps, "deps", torch::kInt32, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
-    TORCH_CHECK(link.numel() == M * S * ana::kLinkWords, "link must be [M, 2K, 2]");
+    TORCH_CHECK(link.numel() == M * S * ana::kLinkWords, "link must be [M, 2K]");
     TORCH_CHECK(deps.numel() == M, "deps must have M entries");
     TORCH_CHECK(ctrl.numel() >= 16, "ctrl must have 16 entries");
     TORCH_CHECK(blocks >= 1 && blocks <= 65535, "blocks must be 1..65535");

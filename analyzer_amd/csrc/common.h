@@ -32,17 +32,16 @@ namespace ana {
 constexpr int kTracks = 7;        // shared + 6 modes
 constexpr int kGranules = 8;      // 16-B granules per player row
 constexpr int kRowFloats = 32;    // floats per player row (128 B)
-// Schedule link of a slot (K5), 8 bytes: word 0 = match of the player's next
-// occurrence (kNoMatch: none) | kLinkHasPred | kLinkHasPredMode, word 1 = match
-// of its next occurrence in the same game mode.  A match publishes each
-// player's shared granule tagged with word 0 and the mode granule tagged with
-// word 1, so the reader of a granule recognises the write it waits for by its
-// own match index (csrc/dataflow.hip).
-constexpr int kLinkWords = 2;
+// Schedule link of a slot (K5), 4 bytes: the match of the player's next
+// occurrence (kNoMatch: none) | kLinkHasPred if the player occurred earlier in
+// the window.  A match publishes each player's shared granule tagged with that
+// next match, so its reader recognises the write it waits for by its own match
+// index; mode granules are verified with per-mode write counters carried in the
+// shared granule's tag (csrc/dataflow.hip).
+constexpr int kLinkWords = 1;
 constexpr uint32_t kNoMatch = 0x0fffffffu;
 constexpr uint32_t kMatchMask = 0x0fffffffu;
 constexpr uint32_t kLinkHasPred = 1u << 30;      // the player occurred earlier in the window
-constexpr uint32_t kLinkHasPredMode = 1u << 31;  // ... earlier in a match of the same mode
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr int kSlotBits = 28;     // sort values carry slot | mode << kSlotBits
 constexpr int64_t kMaxSlots = 1ll << kSlotBits;

@@ -17,15 +17,13 @@
 //    4-B sc1 load per lane.
 //  * The oldest ready matches go to the wave's lane groups (G lanes = one
 //    match, one roster slot per lane).  A group gathers its players' 16-B
-//    granules {mu, epoch, sigma, reader match} (sc1 buffer loads), seeds,
-//    rates both tracks (rate_core.h), publishes the granules (sc1 stores) and
-//    at once decrements the deps counter of each player's next match.  The
-//    notification does not wait for the stores: each granule is tagged with
-//    the match that will read it next (the player's next match for the shared
-//    granule, its next same-mode match for the mode granule: schedule link
-//    words), a reader with an in-window predecessor checks for its own match
-//    index and retries the match otherwise, so a dependency hop costs no
-//    store round trip.
+//    granules (sc1 buffer loads), seeds, rates both tracks (rate_core.h),
+//    publishes the granules (sc1 stores) and at once decrements the deps
+//    counter of each player's next match.  The notification does not wait for
+//    the stores: the shared granule is tagged with the match that reads it
+//    next and carries per-mode write counters, the mode granule its write
+//    count; a reader verifies both and retries the match if a write has not
+//    landed, so a dependency hop costs no store round trip.
 //  * Software pipeline, one memory round trip per iteration: this iteration's
 //    granule/link/attribute loads, the next iteration's counter polls and the
 //    next chunk ticket retire in ONE vmcnt(0) wait.
@@ -72,14 +70,16 @@ __device__ __forceinline__ float group_sum(float x, int j, int gbase) {
   }
 }
 
-// {mu, epoch, sigma, writer match}: the tag words let a reader verify that the
-// write it depends on has landed
-__device__ __forceinline__ v4i granule(float mu, int epoch, float sig, uint32_t m) {
+// {mu, tag A, sigma, tag B}: the tag words let a reader verify that the write it
+// depends on has landed.  Shared granule: A = epoch | per-mode write counters << 8
+// (6 x 4 bits), B = the match that reads it next.  Mode granule: A = epoch,
+// B = that mode's write counter after this write (1..15, cyclic).
+__device__ __forceinline__ v4i granule(float mu, uint32_t a, float sig, uint32_t b) {
   v4i v;
   v.x = __float_as_int(mu);
-  v.y = epoch;
+  v.y = (int)a;
   v.z = __float_as_int(sig);
-  v.w = (int)m;
+  v.w = (int)b;
   return v;
 }
 
@@ -264,7 +264,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     int mode = 0, n0 = 0, n1 = 0, rank0 = 1, rank1 = 1, first = j, prevdup = -1;
     int32_t id = -1;
     bool inr = false, islast = false, own = false;
-    uint32_t lk0 = kNoMatch, lk1 = kNoMatch;  // schedule link words (common.h)
+    uint32_t lk0 = kNoMatch;  // schedule link (common.h): next match | has-earlier
     v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
     float4 at4 = make_float4(NAN, NAN, NAN, 0.f);
     if (my_h >= 0) {
@@ -295,9 +295,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       own = inr && first == j;
       if (inr) {
-        const uint2 lk = reinterpret_cast<const uint2*>(link)[m * S + j];
-        lk0 = lk.x;
-        lk1 = lk.y;
+        lk0 = link[m * S + j];
       }
       if (own) {
         const int off = id * (kRowFloats * 4);
@@ -365,16 +363,23 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // A deps counter can reach 0 before the writes it announces have landed
     // (notifications do not wait for store acknowledgements): a group whose
     // granules do not carry the tags of their last writers retries next iteration.
-    const bool fresh =
-        !own || ((!(lk0 & kLinkHasPred) || (gs.y == epoch && (uint32_t)gs.w == (uint32_t)m)) &&
-                 (!(lk0 & kLinkHasPredMode) || (gm.y == epoch && (uint32_t)gm.w == (uint32_t)m)));
-    // race detector: a granule of this launch tagged for a LATER reader means a
-    // successor wrote before this match read -- the ordering protocol broke
+    // The shared granule must name this match (if the player occurred earlier in
+    // the window); its counters say how many times this launch wrote the mode
+    // granule, and the mode granule must carry exactly that count.
+    const uint32_t sa = (uint32_t)gs.y;
+    const bool s_this = (sa & 0xffu) == (uint32_t)epoch;
+    const uint32_t counters = s_this ? sa >> 8 : 0u;
+    const uint32_t cnt = (counters >> (4 * mode)) & 15u;
+    const bool shared_ok = !(lk0 & kLinkHasPred) || (s_this && (uint32_t)gs.w == (uint32_t)m);
+    const bool mode_ok = cnt == 0u || (gm.y == epoch && (uint32_t)gm.w == cnt);
+    const bool fresh = !own || (shared_ok && mode_ok);
+    // race detector: a shared granule of this launch tagged for a LATER reader, or a
+    // mode granule one write AHEAD of the verified count, means a successor wrote
+    // before this match read -- the ordering protocol broke
     const bool overtaken =
-        own && (((lk0 & kLinkHasPred) && gs.y == epoch && (uint32_t)gs.w != kNoMatch &&
+        own && (((lk0 & kLinkHasPred) && s_this && (uint32_t)gs.w != kNoMatch &&
                  (uint32_t)gs.w > (uint32_t)m) ||
-                ((lk0 & kLinkHasPredMode) && gm.y == epoch && (uint32_t)gm.w != kNoMatch &&
-                 (uint32_t)gm.w > (uint32_t)m));
+                (shared_ok && gm.y == epoch && (uint32_t)gm.w == cnt % 15u + 1u));
     if (__ballot(overtaken) != 0ull && lane == 0) atomicOr(&ctrl[2], 1u);
     const uint64_t stale_lanes = __ballot(!fresh);
     if (stale_lanes) {
@@ -419,6 +424,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       psm = __shfl(psm, src);
       pflags = (uint32_t)__shfl((int)pflags, src);
       const float rsmu = __shfl(smu, src), rssg = __shfl(ssg, src);
+      const uint32_t rcnt = (uint32_t)__shfl((int)counters, src);
       const float rmmu = __shfl(mmu, src), rmsg = __shfl(msg, src);
       if (gst == kRated && (n0 == 0 || n1 == 0)) gst = kErrEmptyRoster;
       float nsm = NAN, nss = NAN, nmm = NAN, nms = NAN, dl = NAN, q = NAN;
@@ -449,13 +455,17 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       const bool ok = gst == kRated && inr;
       if (inr && islast) {  // publish: new values, or the untouched ones on error
         const int off = id * (kRowFloats * 4);
-        // tagged with the match that will read them next (link words 0 and 1)
+        // shared granule: tagged with the next reader + bumped mode counter;
+        // mode granule: tagged with its new write count
         const uint32_t succ = lk0 & kMatchMask;
+        const uint32_t c = ((rcnt >> (4 * mode)) & 15u) % 15u + 1u;
+        const uint32_t ncnt = (rcnt & ~(15u << (4 * mode))) | (c << (4 * mode));
+        const uint32_t stag = (uint32_t)epoch | (ncnt << 8);
         __builtin_amdgcn_raw_buffer_store_b128(
-            ok ? granule(nmm, epoch, nms, lk1) : granule(rmmu, epoch, rmsg, lk1),
+            ok ? granule(nmm, (uint32_t)epoch, nms, c) : granule(rmmu, (uint32_t)epoch, rmsg, c),
             rs, off + 16 * (1 + mode), 0, 16);
         __builtin_amdgcn_raw_buffer_store_b128(
-            ok ? granule(nsm, epoch, nss, succ) : granule(rsmu, epoch, rssg, succ),
+            ok ? granule(nsm, stag, nss, succ) : granule(rsmu, stag, rssg, succ),
             rs, off, 0, 16);
         if (succ != kNoMatch)  // the successor verifies the tags, so no store wait
           __hip_atomic_fetch_add((gu32*)(deps + succ), 0xffffffffu, __ATOMIC_RELAXED,

@@ -36,13 +36,12 @@ int host_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M) {
 }
 
 // Same outputs as the device schedule (common.h kLinkWords): link[slot] =
-// {next match | has-earlier flags, next same-mode match}; deps[m].  Slots of
-// matches that rate nothing are left unwritten.
+// next match of the player | has-earlier flag; deps[m].  Slots of matches that
+// rate nothing are left unwritten.
 template <int K>
 static void schedule_k(const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps) {
   constexpr int S = 2 * K;
   std::vector<uint32_t> last((size_t)P, kNone);
-  std::vector<uint32_t> last_mode((size_t)P * kModes, kNone);
   for (int64_t m = 0; m < M; ++m) {
     MatchWork<float, K> w;
     decode_record<float, K>(rec + m * (S + 2), P, w);
@@ -52,22 +51,13 @@ static void schedule_k(const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
       if (w.id[j] < 0) continue;
       const uint32_t slot = (uint32_t)(m * S + j);
       const size_t p = (size_t)w.id[j];
-      uint32_t* l = link + (size_t)slot * kLinkWords;
-      l[0] = kNoMatch;
-      l[1] = kNoMatch;
-      uint32_t& lm = last_mode[p * kModes + w.mode];
+      link[slot] = kNoMatch;
       if (last[p] != kNone) {
-        uint32_t* pl = link + (size_t)last[p] * kLinkWords;
-        pl[0] = (pl[0] & ~kMatchMask) | (uint32_t)m;
-        l[0] |= kLinkHasPred;
+        link[last[p]] = (link[last[p]] & ~kMatchMask) | (uint32_t)m;
+        link[slot] |= kLinkHasPred;
         if (w.first[j] == j) ++deps[m];
       }
-      if (lm != kNone) {
-        link[(size_t)lm * kLinkWords + 1] = (uint32_t)m;
-        l[0] |= kLinkHasPredMode;
-      }
       last[p] = slot;
-      lm = slot;
     }
   }
 }

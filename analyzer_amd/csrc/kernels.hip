@@ -2,10 +2,9 @@
 //
 //  K7  gen_roster_kernel / gen_stream_kernel: synthetic inputs (counter RNG).
 //  K5  schedule: one stable LSD radix sort of the slots (radix_sort.hip)
-//      by player gives, per slot, the matches of the player's next occurrence
-//      overall and in the same mode plus two has-earlier flags (link, 8 B),
-//      and per match the number of distinct players with an earlier
-//      occurrence (deps).
+//      by player gives, per slot, the match of the player's next occurrence
+//      and a has-earlier flag (link, 4 B), and per match the number of
+//      distinct players with an earlier occurrence (deps).
 //  The executor that consumes the schedule lives in dataflow.hip.
 //
 // Reference semantics: /root/reference/rater.py:69-169; the sequential loop the
@@ -97,7 +96,6 @@ int launch_reset_tags(float* state, int64_t P, hipStream_t s) {
 // ------------------------------------------------------------------- schedule
 // Slots of matches that touch no state (unsupported mode, rosters != 2, AFK,
 // malformed) are keyed past the last player so they neither wait nor publish.
-// The sort value carries the slot and the match's mode (for the same-mode link).
 template <int K>
 __global__ void sched_keys_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t P,
                                   uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
@@ -107,79 +105,27 @@ __global__ void sched_keys_kernel(const int32_t* __restrict__ rec, int64_t M, ui
   MatchWork<float, K> w;
   decode_record<float, K>(rec + m * (S + 2), (int64_t)P, w);
   const bool rates = w.status == kRated;
-  const uint32_t mbits = rates ? (uint32_t)w.mode << kSlotBits : 0u;
 #pragma unroll
   for (int j = 0; j < S; ++j) {
     keys[m * S + j] = rates && w.id[j] >= 0 ? (uint32_t)w.id[j] : P;
-    vals[m * S + j] = (uint32_t)(m * S + j) | mbits;
+    vals[m * S + j] = (uint32_t)(m * S + j);
   }
 }
 
-// link[slot] = {next match of the player | has-earlier | has-earlier-same-mode,
-// next match of the player in the same mode}.  A block stages its 256 sorted
-// positions plus 64-entry halos on both sides in LDS; same-mode neighbours are
-// almost always within a halo (6 modes) and are otherwise found by walking on
-// in global memory, bounded by the player's run.  One 8-B scattered store per
-// slot.
+// link[slot] = next match of the player (kNoMatch: none) | kLinkHasPred.  Sorted
+// neighbours only: three coalesced key loads and one 4-B scattered store per slot.
 template <int K>
 __global__ void __launch_bounds__(256)
 sched_link_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, int64_t n,
                   uint32_t kend, uint32_t* __restrict__ link) {
   constexpr uint32_t S = 2 * K;
-  constexpr uint32_t kSlotMask = (1u << kSlotBits) - 1u;
-  constexpr int kHalo = 64;
-  constexpr int kSpan = kHalo + 256 + kHalo;
-  __shared__ uint32_t sk[kSpan], sv[kSpan];
-  const int64_t base = (int64_t)blockIdx.x * 256 - kHalo;
-  for (int t = threadIdx.x; t < kSpan; t += 256) {
-    const int64_t q = base + t;
-    const bool in = q >= 0 && q < n;
-    sk[t] = in ? keys[q] : 0xffffffffu;  // never equal to a real key (< kend < 2^31)
-    sv[t] = in ? vals[q] : 0u;
-  }
-  __syncthreads();
-  const int li = threadIdx.x + kHalo;
-  if (base + li >= n) return;
-  const uint32_t k = sk[li];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = keys[i];
   if (k >= kend) return;
-  const uint32_t v = sv[li];
-  const uint32_t mode = v >> kSlotBits;
-  uint32_t w0 = kNoMatch, w1 = kNoMatch;
-  if (sk[li + 1] == k) {  // later occurrences: next one, next one in the same mode
-    w0 = (sv[li + 1] & kSlotMask) / S;
-    int q = li + 1;
-    for (; q < kSpan && sk[q] == k; ++q)
-      if ((sv[q] >> kSlotBits) == mode) {
-        w1 = (sv[q] & kSlotMask) / S;
-        break;
-      }
-    if (q == kSpan)  // ran off the halo inside the player's run
-      for (int64_t g = base + kSpan; g < n && keys[g] == k; ++g) {
-        const uint32_t u = vals[g];
-        if ((u >> kSlotBits) == mode) {
-          w1 = (u & kSlotMask) / S;
-          break;
-        }
-      }
-  }
-  if (sk[li - 1] == k) {  // earlier occurrences
-    w0 |= kLinkHasPred;
-    int q = li - 1;
-    bool found = false;
-    for (; q >= 0 && sk[q] == k; --q)
-      if ((sv[q] >> kSlotBits) == mode) {
-        found = true;
-        break;
-      }
-    if (q < 0)
-      for (int64_t g = base - 1; g >= 0 && keys[g] == k; --g)
-        if ((vals[g] >> kSlotBits) == mode) {
-          found = true;
-          break;
-        }
-    if (found) w0 |= kLinkHasPredMode;
-  }
-  reinterpret_cast<uint2*>(link)[v & kSlotMask] = make_uint2(w0, w1);
+  uint32_t w = (i + 1 < n && keys[i + 1] == k) ? vals[i + 1] / S : kNoMatch;
+  if (i > 0 && keys[i - 1] == k) w |= kLinkHasPred;
+  link[vals[i]] = w;
 }
 
 // deps[m] = number of distinct players of m with an earlier occurrence in the window

@@ -44,15 +44,13 @@ class NativeRateError(RuntimeError):
 
 
 class Schedule(NamedTuple):
-    # [M, 2K, 2] int32 per slot: next match of the player (NO_MATCH: none)
-    # | HAS_PRED | HAS_PRED_MODE, next match of the player in the same mode
+    # [M, 2K] int32 per slot: next match of the player (NO_MATCH: none) | HAS_PRED
     link: torch.Tensor
     deps: torch.Tensor  # [M] int32: players with an earlier occurrence in the window
 
     NO_MATCH = 0x0FFFFFFF
     MATCH_MASK = 0x0FFFFFFF
     HAS_PRED = 1 << 30
-    HAS_PRED_MODE = 1 << 31
 
 
 @dataclass
@@ -194,16 +192,15 @@ class BatchRater:
     # ------------------------------------------------------------- schedule
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
                  tag: str = "") -> Schedule:
-        """Dependency structure of a window (K5): per slot the matches of its
-        player's next occurrence (any mode / same mode) and whether it occurred
-        earlier, and per match the number of distinct players with an earlier
-        occurrence.  ``deps`` is consumed (counted
+        """Dependency structure of a window (K5): per slot the match of its
+        player's next occurrence and whether it occurred earlier, and per match
+        the number of distinct players with an earlier occurrence.  ``deps`` is consumed (counted
         down to 0) by the device rate launch, so a schedule is single-use there.
         ``tag`` selects a separate buffer set (to prepare the next window while the
         current one is being rated)."""
         M = rec.shape[0]
         dev = rec.device
-        link = self._buffer(dev, "link" + tag, M * 2 * K * 2, torch.int32).view(M, 2 * K, 2)
+        link = self._buffer(dev, "link" + tag, M * 2 * K, torch.int32).view(M, 2 * K)
         deps = self._buffer(dev, "deps" + tag, M, torch.int32)
         if rec.is_cuda:
             nbytes = native().schedule_workspace_bytes(M * 2 * K, num_players)

@@ -57,7 +57,7 @@ static void run(int K, int64_t P, int64_t M, uint64_t seed) {
     for (int j = 0; j < S; ++j) {
       const int32_t id = rec[m * R + j];
       if (id < 0 || level[m] == 0) continue;
-      const uint32_t succ = link[(m * S + j) * kLinkWords] & kMatchMask;
+      const uint32_t succ = link[m * S + j] & kMatchMask;
       if (succ != kNoMatch) {
         CHECK((int64_t)succ >= m && (int64_t)succ < M);
         bool found = false;  // the successor really contains the player

@@ -68,9 +68,9 @@ def test_schedule_links_host():
 
     rec = make_stream(StreamSpec(team_size=3, seed=9, p_afk=0.1), 300, 20)
     link, deps = BatchRater().schedule(rec, 3, 20)
-    link = link.numpy().reshape(-1, 2).astype(np.int64) & 0xFFFFFFFF
+    link = link.numpy().reshape(-1).astype(np.int64) & 0xFFFFFFFF
     deps = deps.numpy()
-    occ = {}  # player -> [(match, mode, slot)] in stream order
+    occ = {}  # player -> [(match, slot)] in stream order
     expect_deps = np.zeros(rec.shape[0], dtype=np.int64)
     for m in range(rec.shape[0]):
         if int(rec[m, 7]) & 4:  # AFK: no state, not scheduled
@@ -82,17 +82,14 @@ def test_schedule_links_host():
             if pid not in seen_here:
                 seen_here.add(pid)
                 expect_deps[m] += pid in occ
-            occ.setdefault(pid, []).append((m, int(rec[m, 6]) & 0xFF, m * 6 + j))
+            occ.setdefault(pid, []).append((m, m * 6 + j))
     assert (deps == expect_deps).all()
     for pid, lst in occ.items():
-        for i, (m, mode, slot) in enumerate(lst):
-            w0, w1 = int(link[slot, 0]), int(link[slot, 1])
+        for i, (m, slot) in enumerate(lst):
+            w = int(link[slot])
             nxt = lst[i + 1][0] if i + 1 < len(lst) else Schedule.NO_MATCH
-            nxt_mode = next((x[0] for x in lst[i + 1:] if x[1] == mode), Schedule.NO_MATCH)
-            assert w0 & Schedule.MATCH_MASK == nxt
-            assert w1 == nxt_mode
-            assert bool(w0 & Schedule.HAS_PRED) == (i > 0)
-            assert bool(w0 & Schedule.HAS_PRED_MODE) == any(x[1] == mode for x in lst[:i])
+            assert w & Schedule.MATCH_MASK == nxt
+            assert bool(w & Schedule.HAS_PRED) == (i > 0)
 
 
 def test_status_counts_and_any_afk():
