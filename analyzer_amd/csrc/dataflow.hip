@@ -39,6 +39,10 @@
 #include "rate_core.h"
 #include "telemetry_dev.h"
 
+#ifndef ANA_HELD
+#define ANA_HELD 4
+#endif
+
 namespace ana {
 
 typedef __attribute__((address_space(1))) unsigned int gu32;
@@ -48,7 +52,7 @@ constexpr uint64_t kTimeoutTicks = 500000000ull;  // 5 s of the 100 MHz s_memrea
 constexpr uint64_t kProgressTicks = 50000000ull;  // re-read the progress counter every 0.5 s
 constexpr int kHeads = 8;                          // ticket shards
 constexpr int kChunk = 64;                         // matches per ticket = one per lane
-constexpr int kHeld = 4;                           // chunks a wave keeps in flight
+constexpr int kHeld = ANA_HELD;                   // chunks a wave keeps in flight
 constexpr int kWavesPerBlock = 4;
 
 // sum over the G lanes of a group, result in every lane of the group.  Power-of-two
