@@ -269,6 +269,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     int32_t id = -1;
     bool inr = false, islast = false, own = false;
     uint32_t lk0 = kNoMatch;  // schedule link (common.h): next match | has-earlier
+    bool any_dup = false;     // wave-uniform: a match of this batch names a player twice
     v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
     float4 at4 = make_float4(NAN, NAN, NAN, 0.f);
     if (my_h >= 0) {
@@ -286,15 +287,18 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       inr = j < S && rpos < (r0 ? n0 : n1);
       id = inr ? lr[j] : -1;
       islast = true;
+      any_dup = __ballot((m1 >> 3) & 1u) != 0ull;
+      if (any_dup) {  // some match of this batch repeats a player
 #pragma unroll
-      for (int q = 0; q < S; ++q) {
-        const int32_t oid = __shfl(id, gbase + q);
-        if (id >= 0 && oid == id) {
-          if (q < j) {
-            if (first == j) first = q;
-            prevdup = q;
+        for (int q = 0; q < S; ++q) {
+          const int32_t oid = __shfl(id, gbase + q);
+          if (id >= 0 && oid == id) {
+            if (q < j) {
+              if (first == j) first = q;
+              prevdup = q;
+            }
+            if (q > j) islast = false;
           }
-          if (q > j) islast = false;
         }
       }
       own = inr && first == j;
@@ -338,6 +342,15 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
       for (int h = 0; h < kHeld; ++h) if (h == staging) cb = cbase[h];
       const int64_t mm = cb + lane;
+      {  // flag matches that name one player twice (bit 3 of meta1, free in the
+         // stream layout) so processing skips the duplicate scan for the rest
+        bool dup = false;
+#pragma unroll
+        for (int a = 0; a < S; ++a)
+#pragma unroll
+          for (int b = a + 1; b < S; ++b) dup |= r[a] >= 0 && r[a] == r[b];
+        r[S + 1] = dup ? (r[S + 1] | 8) : (r[S + 1] & ~8);
+      }
 #pragma unroll
       for (int k = 0; k < R; ++k) lrec[wv][staging][lane * R + k] = r[k];
       const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
@@ -420,16 +433,23 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       const uint64_t eb = __ballot(lst != kRated) & gmask;
       uint8_t gst = kRated;
       if (eb) gst = (uint8_t)__shfl((int)lst, (int)__builtin_ctzll(eb));
-      // duplicates see the pre-match values of their first occurrence
-      const int src = gbase + first;
-      pms = __shfl(pms, src);
-      pss = __shfl(pss, src);
-      pmm = __shfl(pmm, src);
-      psm = __shfl(psm, src);
-      pflags = (uint32_t)__shfl((int)pflags, src);
-      const float rsmu = __shfl(smu, src), rssg = __shfl(ssg, src);
-      const uint32_t rcnt = (uint32_t)__shfl((int)counters, src);
-      const float rmmu = __shfl(mmu, src), rmsg = __shfl(msg, src);
+      // duplicates see the pre-match values of their first occurrence (the
+      // broadcasts only run when the batch has a repeated player)
+      float rsmu = smu, rssg = ssg, rmmu = mmu, rmsg = msg;
+      uint32_t rcnt = counters;
+      if (any_dup) {
+        const int src = gbase + first;
+        pms = __shfl(pms, src);
+        pss = __shfl(pss, src);
+        pmm = __shfl(pmm, src);
+        psm = __shfl(psm, src);
+        pflags = (uint32_t)__shfl((int)pflags, src);
+        rsmu = __shfl(smu, src);
+        rssg = __shfl(ssg, src);
+        rcnt = (uint32_t)__shfl((int)counters, src);
+        rmmu = __shfl(mmu, src);
+        rmsg = __shfl(msg, src);
+      }
       if (gst == kRated && (n0 == 0 || n1 == 0)) gst = kErrEmptyRoster;
       float nsm = NAN, nss = NAN, nmm = NAN, nms = NAN, dl = NAN, q = NAN;
       if (gst == kRated) {
@@ -451,7 +471,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         if ((__ballot(bad_num) & gmask) != 0ull) gst = kErrNumeric;
         // conservative-skill delta (rater.py:150-153), in slot (= write) order
         const float cur = nsm - nss;
-        const float prevw = __shfl(cur, gbase + (prevdup >= 0 ? prevdup : j));
+        const float prevw = any_dup ? __shfl(cur, gbase + (prevdup >= 0 ? prevdup : j)) : cur;
         if (prevdup >= 0) dl = cur - prevw;
         else if (pflags & 1u) dl = cur - (pms - pss);
         else dl = 0.f;
