@@ -55,14 +55,28 @@ constexpr int kChunk = 64;                         // matches per ticket = one p
 constexpr int kHeld = ANA_HELD;                   // chunks a wave keeps in flight
 constexpr int kWavesPerBlock = 4;
 
-// sum over the G lanes of a group, result in every lane of the group.  Power-of-two
-// groups: xor butterfly.  Other sizes (G = 2K lanes, no idle lanes per match): tree
-// reduction to the group's first lane with bpermutes, then a broadcast.
+// sum over the G lanes of a group, result in every lane of the group.
+// Power-of-two groups up to a DPP row (16 lanes): a butterfly of DPP lane moves
+// (quad_perm xor 1, xor 2, row_half_mirror, row_mirror), one VALU op per step with
+// no LDS round trip -- the previous bpermute butterfly put 15 dependent LDS
+// trips into every rated batch.  After the two quad steps every lane of a quad
+// holds the quad sum, so a mirror (lane i <-> 7-i, or 15-i) lands in the
+// other half and completes the next level.  Wider power-of-two groups finish
+// with xor shuffles; other sizes (G = 2K lanes, no idle lanes per match) use a
+// bpermute tree to the group's first lane and a broadcast.
+template <int Ctrl>
+__device__ __forceinline__ float dpp_mov(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), Ctrl, 0xf, 0xf, true));
+}
 template <int G>
 __device__ __forceinline__ float group_sum(float x, int j, int gbase) {
   if constexpr ((G & (G - 1)) == 0) {
+    if constexpr (G >= 2) x += dpp_mov<0xb1>(x);   // quad_perm [1,0,3,2]
+    if constexpr (G >= 4) x += dpp_mov<0x4e>(x);   // quad_perm [2,3,0,1]
+    if constexpr (G >= 8) x += dpp_mov<0x141>(x);  // row_half_mirror
+    if constexpr (G >= 16) x += dpp_mov<0x140>(x); // row_mirror
 #pragma unroll
-    for (int off = G / 2; off >= 1; off >>= 1) x += __shfl_xor(x, off);
+    for (int off = 16; off < G; off <<= 1) x += __shfl_xor(x, off);
     return x;
   } else {
 #pragma unroll
@@ -456,14 +470,31 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         const float sgn = r0 ? 1.f : -1.f;
         const float s_c2 = group_sum<G>(inr ? pss * pss + tau2 : 0.f, j, gbase);
         const float s_d = group_sum<G>(inr ? sgn * pms : 0.f, j, gbase);
-        const float m_c2 = group_sum<G>(inr ? psm * psm + tau2 : 0.f, j, gbase);
         const float m_d = group_sum<G>(inr ? sgn * pmm : 0.f, j, gbase);
         const float m_q = group_sum<G>(inr ? psm * psm : 0.f, j, gbase);
         const int n = n0 + n1;
         const float nb2 = (float)n * beta2;
+        const float m_c2 = m_q + (float)n * tau2;
         q = quality_from_sums<float>(n, m_q, m_d, beta2);
-        const UpdCoef<float> ks = update_coef<float>(s_d, nb2 + s_c2, rank0, rank1);
-        const UpdCoef<float> km = update_coef<float>(m_d, nb2 + m_c2, rank0, rank1);
+        UpdCoef<float> ks, km;
+        if constexpr (G == 8 || G == 16) {
+          // the two tracks' coefficients in the two halves of the group (one erfc/exp
+          // per lane instead of two), swapped across with a mirror DPP move
+          constexpr int kMirror = G == 8 ? 0x141 : 0x140;
+          const bool sh = j < G / 2;
+          const UpdCoef<float> k =
+              update_coef<float>(sh ? s_d : m_d, nb2 + (sh ? s_c2 : m_c2), rank0, rank1);
+          UpdCoef<float> o;
+          o.a0 = dpp_mov<kMirror>(k.a0);
+          o.a1 = dpp_mov<kMirror>(k.a1);
+          o.wf = dpp_mov<kMirror>(k.wf);
+          o.c2 = dpp_mov<kMirror>(k.c2);
+          ks = sh ? k : o;
+          km = sh ? o : k;
+        } else {
+          ks = update_coef<float>(s_d, nb2 + s_c2, rank0, rank1);
+          km = update_coef<float>(m_d, nb2 + m_c2, rank0, rank1);
+        }
         apply_coef<float>(ks, r0, pms, pss, tau2, nsm, nss);
         apply_coef<float>(km, r0, pmm, psm, tau2, nmm, nms);
         const bool bad_num = inr && !(isfinite(nsm) && isfinite(nss) && isfinite(nmm) &&
@@ -534,6 +565,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
     for (int h = 0; h < kHeld; ++h) held |= cbase[h] >= 0;
     if (exhausted && !held && !tk_pending) {
+      if (lane == 0)  // diagnostics: wave iterations (ctrl[15])
+        __hip_atomic_fetch_add((gu32*)&ctrl[15], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       while (!tele_done) {  // leftover telemetry tiles
         const int64_t t = tele_claim();
         if (t < 0) tele_done = true;
@@ -581,8 +614,9 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
                 const RateParams& prm, const TelemetryParams& tp, int blocks, hipStream_t s) {
   const int64_t M = prm.num_matches;
   // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] retired chunks, [4..11] tickets,
-  // [12] telemetry tile ticket, [13] malformed telemetry events, [14] stale reads retried
-  if (hipMemsetAsync(ctrl + 1, 0, 14 * 4, s) != hipSuccess) return (int)hipGetLastError();
+  // [12] telemetry tile ticket, [13] malformed telemetry events, [14] stale reads retried,
+  // [15] wave iterations
+  if (hipMemsetAsync(ctrl + 1, 0, 15 * 4, s) != hipSuccess) return (int)hipGetLastError();
   if (M <= 0) return 0;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
   if (prm.epoch < 1 || prm.epoch > 255) return (int)hipErrorInvalidValue;

@@ -258,6 +258,10 @@ class BatchRater:
         yet landed and were retried (diagnostics; syncs)."""
         return int(self._buffer(device, "ctrl", 16, torch.int32)[14].item())
 
+    def iterations(self, device) -> int:
+        """Wave iterations of the last executor launch (diagnostics; syncs)."""
+        return int(self._buffer(device, "ctrl", 16, torch.int32)[15].item())
+
     def telemetry_errors(self, device) -> int:
         """Malformed telemetry events seen by the last fused launch (syncs)."""
         return int(self._buffer(device, "ctrl", 16, torch.int32)[13].item())

@@ -68,9 +68,11 @@ def main():
             t2 = time.perf_counter()
             br.check_errors(dev)
             stale = br.stale_retries(dev)
+            iters = br.iterations(dev)
             results.setdefault(key, []).append(((t1 - t0) * 1e3, (t2 - t1) * 1e3))
-            print("round %d %s schedule %7.2f ms rate %8.2f ms stale retries %d"
-                  % (rnd, key, (t1 - t0) * 1e3, (t2 - t1) * 1e3, stale), flush=True)
+            print("round %d %s schedule %7.2f ms rate %8.2f ms stale retries %d iterations %d "
+                  "(%.2f matches/iteration)" % (rnd, key, (t1 - t0) * 1e3, (t2 - t1) * 1e3, stale,
+                                                iters, M / max(iters, 1)), flush=True)
     summary = {b: {"schedule_ms_min": min(x[0] for x in v), "rate_ms_min": min(x[1] for x in v),
                    "rate_ms_median": sorted(x[1] for x in v)[len(v) // 2]} for b, v in results.items()}
     print(json.dumps({"pattern": args.pattern, "players": P, "matches": M, "team_size": K, "hot": args.hot,
