@@ -114,6 +114,27 @@ ANA_HD uint32_t pack_meta1(bool w0, bool w1, uint32_t afk_mask) {
   return (w0 ? 1u : 0u) | (w1 ? 2u : 0u) | (afk_mask ? 4u : 0u) | ((afk_mask & 0xffffffu) << 8);
 }
 
+// Outcome of a stream record that is decided before any state is read: kRated
+// ("to be rated"), or unsupported / malformed / invalid rosters / AFK.  The
+// precedence is rate_core.h decode_record's.
+template <int K>
+ANA_HD uint8_t early_status(const int32_t* r, int64_t P) {
+  constexpr int S = 2 * K;
+  const uint32_t m0 = (uint32_t)r[S], m1 = (uint32_t)r[S + 1];
+  const int n0 = meta_n0(m0), n1 = meta_n1(m0);
+  bool bad = n0 > K || n1 > K;
+#pragma unroll
+  for (int j = 0; j < S; ++j) {
+    const int pos = j < K ? j : j - K;
+    if (pos < (j < K ? n0 : n1) && (r[j] < 0 || (int64_t)r[j] >= P)) bad = true;
+  }
+  if (meta_mode(m0) >= kModes) return kUnsupportedMode;
+  if (bad) return kErrBadRecord;
+  if (meta_nrosters(m0) != 2) return kInvalidRosters;
+  if (meta_afk(m1)) return kAfk;
+  return kRated;
+}
+
 // ---------------------------------------------------------------- RNG (K7)
 // Counter-based: every random number is a pure function of (seed, index,
 // field), so device and host generators produce bit-identical streams and any

@@ -5,20 +5,22 @@
 // ORDER BY created_at + a sequential loop (/root/reference/worker.py:176-192)
 // -- without rounds or grid barriers (Kahn's algorithm over per-player chains):
 //
-//  * The schedule prepass (kernels.hip) gives every slot the slot of its
-//    player's next occurrence (link) and every match the number of distinct
-//    players with an earlier occurrence (deps).
+//  * The schedule prepass (kernels.hip) gives every slot the match of its
+//    player's next occurrence and a has-earlier flag (link).  A match is ready
+//    when its completion counter (deps, zeroed by the prepass) reaches the
+//    number of its distinct players with an earlier occurrence, which the wave
+//    counts from the links when it stages the chunk.
 //  * 8 sharded tickets (MICROARCH "dequeue") hand out chunks of 64
 //    consecutive matches.  A wave holds up to 4 chunks (256 matches; records
 //    cached in LDS), so ~1M matches wait in flight GPU-wide: per-player
 //    dependency levels of a random stream spread over hundreds of thousands of
 //    matches, and a narrower window starves the machine.  Waiting costs nothing
-//    per match: the wave polls its chunks' deps counters with one coalesced
-//    4-B sc1 load per lane.
+//    per match: the wave polls its chunks' counters with one coalesced 4-B sc1
+//    load per lane.
 //  * The oldest ready matches go to the wave's lane groups (G lanes = one
 //    match, one roster slot per lane).  A group gathers its players' 16-B
 //    granules (sc1 buffer loads), seeds, rates both tracks (rate_core.h),
-//    publishes the granules (sc1 stores) and at once decrements the deps
+//    publishes the granules (sc1 stores) and at once increments the
 //    counter of each player's next match.  The notification does not wait for
 //    the stores: the shared granule is tagged with the match that reads it
 //    next and carries per-mode write counters, the mode granule its write
@@ -119,25 +121,6 @@ __device__ __forceinline__ int nth_set_bit(uint64_t x, int k) {
   return pos;
 }
 
-// early outcome of a match that touches no state (decided when its chunk arrives)
-template <int K>
-__device__ __forceinline__ uint8_t early_status(const int32_t* r, int64_t P) {
-  constexpr int S = 2 * K;
-  const uint32_t m0 = (uint32_t)r[S], m1 = (uint32_t)r[S + 1];
-  const int n0 = meta_n0(m0), n1 = meta_n1(m0);
-  bool bad = n0 > K || n1 > K;
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    const int pos = j < K ? j : j - K;
-    if (pos < (j < K ? n0 : n1) && (r[j] < 0 || (int64_t)r[j] >= P)) bad = true;
-  }
-  if (meta_mode(m0) >= kModes) return kUnsupportedMode;
-  if (bad) return kErrBadRecord;
-  if (meta_nrosters(m0) != 2) return kInvalidRosters;
-  if (meta_afk(m1)) return kAfk;
-  return kRated;
-}
-
 template <int K, int G>
 __global__ void __launch_bounds__(256)
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
@@ -172,12 +155,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 
   int64_t cbase[kHeld];   // wave-uniform: first match of each held chunk, -1 = free slot
   uint64_t pend[kHeld];   // wave-uniform: stateful matches not yet handed to a group
-  uint32_t dval[kHeld];   // per lane: deps counter of match cbase+lane, as last polled
+  uint32_t dval[kHeld];   // per lane: completion counter of match cbase+lane, as last polled
+  uint32_t need[kHeld];   // per lane: the count at which that match is ready
 #pragma unroll
   for (int h = 0; h < kHeld; ++h) {
     cbase[h] = -1;
     pend[h] = 0ull;
-    dval[h] = 1u;
+    dval[h] = kNone;
+    need[h] = 0u;
   }
   bool exhausted = false, tk_pending = false;
   unsigned tk = 0;                 // ticket returned to lane 0
@@ -198,8 +183,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // ---------------------------------------------- (1) a ticket came back: stage its chunk
     int staging = -1;
     int32_t r[R];
+    uint32_t lks[S];  // the staged match's links: its readiness count
 #pragma unroll
     for (int k = 0; k < R; ++k) r[k] = -1;
+#pragma unroll
+    for (int k = 0; k < S; ++k) lks[k] = 0u;
     if (tk_pending) {
       const unsigned t = __shfl(tk, 0);
       tk_pending = false;
@@ -226,6 +214,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
             for (int k = 0; k < R; ++k) r[k] = src[k];
           }
+          const uint2* ls = reinterpret_cast<const uint2*>(link + m * S);  // S even: 8-B aligned
+#pragma unroll
+          for (int k = 0; k < S / 2; ++k) {
+            const uint2 v = ls[k];
+            lks[2 * k] = v.x;
+            lks[2 * k + 1] = v.y;
+          }
         }
       }
     }
@@ -233,7 +228,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // ---------------------------------------------- (2) readiness from the last poll
     uint64_t ready[kHeld];
 #pragma unroll
-    for (int h = 0; h < kHeld; ++h) ready[h] = __ballot(dval[h] == 0u) & pend[h];
+    for (int h = 0; h < kHeld; ++h) ready[h] = __ballot(dval[h] == need[h]) & pend[h];
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
 
     // ---------------------------------------------- (3) oldest ready matches -> groups
@@ -271,7 +266,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     if (prm.spec > 0 && nassigned < NG) {
       uint64_t cand[kHeld];
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h) cand[h] = __ballot(dval[h] == 1u) & pend[h];
+      for (int h = 0; h < kHeld; ++h) cand[h] = __ballot(dval[h] + 1u == need[h]) & pend[h];
       const int lim = nassigned + prm.spec < NG ? nassigned + prm.spec : NG;
       assign(cand, lim);
     }
@@ -356,13 +351,27 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
       for (int h = 0; h < kHeld; ++h) if (h == staging) cb = cbase[h];
       const int64_t mm = cb + lane;
-      {  // flag matches that name one player twice (bit 3 of meta1, free in the
-         // stream layout) so processing skips the duplicate scan for the rest
+      // flag matches that name one player twice (bit 3 of meta1, free in the
+      // stream layout) so processing skips the duplicate scan for the rest; the
+      // match is ready once every distinct player with an earlier occurrence
+      // (kLinkHasPred on its first slot) has been published: that many
+      // increments of its completion counter
+      uint32_t nd = 0u;
+      {
+        const uint32_t m0s = (uint32_t)r[S];
         bool dup = false;
 #pragma unroll
-        for (int a = 0; a < S; ++a)
+        for (int a = 0; a < S; ++a) {
+          const bool ina = (a < K ? a : a - K) < (a < K ? meta_n0(m0s) : meta_n1(m0s));
+          bool firsto = ina;
 #pragma unroll
-          for (int b = a + 1; b < S; ++b) dup |= r[a] >= 0 && r[a] == r[b];
+          for (int b = 0; b < a; ++b) {
+            const bool inb = (b < K ? b : b - K) < (b < K ? meta_n0(m0s) : meta_n1(m0s));
+            dup |= r[a] >= 0 && r[a] == r[b];
+            if (inb && r[b] == r[a]) firsto = false;
+          }
+          if (firsto && (lks[a] & kLinkHasPred)) ++nd;
+        }
         r[S + 1] = dup ? (r[S + 1] | 8) : (r[S + 1] & ~8);
       }
 #pragma unroll
@@ -385,13 +394,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       for (int h = 0; h < kHeld; ++h)
         if (h == staging) {
           pend[h] = pm;
-          dval[h] = 1u;  // first poll next iteration
+          dval[h] = kNone;  // first poll next iteration
+          need[h] = nd;
           if (pm == 0ull) cbase[h] = -1;
         }
     }
 
     // ---------------------------------------------- (10) rate this batch
-    // A deps counter can reach 0 before the writes it announces have landed
+    // A counter can reach its count before the writes it announces have landed
     // (notifications do not wait for store acknowledgements): a group whose
     // granules do not carry the tags of their last writers retries next iteration.
     // The shared granule must name this match (if the player occurred earlier in
@@ -523,7 +533,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
             ok ? granule(nsm, stag, nss, succ) : granule(rsmu, stag, rssg, succ),
             rs, off, 0, 16);
         if (succ != kNoMatch)  // the successor verifies the tags, so no store wait
-          __hip_atomic_fetch_add((gu32*)(deps + succ), 0xffffffffu, __ATOMIC_RELAXED,
+          __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_AGENT);
       }
       if (ok && prm.record_first_prior && own) {

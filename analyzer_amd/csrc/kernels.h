@@ -25,9 +25,18 @@ size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
 size_t radix_sort_workspace_bytes(int64_t n);
 int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
                             int64_t n, int bits, void* ws, int* result_in_alt, hipStream_t s);
-// link: uint32 [M][2K] = next slot of the same player (0x7fffffff: none)
-//       | 0x80000000 if the player has an earlier occurrence in the window
-// deps: int32 [M] = distinct players with an earlier occurrence in the window
+// The schedule's sort (radix_sort.hip): link[slot] for every slot of a
+// stateful match (next match of its player | kLinkHasPred), from a stable sort
+// of the stream's slots by player fused with the record decode and the links.
+// ws: radix_sort_workspace_bytes(M * 2K) bytes; ka..vb: M * 2K words each.
+int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
+                      uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
+                      hipStream_t s);
+// link: uint32 [M][2K] = next match of the player (kNoMatch: none) | kLinkHasPred
+//       if the player has an earlier occurrence in the window
+// deps: int32 [M] zeroed: the completion counters the executor counts up (a
+//       match is ready when its counter reaches the number of its players with
+//       kLinkHasPred, which the executor reads from the links)
 // overflow: zeroed (reserved for schedule error reporting)
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s);

@@ -2,9 +2,10 @@
 //
 //  K7  gen_roster_kernel / gen_stream_kernel: synthetic inputs (counter RNG).
 //  K5  schedule: one stable LSD radix sort of the slots (radix_sort.hip)
-//      by player gives, per slot, the match of the player's next occurrence
-//      and a has-earlier flag (link, 4 B), and per match the number of
-//      distinct players with an earlier occurrence (deps).
+//      by player, fused with the record decode and the link write, gives per
+//      slot the match of the player's next occurrence and a has-earlier flag
+//      (link, 4 B); the executor derives each match's dependency count from
+//      its links and counts the (zeroed) deps counters up to it.
 //  The executor that consumes the schedule lives in dataflow.hip.
 //
 // Reference semantics: /root/reference/rater.py:69-169; the sequential loop the
@@ -94,64 +95,6 @@ int launch_reset_tags(float* state, int64_t P, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------- schedule
-// Slots of matches that touch no state (unsupported mode, rosters != 2, AFK,
-// malformed) are keyed past the last player so they neither wait nor publish.
-template <int K>
-__global__ void sched_keys_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t P,
-                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  constexpr int S = 2 * K;
-  MatchWork<float, K> w;
-  decode_record<float, K>(rec + m * (S + 2), (int64_t)P, w);
-  const bool rates = w.status == kRated;
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    keys[m * S + j] = rates && w.id[j] >= 0 ? (uint32_t)w.id[j] : P;
-    vals[m * S + j] = (uint32_t)(m * S + j);
-  }
-}
-
-// link[slot] = next match of the player (kNoMatch: none) | kLinkHasPred.  Sorted
-// neighbours only: three coalesced key loads and one 4-B scattered store per slot.
-template <int K>
-__global__ void __launch_bounds__(256)
-sched_link_kernel(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals, int64_t n,
-                  uint32_t kend, uint32_t* __restrict__ link) {
-  constexpr uint32_t S = 2 * K;
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = keys[i];
-  if (k >= kend) return;
-  uint32_t w = (i + 1 < n && keys[i + 1] == k) ? vals[i + 1] / S : kNoMatch;
-  if (i > 0 && keys[i - 1] == k) w |= kLinkHasPred;
-  link[vals[i]] = w;
-}
-
-// deps[m] = number of distinct players of m with an earlier occurrence in the window
-template <int K>
-__global__ void sched_deps_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
-                                  int64_t M, uint32_t P, int32_t* __restrict__ deps) {
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  constexpr int S = 2 * K;
-  MatchWork<float, K> w;
-  decode_record<float, K>(rec + m * (S + 2), (int64_t)P, w);
-  int d = 0;
-  if (w.status == kRated) {
-#pragma unroll
-    for (int j = 0; j < S; ++j)
-      if (w.first[j] == j && (link[(m * S + j) * kLinkWords] & kLinkHasPred)) ++d;
-  }
-  deps[m] = d;
-}
-
-static int key_bits(uint64_t kmax) {
-  int b = 1;
-  while (b < 32 && (1ull << b) <= kmax) ++b;
-  return b;
-}
-
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players) {
@@ -164,50 +107,15 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
   const int64_t n = M * 2 * K;
   ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 4, s));
   if (n <= 0) return 0;
-  if (n > kMaxSlots || P >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  if (n > kMaxSlots || P >= 0x7fffffffLL || K < 1 || K > 5) return (int)hipErrorInvalidValue;
   if (ws_bytes < schedule_workspace_bytes(n, P)) return (int)hipErrorInvalidValue;
+  ANA_HIP_CHECK(hipMemsetAsync(deps, 0, (size_t)M * 4, s));
   char* p = static_cast<char*>(ws);
   uint32_t* keys_a = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* vals_a = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* keys_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* vals_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
-  const unsigned mb = (unsigned)((M + 255) / 256);
-  const unsigned nb = (unsigned)((n + 255) / 256);
-  switch (K) {
-#define ANA_KEY_CASE(k)                                                                     \
-  case k:                                                                                   \
-    hipLaunchKernelGGL(sched_keys_kernel<k>, dim3(mb), dim3(256), 0, s, rec, M, (uint32_t)P, \
-                       keys_a, vals_a);                                                     \
-    break;
-    ANA_KEY_CASE(1) ANA_KEY_CASE(2) ANA_KEY_CASE(3) ANA_KEY_CASE(4) ANA_KEY_CASE(5)
-#undef ANA_KEY_CASE
-    default: return (int)hipErrorInvalidValue;
-  }
-  ANA_HIP_CHECK(hipGetLastError());
-  int in_alt = 0;
-  ANA_HIP_CHECK((hipError_t)launch_radix_sort_pairs(keys_a, vals_a, keys_b, vals_b, n,
-                                                     key_bits((uint64_t)P), p, &in_alt, s));
-  const uint32_t* keys_out = in_alt ? keys_b : keys_a;
-  const uint32_t* vals_out = in_alt ? vals_b : vals_a;
-  switch (K) {
-#define ANA_LINK_CASE(k)                                                                      \
-  case k:                                                                                     \
-    hipLaunchKernelGGL(sched_link_kernel<k>, dim3(nb), dim3(256), 0, s, keys_out, vals_out, n, \
-                       (uint32_t)P, link);                                                    \
-    break;
-    ANA_LINK_CASE(1) ANA_LINK_CASE(2) ANA_LINK_CASE(3) ANA_LINK_CASE(4) ANA_LINK_CASE(5)
-#undef ANA_LINK_CASE
-  }
-  switch (K) {
-#define ANA_DEPS_CASE(k)                                                                      \
-  case k:                                                                                     \
-    hipLaunchKernelGGL(sched_deps_kernel<k>, dim3(mb), dim3(256), 0, s, rec, link, M,          \
-                       (uint32_t)P, deps);                                                    \
-    break;
-    ANA_DEPS_CASE(1) ANA_DEPS_CASE(2) ANA_DEPS_CASE(3) ANA_DEPS_CASE(4) ANA_DEPS_CASE(5)
-#undef ANA_DEPS_CASE
-  }
-  return (int)hipGetLastError();
+  return launch_sched_sort(K, rec, M, (uint32_t)P, keys_a, vals_a, keys_b, vals_b, p, link, s);
 }
 
 }  // namespace ana

@@ -14,6 +14,12 @@
 //             wave prefixes in LDS, local scatter into an LDS-sorted tile,
 //             then coalesced runs to the global digit offsets.
 // 8-bit digits, 4096-element tiles (256 threads x 16), ceil(bits / 8) passes.
+//
+// The schedule prepass (launch_sched_sort) fuses both ends: pass 0 computes its
+// keys from the match records, and the last pass writes each slot's link from
+// its LDS neighbours instead of the sorted pairs (only run-boundary pairs go out,
+// for the fix-up).  For 10M 3v3 matches that drops a 480-MB key/value write, the
+// re-reads of it and a separate 720-MB link pass.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -28,6 +34,15 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
 constexpr int kRadix = 256;
+
+// Tile of this workgroup.  Workgroups go round-robin over the 8 XCDs; giving
+// each XCD a contiguous range of tiles puts the digit runs that consecutive
+// tiles write next to each other into one L2, which merges them into full
+// lines before they leave for HBM.
+__device__ __forceinline__ int64_t xcd_tile(int64_t tiles) {
+  const int64_t i = blockIdx.x, q = tiles >> 3, r = tiles & 7, x = i & 7;
+  return x * q + (x < r ? x : r) + (i >> 3);
+}
 
 // exclusive scan of one value per thread over a 256-thread block
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* wsum,
@@ -52,24 +67,62 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* w
   return before + inc - x;
 }
 
+// Element idx of the sort: a (key, value) pair of the input arrays, or (KS > 0)
+// slot idx of the match stream -- key = the slot's player (kend if the match
+// touches no state or the slot is empty), value = idx -- so the schedule's
+// first pass reads the records instead of a separately written key array.
+template <int KS>
+__device__ __forceinline__ uint32_t elem_key(const uint32_t* __restrict__ keys,
+                                             const int32_t* __restrict__ rec, uint32_t kend,
+                                             int64_t idx) {
+  if constexpr (KS == 0) {
+    return keys[idx];
+  } else {
+    constexpr int S = 2 * KS, R = S + 2;
+    const uint32_t m = (uint32_t)idx / (uint32_t)S;  // idx < kMaxSlots
+    const int j = (int)((uint32_t)idx - m * (uint32_t)S);
+    const int32_t* src = rec + (int64_t)m * R;
+    int32_t r[R];
+    if constexpr (R % 4 == 0) {
+#pragma unroll
+      for (int k = 0; k < R / 4; ++k) {
+        const int4 v = reinterpret_cast<const int4*>(src)[k];
+        r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < R; ++k) r[k] = src[k];
+    }
+    const uint32_t m0 = (uint32_t)r[S];
+    int32_t id = -1;
+#pragma unroll
+    for (int q = 0; q < S; ++q) if (q == j) id = r[q];
+    const int pos = j < KS ? j : j - KS;
+    const bool in_roster = pos < (j < KS ? meta_n0(m0) : meta_n1(m0));
+    return early_status<KS>(r, (int64_t)kend) == kRated && in_roster ? (uint32_t)id : kend;
+  }
+}
+
+template <int KS>
 __global__ void __launch_bounds__(kThreads)
-radix_upsweep(const uint32_t* __restrict__ keys, int64_t n, int shift, uint32_t* __restrict__ counts,
-              int64_t tiles) {
+radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec, uint32_t kend,
+              int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles) {
   __shared__ uint32_t hist[kWaves][kRadix];
   const int tid = threadIdx.x, wv = tid >> 6;
   for (int i = tid; i < kWaves * kRadix; i += kThreads) (&hist[0][0])[i] = 0u;
   __syncthreads();
-  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int64_t tile = xcd_tile(tiles);
+  const int64_t base = tile * kTile;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
     const int64_t idx = base + k * kThreads + tid;
-    if (idx < n) atomicAdd(&hist[wv][(keys[idx] >> shift) & (kRadix - 1)], 1u);
+    if (idx < n) atomicAdd(&hist[wv][(elem_key<KS>(keys, rec, kend, idx) >> shift) & (kRadix - 1)], 1u);
   }
   __syncthreads();
   uint32_t c = 0;
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) c += hist[w][tid];
-  counts[(int64_t)tid * tiles + blockIdx.x] = c;
+  counts[(int64_t)tid * tiles + tile] = c;
 }
 
 // One workgroup per digit: counts[d][*] <- exclusive prefix over tiles; totals[d] <- row sum.
@@ -100,11 +153,18 @@ radix_rowscan(uint32_t* __restrict__ counts, int64_t tiles, uint32_t* __restrict
   if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
+// KS > 0: elements come from the match stream (elem_key).  LINK (the schedule's
+// last pass): instead of writing the sorted pairs, write every slot's link from
+// its neighbours in the LDS-sorted tile -- within a (tile, digit) run they are
+// its global neighbours -- and only the run-boundary pairs, whose outer
+// neighbour lives in another tile (sched_fixup completes those links).
+template <int KS, bool LINK>
 __global__ void __launch_bounds__(kThreads)
 radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                const int32_t* __restrict__ rec, uint32_t kend,
                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
-                int64_t tiles) {
+                int64_t tiles, int slots_per_match, uint32_t* __restrict__ link) {
   __shared__ uint32_t skey[kTile];
   __shared__ uint32_t sval[kTile];
   __shared__ uint32_t wcnt[kWaves][kRadix];
@@ -112,11 +172,12 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
   __shared__ uint32_t gstart[kRadix];
   __shared__ uint32_t wsum[kWaves];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t base = (int64_t)blockIdx.x * kTile;
+  const int64_t tile = xcd_tile(tiles);
+  const int64_t base = tile * kTile;
   for (int i = tid; i < kWaves * kRadix; i += kThreads) (&wcnt[0][0])[i] = 0u;
   {  // global start of each digit for this tile
     const uint32_t dstart = block_exclusive_scan(totals[tid], wsum, nullptr);
-    gstart[tid] = dstart + counts[(int64_t)tid * tiles + blockIdx.x];
+    gstart[tid] = dstart + counts[(int64_t)tid * tiles + tile];
   }
   __syncthreads();
 
@@ -128,8 +189,10 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
   for (int it = 0; it < kItems; ++it) {
     const int64_t idx = base + (int64_t)(wv * kItems + it) * 64 + lane;
     const bool valid = idx < n;
-    key[it] = valid ? kin[idx] : 0xffffffffu;  // pads sort last: digit 255, after every real key
-    val[it] = valid ? vin[idx] : 0u;
+    // pads sort last: digit 255, after every real key
+    key[it] = valid ? elem_key<KS>(kin, rec, kend, idx) : 0xffffffffu;
+    if constexpr (KS == 0) val[it] = valid ? vin[idx] : 0u;
+    else val[it] = (uint32_t)idx;
   }
 #pragma unroll
   for (int it = 0; it < kItems; ++it) {
@@ -173,9 +236,68 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
       const uint32_t kk = skey[i];
       const uint32_t d = (kk >> shift) & (kRadix - 1);
       const int64_t o = (int64_t)gstart[d] + (i - (int64_t)tstart[d]);
-      kout[o] = kk;
-      vout[o] = sval[i];
+      if constexpr (!LINK) {
+        kout[o] = kk;
+        vout[o] = sval[i];
+      } else {
+        const int hi = d + 1 < (uint32_t)kRadix ? (int)tstart[d + 1] : kTile;
+        const bool first = i == (int)tstart[d];
+        const bool last = i + 1 == hi || i + 1 >= nvalid;
+        const uint32_t v = sval[i];
+        if (first || last) {  // sched_fixup reads the boundary pairs of every run
+          kout[o] = kk;
+          vout[o] = v;
+        }
+        if (kk < kend) {
+          uint32_t w = (!last && skey[i + 1] == kk) ? sval[i + 1] / (uint32_t)slots_per_match
+                                                     : kNoMatch;
+          if (!first && skey[i - 1] == kk) w |= kLinkHasPred;
+          link[v] = w;
+        }
+      }
     }
+  }
+}
+
+// Completes the links of the run-boundary slots of the LINK pass: one thread per
+// (tile, digit) run; its first pair's predecessor and its last pair's successor
+// are the last / first pairs of the neighbouring runs, which that pass wrote.
+// Grid: (tile groups of 256, digits); blocks of empty digits exit at once.
+__global__ void __launch_bounds__(kThreads)
+sched_fixup(const uint32_t* __restrict__ kout, const uint32_t* __restrict__ vout, int64_t n,
+            uint32_t kend, const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
+            int64_t tiles, int slots_per_match, uint32_t* __restrict__ link) {
+  __shared__ uint32_t wsum[kWaves];
+  const int d = blockIdx.y;
+  const uint32_t tot = totals[d];
+  if (tot == 0) return;
+  uint32_t all = 0;
+  const uint32_t before = block_exclusive_scan(threadIdx.x < (unsigned)d ? totals[threadIdx.x] : 0u,
+                                               wsum, &all);
+  (void)before;
+  const uint32_t dstart = all;  // sum of the totals of the digits below d
+  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (t >= tiles) return;
+  const uint32_t* row = counts + (int64_t)d * tiles;
+  const uint32_t c0 = row[t];
+  const uint32_t c1 = t + 1 < tiles ? row[t + 1] : tot;
+  if (c1 == c0) return;
+  const int64_t of = (int64_t)dstart + c0, ol = (int64_t)dstart + c1 - 1;
+  const uint32_t kf = kout[of], kl = kout[ol];
+  const bool pred = kf < kend && of > 0 && kout[of - 1] == kf;
+  const bool succ = kl < kend && ol + 1 < n && kout[ol + 1] == kl;
+  const uint32_t nxt = succ ? vout[ol + 1] / (uint32_t)slots_per_match : kNoMatch;
+  if (of == ol) {
+    if (kf < kend) link[vout[of]] = nxt | (pred ? kLinkHasPred : 0u);
+    return;
+  }
+  if (pred) {
+    const uint32_t v = vout[of];
+    link[v] |= kLinkHasPred;
+  }
+  if (succ) {
+    const uint32_t v = vout[ol];
+    link[v] = (link[v] & ~kMatchMask) | nxt;
   }
 }
 
@@ -196,14 +318,73 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
   uint32_t* totals = counts + tiles * kRadix;
   uint32_t *ki = keys, *vi = vals, *ko = keys_alt, *vo = vals_alt;
   for (int shift = 0; shift < bits; shift += 8) {
-    hipLaunchKernelGGL(radix_upsweep, dim3((unsigned)tiles), dim3(kThreads), 0, s, ki, n, shift,
-                       counts, tiles);
+    hipLaunchKernelGGL(radix_upsweep<0>, dim3((unsigned)tiles), dim3(kThreads), 0, s, ki, nullptr,
+                       0u, n, shift, counts, tiles);
     hipLaunchKernelGGL(radix_rowscan, dim3(kRadix), dim3(kThreads), 0, s, counts, tiles, totals);
-    hipLaunchKernelGGL(radix_downsweep, dim3((unsigned)tiles), dim3(kThreads), 0, s, ki, vi, ko, vo,
-                       n, shift, counts, totals, tiles);
+    hipLaunchKernelGGL((radix_downsweep<0, false>), dim3((unsigned)tiles), dim3(kThreads), 0, s, ki,
+                       vi, nullptr, 0u, ko, vo, n, shift, counts, totals, tiles, 1, nullptr);
     std::swap(ki, ko);
     std::swap(vi, vo);
     *result_in_alt ^= 1;
+  }
+  return (int)hipGetLastError();
+}
+
+// The schedule's sort (K5): the slots of the stream by player, stable, fused at
+// both ends -- the first pass reads the records (no key array is written), the
+// last pass writes links instead of sorted pairs, then sched_fixup.
+template <int K>
+static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits, uint32_t* ka,
+                         uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* counts,
+                         uint32_t* totals, int64_t tiles, uint32_t* link, hipStream_t s) {
+  constexpr int S = 2 * K;
+  const dim3 grid((unsigned)tiles), block(kThreads);
+  const uint32_t *ki = nullptr, *vi = nullptr;
+  uint32_t *ko = kb, *vo = vb;
+  for (int shift = 0; shift < bits; shift += 8) {
+    const bool first = shift == 0, last = shift + 8 >= bits;
+    if (first) hipLaunchKernelGGL(radix_upsweep<K>, grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles);
+    else hipLaunchKernelGGL(radix_upsweep<0>, grid, block, 0, s, ki, nullptr, kend, n, shift, counts, tiles);
+    hipLaunchKernelGGL(radix_rowscan, dim3(kRadix), block, 0, s, counts, tiles, totals);
+    if (first && last)
+      hipLaunchKernelGGL((radix_downsweep<K, true>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko, vo,
+                         n, shift, counts, totals, tiles, S, link);
+    else if (first)
+      hipLaunchKernelGGL((radix_downsweep<K, false>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
+                         vo, n, shift, counts, totals, tiles, S, nullptr);
+    else if (last)
+      hipLaunchKernelGGL((radix_downsweep<0, true>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
+                         shift, counts, totals, tiles, S, link);
+    else
+      hipLaunchKernelGGL((radix_downsweep<0, false>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
+                         shift, counts, totals, tiles, S, nullptr);
+    if (last)
+      hipLaunchKernelGGL(sched_fixup, dim3((unsigned)((tiles + kThreads - 1) / kThreads), kRadix), block,
+                         0, s, ko, vo, n, kend, counts, totals, tiles, S, link);
+    ki = ko;
+    vi = vo;
+    ko = ko == kb ? ka : kb;
+    vo = vo == vb ? va : vb;
+  }
+}
+
+int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
+                      uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
+                      hipStream_t s) {
+  const int64_t n = M * 2 * K;
+  if (n <= 0) return 0;
+  if (n > kMaxSlots) return (int)hipErrorInvalidValue;
+  int bits = 1;  // keys run up to num_players (= "no state")
+  while (bits < 32 && (1ull << bits) <= (uint64_t)num_players) ++bits;
+  const int64_t tiles = (n + kTile - 1) / kTile;
+  uint32_t* counts = static_cast<uint32_t*>(ws);
+  uint32_t* totals = counts + tiles * kRadix;
+  switch (K) {
+#define ANA_SORT_CASE(k) \
+  case k: sched_sort_k<k>(rec, n, num_players, bits, ka, va, kb, vb, counts, totals, tiles, link, s); break;
+    ANA_SORT_CASE(1) ANA_SORT_CASE(2) ANA_SORT_CASE(3) ANA_SORT_CASE(4) ANA_SORT_CASE(5)
+#undef ANA_SORT_CASE
+    default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
 }

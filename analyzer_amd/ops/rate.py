@@ -46,7 +46,11 @@ class NativeRateError(RuntimeError):
 class Schedule(NamedTuple):
     # [M, 2K] int32 per slot: next match of the player (NO_MATCH: none) | HAS_PRED
     link: torch.Tensor
-    deps: torch.Tensor  # [M] int32: players with an earlier occurrence in the window
+    # [M] int32.  Device: completion counters, zeroed by the prepass and counted up
+    # by the executor as predecessors publish (a match is ready at the number of
+    # its distinct players with HAS_PRED on their first slot).  Host mirror: that
+    # number itself.
+    deps: torch.Tensor
 
     NO_MATCH = 0x0FFFFFFF
     MATCH_MASK = 0x0FFFFFFF
@@ -193,9 +197,9 @@ class BatchRater:
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
                  tag: str = "") -> Schedule:
         """Dependency structure of a window (K5): per slot the match of its
-        player's next occurrence and whether it occurred earlier, and per match
-        the number of distinct players with an earlier occurrence.  ``deps`` is consumed (counted
-        down to 0) by the device rate launch, so a schedule is single-use there.
+        player's next occurrence and whether it occurred earlier (``link``), and
+        per match the completion counter ``deps`` (see ``Schedule``).  The device
+        rate launch counts ``deps`` up, so a schedule is single-use there.
         ``tag`` selects a separate buffer set (to prepare the next window while the
         current one is being rated)."""
         M = rec.shape[0]
