@@ -217,7 +217,8 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
           Tensor first_prior, Tensor quality, Tensor status, Tensor s_mu, Tensor s_sig,
           Tensor delta, Tensor m_mu, Tensor m_sig, Tensor ctrl, Tensor vst, double beta2,
           double tau2, double unknown_sigma, bool record_first_prior, int64_t blocks,
-          int64_t epoch, bool host_fp64, Tensor tele_evoff, Tensor tele_events, Tensor tele_stats) {
+          int64_t epoch, bool host_fp64, Tensor tele_evoff, Tensor tele_events, Tensor tele_stats,
+          int64_t progress, int64_t progress_value, int64_t progress_at) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
@@ -262,9 +263,14 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   if (const char* e = std::getenv("ANA_RATE_IDLE")) prm.idle_spins = std::atoi(e);  // tuning knob
   if (const char* e = std::getenv("ANA_RATE_DEBUG")) prm.debug_flags = std::atoi(e);  // experiments
   prm.spec = 0;
+  prm.variant = 0;
+  if (const char* e = std::getenv("ANA_RATE_VARIANT")) prm.variant = std::atoi(e);  // experiments
   if (const char* e = std::getenv("ANA_RATE_SPEC")) prm.spec = std::atoi(e);
   prm.tight_groups = -1;
   if (const char* e = std::getenv("ANA_RATE_TIGHT")) prm.tight_groups = std::atoi(e);
+  prm.progress = reinterpret_cast<uint64_t*>((intptr_t)progress);
+  prm.progress_value = (uint64_t)progress_value;
+  prm.progress_at = progress_at;
   const ana::TelemetryParams tp = telemetry_params(tele_evoff, tele_events, tele_stats, M, K, dev);
   if (dev.is_cuda()) {
     check(link, "link", torch::kInt32, dev);
@@ -280,6 +286,9 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
                                attrs.data_ptr<float>(), fp, out,
                                reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm, tp,
                                (int)blocks, stream_of(rec)), "rate");
+    if (prm.progress)  // releases the waiter even if the launch ended without firing
+      check_hip((int)hipStreamWriteValue64(stream_of(rec), prm.progress, prm.progress_value, 0),
+                "hipStreamWriteValue64");
   } else {
     TORCH_CHECK(ana::host_rate((int)K, host_fp64, rec.data_ptr<int32_t>(), state.data_ptr<float>(),
                                attrs.data_ptr<float>(), fp, out, prm) == 0, "bad K");
@@ -414,6 +423,34 @@ int64_t cu_masked_stream(int64_t device, int64_t num_cus) {
   return (int64_t)reinterpret_cast<intptr_t>(st);
 }
 
+// Tail overlap (runtime/engine.py): an 8-B word in signal memory that the
+// executor stores its launch number to when the launch reaches its tail, and a
+// stream wait on it.  The handle is the device address (lives until exit).
+int64_t progress_signal(int64_t device) {
+  int prev = 0;
+  check_hip((int)hipGetDevice(&prev), "hipGetDevice");
+  check_hip((int)hipSetDevice((int)device), "hipSetDevice");
+  void* p = nullptr;
+  hipError_t e = hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory);
+  if (e == hipSuccess) e = hipMemset(p, 0, 8);
+  check_hip((int)hipSetDevice(prev), "hipSetDevice");
+  check_hip((int)e, "hipExtMallocWithFlags(hipMallocSignalMemory)");
+  return (int64_t)reinterpret_cast<intptr_t>(p);
+}
+
+void stream_wait_value64(int64_t stream, int64_t ptr, int64_t value) {
+  check_hip((int)hipStreamWaitValue64(reinterpret_cast<hipStream_t>((intptr_t)stream),
+                                      reinterpret_cast<void*>((intptr_t)ptr), (uint64_t)value,
+                                      hipStreamWaitValueGte),
+            "hipStreamWaitValue64");
+}
+
+bool can_wait_value(int64_t device) {
+  int v = 0;
+  return hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, (int)device) ==
+             hipSuccess && v != 0;
+}
+
 // ------------------------------------------------------------------ ingest (P3)
 void write_record_file(const std::string& path, Tensor rec, int64_t K) {
   check(rec, "rec", torch::kInt32, torch::Device(torch::kCPU));
@@ -478,6 +515,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
            "next filled window as (slot, base, tensor view of pinned memory) or None at EOF")
       .def("release", &ana::RecordReader::release, "return the oldest acquired slot");
   m.def("cu_masked_stream", &cu_masked_stream, "HIP stream limited to N CUs (spread over XCDs)");
+  m.def("progress_signal", &progress_signal, "8-B signal-memory word for the executor's tail signal");
+  m.def("stream_wait_value64", &stream_wait_value64, "hipStreamWaitValue64(stream, ptr, >= value)");
+  m.def("can_wait_value", &can_wait_value, "hipDeviceAttributeCanUseStreamWaitValue");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
   m.attr("ROW_FLOATS") = ana::kRowFloats;
   m.attr("N_TRACKS") = ana::kTracks;

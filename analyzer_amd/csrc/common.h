@@ -13,9 +13,8 @@
 //  * match stream: int32 rec[M][2K+2]: 2K player ids (-1 = empty slot; slots
 //    0..K-1 roster 0, K..2K-1 roster 1), then meta0 = mode | n0<<8 | n1<<16 |
 //    nrosters<<24 and meta1 = winner0 | winner1<<1 | afk_any<<2 | afk_mask<<8.
-//  * schedule: uint32 occ[M][2K][2] = (occurrence index of the slot's player
-//    among earlier stateful matches of the window, same but counting only
-//    matches of the same game mode).
+//  * schedule: uint32 link[M][2K] (kLinkWords below) and int32 deps[M], the
+//    executor's completion counters (kernels.h launch_schedule).
 #pragma once
 
 #include <stdint.h>
@@ -43,7 +42,7 @@ constexpr uint32_t kNoMatch = 0x0fffffffu;
 constexpr uint32_t kMatchMask = 0x0fffffffu;
 constexpr uint32_t kLinkHasPred = 1u << 30;      // the player occurred earlier in the window
 constexpr uint32_t kNone = 0xffffffffu;
-constexpr int kSlotBits = 28;     // sort values carry slot | mode << kSlotBits
+constexpr int kSlotBits = 28;     // slots of a window < 2^28 (sort values, link match fields)
 constexpr int64_t kMaxSlots = 1ll << kSlotBits;
 constexpr int kModes = 6;
 constexpr int kModeUnsupported = 255;
@@ -77,6 +76,14 @@ struct RateParams {
   int32_t spec;                // dataflow: speculative one-dependency matches per wave iteration
   int32_t tight_groups;        // dataflow: 2K lanes per match instead of the next power of two
                                // (-1 auto, 0 off, 1 on)
+  int32_t variant;             // dataflow: executor variant for A/B experiments (0 = production)
+  // Tail signal: once chunks from progress_at on are being claimed (every
+  // earlier chunk is claimed, the launch is in its tail), waves store
+  // progress_value to *progress (signal memory a side stream waits on with
+  // hipStreamWaitValue64 before the next window's prepass).  null = off.
+  uint64_t* progress;
+  uint64_t progress_value;
+  int64_t progress_at;         // chunk index (64 matches per chunk)
 };
 
 // Per-match outputs.  The participant record of the reference

@@ -121,7 +121,18 @@ __device__ __forceinline__ int nth_set_bit(uint64_t x, int k) {
   return pos;
 }
 
-template <int K, int G>
+// a value every lane holds identically, marked wave-uniform for the compiler
+// (values built from shuffles are otherwise assumed divergent, which drags the
+// chunk bookkeeping into vector registers)
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// V: executor variant for same-process A/B experiments (ANA_RATE_VARIANT);
+// 0 = the production path.
+template <int K, int G, int V>
 __global__ void __launch_bounds__(256)
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
@@ -152,6 +163,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // (ctrl[3] counts retired chunks), so long dependency chains never trip it
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_progress = 0;
+  // experiment: issue priority over co-running kernels (the next window's prepass)
+  if (prm.debug_flags & 8) __builtin_amdgcn_s_setprio(3);
 
   int64_t cbase[kHeld];   // wave-uniform: first match of each held chunk, -1 = free slot
   uint64_t pend[kHeld];   // wave-uniform: stateful matches not yet handed to a group
@@ -174,7 +187,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     unsigned t = 0;
     if (lane == 0)
       t = __hip_atomic_fetch_add((gu32*)&ctrl[12], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t = __shfl(t, 0);
+    t = V == 1 ? __builtin_amdgcn_readfirstlane(t) : __shfl(t, 0);
     return (int64_t)t < tele_tiles ? (int64_t)t : -1;
   };
   const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : 8u;
@@ -189,9 +202,19 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
     for (int k = 0; k < S; ++k) lks[k] = 0u;
     if (tk_pending) {
-      const unsigned t = __shfl(tk, 0);
+      // readfirstlane, not a shuffle: the compiler then knows the chunk bases and
+      // masks derived from it are wave-uniform and keeps the bookkeeping scalar
+      const unsigned t = V == 1 ? __builtin_amdgcn_readfirstlane(tk) : __shfl(tk, 0);
       tk_pending = false;
       const int64_t c = (int64_t)t * kHeads + head;
+      // tail signal: the first ticket of each shard at or past progress_at, and its
+      // first ticket past the end (so a threshold beyond the window still fires)
+      const int64_t nchunks = (M + kChunk - 1) / kChunk;
+      if (prm.progress && lane == 0 &&
+          ((c >= prm.progress_at && c < prm.progress_at + kHeads) ||
+           (c >= nchunks && c < nchunks + kHeads)))
+        __hip_atomic_store(prm.progress, prm.progress_value, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
       if (c * kChunk >= M) {
         exhausted = true;
       } else {
@@ -236,30 +259,61 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // predecessor: their loads race the predecessor's stores and the tag check
     // accepts them if the stores won (saves the poll round trip on the hop)
     int my_h = -1, my_bit = 0, nassigned = 0;
+    // scalar: the sets, chunk bases and counts are wave-uniform; group g of
+    // the wave takes the g-th pick (s_ff1 over the set of the oldest chunk)
     auto assign = [&](uint64_t (&sets)[kHeld], int limit) {
+      if constexpr (V == 1) {
 #pragma unroll
-      for (int pass = 0; pass < kHeld; ++pass) {
-        int best = -1;
-        int64_t bb = 0;
-#pragma unroll
-        for (int h = 0; h < kHeld; ++h)
-          if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
-        if (best < 0 || nassigned >= limit) break;
-        uint64_t rdy = 0;
-#pragma unroll
-        for (int h = 0; h < kHeld; ++h) if (h == best) rdy = sets[h];
-        const int cnt = __popcll(rdy);
-        const int take = cnt < limit - nassigned ? cnt : limit - nassigned;
-        if (g >= nassigned && g < nassigned + take) {
-          my_h = best;
-          my_bit = nth_set_bit(rdy, g - nassigned);
+        for (int pass = 0; pass < kHeld; ++pass) {
+          int best = -1;
+          int64_t bb = 0;
+  #pragma unroll
+          for (int h = 0; h < kHeld; ++h)
+            if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
+          if (best < 0 || nassigned >= limit) break;
+          uint64_t rdy = 0;
+  #pragma unroll
+          for (int h = 0; h < kHeld; ++h) if (h == best) rdy = sets[h];
+          uint64_t taken = 0;
+          while (rdy != 0ull && nassigned < limit) {
+            const int b = __builtin_ctzll(rdy);
+            rdy &= rdy - 1ull;
+            taken |= 1ull << b;
+            if (g == nassigned) {
+              my_h = best;
+              my_bit = b;
+            }
+            ++nassigned;
+          }
+  #pragma unroll
+          for (int h = 0; h < kHeld; ++h)
+            if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
         }
-        uint64_t taken = rdy;
-        if (take < cnt) taken &= (1ull << nth_set_bit(rdy, take)) - 1ull;
+      } else {
 #pragma unroll
-        for (int h = 0; h < kHeld; ++h)
-          if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
-        nassigned += take;
+        for (int pass = 0; pass < kHeld; ++pass) {
+          int best = -1;
+          int64_t bb = 0;
+#pragma unroll
+          for (int h = 0; h < kHeld; ++h)
+            if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
+          if (best < 0 || nassigned >= limit) break;
+          uint64_t rdy = 0;
+#pragma unroll
+          for (int h = 0; h < kHeld; ++h) if (h == best) rdy = sets[h];
+          const int cnt = __popcll(rdy);
+          const int take = cnt < limit - nassigned ? cnt : limit - nassigned;
+          if (g >= nassigned && g < nassigned + take) {
+            my_h = best;
+            my_bit = nth_set_bit(rdy, g - nassigned);
+          }
+          uint64_t taken = rdy;
+          if (take < cnt) taken &= (1ull << nth_set_bit(rdy, take)) - 1ull;
+#pragma unroll
+          for (int h = 0; h < kHeld; ++h)
+            if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
+          nassigned += take;
+        }
       }
     };
     assign(ready, NG);
@@ -435,7 +489,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           const int bq = __shfl(gstale && my_h == h ? my_bit : -1, q * G);
           if (bq >= 0) back |= 1ull << bq;
         }
-        pend[h] |= back;
+        pend[h] |= V == 1 ? uniform64(back) : back;
       }
       if (gstale) my_h = -1;
     }
@@ -635,18 +689,24 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // (more matches per wave iteration, bpermute-tree sums).  Measured on MI355X:
   // 5v5 -7% with 10-lane groups, 3v3 +5% with 6-lane groups -> auto = K == 5.
   const bool tight = prm.tight_groups < 0 ? K == 5 : prm.tight_groups != 0;
-#define ANA_RATE_LAUNCH(k, g)                                                                 \
-  hipLaunchKernelGGL((rate_dataflow_kernel<k, g>), dim3((unsigned)blocks), dim3(256), 0, s, rec, \
+#define ANA_RATE_LAUNCH_V(k, g, v)                                                               \
+  hipLaunchKernelGGL((rate_dataflow_kernel<k, g, v>), dim3((unsigned)blocks), dim3(256), 0, s, rec, \
                      link, deps, state, attrs, first_prior, out, ctrl, prm, tp)
+#define ANA_RATE_LAUNCH(k, g) ANA_RATE_LAUNCH_V(k, g, 0)
   switch (K) {
     case 1: ANA_RATE_LAUNCH(1, 2); break;
     case 2: ANA_RATE_LAUNCH(2, 4); break;
-    case 3: if (tight) ANA_RATE_LAUNCH(3, 6); else ANA_RATE_LAUNCH(3, 8); break;
+    case 3:
+      if (tight) ANA_RATE_LAUNCH(3, 6);
+      else if (prm.variant == 1) ANA_RATE_LAUNCH_V(3, 8, 1);
+      else ANA_RATE_LAUNCH(3, 8);
+      break;
     case 4: ANA_RATE_LAUNCH(4, 8); break;
     case 5: if (tight) ANA_RATE_LAUNCH(5, 10); else ANA_RATE_LAUNCH(5, 16); break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef ANA_RATE_LAUNCH
+#undef ANA_RATE_LAUNCH_V
   return (int)hipGetLastError();
 }
 

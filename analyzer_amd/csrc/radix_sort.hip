@@ -67,20 +67,19 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* w
   return before + inc - x;
 }
 
-// Element idx of the sort: a (key, value) pair of the input arrays, or (KS > 0)
-// slot idx of the match stream -- key = the slot's player (kend if the match
-// touches no state or the slot is empty), value = idx -- so the schedule's
-// first pass reads the records instead of a separately written key array.
+// The schedule's first pass sorts the slots of the match stream straight from
+// the records: key = the slot's player (kend if the match touches no state or
+// the slot is empty), value = the slot index.  A workgroup decodes each match
+// of its tile once (one thread per match, one 16-B-vector record load) into an
+// LDS key array, instead of every slot re-decoding its whole match.
 template <int KS>
-__device__ __forceinline__ uint32_t elem_key(const uint32_t* __restrict__ keys,
-                                             const int32_t* __restrict__ rec, uint32_t kend,
-                                             int64_t idx) {
-  if constexpr (KS == 0) {
-    return keys[idx];
-  } else {
-    constexpr int S = 2 * KS, R = S + 2;
-    const uint32_t m = (uint32_t)idx / (uint32_t)S;  // idx < kMaxSlots
-    const int j = (int)((uint32_t)idx - m * (uint32_t)S);
+__device__ __forceinline__ void decode_tile_keys(const int32_t* __restrict__ rec, uint32_t kend,
+                                                 int64_t base, int64_t n, uint32_t* lk) {
+  constexpr int S = 2 * KS, R = S + 2;
+  const uint32_t lo = (uint32_t)base;  // slots < kMaxSlots
+  const uint32_t hi = (uint32_t)(base + kTile < n ? base + kTile : n);
+  const uint32_t m_lo = lo / S, m_hi = (hi + S - 1) / S;
+  for (uint32_t m = m_lo + threadIdx.x; m < m_hi; m += kThreads) {
     const int32_t* src = rec + (int64_t)m * R;
     int32_t r[R];
     if constexpr (R % 4 == 0) {
@@ -93,30 +92,38 @@ __device__ __forceinline__ uint32_t elem_key(const uint32_t* __restrict__ keys,
 #pragma unroll
       for (int k = 0; k < R; ++k) r[k] = src[k];
     }
+    const bool rates = early_status<KS>(r, (int64_t)kend) == kRated;
     const uint32_t m0 = (uint32_t)r[S];
-    int32_t id = -1;
 #pragma unroll
-    for (int q = 0; q < S; ++q) if (q == j) id = r[q];
-    const int pos = j < KS ? j : j - KS;
-    const bool in_roster = pos < (j < KS ? meta_n0(m0) : meta_n1(m0));
-    return early_status<KS>(r, (int64_t)kend) == kRated && in_roster ? (uint32_t)id : kend;
+    for (int j = 0; j < S; ++j) {
+      const uint32_t slot = m * S + j;
+      const int pos = j < KS ? j : j - KS;
+      const bool in_roster = pos < (j < KS ? meta_n0(m0) : meta_n1(m0));
+      if (slot >= lo && slot < hi) lk[slot - lo] = rates && in_roster ? (uint32_t)r[j] : kend;
+    }
   }
 }
 
+// KS > 0: keys from the match stream (decode_tile_keys).
 template <int KS>
 __global__ void __launch_bounds__(kThreads)
 radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec, uint32_t kend,
               int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles) {
   __shared__ uint32_t hist[kWaves][kRadix];
+  __shared__ uint32_t lkeys[KS > 0 ? kTile : 1];
   const int tid = threadIdx.x, wv = tid >> 6;
   for (int i = tid; i < kWaves * kRadix; i += kThreads) (&hist[0][0])[i] = 0u;
-  __syncthreads();
   const int64_t tile = xcd_tile(tiles);
   const int64_t base = tile * kTile;
+  if constexpr (KS > 0) decode_tile_keys<KS>(rec, kend, base, n, lkeys);
+  __syncthreads();
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
     const int64_t idx = base + k * kThreads + tid;
-    if (idx < n) atomicAdd(&hist[wv][(elem_key<KS>(keys, rec, kend, idx) >> shift) & (kRadix - 1)], 1u);
+    if (idx < n) {
+      const uint32_t key = KS > 0 ? lkeys[k * kThreads + tid] : keys[idx];
+      atomicAdd(&hist[wv][(key >> shift) & (kRadix - 1)], 1u);
+    }
   }
   __syncthreads();
   uint32_t c = 0;
@@ -153,7 +160,7 @@ radix_rowscan(uint32_t* __restrict__ counts, int64_t tiles, uint32_t* __restrict
   if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
-// KS > 0: elements come from the match stream (elem_key).  LINK (the schedule's
+// KS > 0: elements come from the match stream (decode_tile_keys).  LINK (the schedule's
 // last pass): instead of writing the sorted pairs, write every slot's link from
 // its neighbours in the LDS-sorted tile -- within a (tile, digit) run they are
 // its global neighbours -- and only the run-boundary pairs, whose outer
@@ -179,6 +186,7 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
     const uint32_t dstart = block_exclusive_scan(totals[tid], wsum, nullptr);
     gstart[tid] = dstart + counts[(int64_t)tid * tiles + tile];
   }
+  if constexpr (KS > 0) decode_tile_keys<KS>(rec, kend, base, n, sval);  // sval: scratch until the scatter
   __syncthreads();
 
   // wave wv owns tile elements [wv*kItems*64, (wv+1)*kItems*64) in (item, lane) order,
@@ -190,7 +198,8 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
     const int64_t idx = base + (int64_t)(wv * kItems + it) * 64 + lane;
     const bool valid = idx < n;
     // pads sort last: digit 255, after every real key
-    key[it] = valid ? elem_key<KS>(kin, rec, kend, idx) : 0xffffffffu;
+    if constexpr (KS > 0) key[it] = valid ? sval[(wv * kItems + it) * 64 + lane] : 0xffffffffu;
+    else key[it] = valid ? kin[idx] : 0xffffffffu;
     if constexpr (KS == 0) val[it] = valid ? vin[idx] : 0u;
     else val[it] = (uint32_t)idx;
   }

@@ -220,12 +220,14 @@ class BatchRater:
     def rate(self, roster: Roster, rec: torch.Tensor, K: Optional[int] = None,
              out: Optional[RateResult] = None, first_prior: Optional[torch.Tensor] = None,
              check: bool = True, schedule: Optional[Schedule] = None,
-             telemetry=None) -> RateResult:
+             telemetry=None, progress=None) -> RateResult:
         """Rate every match of ``rec`` in order, updating ``roster`` in place.
 
         ``telemetry`` = (evoff [M+1] int64, events [E,4] int32, stats [M,2K,8] f32):
         per-participant telemetry is aggregated into ``stats`` in the same launch
-        (K8 fused streaming mode: idle dataflow waves take telemetry tiles)."""
+        (K8 fused streaming mode: idle dataflow waves take telemetry tiles).
+        ``progress`` = (signal address, launch number, chunk index): the tail
+        signal of runtime/engine.py (device only)."""
         K = int(K or (rec.shape[1] - 2) // 2)
         M = int(rec.shape[0])
         dev = rec.device
@@ -252,7 +254,8 @@ class BatchRater:
         native().rate(rec, K, link, deps, roster.state, roster.attrs, fp, out.quality, out.status,
                       out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
                       float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
-                      record, self.blocks, epoch, self.host_fp64, *telemetry)
+                      record, self.blocks, epoch, self.host_fp64, *telemetry,
+                      *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)))
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out

@@ -12,16 +12,30 @@ windows flows through two device queues:
 Two schedule buffer sets alternate; events order "schedule(i+1) may reuse the
 set that rate(i-1) consumed" and "rate(i) needs schedule(i)".  On the CPU the
 same API runs the host mirror sequentially.
+
+Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.7): the
+prepass of window i+1 does not start with rate(i) -- co-running the two for the
+whole launch costs the latency-bound executor about as much as the prepass
+itself -- but when rate(i) reaches its tail: the executor stores its launch
+number to a signal-memory word once the chunks from that fraction of the window
+on are being claimed, and the side stream waits on that word
+(hipStreamWaitValue64).  The rest of the launch is draining in-flight
+dependency chains and leaves most of the machine idle.  ``step()`` enqueues in
+that order (rate(i), then prepare(i+1)); ``0`` restores start-to-start overlap.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
 from typing import Callable, Iterable, Iterator, List, Optional
 
+import os
+
 import torch
 
 from ..ops.rate import BatchRater, RateResult, Roster, Schedule
 from ..utils.trace import trace_range
+
+CHUNK = 64  # matches per executor ticket (csrc/dataflow.hip kChunk)
 
 
 @dataclass
@@ -46,6 +60,16 @@ class WindowPipeline:
         self._set = 0
         self._free: List[Optional[torch.cuda.Event]] = [None, None]
         self.windows_rated = 0
+        # tail overlap: signal word + number of the last enqueued rate launch
+        self.tail = float(os.environ.get("ANA_PREPASS_AT", "0.7") or 0)
+        self._signal = 0
+        self._seq = 0
+        if self.cuda and self.tail > 0:
+            from ..ops.native import native
+
+            dev = self.device.index or 0
+            if native().can_wait_value(dev):
+                self._signal = native().progress_signal(dev)
 
     def _side_stream(self):
         """Side stream of the prepass; ``ANA_PREPASS_CUS=n`` confines it to n CUs
@@ -62,16 +86,25 @@ class WindowPipeline:
             return torch.cuda.ExternalStream(handle, device=self.device)
         return torch.cuda.Stream(self.device)
 
-    def prepare(self, rec: torch.Tensor) -> Prepared:
-        """Enqueue the schedule prepass of ``rec`` on the side stream."""
+    def prepare(self, rec: torch.Tensor,
+                produced: Optional[torch.cuda.Event] = None) -> Prepared:
+        """Enqueue the schedule prepass of ``rec`` on the side stream, after the
+        tail of the last enqueued rate launch (tail overlap) and after
+        ``produced`` (default: everything enqueued on the main stream so far,
+        which is where ``rec`` was made)."""
         if not self.cuda:
             return Prepared(rec, None, None)
         tag = "_set%d" % self._set
         main = torch.cuda.current_stream(self.device)
-        produced = torch.cuda.Event()
-        produced.record(main)  # rec was produced on the main stream
+        if produced is None:
+            produced = torch.cuda.Event()
+            produced.record(main)
         with torch.cuda.stream(self.side), trace_range("schedule", window=self.windows_rated + 1):
             self.side.wait_event(produced)
+            if self._signal and self._seq > 0:
+                from ..ops.native import native
+
+                native().stream_wait_value64(self.side.cuda_stream, self._signal, self._seq)
             if self._free[self._set] is not None:  # previous user of this buffer set is done
                 self.side.wait_event(self._free[self._set])
             sched = self.rater.schedule(rec, self.K, self.roster.num_players, tag=tag)
@@ -90,9 +123,15 @@ class WindowPipeline:
             main.wait_event(prep.ready)
         if self.merger is not None:
             self.merger.begin(self.roster)
+        progress = None
+        if self._signal:
+            self._seq += 1
+            M = int(prep.rec.shape[0])
+            at = int(self.tail * ((M + CHUNK - 1) // CHUNK))
+            progress = (self._signal, self._seq, at)
         with trace_range("rate", window=self.windows_rated, matches=int(prep.rec.shape[0])):
             res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
-                                  schedule=prep.schedule, telemetry=telemetry)
+                                  schedule=prep.schedule, telemetry=telemetry, progress=progress)
         if self.cuda:
             done = torch.cuda.Event()
             done.record(main)
@@ -103,6 +142,18 @@ class WindowPipeline:
                 self.merger.merge(self.roster)
         self.windows_rated += 1
         return res
+
+    def step(self, prep: Prepared, next_rec: Optional[torch.Tensor], **rate_kwargs):
+        """Rate ``prep`` and enqueue the prepass of ``next_rec`` behind its tail.
+        ``next_rec`` must already be enqueued (made) on the main stream.
+        Returns (result, prepared next window or None)."""
+        produced = None
+        if self.cuda and next_rec is not None:
+            produced = torch.cuda.Event()
+            produced.record(torch.cuda.current_stream(self.device))
+        res = self.rate(prep, **rate_kwargs)
+        nxt = self.prepare(next_rec, produced=produced) if next_rec is not None else None
+        return res, nxt
 
     def run(self, windows: Iterable[torch.Tensor], out: Optional[RateResult] = None,
             on_result: Optional[Callable[[int, RateResult], None]] = None) -> int:
@@ -116,10 +167,10 @@ class WindowPipeline:
         while nxt is not None:
             cur = nxt
             try:
-                nxt = self.prepare(next(it))
+                following = next(it)
             except StopIteration:
-                nxt = None
-            res = self.rate(cur, out=out)
+                following = None
+            res, nxt = self.step(cur, following, out=out)
             if on_result is not None:
                 on_result(n, res)
             n += 1

@@ -113,11 +113,11 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
     nxt = pipe.prepare(window_rec(start_window)) if start_window < total else None
     for g in range(start_window, total):
         cur = nxt
-        nxt = pipe.prepare(window_rec(g + 1)) if g + 1 < total else None
         M = cur.rec.shape[0]
         if out is None or out.quality.shape[0] != M:
             out = R.RateResult.allocate(M, K, dev)
-        res = pipe.rate(cur, out=out)
+        # window g+1 is generated before rate(g) is enqueued; its prepass waits for the tail
+        res, nxt = pipe.step(cur, window_rec(g + 1) if g + 1 < total else None, out=out)
         counts += torch.bincount(res.status.to(torch.int64), minlength=256)
         rated += M
         if on_window is not None:

@@ -122,17 +122,17 @@ def main(argv=None) -> int:
     prepared = {0: pipe.prepare(windows[0])}
 
     def step(i):
-        # the prepass of window i+1 runs on the side stream while window i is rated
-        # (every timed step carries exactly one prepass and one rating)
-        prepared[i + 1] = pipe.prepare(windows[(i + 1) % n_windows])
-        if tele is None:
-            pipe.rate(prepared.pop(i), out=out)
-        elif args.telemetry_mode == "fused":
-            t = tele[i % n_windows]
-            pipe.rate(prepared.pop(i), out=out, telemetry=(t.evoff, t.events, stats))
+        # rate window i, then the prepass of window i+1 on the side stream behind
+        # its tail (every timed step carries exactly one prepass and one rating)
+        nxt = windows[(i + 1) % n_windows]
+        if tele is None or args.telemetry_mode == "separate":
+            _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out)
+            if tele is not None:
+                aggregate(tele[i % n_windows], K, stats)
         else:
-            pipe.rate(prepared.pop(i), out=out)
-            aggregate(tele[i % n_windows], K, stats)
+            t = tele[i % n_windows]
+            _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out,
+                                           telemetry=(t.evoff, t.events, stats))
         err.bitwise_or_(rater.error_flags(dev))
 
     for i in range(args.warmup):

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--debug", default="0", help="ANA_RATE_DEBUG values (experiments)")
     ap.add_argument("--spec", default="0", help="ANA_RATE_SPEC values (speculative matches/iteration)")
     ap.add_argument("--tight", default="-1", help="ANA_RATE_TIGHT values (2K lanes per match; -1 auto)")
+    ap.add_argument("--variant", default="0", help="ANA_RATE_VARIANT values (executor A/B variants)")
     ap.add_argument("--packed", default="1", help="output layout: 1 packed rows, 0 separate arrays")
     ap.add_argument("--hot", type=float, default=0.0)
     ap.add_argument("--rated", type=float, default=1.0,
@@ -44,16 +45,18 @@ def main():
     outs = {1: RateResult.allocate(M, K, dev), 0: RateResult.allocate(M, K, dev, packed=False)}
     results = {}
     for rnd in range(args.rounds):
-        for b, idle, dbg, sp, tg, pk in [(int(x), int(y), int(z), int(w), int(v), int(u))
-                                         for x in args.blocks.split(",") for y in args.idle.split(",")
-                                         for z in args.debug.split(",") for w in args.spec.split(",")
-                                         for v in args.tight.split(",") for u in args.packed.split(",")]:
+        for b, idle, dbg, sp, tg, pk, va in [(int(x), int(y), int(z), int(w), int(v), int(u), int(t))
+                                             for x in args.blocks.split(",") for y in args.idle.split(",")
+                                             for z in args.debug.split(",") for w in args.spec.split(",")
+                                             for v in args.tight.split(",") for u in args.packed.split(",")
+                                             for t in args.variant.split(",")]:
             out = outs[pk]
             os.environ["ANA_RATE_TIGHT"] = str(tg)
             os.environ["ANA_RATE_IDLE"] = str(idle)
             os.environ["ANA_RATE_DEBUG"] = str(dbg)
             os.environ["ANA_RATE_SPEC"] = str(sp)
-            key = "b%d/i%d/d%d/s%d/t%d/p%d" % (b, idle, dbg, sp, tg, pk)
+            os.environ["ANA_RATE_VARIANT"] = str(va)
+            key = "b%d/i%d/d%d/s%d/t%d/p%d/v%d" % (b, idle, dbg, sp, tg, pk, va)
             roster = make_roster(RosterSpec(num_players=P, seed=1, p_rated=args.rated,
                                             p_mode_rated=args.rated), device=dev)
             br = BatchRater(blocks=b)
