@@ -280,12 +280,35 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
     TORCH_CHECK(deps.numel() == M, "deps must have M entries");
     TORCH_CHECK(ctrl.numel() >= 16, "ctrl must have 16 entries");
     TORCH_CHECK(blocks >= 1 && blocks <= 65535, "blocks must be 1..65535");
+    // the executor writes packed rows; other layouts go through a packed buffer
+    const bool packed = out.s_sig == out.s_mu + S && out.delta == out.s_mu + 2 * S &&
+                        out.m_mu == out.s_mu + 3 * S && out.m_sig == out.s_mu + 4 * S &&
+                        out.quality == out.s_mu + 5 * S && qrow == row &&
+                        (void*)out.status == (void*)(out.s_mu + 5 * S + 1) && srow == row * 4;
+    Tensor staged;
+    if (!packed) {
+      const int64_t W = (5 * S + 2 + 31) / 32 * 32;
+      staged = torch::empty({M, W}, state.options());
+      float* b = staged.data_ptr<float>();
+      out = ana::RateOut{b + 5 * S, reinterpret_cast<uint8_t*>(b + 5 * S + 1), b, b + S, b + 2 * S,
+                         b + 3 * S, b + 4 * S, W, W, W * 4};
+    }
     check_hip(ana::launch_rate((int)K, rec.data_ptr<int32_t>(),
                                reinterpret_cast<const uint32_t*>(link.data_ptr<int32_t>()),
                                deps.data_ptr<int32_t>(), state.data_ptr<float>(),
                                attrs.data_ptr<float>(), fp, out,
                                reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm, tp,
                                (int)blocks, stream_of(rec)), "rate");
+    if (!packed) {
+      using torch::indexing::Slice;
+      s_mu.copy_(staged.index({Slice(), Slice(0, S)}));
+      s_sig.copy_(staged.index({Slice(), Slice(S, 2 * S)}));
+      delta.copy_(staged.index({Slice(), Slice(2 * S, 3 * S)}));
+      m_mu.copy_(staged.index({Slice(), Slice(3 * S, 4 * S)}));
+      m_sig.copy_(staged.index({Slice(), Slice(4 * S, 5 * S)}));
+      quality.copy_(staged.index({Slice(), 5 * S}));
+      status.copy_(staged.view(torch::kUInt8).index({Slice(), 4 * (5 * S + 1)}));
+    }
     if (prm.progress)  // releases the waiter even if the launch ended without firing
       check_hip((int)hipStreamWriteValue64(stream_of(rec), prm.progress, prm.progress_value, 0),
                 "hipStreamWriteValue64");

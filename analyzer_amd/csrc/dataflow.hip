@@ -103,24 +103,6 @@ __device__ __forceinline__ v4i granule(float mu, uint32_t a, float sig, uint32_t
   return v;
 }
 
-// position of the k-th (0-based) set bit of x (x has more than k bits set)
-__device__ __forceinline__ int nth_set_bit(uint64_t x, int k) {
-  int pos = 0;
-#pragma unroll
-  for (int w = 32; w >= 1; w >>= 1) {
-    const uint64_t low = x & ((1ull << w) - 1ull);
-    const int c = __popcll(low);
-    if (k >= c) {
-      k -= c;
-      x >>= w;
-      pos += w;
-    } else {
-      x = low;
-    }
-  }
-  return pos;
-}
-
 // a value every lane holds identically, marked wave-uniform for the compiler
 // (values built from shuffles are otherwise assumed divergent, which drags the
 // chunk bookkeeping into vector registers)
@@ -131,19 +113,21 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 }
 
 // V: executor variant for same-process A/B experiments (ANA_RATE_VARIANT);
-// 0 = the production path.
-template <int K, int G, int V>
+// 0 = the production path.  TELE: K8 fused telemetry compiled in (the plain
+// rating launch leaves it out, which frees the registers its code pins).
+template <int K, int G, int V, bool TELE>
 __global__ void __launch_bounds__(256)
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
-                     float* __restrict__ first_prior, RateOut out, uint32_t* ctrl,
+                     float* __restrict__ first_prior, float* __restrict__ orows, int64_t orow,
+                     uint32_t* ctrl,
                      RateParams prm, TelemetryParams tp) {
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
   __shared__ int32_t lrec[kWavesPerBlock][kHeld][kChunk * R];
-  __shared__ float tele[kWavesPerBlock][kTeleTile * S * (kStatFeatures + 1)];  // K8 scratch
+  __shared__ float tele[kWavesPerBlock][TELE ? kTeleTile * S * (kStatFeatures + 1) : 1];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int j = lane % G;
@@ -181,13 +165,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   unsigned tk = 0;                 // ticket returned to lane 0
   uint32_t spins = 0, iter = 0;
   // K8 fused mode: telemetry tiles fill the time a wave would spend waiting
-  const int64_t tele_tiles = tp.evoff ? (tp.num_matches + kTeleTile - 1) / kTeleTile : 0;
+  const int64_t tele_tiles = TELE && tp.evoff ? (tp.num_matches + kTeleTile - 1) / kTeleTile : 0;
   bool tele_done = tele_tiles == 0;
   auto tele_claim = [&]() -> int64_t {
     unsigned t = 0;
     if (lane == 0)
       t = __hip_atomic_fetch_add((gu32*)&ctrl[12], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t = V == 1 ? __builtin_amdgcn_readfirstlane(t) : __shfl(t, 0);
+    t = __builtin_amdgcn_readfirstlane(t);
     return (int64_t)t < tele_tiles ? (int64_t)t : -1;
   };
   const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : 8u;
@@ -204,7 +188,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     if (tk_pending) {
       // readfirstlane, not a shuffle: the compiler then knows the chunk bases and
       // masks derived from it are wave-uniform and keeps the bookkeeping scalar
-      const unsigned t = V == 1 ? __builtin_amdgcn_readfirstlane(tk) : __shfl(tk, 0);
+      const unsigned t = __builtin_amdgcn_readfirstlane(tk);
       tk_pending = false;
       const int64_t c = (int64_t)t * kHeads + head;
       // tail signal: the first ticket of each shard at or past progress_at, and its
@@ -262,58 +246,31 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // scalar: the sets, chunk bases and counts are wave-uniform; group g of
     // the wave takes the g-th pick (s_ff1 over the set of the oldest chunk)
     auto assign = [&](uint64_t (&sets)[kHeld], int limit) {
-      if constexpr (V == 1) {
 #pragma unroll
-        for (int pass = 0; pass < kHeld; ++pass) {
-          int best = -1;
-          int64_t bb = 0;
-  #pragma unroll
-          for (int h = 0; h < kHeld; ++h)
-            if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
-          if (best < 0 || nassigned >= limit) break;
-          uint64_t rdy = 0;
-  #pragma unroll
-          for (int h = 0; h < kHeld; ++h) if (h == best) rdy = sets[h];
-          uint64_t taken = 0;
-          while (rdy != 0ull && nassigned < limit) {
-            const int b = __builtin_ctzll(rdy);
-            rdy &= rdy - 1ull;
-            taken |= 1ull << b;
-            if (g == nassigned) {
-              my_h = best;
-              my_bit = b;
-            }
-            ++nassigned;
-          }
-  #pragma unroll
-          for (int h = 0; h < kHeld; ++h)
-            if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
-        }
-      } else {
+      for (int pass = 0; pass < kHeld; ++pass) {
+        int best = -1;
+        int64_t bb = 0;
 #pragma unroll
-        for (int pass = 0; pass < kHeld; ++pass) {
-          int best = -1;
-          int64_t bb = 0;
+        for (int h = 0; h < kHeld; ++h)
+          if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
+        if (best < 0 || nassigned >= limit) break;
+        uint64_t rdy = 0;
 #pragma unroll
-          for (int h = 0; h < kHeld; ++h)
-            if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
-          if (best < 0 || nassigned >= limit) break;
-          uint64_t rdy = 0;
-#pragma unroll
-          for (int h = 0; h < kHeld; ++h) if (h == best) rdy = sets[h];
-          const int cnt = __popcll(rdy);
-          const int take = cnt < limit - nassigned ? cnt : limit - nassigned;
-          if (g >= nassigned && g < nassigned + take) {
+        for (int h = 0; h < kHeld; ++h) if (h == best) rdy = sets[h];
+        uint64_t taken = 0;
+        while (rdy != 0ull && nassigned < limit) {
+          const int b = __builtin_ctzll(rdy);
+          rdy &= rdy - 1ull;
+          taken |= 1ull << b;
+          if (g == nassigned) {
             my_h = best;
-            my_bit = nth_set_bit(rdy, g - nassigned);
+            my_bit = b;
           }
-          uint64_t taken = rdy;
-          if (take < cnt) taken &= (1ull << nth_set_bit(rdy, take)) - 1ull;
-#pragma unroll
-          for (int h = 0; h < kHeld; ++h)
-            if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
-          nassigned += take;
+          ++nassigned;
         }
+#pragma unroll
+        for (int h = 0; h < kHeld; ++h)
+          if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
       }
     };
     assign(ready, NG);
@@ -433,15 +390,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
       if (mm < M && est != kRated) {  // no state, no dependencies: finish it now
 #pragma unroll
-        for (int q = 0; q < S; ++q) {
-          out.s_mu[mm * out.row + q] = NAN;
-          out.s_sig[mm * out.row + q] = NAN;
-          out.delta[mm * out.row + q] = NAN;
-          out.m_mu[mm * out.row + q] = NAN;
-          out.m_sig[mm * out.row + q] = NAN;
-        }
-        out.quality[mm * out.qrow] = (est == kAfk || est == kInvalidRosters) ? 0.f : NAN;
-        out.status[mm * out.srow] = est;
+        for (int q = 0; q < 5 * S; ++q) orows[mm * orow + q] = NAN;
+        orows[mm * orow + 5 * S] = (est == kAfk || est == kInvalidRosters) ? 0.f : NAN;
+        reinterpret_cast<uint8_t*>(orows + mm * orow + 5 * S + 1)[0] = est;
       }
       const uint64_t pm = __ballot(mm < M && est == kRated);
 #pragma unroll
@@ -489,7 +440,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           const int bq = __shfl(gstale && my_h == h ? my_bit : -1, q * G);
           if (bq >= 0) back |= 1ull << bq;
         }
-        pend[h] |= V == 1 ? uniform64(back) : back;
+        pend[h] |= uniform64(back);
       }
       if (gstale) my_h = -1;
     }
@@ -598,16 +549,17 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       // output records are a write-once stream: non-temporal stores into the
       // match's packed 128-B row (ops/rate.py RateResult) keep them from competing
       // with the roster for cache (-6%) and make each match one line (-3%)
+      float* const orm = orows + m * orow;  // [s_mu | s_sig | delta | m_mu | m_sig][S], quality, status
       if (j < S && !(prm.debug_flags & 2)) {
-        __builtin_nontemporal_store(ok ? nsm : NAN, out.s_mu + m * out.row + j);
-        __builtin_nontemporal_store(ok ? nss : NAN, out.s_sig + m * out.row + j);
-        __builtin_nontemporal_store(ok ? dl : NAN, out.delta + m * out.row + j);
-        __builtin_nontemporal_store(ok ? nmm : NAN, out.m_mu + m * out.row + j);
-        __builtin_nontemporal_store(ok ? nms : NAN, out.m_sig + m * out.row + j);
+        __builtin_nontemporal_store(ok ? nsm : NAN, orm + j);
+        __builtin_nontemporal_store(ok ? nss : NAN, orm + S + j);
+        __builtin_nontemporal_store(ok ? dl : NAN, orm + 2 * S + j);
+        __builtin_nontemporal_store(ok ? nmm : NAN, orm + 3 * S + j);
+        __builtin_nontemporal_store(ok ? nms : NAN, orm + 4 * S + j);
       }
       if (j == 0) {
-        __builtin_nontemporal_store(gst == kRated ? q : NAN, out.quality + m * out.qrow);
-        out.status[m * out.srow] = gst;
+        __builtin_nontemporal_store(gst == kRated ? q : NAN, orm + 5 * S);
+        reinterpret_cast<uint8_t*>(orm + 5 * S + 1)[0] = gst;
       }
     }
 
@@ -631,10 +583,12 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     if (exhausted && !held && !tk_pending) {
       if (lane == 0)  // diagnostics: wave iterations (ctrl[15])
         __hip_atomic_fetch_add((gu32*)&ctrl[15], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      while (!tele_done) {  // leftover telemetry tiles
-        const int64_t t = tele_claim();
-        if (t < 0) tele_done = true;
-        else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+      if constexpr (TELE) {
+        while (!tele_done) {  // leftover telemetry tiles
+          const int64_t t = tele_claim();
+          if (t < 0) tele_done = true;
+          else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+        }
       }
       break;
     }
@@ -655,17 +609,20 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         if (lane == 0) atomicOr(&ctrl[1], 1u);
 #pragma unroll
         for (int h = 0; h < kHeld; ++h)
-          if (cbase[h] >= 0 && ((pend[h] >> lane) & 1ull)) out.status[(cbase[h] + lane) * out.srow] = kNotProcessed;
+          if (cbase[h] >= 0 && ((pend[h] >> lane) & 1ull))
+            reinterpret_cast<uint8_t*>(orows + (cbase[h] + lane) * orow + 5 * S + 1)[0] = kNotProcessed;
         return;  // give up: the host sees ctrl[1] and raises
       }
-      if (!tele_done) {  // nothing ready: aggregate a telemetry tile instead of sleeping
-        const int64_t t = tele_claim();
-        if (t >= 0) {
-          telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
-          spins = 0;
-          continue;
+      if constexpr (TELE) {
+        if (!tele_done) {  // nothing ready: aggregate a telemetry tile instead of sleeping
+          const int64_t t = tele_claim();
+          if (t >= 0) {
+            telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+            spins = 0;
+            continue;
+          }
+          tele_done = true;
         }
-        tele_done = true;
       }
       spins = spins < max_spins ? spins + 1u : max_spins;
       for (uint32_t k = 0; k < spins; ++k) __builtin_amdgcn_s_sleep(2);
@@ -684,14 +641,28 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   if (M <= 0) return 0;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
   if (prm.epoch < 1 || prm.epoch > 255) return (int)hipErrorInvalidValue;
+  // the executor writes one packed row per match (ops/rate.py RateResult.allocate)
+  const int S = 2 * K;
+  if (!(out.s_sig == out.s_mu + S && out.delta == out.s_mu + 2 * S && out.m_mu == out.s_mu + 3 * S &&
+        out.m_sig == out.s_mu + 4 * S && out.quality == out.s_mu + 5 * S && out.qrow == out.row &&
+        (void*)out.status == (void*)(out.s_mu + 5 * S + 1) && out.srow == out.row * 4))
+    return (int)hipErrorInvalidValue;
   if (blocks < kHeads) blocks = kHeads;
   // lanes per match: the next power of two (xor-butterfly sums) or exactly 2K
   // (more matches per wave iteration, bpermute-tree sums).  Measured on MI355X:
   // 5v5 -7% with 10-lane groups, 3v3 +5% with 6-lane groups -> auto = K == 5.
   const bool tight = prm.tight_groups < 0 ? K == 5 : prm.tight_groups != 0;
-#define ANA_RATE_LAUNCH_V(k, g, v)                                                               \
-  hipLaunchKernelGGL((rate_dataflow_kernel<k, g, v>), dim3((unsigned)blocks), dim3(256), 0, s, rec, \
-                     link, deps, state, attrs, first_prior, out, ctrl, prm, tp)
+#define ANA_RATE_LAUNCH_V(k, g, v)                                                                 \
+  do {                                                                                             \
+    if (tp.evoff)                                                                                  \
+      hipLaunchKernelGGL((rate_dataflow_kernel<k, g, v, true>), dim3((unsigned)blocks), dim3(256), 0, \
+                         s, rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, \
+                         tp);                                                                      \
+    else                                                                                           \
+      hipLaunchKernelGGL((rate_dataflow_kernel<k, g, v, false>), dim3((unsigned)blocks), dim3(256), 0, \
+                         s, rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, \
+                         tp);                                                                      \
+  } while (0)
 #define ANA_RATE_LAUNCH(k, g) ANA_RATE_LAUNCH_V(k, g, 0)
   switch (K) {
     case 1: ANA_RATE_LAUNCH(1, 2); break;
