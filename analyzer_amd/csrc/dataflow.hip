@@ -614,7 +614,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         return;  // give up: the host sees ctrl[1] and raises
       }
       if constexpr (TELE) {
-        if (!tele_done) {  // nothing ready: aggregate a telemetry tile instead of sleeping
+        // nothing ready for a while: aggregate a telemetry tile instead of sleeping
+        // (V1: only after 4 idle iterations, so the hand-off path keeps polling)
+        if (!tele_done && (V != 1 || spins >= 4)) {
           const int64_t t = tele_claim();
           if (t >= 0) {
             telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
@@ -648,10 +650,11 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
         (void*)out.status == (void*)(out.s_mu + 5 * S + 1) && out.srow == out.row * 4))
     return (int)hipErrorInvalidValue;
   if (blocks < kHeads) blocks = kHeads;
-  // lanes per match: the next power of two (xor-butterfly sums) or exactly 2K
-  // (more matches per wave iteration, bpermute-tree sums).  Measured on MI355X:
-  // 5v5 -7% with 10-lane groups, 3v3 +5% with 6-lane groups -> auto = K == 5.
-  const bool tight = prm.tight_groups < 0 ? K == 5 : prm.tight_groups != 0;
+  // lanes per match: the next power of two (DPP butterfly sums) or exactly 2K
+  // (more matches per wave iteration, bpermute-tree sums).  Measured on MI355X
+  // with the scalar-bookkeeping executor: 3v3 8 lanes, 5v5 16 lanes (20.0 vs
+  // 21.2 ms for 12.5M matches with 10) -> auto = off.
+  const bool tight = prm.tight_groups > 0;
 #define ANA_RATE_LAUNCH_V(k, g, v)                                                                 \
   do {                                                                                             \
     if (tp.evoff)                                                                                  \

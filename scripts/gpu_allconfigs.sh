@@ -7,3 +7,8 @@ for args in "--config 2" "--config 3" "--config 4 --telemetry-mode fused" "--con
   tail -1 gpurun_out/b.log >> gpurun_out/bench_configs.log
   tail -1 gpurun_out/b.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('%-40s %8.3f ms  %.4g %s' % ('$args', d['ms_per_step'], d['value'], d['unit']))"
 done
+# 2-rank rehearsal of the DP merge path on one GPU (gloo; production N>1 uses RCCL)
+if [ -n "$DP2" ]; then
+  ANA_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 2 --steps 5 --warmup 2 --matches-per-gpu 2000000 > gpurun_out/b2.log 2>&1 || { tail -20 gpurun_out/b2.log; exit 1; }
+  grep '"metric"' gpurun_out/b2.log | cut -c1-300
+fi
