@@ -209,6 +209,7 @@ static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& 
   tp.evoff = evoff.data_ptr<int64_t>();
   tp.events = events.data_ptr<int32_t>();
   tp.stats = stats.data_ptr<float>();
+  if (dev.is_cuda()) tp.impl = ana::tele_impl();
   return tp;
 }
 

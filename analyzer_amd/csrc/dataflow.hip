@@ -127,7 +127,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
   __shared__ int32_t lrec[kWavesPerBlock][kHeld][kChunk * R];
-  __shared__ float tele[kWavesPerBlock][TELE ? kTeleTile * S * (kStatFeatures + 1) : 1];  // K8 scratch
+  __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int j = lane % G;
@@ -587,6 +587,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         while (!tele_done) {  // leftover telemetry tiles
           const int64_t t = tele_claim();
           if (t < 0) tele_done = true;
+          else if (tp.impl) telemetry_tile_mfma<K>(tp, t, lane, tele[wv], &ctrl[13]);
           else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
         }
       }
@@ -619,7 +620,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         if (!tele_done && (V != 1 || spins >= 4)) {
           const int64_t t = tele_claim();
           if (t >= 0) {
-            telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+            if (tp.impl) telemetry_tile_mfma<K>(tp, t, lane, tele[wv], &ctrl[13]);
+            else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
             spins = 0;
             continue;
           }

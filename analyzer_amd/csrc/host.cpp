@@ -92,7 +92,7 @@ int64_t host_telemetry(int K, const TelemetryParams& tp) {
     for (int64_t e = tp.evoff[m]; e < tp.evoff[m + 1]; ++e) {
       const int32_t* ev = tp.events + e * 4;
       const int slot = event_slot(ev[1]);
-      if (ev[0] < 0 || (int64_t)ev[0] / kTeleTile != m / kTeleTile || ev[0] >= M || slot >= S) {
+      if (ev[0] != m || slot >= S) {  // strict: the event must name the match whose CSR range holds it
         ++bad;
         continue;
       }

@@ -55,6 +55,8 @@ int launch_gen_event_counts(const GenEventParams& g, int64_t base, int64_t M, in
                             hipStream_t s);
 int launch_gen_events(int K, const GenEventParams& g, int64_t base, const int32_t* rec,
                       const int64_t* evoff, int64_t M, int32_t* events, hipStream_t s);
+// K8 implementation: 1 = one-hot MFMA (default), 0 = LDS float atomics (ANA_TELE_IMPL)
+int tele_impl();
 int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_t s);
 
 }  // namespace ana

@@ -4,6 +4,8 @@
 // (dataflow.hip), which is the fused streaming mode of BASELINE config 4.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 #include "telemetry_dev.h"
@@ -39,13 +41,18 @@ gen_events_kernel(GenEventParams g, int64_t base, const int32_t* __restrict__ re
   }
 }
 
-template <int K>
+// D: 0 = LDS float atomics (telemetry_tile, 16-match tiles), 3 = one-hot MFMA
+// (telemetry_tile_mfma over SPAN-match spans), 1 / 2 = timing-only diagnostics
+// of the atomic version, 6 / 7 = of the MFMA version (ANA_TELE_DEBUG)
+template <int K, int D, int SPAN>
 __global__ void __launch_bounds__(256) telemetry_kernel(TelemetryParams tp, uint32_t* bad) {
-  __shared__ float scratch[4][kTeleTile * 2 * K * (kStatFeatures + 1)];
-  const int wv = threadIdx.x >> 6;
-  const int64_t tiles = (tp.num_matches + kTeleTile - 1) / kTeleTile;
+  __shared__ float scratch[4][tele_scratch_floats<K>()];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t tiles = (tp.num_matches + SPAN - 1) / SPAN;
   const int64_t t = (int64_t)blockIdx.x * 4 + wv;
-  if (t < tiles) telemetry_tile<K>(tp, t, threadIdx.x & 63, scratch[wv], bad);
+  if (t >= tiles) return;
+  if constexpr (D >= 3) telemetry_tile_mfma<K, D - 3, SPAN>(tp, t, threadIdx.x & 63, scratch[wv], bad);
+  else telemetry_tile<K, D>(tp, t, threadIdx.x & 63, scratch[wv], bad);
 }
 
 int launch_gen_event_counts(const GenEventParams& g, int64_t base, int64_t M, int64_t* counts,
@@ -73,15 +80,54 @@ int launch_gen_events(int K, const GenEventParams& g, int64_t base, const int32_
   return (int)hipGetLastError();
 }
 
+int tele_impl() {
+  const char* e = getenv("ANA_TELE_IMPL");
+  return e ? atoi(e) : 1;
+}
+
+template <int K, int D, int SPAN>
+static void launch_tele(const TelemetryParams& tp, uint32_t* bad, hipStream_t s) {
+  const int64_t tiles = (tp.num_matches + SPAN - 1) / SPAN;
+  hipLaunchKernelGGL((telemetry_kernel<K, D, SPAN>), dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, s,
+                     tp, bad);
+}
+
+template <int K>
+static void launch_tele_k(const TelemetryParams& tp, uint32_t* bad, hipStream_t s, int impl, int dbg,
+                          int span) {
+  if (dbg == 1) return launch_tele<K, 1, kTeleTile>(tp, bad, s);
+  if (dbg == 2) return launch_tele<K, 2, kTeleTile>(tp, bad, s);
+  if (impl == 0) return launch_tele<K, 0, kTeleTile>(tp, bad, s);
+  const int d = dbg == 6 ? 6 : dbg == 7 ? 7 : 3;
+#define ANA_TELE_SPAN(sp)                                                                     \
+  if (span == sp) {                                                                           \
+    if (d == 6) return launch_tele<K, 6, sp>(tp, bad, s);                                     \
+    if (d == 7) return launch_tele<K, 7, sp>(tp, bad, s);                                     \
+    return launch_tele<K, 3, sp>(tp, bad, s);                                                 \
+  }
+  ANA_TELE_SPAN(16) ANA_TELE_SPAN(32)
+#undef ANA_TELE_SPAN
+  if (d == 6) return launch_tele<K, 6, kTeleMaxSpan>(tp, bad, s);
+  if (d == 7) return launch_tele<K, 7, kTeleMaxSpan>(tp, bad, s);
+  return launch_tele<K, 3, kTeleMaxSpan>(tp, bad, s);
+}
+
 int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_t s) {
   if (tp.num_matches <= 0) return 0;
-  const int64_t tiles = (tp.num_matches + kTeleTile - 1) / kTeleTile;
-  const unsigned blocks = (unsigned)((tiles + 3) / 4);
+  // ANA_TELE_IMPL: 1 (default) one-hot MFMA, 0 LDS atomics; ANA_TELE_SPAN: matches per
+  // wave of the MFMA kernel (16, 32, 63); ANA_TELE_DEBUG (diagnostic, timing only):
+  // atomic version 1 = no LDS adds, 2 = no count adds; MFMA version 6 = no MFMA, 7 = decode only
+  const char* dbg_env = getenv("ANA_TELE_DEBUG");
+  const char* span_env = getenv("ANA_TELE_SPAN");
+  const int dbg = dbg_env ? atoi(dbg_env) : 0;
+  const int span = span_env ? atoi(span_env) : kTeleMaxSpan;
+  const int impl = tele_impl();
   switch (K) {
-#define ANA_TELE_CASE(k)                                                                         \
-  case k: hipLaunchKernelGGL(telemetry_kernel<k>, dim3(blocks), dim3(256), 0, s, tp, bad); break;
-    ANA_TELE_CASE(1) ANA_TELE_CASE(2) ANA_TELE_CASE(3) ANA_TELE_CASE(4) ANA_TELE_CASE(5)
-#undef ANA_TELE_CASE
+    case 1: launch_tele_k<1>(tp, bad, s, impl, dbg, span); break;
+    case 2: launch_tele_k<2>(tp, bad, s, impl, dbg, span); break;
+    case 3: launch_tele_k<3>(tp, bad, s, impl, dbg, span); break;
+    case 4: launch_tele_k<4>(tp, bad, s, impl, dbg, span); break;
+    case 5: launch_tele_k<5>(tp, bad, s, impl, dbg, span); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();

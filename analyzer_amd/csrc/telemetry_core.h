@@ -8,8 +8,8 @@
 // z = value (float bits), w = game time in seconds (float bits).  Events of a
 // window are grouped by match (one telemetry file per match) and indexed by a
 // CSR offset array evoff[M + 1].  An event is attributed to the match it
-// names if that match lies in the same kTeleTile-match tile as the CSR range
-// it sits in; other events and slots >= 2K are counted as malformed.
+// names iff it sits in that match's CSR range and its slot is < 2K; other
+// events are counted as malformed.
 #pragma once
 
 #include <math.h>
@@ -65,6 +65,7 @@ struct TelemetryParams {
   const int32_t* events;  // [E, 4]
   float* stats;           // [M, 2K, kStatFeatures]
   int64_t num_matches;
+  int32_t impl = 1;       // device tile routine: 1 one-hot MFMA, 0 LDS float atomics
 };
 
 struct GenEventParams {

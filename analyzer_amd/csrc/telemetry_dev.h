@@ -15,7 +15,7 @@
 
 namespace ana {
 
-template <int K>
+template <int K, int D = 0>
 __device__ __forceinline__ void telemetry_tile(const TelemetryParams& tp, int64_t tile, int lane,
                                                float* lds, uint32_t* bad_events) {
   constexpr int S = 2 * K;
@@ -44,21 +44,291 @@ __device__ __forceinline__ void telemetry_tile(const TelemetryParams& tp, int64_
       if (base + q * 64 + lane >= e1) continue;
       const int64_t ml = (int64_t)ev[q].x - m0;
       const int slot = event_slot(ev[q].y);
-      if (ml < 0 || ml >= m1 - m0 || slot >= S) {
+      const int64_t e = base + q * 64 + lane;
+      if (ml < 0 || ml >= m1 - m0 || slot >= S || e < tp.evoff[m0 + ml] || e >= tp.evoff[m0 + ml + 1]) {
         ++bad;
         continue;
       }
       float add;
       const int f = event_feature(event_type(ev[q].y), __int_as_float(ev[q].z), add);
       float* row = lds + (ml * S + slot) * kPad;
+      if constexpr (D == 1) {  // diagnostic: no LDS adds (timing only)
+        bad += f == 99;
+        continue;
+      }
       if (f >= 0) atomicAdd(row + f, add);
-      atomicAdd(row + kStatEvents, 1.f);
+      if constexpr (D != 2) atomicAdd(row + kStatEvents, 1.f);  // D == 2: diagnostic
     }
   }
   if (bad) atomicAdd(bad_events, bad);
   __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS adds have landed (wave-local)
   float* dst = tp.stats + m0 * kRow;
   for (int i = lane; i < n; i += 64) dst[i] = lds[(i / kStatFeatures) * kPad + i % kStatFeatures];
+}
+
+}  // namespace ana
+
+namespace ana {
+
+// ---------------------------------------------------------------------------
+// K8 on the matrix cores: the per-participant aggregation is a one-hot GEMM.
+//
+//   stats_tile[row][col] = sum_e  A[row][e] * B[e][col]
+//
+// rows = (match, slot) of the wave's span of matches (span x 2K rows, in tiles
+// of 16 rows); A[row][e] = 1 iff event e is attributed to that row; B[e][col] =
+// the event's contribution to 16 columns: [0] count, [1..3] kills/deaths/
+// assists (1.0), [4..15] damage/gold/farm/heal as exact 3-way bf16 splits (hi,
+// mid, lo: 8+8+8 significand bits = the full fp32 value).  One
+// v_mfma_f32_16x16x32_bf16 folds 32 events into a 16-row tile.  This replaces
+// the LDS float atomics of telemetry_tile, whose same-address conflicts
+// serialise (4.45 ms for 400M events; 1.57 ms with the adds removed).
+//
+// Events stream linearly through the tile, 64 per lane-parallel load with
+// kTeleMfmaLoads loads in flight, rotated through registers by a rolled loop.
+// Each load is decoded once and scattered (b16 stores) into two operand tile
+// sets in LDS, one per 32-event chunk: B^T [16 columns][32 events] and an A^T
+// window [32 rows][32 events] starting at the chunk's first row tile.  All six
+// fragments are read back with one wait, then MFMAs fold each chunk into two
+// live accumulators that slide over the tile's row tiles (the stream visits
+// them in order; a chunk whose events reach a third row tile takes extra
+// windows).  A finished row tile leaves through a [16][17] LDS stage as 512
+// contiguous bytes of stats rows.
+//
+// Attribution is strict: an event counts for the match it names iff it sits in
+// that match's CSR range and its slot is < 2K; every other event is malformed
+// (counted in *bad_events).  Non-finite values stay out of the GEMM (0 x Inf
+// in another row's product would be NaN) and are added afterwards by a rare
+// slow path.  Tile rows are 32 bf16 + 16 B of pad (80 B).
+constexpr int kTeleChunk = 32;
+constexpr int kTeleRowBytes = kTeleChunk * 2 + 16;
+constexpr int kTeleARows = 32;
+constexpr int kTeleMfmaLoads = 4;
+constexpr int kTeleBOffset = kTeleARows * kTeleRowBytes;           // within a set
+constexpr int kTeleSetBytes = kTeleBOffset + 16 * kTeleRowBytes;   // A^T window + B^T
+constexpr int kTeleRelOffset = 2 * kTeleSetBytes;
+constexpr int kTeleMaxSpan = 63;  // matches per call: span + 1 CSR offsets on the lanes
+constexpr int kTeleMfmaBytes = kTeleRelOffset + (kTeleMaxSpan + 4) / 4 * 16;
+// per-wave LDS scratch (floats) that fits either tile routine
+template <int K>
+constexpr int tele_scratch_floats() {
+  constexpr int atomic_floats = kTeleTile * 2 * K * (kStatFeatures + 1);
+  constexpr int mfma_floats = (kTeleMfmaBytes + 15) / 16 * 4;
+  return atomic_floats > mfma_floats ? atomic_floats : mfma_floats;
+}
+
+typedef __bf16 tele_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float tele_f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void tele_lds_fence() {
+  // LDS ops of one wave execute in order; this only pins the program order
+  __asm__ __volatile__("" ::: "memory");
+}
+
+__device__ __forceinline__ void tele_st16(uint8_t* p, uint32_t v) {
+  *reinterpret_cast<uint16_t*>(p) = (uint16_t)v;
+}
+
+__device__ __forceinline__ tele_f32x4 tele_mfma(uint4 a, uint4 b, tele_f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(tele_bf16x8, a),
+                                                 __builtin_bit_cast(tele_bf16x8, b), c, 0, 0, 0);
+}
+
+// Aggregates the SPAN matches [tile * SPAN, +SPAN) (the fused executor claims
+// kTeleTile-match tiles; the standalone kernel takes longer spans per wave).
+// DIAG (timing-only builds, ANA_TELE_DEBUG 6 / 7): 3 = no MFMA, 4 = decode only
+template <int K, int DIAG = 0, int SPAN = kTeleTile>
+__device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, int64_t tile, int lane,
+                                                    float* lds_f, uint32_t* bad_events) {
+  constexpr int S = 2 * K;
+  constexpr int NB = kTeleMfmaLoads;
+  constexpr uint32_t kOne = 0x3f80;  // bf16 1.0
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_f);
+  int32_t* rel = reinterpret_cast<int32_t*>(lds + kTeleRelOffset);  // tile CSR, relative
+  // the tile is wave-uniform (callers derive it from threadIdx.x >> 6, which the
+  // compiler cannot prove): pin it, and everything derived from it, to SGPRs
+  tile = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(tile >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)tile));
+  static_assert(SPAN >= 1 && SPAN <= kTeleMaxSpan, "span must fit the lanes");
+  const int64_t m0 = tile * SPAN;
+  const int nm = (int)(tp.num_matches - m0 < SPAN ? tp.num_matches - m0 : SPAN);
+  const int64_t off = lane <= nm ? tp.evoff[m0 + lane] : 0;
+  const int64_t e0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off >> 32), 0) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)off, 0));
+  const int32_t roff = (int32_t)(off - e0);  // lane j <= nm: first event of match j
+  tele_lds_fence();
+  if (lane <= nm) rel[lane] = roff;
+  tele_lds_fence();
+  auto bound = [&](int j) { return __builtin_amdgcn_readlane(roff, j); };
+  const int ne = __builtin_amdgcn_readfirstlane(bound(nm));
+  const int t = lane & 31, half = lane >> 5;
+  const int fr = lane & 15, fg = lane >> 4;  // fragment row/column and k-group
+  uint8_t* mine_set = lds + half * kTeleSetBytes;
+  const int4* __restrict__ evs = reinterpret_cast<const int4*>(tp.events) + e0;
+  // two live 16-row accumulators: row tiles c and c + 1
+  tele_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  int c = 0;
+  const int nrows = nm * S;
+  float* dst = tp.stats + m0 * S * kStatFeatures;
+  float* st = reinterpret_cast<float*>(lds);  // [16][17] stage over set 0's A^T window
+  auto shift = [&]() {  // row tile c is final: store it, slide by one
+    tele_lds_fence();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[(4 * fg + j) * 17 + fr] = acc0[j];
+    tele_lds_fence();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = lane + 64 * h;
+      const float* r = st + (o >> 3) * 17;
+      const int f = o & 7;
+      // column of feature f: 1 + f (kills..assists), 3f - 5 (+1, +2: value splits), 0 (count)
+      const bool split = f >= 3 && f < kStatEvents;
+      const int c0 = f < 3 ? f + 1 : split ? 3 * f - 5 : 0;
+      const float x0 = r[c0], x1 = r[split ? c0 + 1 : 16], x2 = r[split ? c0 + 2 : 16];
+      const float v = split ? (x0 + x1) + x2 : x0;
+      if (16 * c + (o >> 3) < nrows) dst[16 * c * kStatFeatures + o] = v;
+    }
+    tele_lds_fence();
+    acc0 = acc1;
+    acc1 = tele_f32x4{0.f, 0.f, 0.f, 0.f};
+    ++c;
+  };
+  uint32_t bad = 0;
+  bool nonfinite = false;
+  int mc = 0;  // wave-uniform cursor: a match at or before the next chunk's first event
+  auto match_at = [&](int pos) {  // the match whose CSR range holds position pos (advances mc)
+    while (mc + 1 < nm && bound(mc + 1) <= pos) ++mc;
+    return mc;
+  };
+  int4 ev[NB];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int e = 64 * q + lane;
+    ev[q] = e < ne ? evs[e] : make_int4(-1, 0, 0, 0);
+  }
+  for (int pb = 0; pb < ne; pb += 64) {
+    const int4 cur = ev[0];
+#pragma unroll
+    for (int q = 0; q + 1 < NB; ++q) ev[q] = ev[q + 1];
+    {
+      const int e = pb + 64 * NB + lane;
+      ev[NB - 1] = e < ne ? evs[e] : make_int4(-1, 0, 0, 0);
+    }
+    // the two chunks: first/last positions and the row tiles they can touch
+    const int n1 = ne - pb - kTeleChunk;  // events of chunk 1 (<= 0: none)
+    const int ms0 = match_at(pb);
+    const int me0 = match_at((n1 > 0 ? pb + kTeleChunk : ne) - 1);
+    const int ms1 = n1 > 0 ? match_at(pb + kTeleChunk) : me0;
+    const int me1 = n1 > 0 ? match_at(pb + kTeleChunk + (n1 < kTeleChunk ? n1 : kTeleChunk) - 1) : me0;
+    const int ilo0 = (ms0 * S) >> 4, ihi0 = ((me0 + 1) * S - 1) >> 4;
+    const int ilo1 = (ms1 * S) >> 4, ihi1 = ((me1 + 1) * S - 1) >> 4;
+    // decode this lane's event: its CSR segment from the (few) boundaries in the load
+    const int e = pb + lane;
+    int seg = ms0;
+    for (int j = ms0 + 1; j <= me1; ++j) seg += e >= bound(j) ? 1 : 0;
+    const int slot = event_slot(cur.y);
+    const bool ok = e < ne && (int64_t)cur.x - m0 == seg && slot < S;
+    bad += (e < ne && !ok) ? 1u : 0u;
+    const int row = seg * S + slot;
+    float add = 0.f;
+    const int f = ok ? event_feature(event_type(cur.y), __int_as_float(cur.z), add) : -1;
+    int col = -1;  // first B column of the feature, then up to 3 parts
+    uint32_t p0 = kOne, p1 = 0, p2 = 0;
+    if (f >= 0 && f < 3) {
+      col = 1 + f;
+    } else if (f >= 3) {
+      if (__builtin_isfinite(add)) {
+        // exact split: hi/mid by truncation, the rest (<= 8 significant bits) in lo
+        const uint32_t hb = __float_as_uint(add) & 0xffff0000u;
+        const float r1 = add - __uint_as_float(hb);
+        const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
+        col = 4 + 3 * (f - 3);
+        p0 = hb >> 16;
+        p1 = mb >> 16;
+        p2 = __float_as_uint(r1 - __uint_as_float(mb)) >> 16;
+      } else {
+        nonfinite = true;
+      }
+    }
+    if constexpr (DIAG == 4) {
+      if (ok) acc0[0] += (float)(col + p0 + p1 + p2 + row);
+      continue;
+    }
+    // zero both operand sets, scatter this lane's event into its chunk's set
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint8_t* z = lds + h * kTeleSetBytes + (lane >> 2) * kTeleRowBytes + (lane & 3) * 16;
+      *reinterpret_cast<uint4*>(z) = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(z + 16 * kTeleRowBytes) = make_uint4(0, 0, 0, 0);
+      *reinterpret_cast<uint4*>(z + kTeleBOffset) = make_uint4(0, 0, 0, 0);
+    }
+    tele_lds_fence();
+    const int lr = row - 16 * (half ? ilo1 : ilo0);
+    if (ok) {
+      uint8_t* bcol = mine_set + kTeleBOffset + 2 * t;
+      tele_st16(bcol, kOne);  // column 0: count
+      if (col >= 0) {
+        tele_st16(bcol + col * kTeleRowBytes, p0);
+        if (col >= 4) {
+          tele_st16(bcol + (col + 1) * kTeleRowBytes, p1);
+          tele_st16(bcol + (col + 2) * kTeleRowBytes, p2);
+        }
+      }
+      if (lr < kTeleARows) tele_st16(mine_set + lr * kTeleRowBytes + 2 * t, kOne);
+    }
+    tele_lds_fence();
+    uint4 a[2][2], b[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint8_t* sb = lds + h * kTeleSetBytes + fr * kTeleRowBytes + fg * 16;
+      b[h] = *reinterpret_cast<const uint4*>(sb + kTeleBOffset);
+      a[h][0] = *reinterpret_cast<const uint4*>(sb);
+      a[h][1] = *reinterpret_cast<const uint4*>(sb + 16 * kTeleRowBytes);
+    }
+    tele_lds_fence();
+    if constexpr (DIAG == 3) {
+      acc0[0] += __uint_as_float(a[0][0].x ^ a[0][1].y ^ b[0].z ^ a[1][0].x ^ a[1][1].y ^ b[1].z);
+      continue;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && n1 <= 0) break;
+      const int ilo = h ? ilo1 : ilo0, ihi = h ? ihi1 : ihi0;
+      while (c < ilo) shift();
+      acc0 = tele_mfma(a[h][0], b[h], acc0);
+      if (ihi > c) acc1 = tele_mfma(a[h][1], b[h], acc1);
+      while (ihi > c + 1) {
+        // rare: the chunk reaches a third row tile.  Tile c is final; the window
+        // at the new c folds only its upper half (the new tile c + 1)
+        shift();
+        uint8_t* sa = lds + h * kTeleSetBytes;
+        *reinterpret_cast<uint4*>(sa + (16 + (lane >> 2)) * kTeleRowBytes + (lane & 3) * 16) =
+            make_uint4(0, 0, 0, 0);
+        tele_lds_fence();
+        const int lr2 = row - 16 * c;
+        if (ok && half == h && lr2 >= 16 && lr2 < kTeleARows) tele_st16(sa + lr2 * kTeleRowBytes + 2 * t, kOne);
+        tele_lds_fence();
+        const uint4 a1 = *reinterpret_cast<const uint4*>(sa + (16 + fr) * kTeleRowBytes + fg * 16);
+        tele_lds_fence();
+        acc1 = tele_mfma(a1, b[h], acc1);
+      }
+    }
+  }
+  while (16 * c < nrows) shift();  // the last live tiles and any tiles without events
+  if (__builtin_amdgcn_ballot_w64(nonfinite)) {
+    // rare slow path: add the tile's Inf/NaN values on top of the stored sums
+    __threadfence();
+    for (int e = lane; e < ne; e += 64) {
+      const int4 x = evs[e];
+      const int xm = (int)((int64_t)x.x - m0);
+      const int slot = event_slot(x.y);
+      if (xm < 0 || xm >= nm || slot >= S || e < rel[xm] || e >= rel[xm + 1]) continue;
+      float add;
+      const int f = event_feature(event_type(x.y), __int_as_float(x.z), add);
+      if (f >= 3 && !__builtin_isfinite(add)) atomicAdd(dst + (xm * S + slot) * kStatFeatures + f, add);
+    }
+  }
+  if (bad) atomicAdd(bad_events, bad);
 }
 
 }  // namespace ana

@@ -51,7 +51,10 @@ def parse(argv=None):
                          "5 = full-history re-rate windows: 16M 3v3/GPU over a 10M-player roster, "
                          "fp16 merge messages")
     ap.add_argument("--events", default="20,60", help="config 4: min,max telemetry events per match")
-    ap.add_argument("--telemetry-mode", default="fused", choices=["fused", "separate"])
+    ap.add_argument("--telemetry-mode", default="separate", choices=["overlap", "fused", "separate"],
+                    help="config 4: overlap = the MFMA aggregation kernel co-runs with the rating "
+                         "launch on its own stream; fused = executor waves aggregate in their idle "
+                         "time; separate = aggregation after the rating on the same stream")
     ap.add_argument("--comm-dtype", default=os.environ.get("COMM_DTYPE") or "fp32",
                     choices=["fp32", "fp16", "bf16"], help="sweep-merge message precision (N > 1)")
     args = ap.parse_args(argv)
@@ -121,11 +124,21 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     prepared = {0: pipe.prepare(windows[0])}
 
+    tstream = torch.cuda.Stream(dev) if tele is not None and args.telemetry_mode == "overlap" else None
+
     def step(i):
         # rate window i, then the prepass of window i+1 on the side stream behind
         # its tail (every timed step carries exactly one prepass and one rating)
         nxt = windows[(i + 1) % n_windows]
-        if tele is None or args.telemetry_mode == "separate":
+        if tstream is not None:
+            # window i's telemetry co-runs with its rating; the step ends when both have
+            main = torch.cuda.current_stream(dev)
+            tstream.wait_stream(main)
+            with torch.cuda.stream(tstream):
+                aggregate(tele[i % n_windows], K, stats)
+            _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out)
+            main.wait_stream(tstream)
+        elif tele is None or args.telemetry_mode == "separate":
             _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out)
             if tele is not None:
                 aggregate(tele[i % n_windows], K, stats)

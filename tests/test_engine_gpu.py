@@ -176,6 +176,48 @@ def test_telemetry_device_generator_and_aggregation(gpu_device):
     np.testing.assert_allclose(sd.cpu().numpy(), aggregate_reference(th, K), rtol=2e-5, atol=0.05)
 
 
+@pytest.mark.parametrize("impl", ["1", "0"])
+@pytest.mark.parametrize("K", [1, 2, 3, 4, 5])
+def test_telemetry_impls_vs_oracle_edges(gpu_device, monkeypatch, K, impl):
+    """K8 one-hot MFMA (impl 1) and LDS-atomic (impl 0) tiles vs an fp64 oracle:
+    every team size (16-row blocks of 8/4/2/2/1 matches), empty matches, a
+    partial last tile, malformed events (strict attribution) and non-finite
+    values; the host mirror counts the same malformed events."""
+    from analyzer_amd.ops.native import native
+    from analyzer_amd.ops.telemetry import Telemetry, TelemetrySpec, aggregate, make_telemetry
+
+    monkeypatch.setenv("ANA_TELE_IMPL", impl)
+    M = 4099
+    rec = make_stream(StreamSpec(team_size=K, seed=40 + K, p_uneven=0.2), M, 3000, K=K)
+    tel = make_telemetry(TelemetrySpec(seed=5, min_events=0, max_events=90), rec, K)
+    ev = tel.events.clone()
+    idx = torch.randperm(ev.shape[0], generator=torch.Generator().manual_seed(K))[:60]
+    ev[idx[:20], 1] = (ev[idx[:20], 1] & ~0xFF) | (2 * K)            # slot out of range
+    ev[idx[20:40], 0] = (ev[idx[20:40], 0] + 1) % M                  # names the next match
+    ev[idx[40:50], 1] = (ev[idx[40:50], 1] & 0xFF) | (3 << 8)        # damage events ...
+    ev[:, 2].view(torch.float32)[idx[40:50]] = float("inf")          # ... of infinite value
+    evn = ev.numpy()
+    m = evn[:, 0].astype(np.int64)
+    seg = np.repeat(np.arange(M), np.diff(tel.evoff.numpy()))
+    slot, typ = evn[:, 1] & 0xFF, (evn[:, 1] >> 8) & 0xFF
+    ok = (m == seg) & (slot < 2 * K)
+    val = evn[:, 2].view(np.float32).astype(np.float64)
+    add, feat = np.where(typ <= 2, 1.0, val), np.where(typ <= 6, typ, -1)
+    ref = np.zeros((M, 2 * K, 8))
+    sel = ok & (feat >= 0)
+    np.add.at(ref, (m[sel], slot[sel], feat[sel]), add[sel])
+    np.add.at(ref, (m[ok], slot[ok], np.full(int(ok.sum()), 7)), 1.0)
+    host = torch.zeros(M, 2 * K, 8)
+    assert native().telemetry(tel.evoff, ev, K, host, torch.zeros(1, dtype=torch.int32)) == int((~ok).sum())
+    bad = torch.zeros(1, dtype=torch.int32, device=gpu_device)
+    stats = torch.full((M, 2 * K, 8), -1.0, device=gpu_device)  # every entry must be written
+    aggregate(Telemetry(tel.evoff.to(gpu_device), ev.to(gpu_device)), K, stats, bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == int((~ok).sum())
+    np.testing.assert_allclose(stats.cpu().numpy(), ref, rtol=2e-6, atol=1e-3)
+    np.testing.assert_allclose(host.numpy(), ref, rtol=2e-6, atol=1e-3)
+
+
 def test_fused_rate_telemetry_on_device(gpu_device):
     from analyzer_amd.ops.telemetry import (TelemetrySpec, aggregate_reference, allocate_stats,
                                             make_telemetry)
