@@ -195,10 +195,10 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   };
   uint32_t bad = 0;
   bool nonfinite = false;
-  int mc = 0;  // wave-uniform cursor: a match at or before the next chunk's first event
-  auto match_at = [&](int pos) {  // the match whose CSR range holds position pos (advances mc)
-    while (mc + 1 < nm && bound(mc + 1) <= pos) ++mc;
-    return mc;
+  // the match whose CSR range holds position pos: the last j < nm with start_j <= pos
+  // (starts are non-decreasing; empty matches share their successor's start)
+  auto match_at = [&](int pos) {
+    return (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(lane < nm && roff <= pos)) - 1;
   };
   int4 ev[NB];
 #pragma unroll
@@ -222,12 +222,12 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
     const int me1 = n1 > 0 ? match_at(pb + kTeleChunk + (n1 < kTeleChunk ? n1 : kTeleChunk) - 1) : me0;
     const int ilo0 = (ms0 * S) >> 4, ihi0 = ((me0 + 1) * S - 1) >> 4;
     const int ilo1 = (ms1 * S) >> 4, ihi1 = ((me1 + 1) * S - 1) >> 4;
-    // decode this lane's event: its CSR segment from the (few) boundaries in the load
+    // decode this lane's event; it must sit in the CSR range of the match it names
     const int e = pb + lane;
-    int seg = ms0;
-    for (int j = ms0 + 1; j <= me1; ++j) seg += e >= bound(j) ? 1 : 0;
+    const int64_t xw = (int64_t)cur.x - m0;
+    const int seg = xw < 0 ? 0 : xw >= nm ? nm - 1 : (int)xw;
     const int slot = event_slot(cur.y);
-    const bool ok = e < ne && (int64_t)cur.x - m0 == seg && slot < S;
+    const bool ok = e < ne && xw == seg && slot < S && e >= rel[seg] && e < rel[seg + 1];
     bad += (e < ne && !ok) ? 1u : 0u;
     const int row = seg * S + slot;
     float add = 0.f;
