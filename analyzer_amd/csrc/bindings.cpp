@@ -210,6 +210,7 @@ static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& 
   tp.events = events.data_ptr<int32_t>();
   tp.stats = stats.data_ptr<float>();
   if (dev.is_cuda()) tp.impl = ana::tele_impl();
+  if (const char* e = std::getenv("ANA_TELE_FUSED_TAIL")) tp.fused_tail = std::atoi(e);  // A/B knob
   return tp;
 }
 

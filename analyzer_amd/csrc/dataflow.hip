@@ -617,7 +617,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       if constexpr (TELE) {
         // nothing ready for a while: aggregate a telemetry tile instead of sleeping
         // (V1: only after 4 idle iterations, so the hand-off path keeps polling)
-        if (!tele_done && (V != 1 || spins >= 4)) {
+        if (!tele_done && (V != 1 || spins >= 4) && (!tp.fused_tail || !held)) {
           const int64_t t = tele_claim();
           if (t >= 0) {
             if (tp.impl) telemetry_tile_mfma<K>(tp, t, lane, tele[wv], &ctrl[13]);

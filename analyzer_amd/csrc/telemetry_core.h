@@ -66,6 +66,8 @@ struct TelemetryParams {
   float* stats;           // [M, 2K, kStatFeatures]
   int64_t num_matches;
   int32_t impl = 1;       // device tile routine: 1 one-hot MFMA, 0 LDS float atomics
+  int32_t fused_tail = 0; // fused executor: 0 = any idle wave aggregates, 1 = only waves
+                          // holding no chunks (the window's tail; measured slower: 15.9 vs 14.6 ms)
 };
 
 struct GenEventParams {

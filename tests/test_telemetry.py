@@ -69,3 +69,18 @@ def test_malformed_events_are_dropped_and_counted():
     bad = native().telemetry(tel.evoff, ev, K, stats, torch.zeros(1, dtype=torch.int32))
     assert bad == 2
     assert stats[..., 7].sum() == tel.num_events - 2
+
+
+def test_strict_attribution_same_tile_other_match():
+    """An event counts only for the match whose CSR range holds it: naming another
+    match of the same 16-match tile is malformed too (host mirror = device rule)."""
+    K = 1
+    rec = _stream(M=20, K=K, P=10, seed=7)
+    tel = make_telemetry(TelemetrySpec(seed=3, min_events=2, max_events=2), rec, K)
+    ev = tel.events.clone()
+    ev[4, 0] = 3                         # event of match 2 names match 3 (same tile)
+    from analyzer_amd.ops.native import native
+    stats = allocate_stats(20, K, "cpu")
+    bad = native().telemetry(tel.evoff, ev, K, stats, torch.zeros(1, dtype=torch.int32))
+    assert bad == 1
+    assert stats[2, :, 7].sum() == 1 and stats[3, :, 7].sum() == 2
