@@ -200,20 +200,20 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   auto match_at = [&](int pos) {
     return (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(lane < nm && roff <= pos)) - 1;
   };
-  int4 ev[NB];
+  // groups of NB 64-event loads: all issued, then consumed in order (counted
+  // vmcnt waits); other waves on the SIMD cover the gap between groups.  Loads
+  // are unconditional (positions past the span re-read its last event; the
+  // decode masks them): conditional loads make the compiler wait for all.
+  const int elast = ne > 0 ? ne - 1 : 0;
+  for (int pr = 0; pr < ne; pr += 64 * NB) {
+    int4 ev[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) ev[q] = evs[min(pr + 64 * q + lane, elast)];
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
-    const int e = 64 * q + lane;
-    ev[q] = e < ne ? evs[e] : make_int4(-1, 0, 0, 0);
-  }
-  for (int pb = 0; pb < ne; pb += 64) {
-    const int4 cur = ev[0];
-#pragma unroll
-    for (int q = 0; q + 1 < NB; ++q) ev[q] = ev[q + 1];
-    {
-      const int e = pb + 64 * NB + lane;
-      ev[NB - 1] = e < ne ? evs[e] : make_int4(-1, 0, 0, 0);
-    }
+    const int pb = pr + 64 * q;
+    if (pb >= ne) break;
+    const int4 cur = ev[q];
     // the two chunks: first/last positions and the row tiles they can touch
     const int n1 = ne - pb - kTeleChunk;  // events of chunk 1 (<= 0: none)
     const int ms0 = match_at(pb);
@@ -222,34 +222,31 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
     const int me1 = n1 > 0 ? match_at(pb + kTeleChunk + (n1 < kTeleChunk ? n1 : kTeleChunk) - 1) : me0;
     const int ilo0 = (ms0 * S) >> 4, ihi0 = ((me0 + 1) * S - 1) >> 4;
     const int ilo1 = (ms1 * S) >> 4, ihi1 = ((me1 + 1) * S - 1) >> 4;
-    // decode this lane's event; it must sit in the CSR range of the match it names
+    // decode this lane's event (branch-free); it must sit in the CSR range of the
+    // match it names, and its slot must be < 2K
     const int e = pb + lane;
     const int64_t xw = (int64_t)cur.x - m0;
     const int seg = xw < 0 ? 0 : xw >= nm ? nm - 1 : (int)xw;
     const int slot = event_slot(cur.y);
-    const bool ok = e < ne && xw == seg && slot < S && e >= rel[seg] && e < rel[seg + 1];
+    const int r0 = rel[seg], r1e = rel[seg + 1];
+    const bool ok = e < ne && xw == seg && slot < S && e >= r0 && e < r1e;
     bad += (e < ne && !ok) ? 1u : 0u;
     const int row = seg * S + slot;
-    float add = 0.f;
-    const int f = ok ? event_feature(event_type(cur.y), __int_as_float(cur.z), add) : -1;
-    int col = -1;  // first B column of the feature, then up to 3 parts
-    uint32_t p0 = kOne, p1 = 0, p2 = 0;
-    if (f >= 0 && f < 3) {
-      col = 1 + f;
-    } else if (f >= 3) {
-      if (__builtin_isfinite(add)) {
-        // exact split: hi/mid by truncation, the rest (<= 8 significant bits) in lo
-        const uint32_t hb = __float_as_uint(add) & 0xffff0000u;
-        const float r1 = add - __uint_as_float(hb);
-        const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
-        col = 4 + 3 * (f - 3);
-        p0 = hb >> 16;
-        p1 = mb >> 16;
-        p2 = __float_as_uint(r1 - __uint_as_float(mb)) >> 16;
-      } else {
-        nonfinite = true;
-      }
-    }
+    // type -> B columns (event_feature): 0..2 kills/deaths/assists at column 1 + type,
+    // 3..6 damage/gold/farm/heal as (hi, mid, lo) at columns 3 type - 5 .. 3 type - 3
+    const int type = event_type(cur.y);
+    const float value = __int_as_float(cur.z);
+    const bool counted = ok && type < 3;
+    const bool summed = ok && type >= 3 && type <= 6;
+    const bool finite = __builtin_isfinite(value);
+    nonfinite |= summed && !finite;
+    const int col = counted ? type + 1 : (summed && finite) ? 3 * type - 5 : -1;
+    const uint32_t hb = __float_as_uint(value) & 0xffff0000u;
+    const float rv = value - __uint_as_float(hb);
+    const uint32_t mb = __float_as_uint(rv) & 0xffff0000u;
+    const uint32_t p0 = counted ? kOne : hb >> 16;
+    const uint32_t p1 = mb >> 16;
+    const uint32_t p2 = __float_as_uint(rv - __uint_as_float(mb)) >> 16;
     if constexpr (DIAG == 4) {
       if (ok) acc0[0] += (float)(col + p0 + p1 + p2 + row);
       continue;
@@ -313,6 +310,7 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
         acc1 = tele_mfma(a1, b[h], acc1);
       }
     }
+  }
   }
   while (16 * c < nrows) shift();  // the last live tiles and any tiles without events
   if (__builtin_amdgcn_ballot_w64(nonfinite)) {
