@@ -105,7 +105,8 @@ constexpr int kTeleRowBytes = kTeleChunk * 2 + 16;
 constexpr int kTeleARows = 32;
 constexpr int kTeleMfmaLoads = 4;
 constexpr int kTeleBOffset = kTeleARows * kTeleRowBytes;           // within a set
-constexpr int kTeleSetBytes = kTeleBOffset + 16 * kTeleRowBytes;   // A^T window + B^T
+// A^T window + B^T, + 64 B so set 1 starts 16 banks over (both sets take stores together)
+constexpr int kTeleSetBytes = kTeleBOffset + 16 * kTeleRowBytes + 64;
 constexpr int kTeleRelOffset = 2 * kTeleSetBytes;
 constexpr int kTeleMaxSpan = 63;  // matches per call: span + 1 CSR offsets on the lanes
 constexpr int kTeleMfmaBytes = kTeleRelOffset + (kTeleMaxSpan + 4) / 4 * 16;
@@ -158,6 +159,8 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   const int32_t roff = (int32_t)(off - e0);  // lane j <= nm: first event of match j
   tele_lds_fence();
   if (lane <= nm) rel[lane] = roff;
+  for (int i = lane; i < kTeleRelOffset / 16; i += 64)  // both operand sets start zero
+    reinterpret_cast<uint4*>(lds)[i] = make_uint4(0, 0, 0, 0);
   tele_lds_fence();
   auto bound = [&](int j) { return __builtin_amdgcn_readlane(roff, j); };
   const int ne = __builtin_amdgcn_readfirstlane(bound(nm));
@@ -188,6 +191,10 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
       const float v = split ? (x0 + x1) + x2 : x0;
       if (16 * c + (o >> 3) < nrows) dst[16 * c * kStatFeatures + o] = v;
     }
+    tele_lds_fence();
+    // the operand tiles are kept zero between uses: clear the stage's 1088 B
+    *reinterpret_cast<uint4*>(lds + 16 * lane) = make_uint4(0, 0, 0, 0);
+    if (lane < 4) *reinterpret_cast<uint4*>(lds + 1024 + 16 * lane) = make_uint4(0, 0, 0, 0);
     tele_lds_fence();
     acc0 = acc1;
     acc1 = tele_f32x4{0.f, 0.f, 0.f, 0.f};
@@ -251,18 +258,13 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
       if (ok) acc0[0] += (float)(col + p0 + p1 + p2 + row);
       continue;
     }
-    // zero both operand sets, scatter this lane's event into its chunk's set
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      uint8_t* z = lds + h * kTeleSetBytes + (lane >> 2) * kTeleRowBytes + (lane & 3) * 16;
-      *reinterpret_cast<uint4*>(z) = make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(z + 16 * kTeleRowBytes) = make_uint4(0, 0, 0, 0);
-      *reinterpret_cast<uint4*>(z + kTeleBOffset) = make_uint4(0, 0, 0, 0);
-    }
-    tele_lds_fence();
+    // scatter this lane's event into its chunk's operand set (the tiles are zero
+    // between uses: every store is undone once the fragments are read)
     const int lr = row - 16 * (half ? ilo1 : ilo0);
+    uint8_t* bcol = mine_set + kTeleBOffset + 2 * t;
+    uint8_t* arow = mine_set + lr * kTeleRowBytes + 2 * t;
+    const bool in_a = ok && lr < kTeleARows;
     if (ok) {
-      uint8_t* bcol = mine_set + kTeleBOffset + 2 * t;
       tele_st16(bcol, kOne);  // column 0: count
       if (col >= 0) {
         tele_st16(bcol + col * kTeleRowBytes, p0);
@@ -271,8 +273,8 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
           tele_st16(bcol + (col + 2) * kTeleRowBytes, p2);
         }
       }
-      if (lr < kTeleARows) tele_st16(mine_set + lr * kTeleRowBytes + 2 * t, kOne);
     }
+    if (in_a) tele_st16(arow, kOne);
     tele_lds_fence();
     uint4 a[2][2], b[2];
 #pragma unroll
@@ -282,6 +284,18 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
       a[h][0] = *reinterpret_cast<const uint4*>(sb);
       a[h][1] = *reinterpret_cast<const uint4*>(sb + 16 * kTeleRowBytes);
     }
+    tele_lds_fence();
+    if (ok) {
+      tele_st16(bcol, 0);
+      if (col >= 0) {
+        tele_st16(bcol + col * kTeleRowBytes, 0);
+        if (col >= 4) {
+          tele_st16(bcol + (col + 1) * kTeleRowBytes, 0);
+          tele_st16(bcol + (col + 2) * kTeleRowBytes, 0);
+        }
+      }
+    }
+    if (in_a) tele_st16(arow, 0);
     tele_lds_fence();
     if constexpr (DIAG == 3) {
       acc0[0] += __uint_as_float(a[0][0].x ^ a[0][1].y ^ b[0].z ^ a[1][0].x ^ a[1][1].y ^ b[1].z);
@@ -299,13 +313,13 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
         // at the new c folds only its upper half (the new tile c + 1)
         shift();
         uint8_t* sa = lds + h * kTeleSetBytes;
-        *reinterpret_cast<uint4*>(sa + (16 + (lane >> 2)) * kTeleRowBytes + (lane & 3) * 16) =
-            make_uint4(0, 0, 0, 0);
-        tele_lds_fence();
         const int lr2 = row - 16 * c;
-        if (ok && half == h && lr2 >= 16 && lr2 < kTeleARows) tele_st16(sa + lr2 * kTeleRowBytes + 2 * t, kOne);
+        const bool in2 = ok && half == h && lr2 >= 16 && lr2 < kTeleARows;
+        if (in2) tele_st16(sa + lr2 * kTeleRowBytes + 2 * t, kOne);
         tele_lds_fence();
         const uint4 a1 = *reinterpret_cast<const uint4*>(sa + (16 + fr) * kTeleRowBytes + fg * 16);
+        tele_lds_fence();
+        if (in2) tele_st16(sa + lr2 * kTeleRowBytes + 2 * t, 0);
         tele_lds_fence();
         acc1 = tele_mfma(a1, b[h], acc1);
       }
