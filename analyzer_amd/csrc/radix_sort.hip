@@ -13,7 +13,8 @@
 //   downsweep per tile: stable rank in wave order (8 ballots -> peer mask),
 //             wave prefixes in LDS, local scatter into an LDS-sorted tile,
 //             then coalesced runs to the global digit offsets.
-// 8-bit digits, 4096-element tiles (256 threads x 16), ceil(bits / 8) passes.
+// 4096-element tiles (256 threads x 16); 8-bit digits (10-bit ones for the schedule
+// are an opt-in experiment, ANA_SORT_RB: fewer passes but measured slower).
 //
 // The schedule prepass (launch_sched_sort) fuses both ends: pass 0 computes its
 // keys from the match records, and the last pass writes each slot's link from
@@ -21,6 +22,8 @@
 // for the fix-up).  For 10M 3v3 matches that drops a 480-MB key/value write, the
 // re-reads of it and a separate 720-MB link pass.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "common.h"
 #include "kernels.h"
@@ -33,7 +36,8 @@ constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
-constexpr int kRadix = 256;
+constexpr int kRadix = 256;      // 8-bit digits (generic sort; schedule keys > 20 bits)
+constexpr int kRadixMax = 1024;  // 10-bit digits: the schedule of <= 2^20 players in 2 passes
 
 // Tile of this workgroup.  Workgroups go round-robin over the 8 XCDs; giving
 // each XCD a contiguous range of tiles puts the digit runs that consecutive
@@ -105,14 +109,15 @@ __device__ __forceinline__ void decode_tile_keys(const int32_t* __restrict__ rec
 }
 
 // KS > 0: keys from the match stream (decode_tile_keys).
-template <int KS>
+template <int KS, int RB = 8>
 __global__ void __launch_bounds__(kThreads)
 radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec, uint32_t kend,
               int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles) {
-  __shared__ uint32_t hist[kWaves][kRadix];
+  constexpr int kR = 1 << RB;
+  __shared__ uint32_t hist[kWaves][kR];
   __shared__ uint32_t lkeys[KS > 0 ? kTile : 1];
   const int tid = threadIdx.x, wv = tid >> 6;
-  for (int i = tid; i < kWaves * kRadix; i += kThreads) (&hist[0][0])[i] = 0u;
+  for (int i = tid; i < kWaves * kR; i += kThreads) (&hist[0][0])[i] = 0u;
   const int64_t tile = xcd_tile(tiles);
   const int64_t base = tile * kTile;
   if constexpr (KS > 0) decode_tile_keys<KS>(rec, kend, base, n, lkeys);
@@ -122,14 +127,34 @@ radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec
     const int64_t idx = base + k * kThreads + tid;
     if (idx < n) {
       const uint32_t key = KS > 0 ? lkeys[k * kThreads + tid] : keys[idx];
-      atomicAdd(&hist[wv][(key >> shift) & (kRadix - 1)], 1u);
+      atomicAdd(&hist[wv][(key >> shift) & (kR - 1)], 1u);
     }
   }
   __syncthreads();
-  uint32_t c = 0;
 #pragma unroll
-  for (int w = 0; w < kWaves; ++w) c += hist[w][tid];
-  counts[(int64_t)tid * tiles + tile] = c;
+  for (int d = tid; d < kR; d += kThreads) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) c += hist[w][d];
+    counts[(int64_t)d * tiles + tile] = c;
+  }
+}
+
+// exclusive scan over kR per-digit values held as DPT = kR / kThreads consecutive
+// digits per thread (v[] in, prefixes out); *total = the sum of all
+template <int DPT>
+__device__ __forceinline__ void digits_exclusive_scan(uint32_t (&v)[DPT], uint32_t* wsum,
+                                                      uint32_t* total) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    const uint32_t x = v[j];
+    v[j] = s;
+    s += x;
+  }
+  const uint32_t before = block_exclusive_scan(s, wsum, total);
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) v[j] += before;
 }
 
 // One workgroup per digit: counts[d][*] <- exclusive prefix over tiles; totals[d] <- row sum.
@@ -165,26 +190,34 @@ radix_rowscan(uint32_t* __restrict__ counts, int64_t tiles, uint32_t* __restrict
 // its neighbours in the LDS-sorted tile -- within a (tile, digit) run they are
 // its global neighbours -- and only the run-boundary pairs, whose outer
 // neighbour lives in another tile (sched_fixup completes those links).
-template <int KS, bool LINK>
+template <int KS, bool LINK, int RB = 8>
 __global__ void __launch_bounds__(kThreads)
 radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                 const int32_t* __restrict__ rec, uint32_t kend,
                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
                 int64_t tiles, int slots_per_match, uint32_t* __restrict__ link) {
+  constexpr int kR = 1 << RB;
+  constexpr int DPT = kR / kThreads;  // digits per thread in the scans
+  static_assert(DPT >= 1 && DPT * kThreads == kR, "radix must be a multiple of the block");
   __shared__ uint32_t skey[kTile];
   __shared__ uint32_t sval[kTile];
-  __shared__ uint32_t wcnt[kWaves][kRadix];
-  __shared__ uint32_t tstart[kRadix];
-  __shared__ uint32_t gstart[kRadix];
+  __shared__ uint32_t wcnt[kWaves][kR];
+  __shared__ uint32_t tstart[kR];
+  __shared__ uint32_t gstart[kR];
   __shared__ uint32_t wsum[kWaves];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t tile = xcd_tile(tiles);
   const int64_t base = tile * kTile;
-  for (int i = tid; i < kWaves * kRadix; i += kThreads) (&wcnt[0][0])[i] = 0u;
+  for (int i = tid; i < kWaves * kR; i += kThreads) (&wcnt[0][0])[i] = 0u;
   {  // global start of each digit for this tile
-    const uint32_t dstart = block_exclusive_scan(totals[tid], wsum, nullptr);
-    gstart[tid] = dstart + counts[(int64_t)tid * tiles + tile];
+    uint32_t v[DPT];
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) v[j] = totals[tid * DPT + j];
+    digits_exclusive_scan<DPT>(v, wsum, nullptr);
+#pragma unroll
+    for (int j = 0; j < DPT; ++j)
+      gstart[tid * DPT + j] = v[j] + counts[(int64_t)(tid * DPT + j) * tiles + tile];
   }
   if constexpr (KS > 0) decode_tile_keys<KS>(rec, kend, base, n, sval);  // sval: scratch until the scatter
   __syncthreads();
@@ -205,10 +238,10 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
   }
 #pragma unroll
   for (int it = 0; it < kItems; ++it) {
-    const uint32_t d = (key[it] >> shift) & (kRadix - 1);
+    const uint32_t d = (key[it] >> shift) & (kR - 1);
     uint64_t peers = ~0ull;
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < RB; ++b) {
       const uint64_t bal = __ballot((d >> b) & 1u);
       peers &= ((d >> b) & 1u) ? bal : ~bal;
     }
@@ -219,19 +252,27 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
   }
   __syncthreads();
   {  // per-digit prefix over waves, then tile-local digit starts
-    uint32_t c[kWaves], s = 0;
+    uint32_t v[DPT];
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
-      c[w] = wcnt[w][tid];
-      wcnt[w][tid] = s;
-      s += c[w];
+    for (int j = 0; j < DPT; ++j) {
+      const int d = tid * DPT + j;
+      uint32_t s = 0;
+#pragma unroll
+      for (int w = 0; w < kWaves; ++w) {
+        const uint32_t c = wcnt[w][d];
+        wcnt[w][d] = s;
+        s += c;
+      }
+      v[j] = s;
     }
-    tstart[tid] = block_exclusive_scan(s, wsum, nullptr);
+    digits_exclusive_scan<DPT>(v, wsum, nullptr);
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) tstart[tid * DPT + j] = v[j];
   }
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < kItems; ++it) {
-    const uint32_t d = (key[it] >> shift) & (kRadix - 1);
+    const uint32_t d = (key[it] >> shift) & (kR - 1);
     const uint32_t pos = tstart[d] + wcnt[wv][d] + rank[it];
     skey[pos] = key[it];
     sval[pos] = val[it];
@@ -243,13 +284,13 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
     const int i = k * kThreads + tid;
     if (i < nvalid) {
       const uint32_t kk = skey[i];
-      const uint32_t d = (kk >> shift) & (kRadix - 1);
+      const uint32_t d = (kk >> shift) & (kR - 1);
       const int64_t o = (int64_t)gstart[d] + (i - (int64_t)tstart[d]);
       if constexpr (!LINK) {
         kout[o] = kk;
         vout[o] = sval[i];
       } else {
-        const int hi = d + 1 < (uint32_t)kRadix ? (int)tstart[d + 1] : kTile;
+        const int hi = d + 1 < (uint32_t)kR ? (int)tstart[d + 1] : kTile;
         const bool first = i == (int)tstart[d];
         const bool last = i + 1 == hi || i + 1 >= nvalid;
         const uint32_t v = sval[i];
@@ -272,17 +313,21 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
 // (tile, digit) run; its first pair's predecessor and its last pair's successor
 // are the last / first pairs of the neighbouring runs, which that pass wrote.
 // Grid: (tile groups of 256, digits); blocks of empty digits exit at once.
+template <int RB = 8>
 __global__ void __launch_bounds__(kThreads)
 sched_fixup(const uint32_t* __restrict__ kout, const uint32_t* __restrict__ vout, int64_t n,
             uint32_t kend, const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
             int64_t tiles, int slots_per_match, uint32_t* __restrict__ link) {
+  constexpr int kR = 1 << RB;
   __shared__ uint32_t wsum[kWaves];
   const int d = blockIdx.y;
   const uint32_t tot = totals[d];
   if (tot == 0) return;
+  uint32_t below = 0;
+#pragma unroll
+  for (int j = threadIdx.x; j < kR; j += kThreads) below += j < d ? totals[j] : 0u;
   uint32_t all = 0;
-  const uint32_t before = block_exclusive_scan(threadIdx.x < (unsigned)d ? totals[threadIdx.x] : 0u,
-                                               wsum, &all);
+  const uint32_t before = block_exclusive_scan(below, wsum, &all);
   (void)before;
   const uint32_t dstart = all;  // sum of the totals of the digits below d
   const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -314,7 +359,7 @@ sched_fixup(const uint32_t* __restrict__ kout, const uint32_t* __restrict__ vout
 
 size_t radix_sort_workspace_bytes(int64_t n) {
   const int64_t tiles = (n + kTile - 1) / kTile;
-  return (size_t)(tiles * kRadix + kRadix) * 4;
+  return (size_t)(tiles * kRadixMax + kRadixMax) * 4;
 }
 
 int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
@@ -341,34 +386,39 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 
 // The schedule's sort (K5): the slots of the stream by player, stable, fused at
 // both ends -- the first pass reads the records (no key array is written), the
-// last pass writes links instead of sorted pairs, then sched_fixup.
-template <int K>
+// last pass writes links instead of sorted pairs, then sched_fixup.  RB-bit
+// digits (8; 10 as an experiment).
+template <int K, int RB>
 static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits, uint32_t* ka,
                          uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* counts,
-                         uint32_t* totals, int64_t tiles, uint32_t* link, hipStream_t s) {
+                         int64_t tiles, uint32_t* link, hipStream_t s) {
   constexpr int S = 2 * K;
+  constexpr int kR = 1 << RB;
+  uint32_t* totals = counts + tiles * kR;
   const dim3 grid((unsigned)tiles), block(kThreads);
   const uint32_t *ki = nullptr, *vi = nullptr;
   uint32_t *ko = kb, *vo = vb;
-  for (int shift = 0; shift < bits; shift += 8) {
-    const bool first = shift == 0, last = shift + 8 >= bits;
-    if (first) hipLaunchKernelGGL(radix_upsweep<K>, grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles);
-    else hipLaunchKernelGGL(radix_upsweep<0>, grid, block, 0, s, ki, nullptr, kend, n, shift, counts, tiles);
-    hipLaunchKernelGGL(radix_rowscan, dim3(kRadix), block, 0, s, counts, tiles, totals);
+  for (int shift = 0; shift < bits; shift += RB) {
+    const bool first = shift == 0, last = shift + RB >= bits;
+    if (first)
+      hipLaunchKernelGGL((radix_upsweep<K, RB>), grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles);
+    else
+      hipLaunchKernelGGL((radix_upsweep<0, RB>), grid, block, 0, s, ki, nullptr, kend, n, shift, counts, tiles);
+    hipLaunchKernelGGL(radix_rowscan, dim3(kR), block, 0, s, counts, tiles, totals);
     if (first && last)
-      hipLaunchKernelGGL((radix_downsweep<K, true>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko, vo,
+      hipLaunchKernelGGL((radix_downsweep<K, true, RB>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko, vo,
                          n, shift, counts, totals, tiles, S, link);
     else if (first)
-      hipLaunchKernelGGL((radix_downsweep<K, false>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
+      hipLaunchKernelGGL((radix_downsweep<K, false, RB>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
                          vo, n, shift, counts, totals, tiles, S, nullptr);
     else if (last)
-      hipLaunchKernelGGL((radix_downsweep<0, true>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
+      hipLaunchKernelGGL((radix_downsweep<0, true, RB>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
                          shift, counts, totals, tiles, S, link);
     else
-      hipLaunchKernelGGL((radix_downsweep<0, false>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
+      hipLaunchKernelGGL((radix_downsweep<0, false, RB>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
                          shift, counts, totals, tiles, S, nullptr);
     if (last)
-      hipLaunchKernelGGL(sched_fixup, dim3((unsigned)((tiles + kThreads - 1) / kThreads), kRadix), block,
+      hipLaunchKernelGGL((sched_fixup<RB>), dim3((unsigned)((tiles + kThreads - 1) / kThreads), kR), block,
                          0, s, ko, vo, n, kend, counts, totals, tiles, S, link);
     ki = ko;
     vi = vo;
@@ -387,10 +437,17 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
   while (bits < 32 && (1ull << bits) <= (uint64_t)num_players) ++bits;
   const int64_t tiles = (n + kTile - 1) / kTile;
   uint32_t* counts = static_cast<uint32_t*>(ws);
-  uint32_t* totals = counts + tiles * kRadix;
+  // ANA_SORT_RB=10: 10-bit digits (2 passes for <= 2^20 players instead of 3).  Measured
+  // on MI355X, 10M 3v3 / 1M players: 3.11 ms vs 1.76 ms for 8-bit digits (1024
+  // per-tile runs of ~4 elements scatter the pass's writes) -> off by default.
+  const char* rb_env = getenv("ANA_SORT_RB");
+  const bool wide = bits <= 20 && rb_env && atoi(rb_env) == 10;
   switch (K) {
-#define ANA_SORT_CASE(k) \
-  case k: sched_sort_k<k>(rec, n, num_players, bits, ka, va, kb, vb, counts, totals, tiles, link, s); break;
+#define ANA_SORT_CASE(k)                                                                         \
+  case k:                                                                                        \
+    if (wide) sched_sort_k<k, 10>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s); \
+    else sched_sort_k<k, 8>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s);  \
+    break;
     ANA_SORT_CASE(1) ANA_SORT_CASE(2) ANA_SORT_CASE(3) ANA_SORT_CASE(4) ANA_SORT_CASE(5)
 #undef ANA_SORT_CASE
     default: return (int)hipErrorInvalidValue;
