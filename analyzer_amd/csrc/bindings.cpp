@@ -220,7 +220,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
           Tensor delta, Tensor m_mu, Tensor m_sig, Tensor ctrl, Tensor vst, double beta2,
           double tau2, double unknown_sigma, bool record_first_prior, int64_t blocks,
           int64_t epoch, bool host_fp64, Tensor tele_evoff, Tensor tele_events, Tensor tele_stats,
-          int64_t progress, int64_t progress_value, int64_t progress_at) {
+          int64_t progress, int64_t progress_value, int64_t progress_at, int64_t epoch_ptr) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
@@ -259,7 +259,8 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   prm.num_players = (int32_t)P;
   prm.num_matches = M;
   prm.record_first_prior = record_first_prior ? 1 : 0;
-  TORCH_CHECK(epoch >= 1 && epoch <= 255, "epoch must be 1..255");
+  prm.epoch_ptr = reinterpret_cast<const int32_t*>((intptr_t)epoch_ptr);
+  TORCH_CHECK(prm.epoch_ptr ? dev.is_cuda() : (epoch >= 1 && epoch <= 255), "epoch must be 1..255");
   prm.epoch = (int32_t)epoch;
   prm.vst = vst.data_ptr<float>();
   if (const char* e = std::getenv("ANA_RATE_IDLE")) prm.idle_spins = std::atoi(e);  // tuning knob
@@ -497,6 +498,11 @@ static py::object reader_acquire(ana::RecordReader& r) {
   return py::make_tuple(slot, base, t);
 }
 
+void epoch_bump(Tensor e) {
+  TORCH_CHECK(e.is_cuda() && e.scalar_type() == torch::kInt32 && e.numel() >= 1, "epoch must be a device int32 tensor");
+  check_hip(ana::launch_epoch_bump(e.data_ptr<int32_t>(), stream_of(e)), "epoch_bump");
+}
+
 void reset_tags(Tensor state) {
   const auto dev = state.device();
   check(state, "state", torch::kFloat32, dev);
@@ -544,6 +550,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stream_wait_value64", &stream_wait_value64, "hipStreamWaitValue64(stream, ptr, >= value)");
   m.def("can_wait_value", &can_wait_value, "hipDeviceAttributeCanUseStreamWaitValue");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
+  m.def("epoch_bump", &epoch_bump, "device launch epoch += 1 (graph replays)");
   m.attr("ROW_FLOATS") = ana::kRowFloats;
   m.attr("N_TRACKS") = ana::kTracks;
   m.attr("VST_TIERS") = ana::kVstTiers;

@@ -70,6 +70,7 @@ struct RateParams {
   int64_t num_matches;
   int32_t record_first_prior;  // sweep mode: remember priors of NULL tracks
   int32_t epoch;               // 1..255: granule tag word 1 of this launch (word 3 = match)
+  const int32_t* epoch_ptr;    // device: read the epoch here instead (graph replays bump it)
   const float* vst;            // vst_points[tier + 1], kVstTiers entries (device/host memory)
   int32_t idle_spins;          // dataflow: max s_sleep(2) rounds of an idle wave (0 = default)
   int32_t debug_flags;         // experiments only (ANA_RATE_DEBUG): 2 skip slot outputs

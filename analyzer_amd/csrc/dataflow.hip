@@ -139,7 +139,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   const int64_t M = prm.num_matches;
   const int64_t P = prm.num_players;
   const float beta2 = prm.beta2, tau2 = prm.tau2, us = prm.unknown_sigma;
-  const int epoch = prm.epoch;
+  // graph replays (ops/graph.py) keep the epoch in device memory, bumped before each launch
+  const int epoch = prm.epoch_ptr ? __builtin_amdgcn_readfirstlane(*prm.epoch_ptr) : prm.epoch;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(state, 0, (int)(P * kRowFloats * 4), 0x00020000);
   const int head = blockIdx.x % kHeads;
@@ -644,7 +645,7 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   if (hipMemsetAsync(ctrl + 1, 0, 15 * 4, s) != hipSuccess) return (int)hipGetLastError();
   if (M <= 0) return 0;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
-  if (prm.epoch < 1 || prm.epoch > 255) return (int)hipErrorInvalidValue;
+  if (!prm.epoch_ptr && (prm.epoch < 1 || prm.epoch > 255)) return (int)hipErrorInvalidValue;
   // the executor writes one packed row per match (ops/rate.py RateResult.allocate)
   const int S = 2 * K;
   if (!(out.s_sig == out.s_mu + S && out.delta == out.s_mu + 2 * S && out.m_mu == out.s_mu + 3 * S &&

@@ -16,6 +16,8 @@ int launch_gen_roster(const GenRosterParams& g, float* state, float* attrs, hipS
 int launch_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M, hipStream_t s);
 
 int launch_reset_tags(float* state, int64_t P, hipStream_t s);
+// e[0] += 1 on the stream (the device epoch of graph replays, RateParams::epoch_ptr)
+int launch_epoch_bump(int32_t* e, hipStream_t s);
 
 size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
 

@@ -94,6 +94,15 @@ int launch_reset_tags(float* state, int64_t P, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Device-side launch epoch of a captured graph: one bump per replay, before the
+// rate launch that reads it (the host resets the tags and the counter before 255).
+__global__ void epoch_bump_kernel(int32_t* e) { e[0] += 1; }
+
+int launch_epoch_bump(int32_t* e, hipStream_t s) {
+  hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(1), 0, s, e);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------- schedule
 static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -102,9 +111,129 @@ size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players) {
   return 4 * align_up(nslots * 4) + align_up(radix_sort_workspace_bytes(nslots));
 }
 
+// Micro-batch schedule (a worker batch of <= kSmallSched slots, e.g. 500 3v3 or
+// 5v5 matches): ONE workgroup keys the slots (player, or past the last player
+// for matches that touch no state), sorts (key << 32 | slot) -- stable by slot,
+// like the radix path --, writes every slot's link from its sorted neighbours
+// and zeroes the completion counters: one dispatch instead of the radix path's
+// ~12, which are launch-bound at this size.  The bitonic network keeps E
+// consecutive elements per thread in registers: exchanges closer than E run in
+// registers, closer than 64 E (one wave) through lane shuffles, and only the
+// few wider ones through LDS with a barrier.
+constexpr int kSmallSched = 8192;
+constexpr int kSmallThreads = 512;
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+template <int K, int E>
+__global__ void __launch_bounds__(kSmallThreads)
+sched_small_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uint32_t* __restrict__ link,
+                   int32_t* __restrict__ deps, uint32_t* __restrict__ overflow) {
+  constexpr int S = 2 * K, R = S + 2;
+  constexpr int NP = kSmallThreads * E;  // padded sort size
+  __shared__ uint64_t kv[NP];
+  const int tid = threadIdx.x;
+  const int n = (int)(M * S);
+  for (int m = tid; m < (int)M; m += kSmallThreads) {
+    int32_t r[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) r[k] = rec[(int64_t)m * R + k];
+    const bool rates = early_status<K>(r, (int64_t)kend) == kRated;
+    const uint32_t m0 = (uint32_t)r[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int pos = j < K ? j : j - K;
+      const bool in_roster = pos < (j < K ? meta_n0(m0) : meta_n1(m0));
+      const uint32_t key = rates && in_roster ? (uint32_t)r[j] : kend;
+      kv[m * S + j] = ((uint64_t)key << 32) | (uint32_t)(m * S + j);
+    }
+    deps[m] = 0;
+  }
+  for (int i = n + tid; i < NP; i += kSmallThreads) kv[i] = ~0ull;
+  if (tid == 0) *overflow = 0u;
+  __syncthreads();
+  uint64_t x[E];
+#pragma unroll
+  for (int q = 0; q < E; ++q) x[q] = kv[tid * E + q];
+  for (int k = 2; k <= NP; k <<= 1) {
+    for (int j = k >> 1; j >= E; j >>= 1) {
+      const bool wave = j < 64 * E;
+      if (!wave) {  // partner in another wave: exchange through LDS
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < E; ++q) kv[tid * E + q] = x[q];
+        __syncthreads();
+      }
+#pragma unroll
+      for (int q = 0; q < E; ++q) {  // partner: same register of lane ^ j / E, or LDS
+        const int i = tid * E + q;
+        const uint64_t y = wave ? shfl_xor64(x[q], j / E) : kv[i ^ j];
+        const bool lower = (i & j) == 0, asc = (i & k) == 0;
+        const uint64_t lo = x[q] < y ? x[q] : y, hi = x[q] < y ? y : x[q];
+        x[q] = lower == asc ? lo : hi;
+      }
+    }
+    // partners in this thread's registers (compile-time indices: no scratch)
+#pragma unroll
+    for (int jj = E / 2; jj > 0; jj >>= 1) {
+      if (jj >= k) continue;
+#pragma unroll
+      for (int q = 0; q < E; ++q) {
+        const int qp = q ^ jj;
+        if (qp > q) {
+          const int i = tid * E + q;
+          const uint64_t a = x[q], b = x[qp];
+          if ((a > b) == ((i & k) == 0)) {
+            x[q] = b;
+            x[qp] = a;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < E; ++q) kv[tid * E + q] = x[q];
+  __syncthreads();
+  for (int p = tid; p < n; p += kSmallThreads) {
+    const uint64_t v64 = kv[p];
+    const uint32_t key = (uint32_t)(v64 >> 32), v = (uint32_t)v64;
+    uint32_t w = kNoMatch;
+    if (key < kend) {
+      if (p + 1 < n && (uint32_t)(kv[p + 1] >> 32) == key) w = (uint32_t)kv[p + 1] / (uint32_t)S;
+      if (p > 0 && (uint32_t)(kv[p - 1] >> 32) == key) w |= kLinkHasPred;
+    }
+    link[v] = w;
+  }
+}
+
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s) {
   const int64_t n = M * 2 * K;
+  if (n > 0 && n <= kSmallSched && P < 0x7fffffffLL && K >= 1 && K <= 5) {
+    const int e = n <= 2048 ? 4 : n <= 4096 ? 8 : 16;  // elements per thread
+    switch (K) {
+#define ANA_SMALL_CASE(k)                                                                            \
+  case k:                                                                                            \
+    if (e == 4)                                                                                      \
+      hipLaunchKernelGGL((sched_small_kernel<k, 4>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
+                         (uint32_t)P, link, deps, overflow);                                         \
+    else if (e == 8)                                                                                 \
+      hipLaunchKernelGGL((sched_small_kernel<k, 8>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
+                         (uint32_t)P, link, deps, overflow);                                         \
+    else                                                                                             \
+      hipLaunchKernelGGL((sched_small_kernel<k, 16>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,    \
+                         (uint32_t)P, link, deps, overflow);                                         \
+    break;
+      ANA_SMALL_CASE(1) ANA_SMALL_CASE(2) ANA_SMALL_CASE(3) ANA_SMALL_CASE(4) ANA_SMALL_CASE(5)
+#undef ANA_SMALL_CASE
+    }
+    return (int)hipGetLastError();
+  }
   ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 4, s));
   if (n <= 0) return 0;
   if (n > kMaxSlots || P >= 0x7fffffffLL || K < 1 || K > 5) return (int)hipErrorInvalidValue;

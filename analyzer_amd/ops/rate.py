@@ -178,6 +178,17 @@ class BatchRater:
         self._vst: Dict[str, torch.Tensor] = {}
         self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
 
+    def grid_blocks(self, M: int, telemetry: bool = False) -> int:
+        """Persistent-grid size for a window of M matches: ``self.blocks`` (512,
+        measured best for 10M-match windows), but no more than one wave per
+        64-match chunk -- a micro-batch of 500 matches needs 8 waves, not 2048
+        (the extra workgroups only cost launch and exit time).  Fused telemetry
+        keeps the full grid (its tiles need the waves)."""
+        if telemetry:
+            return self.blocks
+        chunks = -(-M // 64)
+        return max(1, min(self.blocks, -(-chunks // 4)))
+
     # ------------------------------------------------------------- buffers
     def vst(self, device) -> torch.Tensor:
         key = str(device)
@@ -220,14 +231,16 @@ class BatchRater:
     def rate(self, roster: Roster, rec: torch.Tensor, K: Optional[int] = None,
              out: Optional[RateResult] = None, first_prior: Optional[torch.Tensor] = None,
              check: bool = True, schedule: Optional[Schedule] = None,
-             telemetry=None, progress=None) -> RateResult:
+             telemetry=None, progress=None, epoch_dev: Optional[torch.Tensor] = None) -> RateResult:
         """Rate every match of ``rec`` in order, updating ``roster`` in place.
 
         ``telemetry`` = (evoff [M+1] int64, events [E,4] int32, stats [M,2K,8] f32):
         per-participant telemetry is aggregated into ``stats`` in the same launch
         (K8 fused streaming mode: idle dataflow waves take telemetry tiles).
         ``progress`` = (signal address, launch number, chunk index): the tail
-        signal of runtime/engine.py (device only)."""
+        signal of runtime/engine.py (device only).  ``epoch_dev``: a device int32
+        tensor holding the launch epoch (graph replays, ops/graph.py); the
+        roster's host-side epoch is then left alone."""
         K = int(K or (rec.shape[1] - 2) // 2)
         M = int(rec.shape[0])
         dev = rec.device
@@ -244,7 +257,7 @@ class BatchRater:
                 schedule = self.schedule(rec, K, P)
             link, deps = schedule
             ctrl = self._buffer(dev, "ctrl", 16, torch.int32)
-            epoch = roster.next_epoch()
+            epoch = roster.next_epoch() if epoch_dev is None else 1
         else:
             link = deps = ctrl = torch.empty(0, dtype=torch.int32)
             epoch = 1
@@ -254,8 +267,10 @@ class BatchRater:
         native().rate(rec, K, link, deps, roster.state, roster.attrs, fp, out.quality, out.status,
                       out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
                       float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
-                      record, self.blocks, epoch, self.host_fp64, *telemetry,
-                      *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)))
+                      record, self.grid_blocks(M, telemetry[0].numel() > 0), epoch,
+                      self.host_fp64, *telemetry,
+                      *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
+                      epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0)
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out

@@ -52,8 +52,11 @@ def _stateful_slots(rec: np.ndarray, K: int, P: int):
 
 # 1 (P=20), 2 (P=300, 5000), 3 (P=70k) and 4 (P=17M) radix passes: every
 # combination of the fused first / last passes of the schedule sort
+# + micro-batches (<= 8192 slots): the one-workgroup LDS bitonic schedule
 @pytest.mark.parametrize("P,M,K", [(20, 3000, 3), (5000, 100000, 3), (300, 20000, 5),
-                                   (70_000, 400_000, 3), (17_000_000, 300_000, 3)])
+                                   (70_000, 400_000, 3), (17_000_000, 300_000, 3),
+                                   (50, 400, 3), (5000, 819, 5), (1_000_000, 1365, 3), (20, 1, 1),
+                                   (40, 700, 2)])
 def test_schedule_matches_host(gpu_device, P, M, K):
     ss = StreamSpec(team_size=K, seed=P, p_afk=0.05, p_unsupported=0.05, p_uneven=0.05, p_hot=0.2)
     rec = make_stream(ss, M, P, K=K)
@@ -216,6 +219,34 @@ def test_telemetry_impls_vs_oracle_edges(gpu_device, monkeypatch, K, impl):
     assert int(bad.item()) == int((~ok).sum())
     np.testing.assert_allclose(stats.cpu().numpy(), ref, rtol=2e-6, atol=1e-3)
     np.testing.assert_allclose(host.numpy(), ref, rtol=2e-6, atol=1e-3)
+
+
+def test_graph_rater_matches_eager(gpu_device):
+    """Micro-batches replayed as one HIP graph (ops/graph.py) rate exactly like
+    eager launches: every batch size up to the capacity, and across the epoch
+    wrap (tag reset) of the device-side launch epoch."""
+    from analyzer_amd.ops.graph import GraphRater
+
+    K, P = 3, 20000
+    roster = make_roster(RosterSpec(num_players=P, seed=11), device=gpu_device)
+    ref = roster.clone()
+    stream = make_stream(StreamSpec(team_size=K, seed=12, p_afk=0.05, p_tie=0.05), 6000, P, K=K,
+                         device=gpu_device)
+    gr = GraphRater(roster, K, capacity=512)
+    br = R.BatchRater()
+    off = 0
+    for i, m in enumerate([500, 100, 512, 37, 400, 1, 512, 300]):
+        if i == 5:
+            gr._bumps = gr.MAX_EPOCH - 2  # the next replays pass the wrap: tags reset
+        batch = stream[off:off + m]
+        off += m
+        got = gr.rate(batch)
+        gr.check()
+        exp = br.rate(ref, batch, K)
+        assert torch.equal(got.status, exp.status)
+        for f in ("quality", "s_mu", "s_sig", "delta", "m_mu", "m_sig"):
+            assert torch.equal(getattr(got, f).nan_to_num(-7), getattr(exp, f).nan_to_num(-7)), f
+        assert torch.equal(roster.state[:, 0::2].nan_to_num(-7), ref.state[:, 0::2].nan_to_num(-7))
 
 
 def test_fused_rate_telemetry_on_device(gpu_device):
