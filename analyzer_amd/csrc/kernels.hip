@@ -121,7 +121,7 @@ size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players) {
 // registers, closer than 64 E (one wave) through lane shuffles, and only the
 // few wider ones through LDS with a barrier.
 constexpr int kSmallSched = 8192;
-constexpr int kSmallThreads = 512;
+constexpr int kSmallThreads = 1024;
 
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
@@ -215,18 +215,18 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s) {
   const int64_t n = M * 2 * K;
   if (n > 0 && n <= kSmallSched && P < 0x7fffffffLL && K >= 1 && K <= 5) {
-    const int e = n <= 2048 ? 4 : n <= 4096 ? 8 : 16;  // elements per thread
+    const int e = n <= 2048 ? 2 : n <= 4096 ? 4 : 8;  // elements per thread
     switch (K) {
 #define ANA_SMALL_CASE(k)                                                                            \
   case k:                                                                                            \
-    if (e == 4)                                                                                      \
+    if (e == 2)                                                                                      \
+      hipLaunchKernelGGL((sched_small_kernel<k, 2>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
+                         (uint32_t)P, link, deps, overflow);                                         \
+    else if (e == 4)                                                                                 \
       hipLaunchKernelGGL((sched_small_kernel<k, 4>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
                          (uint32_t)P, link, deps, overflow);                                         \
-    else if (e == 8)                                                                                 \
-      hipLaunchKernelGGL((sched_small_kernel<k, 8>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
-                         (uint32_t)P, link, deps, overflow);                                         \
     else                                                                                             \
-      hipLaunchKernelGGL((sched_small_kernel<k, 16>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,    \
+      hipLaunchKernelGGL((sched_small_kernel<k, 8>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
                          (uint32_t)P, link, deps, overflow);                                         \
     break;
       ANA_SMALL_CASE(1) ANA_SMALL_CASE(2) ANA_SMALL_CASE(3) ANA_SMALL_CASE(4) ANA_SMALL_CASE(5)
