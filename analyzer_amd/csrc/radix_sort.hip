@@ -48,6 +48,22 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t tiles) {
   return x * q + (x < r ? x : r) + (i >> 3);
 }
 
+// NT: streaming (non-temporal) accesses for the sort's key/value/link traffic, so
+// a prepass that co-runs with the dataflow executor does not evict the roster
+// the executor keeps in the Infinity Cache.  Opt-in (ANA_SORT_NT=1): measured on
+// MI355X the prepass slows 1.75 -> 4.35 ms (the digit runs lose L2 write
+// combining) and the bench step 8.1 -> 9.2 ms.
+template <bool NT>
+__device__ __forceinline__ uint32_t ld32(const uint32_t* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st32(uint32_t* p, uint32_t v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 // exclusive scan of one value per thread over a 256-thread block
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* wsum,
                                                          uint32_t* total) {
@@ -109,7 +125,7 @@ __device__ __forceinline__ void decode_tile_keys(const int32_t* __restrict__ rec
 }
 
 // KS > 0: keys from the match stream (decode_tile_keys).
-template <int KS, int RB = 8>
+template <int KS, int RB = 8, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
 radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec, uint32_t kend,
               int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles) {
@@ -126,7 +142,7 @@ radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec
   for (int k = 0; k < kItems; ++k) {
     const int64_t idx = base + k * kThreads + tid;
     if (idx < n) {
-      const uint32_t key = KS > 0 ? lkeys[k * kThreads + tid] : keys[idx];
+      const uint32_t key = KS > 0 ? lkeys[k * kThreads + tid] : ld32<NT>(keys + idx);
       atomicAdd(&hist[wv][(key >> shift) & (kR - 1)], 1u);
     }
   }
@@ -190,7 +206,7 @@ radix_rowscan(uint32_t* __restrict__ counts, int64_t tiles, uint32_t* __restrict
 // its neighbours in the LDS-sorted tile -- within a (tile, digit) run they are
 // its global neighbours -- and only the run-boundary pairs, whose outer
 // neighbour lives in another tile (sched_fixup completes those links).
-template <int KS, bool LINK, int RB = 8>
+template <int KS, bool LINK, int RB = 8, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
 radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                 const int32_t* __restrict__ rec, uint32_t kend,
@@ -232,8 +248,8 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
     const bool valid = idx < n;
     // pads sort last: digit 255, after every real key
     if constexpr (KS > 0) key[it] = valid ? sval[(wv * kItems + it) * 64 + lane] : 0xffffffffu;
-    else key[it] = valid ? kin[idx] : 0xffffffffu;
-    if constexpr (KS == 0) val[it] = valid ? vin[idx] : 0u;
+    else key[it] = valid ? ld32<NT>(kin + idx) : 0xffffffffu;
+    if constexpr (KS == 0) val[it] = valid ? ld32<NT>(vin + idx) : 0u;
     else val[it] = (uint32_t)idx;
   }
 #pragma unroll
@@ -287,22 +303,22 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
       const uint32_t d = (kk >> shift) & (kR - 1);
       const int64_t o = (int64_t)gstart[d] + (i - (int64_t)tstart[d]);
       if constexpr (!LINK) {
-        kout[o] = kk;
-        vout[o] = sval[i];
+        st32<NT>(kout + o, kk);
+        st32<NT>(vout + o, sval[i]);
       } else {
         const int hi = d + 1 < (uint32_t)kR ? (int)tstart[d + 1] : kTile;
         const bool first = i == (int)tstart[d];
         const bool last = i + 1 == hi || i + 1 >= nvalid;
         const uint32_t v = sval[i];
         if (first || last) {  // sched_fixup reads the boundary pairs of every run
-          kout[o] = kk;
-          vout[o] = v;
+          st32<NT>(kout + o, kk);
+          st32<NT>(vout + o, v);
         }
         if (kk < kend) {
           uint32_t w = (!last && skey[i + 1] == kk) ? sval[i + 1] / (uint32_t)slots_per_match
                                                      : kNoMatch;
           if (!first && skey[i - 1] == kk) w |= kLinkHasPred;
-          link[v] = w;
+          st32<NT>(link + v, w);
         }
       }
     }
@@ -388,7 +404,7 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 // both ends -- the first pass reads the records (no key array is written), the
 // last pass writes links instead of sorted pairs, then sched_fixup.  RB-bit
 // digits (8; 10 as an experiment).
-template <int K, int RB>
+template <int K, int RB, bool NT>
 static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits, uint32_t* ka,
                          uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* counts,
                          int64_t tiles, uint32_t* link, hipStream_t s) {
@@ -401,21 +417,21 @@ static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits,
   for (int shift = 0; shift < bits; shift += RB) {
     const bool first = shift == 0, last = shift + RB >= bits;
     if (first)
-      hipLaunchKernelGGL((radix_upsweep<K, RB>), grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles);
+      hipLaunchKernelGGL((radix_upsweep<K, RB, NT>), grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles);
     else
-      hipLaunchKernelGGL((radix_upsweep<0, RB>), grid, block, 0, s, ki, nullptr, kend, n, shift, counts, tiles);
+      hipLaunchKernelGGL((radix_upsweep<0, RB, NT>), grid, block, 0, s, ki, nullptr, kend, n, shift, counts, tiles);
     hipLaunchKernelGGL(radix_rowscan, dim3(kR), block, 0, s, counts, tiles, totals);
     if (first && last)
-      hipLaunchKernelGGL((radix_downsweep<K, true, RB>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko, vo,
+      hipLaunchKernelGGL((radix_downsweep<K, true, RB, NT>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko, vo,
                          n, shift, counts, totals, tiles, S, link);
     else if (first)
-      hipLaunchKernelGGL((radix_downsweep<K, false, RB>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
+      hipLaunchKernelGGL((radix_downsweep<K, false, RB, NT>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
                          vo, n, shift, counts, totals, tiles, S, nullptr);
     else if (last)
-      hipLaunchKernelGGL((radix_downsweep<0, true, RB>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
+      hipLaunchKernelGGL((radix_downsweep<0, true, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
                          shift, counts, totals, tiles, S, link);
     else
-      hipLaunchKernelGGL((radix_downsweep<0, false, RB>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
+      hipLaunchKernelGGL((radix_downsweep<0, false, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
                          shift, counts, totals, tiles, S, nullptr);
     if (last)
       hipLaunchKernelGGL((sched_fixup<RB>), dim3((unsigned)((tiles + kThreads - 1) / kThreads), kR), block,
@@ -442,11 +458,14 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
   // per-tile runs of ~4 elements scatter the pass's writes) -> off by default.
   const char* rb_env = getenv("ANA_SORT_RB");
   const bool wide = bits <= 20 && rb_env && atoi(rb_env) == 10;
+  const char* nt_env = getenv("ANA_SORT_NT");
+  const bool nt = nt_env ? atoi(nt_env) != 0 : false;
   switch (K) {
 #define ANA_SORT_CASE(k)                                                                         \
   case k:                                                                                        \
-    if (wide) sched_sort_k<k, 10>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s); \
-    else sched_sort_k<k, 8>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s);  \
+    if (wide) sched_sort_k<k, 10, false>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s); \
+    else if (nt) sched_sort_k<k, 8, true>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s); \
+    else sched_sort_k<k, 8, false>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s); \
     break;
     ANA_SORT_CASE(1) ANA_SORT_CASE(2) ANA_SORT_CASE(3) ANA_SORT_CASE(4) ANA_SORT_CASE(5)
 #undef ANA_SORT_CASE
