@@ -13,7 +13,7 @@ Two schedule buffer sets alternate; events order "schedule(i+1) may reuse the
 set that rate(i-1) consumed" and "rate(i) needs schedule(i)".  On the CPU the
 same API runs the host mirror sequentially.
 
-Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.7): the
+Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.8): the
 prepass of window i+1 does not start with rate(i) -- co-running the two for the
 whole launch costs the latency-bound executor about as much as the prepass
 itself -- but when rate(i) reaches its tail: the executor stores its launch
@@ -61,7 +61,7 @@ class WindowPipeline:
         self._free: List[Optional[torch.cuda.Event]] = [None, None]
         self.windows_rated = 0
         # tail overlap: signal word + number of the last enqueued rate launch
-        self.tail = float(os.environ.get("ANA_PREPASS_AT", "0.7") or 0)
+        self.tail = float(os.environ.get("ANA_PREPASS_AT", "0.8") or 0)
         self._signal = 0
         self._seq = 0
         if self.cuda and self.tail > 0:
