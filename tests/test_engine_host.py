@@ -102,3 +102,32 @@ def test_status_counts_and_any_afk():
     assert bool(res.any_afk[res.status == R.AFK].all())
     assert torch.isnan(res.quality[res.status == R.UNSUPPORTED_MODE]).all()
     assert (res.quality[res.status == R.AFK] == 0).all()
+
+
+def test_noop_padding_records_touch_nothing():
+    """The graph rater pads short batches with 'unsupported mode' records
+    (ops/graph.py): they rate as UNSUPPORTED_MODE and leave the roster alone."""
+    from analyzer_amd.ops.graph import noop_records
+
+    K, P = 3, 50
+    roster = make_roster(RosterSpec(num_players=P, seed=3))
+    before = roster.state.clone()
+    rec = torch.cat([noop_records(7, K, "cpu"),
+                     make_stream(StreamSpec(team_size=K, seed=4), 5, P, K=K),
+                     noop_records(3, K, "cpu")])
+    ref = make_roster(RosterSpec(num_players=P, seed=3))
+    res = R.BatchRater().rate(roster, rec, K)
+    exp = R.BatchRater().rate(ref, rec[7:12], K)
+    assert (res.status[:7] == R.UNSUPPORTED_MODE).all() and (res.status[12:] == R.UNSUPPORTED_MODE).all()
+    assert torch.equal(res.status[7:12], exp.status)
+    assert torch.equal(roster.state.nan_to_num(-7), ref.state.nan_to_num(-7))
+    assert not torch.equal(roster.state.nan_to_num(-7), before.nan_to_num(-7))
+
+
+def test_grid_blocks_scale_with_the_window():
+    br = R.BatchRater(blocks=512)
+    assert br.grid_blocks(500) == 2          # 8 chunks of 64 -> 8 waves
+    assert br.grid_blocks(1) == 1
+    assert br.grid_blocks(64 * 4 * 100) == 100
+    assert br.grid_blocks(10_000_000) == 512
+    assert br.grid_blocks(500, telemetry=True) == 512
