@@ -62,6 +62,14 @@ def _compile(cmd, src: Path, obj: Path, force: bool) -> str:
 
 
 def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
+    out = target_path()
+    sources = [CSRC / n for n in HIP_SOURCES + CPP_SOURCES if (CSRC / n).exists()]
+    if not force and out.exists() and out.stat().st_mtime >= max(_deps_mtime(s) for s in sources):
+        # the in-tree library is newer than every source: nothing to do (a GPU box
+        # that got the tree without build/ objects must not recompile it)
+        if verbose:
+            print("up-to-date", out, flush=True)
+        return out
     incs, libs = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     objs = []
