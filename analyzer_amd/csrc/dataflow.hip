@@ -124,9 +124,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
                      RateParams prm, TelemetryParams tp) {
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
+  // chunks held per wave: kHeld, or 2V for the A/B variants V >= 3 (ANA_RATE_VARIANT)
+  constexpr int kH = V >= 3 ? 2 * V : kHeld;
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
-  __shared__ int32_t lrec[kWavesPerBlock][kHeld][kChunk * R];
+  __shared__ int32_t lrec[kWavesPerBlock][kH][kChunk * R];
   __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -151,12 +153,12 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // experiment: issue priority over co-running kernels (the next window's prepass)
   if (prm.debug_flags & 8) __builtin_amdgcn_s_setprio(3);
 
-  int64_t cbase[kHeld];   // wave-uniform: first match of each held chunk, -1 = free slot
-  uint64_t pend[kHeld];   // wave-uniform: stateful matches not yet handed to a group
-  uint32_t dval[kHeld];   // per lane: completion counter of match cbase+lane, as last polled
-  uint32_t need[kHeld];   // per lane: the count at which that match is ready
+  int64_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
+  uint64_t pend[kH];   // wave-uniform: stateful matches not yet handed to a group
+  uint32_t dval[kH];   // per lane: completion counter of match cbase+lane, as last polled
+  uint32_t need[kH];   // per lane: the count at which that match is ready
 #pragma unroll
-  for (int h = 0; h < kHeld; ++h) {
+  for (int h = 0; h < kH; ++h) {
     cbase[h] = -1;
     pend[h] = 0ull;
     dval[h] = kNone;
@@ -204,10 +206,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         exhausted = true;
       } else {
 #pragma unroll
-        for (int h = kHeld - 1; h >= 0; --h)
+        for (int h = kH - 1; h >= 0; --h)
           if (cbase[h] < 0) staging = h;
 #pragma unroll
-        for (int h = 0; h < kHeld; ++h)
+        for (int h = 0; h < kH; ++h)
           if (h == staging) cbase[h] = c * kChunk;
         const int64_t m = c * kChunk + lane;
         if (m < M) {
@@ -234,9 +236,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
 
     // ---------------------------------------------- (2) readiness from the last poll
-    uint64_t ready[kHeld];
+    uint64_t ready[kH];
 #pragma unroll
-    for (int h = 0; h < kHeld; ++h) ready[h] = __ballot(dval[h] == need[h]) & pend[h];
+    for (int h = 0; h < kH; ++h) ready[h] = __ballot(dval[h] == need[h]) & pend[h];
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
 
     // ---------------------------------------------- (3) oldest ready matches -> groups
@@ -246,18 +248,18 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     int my_h = -1, my_bit = 0, nassigned = 0;
     // scalar: the sets, chunk bases and counts are wave-uniform; group g of
     // the wave takes the g-th pick (s_ff1 over the set of the oldest chunk)
-    auto assign = [&](uint64_t (&sets)[kHeld], int limit) {
+    auto assign = [&](uint64_t (&sets)[kH], int limit) {
 #pragma unroll
-      for (int pass = 0; pass < kHeld; ++pass) {
+      for (int pass = 0; pass < kH; ++pass) {
         int best = -1;
         int64_t bb = 0;
 #pragma unroll
-        for (int h = 0; h < kHeld; ++h)
+        for (int h = 0; h < kH; ++h)
           if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
         if (best < 0 || nassigned >= limit) break;
         uint64_t rdy = 0;
 #pragma unroll
-        for (int h = 0; h < kHeld; ++h) if (h == best) rdy = sets[h];
+        for (int h = 0; h < kH; ++h) if (h == best) rdy = sets[h];
         uint64_t taken = 0;
         while (rdy != 0ull && nassigned < limit) {
           const int b = __builtin_ctzll(rdy);
@@ -270,15 +272,15 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           ++nassigned;
         }
 #pragma unroll
-        for (int h = 0; h < kHeld; ++h)
+        for (int h = 0; h < kH; ++h)
           if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
       }
     };
     assign(ready, NG);
     if (prm.spec > 0 && nassigned < NG) {
-      uint64_t cand[kHeld];
+      uint64_t cand[kH];
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h) cand[h] = __ballot(dval[h] + 1u == need[h]) & pend[h];
+      for (int h = 0; h < kH; ++h) cand[h] = __ballot(dval[h] + 1u == need[h]) & pend[h];
       const int lim = nassigned + prm.spec < NG ? nassigned + prm.spec : NG;
       assign(cand, lim);
     }
@@ -296,7 +298,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     if (my_h >= 0) {
       int64_t cb = 0;
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h) if (h == my_h) cb = cbase[h];
+      for (int h = 0; h < kH; ++h) if (h == my_h) cb = cbase[h];
       m = cb + my_bit;
       const int32_t* lr = &lrec[wv][my_h][my_bit * R];
       const uint32_t m0 = (uint32_t)lr[S], m1 = (uint32_t)lr[S + 1];
@@ -336,7 +338,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // ---------------------------------------------- (5) next iteration's counter polls
     ++iter;
 #pragma unroll
-    for (int h = 0; h < kHeld; ++h)
+    for (int h = 0; h < kH; ++h)
       if (((pend[h] >> lane) & 1ull) && (!(prm.debug_flags & 4) || (iter & 1u)))
         dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
@@ -345,7 +347,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     {
       bool free_slot = false;
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h) free_slot |= cbase[h] < 0;
+      for (int h = 0; h < kH; ++h) free_slot |= cbase[h] < 0;
       if (free_slot && !exhausted) {
         if (lane == 0)
           tk = __hip_atomic_fetch_add((gu32*)&ctrl[4 + head], 1u, __ATOMIC_RELAXED,
@@ -361,7 +363,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     if (staging >= 0) {
       int64_t cb = 0;
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h) if (h == staging) cb = cbase[h];
+      for (int h = 0; h < kH; ++h) if (h == staging) cb = cbase[h];
       const int64_t mm = cb + lane;
       // flag matches that name one player twice (bit 3 of meta1, free in the
       // stream layout) so processing skips the duplicate scan for the rest; the
@@ -397,7 +399,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       const uint64_t pm = __ballot(mm < M && est == kRated);
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h)
+      for (int h = 0; h < kH; ++h)
         if (h == staging) {
           pend[h] = pm;
           dval[h] = kNone;  // first poll next iteration
@@ -435,7 +437,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
                                __HIP_MEMORY_SCOPE_AGENT);
       const bool gstale = (stale_lanes & gmask) != 0ull;
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h) {
+      for (int h = 0; h < kH; ++h) {
         uint64_t back = 0ull;
         for (int q = 0; q < NG; ++q) {
           const int bq = __shfl(gstale && my_h == h ? my_bit : -1, q * G);
@@ -568,7 +570,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     {
       uint32_t retired = 0;
 #pragma unroll
-      for (int h = 0; h < kHeld; ++h)
+      for (int h = 0; h < kH; ++h)
         if (cbase[h] >= 0 && pend[h] == 0ull) {
           cbase[h] = -1;
           ++retired;
@@ -580,7 +582,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // ---------------------------------------------- (12) done?
     bool held = false;
 #pragma unroll
-    for (int h = 0; h < kHeld; ++h) held |= cbase[h] >= 0;
+    for (int h = 0; h < kH; ++h) held |= cbase[h] >= 0;
     if (exhausted && !held && !tk_pending) {
       if (lane == 0)  // diagnostics: wave iterations (ctrl[15])
         __hip_atomic_fetch_add((gu32*)&ctrl[15], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -610,7 +612,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       if (now - t0 > kTimeoutTicks) {
         if (lane == 0) atomicOr(&ctrl[1], 1u);
 #pragma unroll
-        for (int h = 0; h < kHeld; ++h)
+        for (int h = 0; h < kH; ++h)
           if (cbase[h] >= 0 && ((pend[h] >> lane) & 1ull))
             reinterpret_cast<uint8_t*>(orows + (cbase[h] + lane) * orow + 5 * S + 1)[0] = kNotProcessed;
         return;  // give up: the host sees ctrl[1] and raises
@@ -676,6 +678,8 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
     case 3:
       if (tight) ANA_RATE_LAUNCH(3, 6);
       else if (prm.variant == 1) ANA_RATE_LAUNCH_V(3, 8, 1);
+      else if (prm.variant == 3) ANA_RATE_LAUNCH_V(3, 8, 3);  // 6 held chunks per wave
+      else if (prm.variant == 4) ANA_RATE_LAUNCH_V(3, 8, 4);  // 8 held chunks per wave
       else ANA_RATE_LAUNCH(3, 8);
       break;
     case 4: ANA_RATE_LAUNCH(4, 8); break;
