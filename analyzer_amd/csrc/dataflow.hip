@@ -112,7 +112,21 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// One wave iteration's assignment: per lane, its group's match and the
+// participant's slot facts and granules (section 4 of the executor loop).
+struct Batch {
+  int64_t m = 0;
+  int my_h = -1, my_bit = 0, mode = 0, n0 = 0, n1 = 0, rank0 = 1, rank1 = 1, first = 0, prevdup = -1;
+  int32_t id = -1;
+  bool inr = false, islast = false, own = false, any_dup = false;
+  uint32_t lk0 = kNoMatch;  // schedule link (common.h): next match | has-earlier
+  v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
+};
+
 // V: executor variant for same-process A/B experiments (ANA_RATE_VARIANT);
+// V == 5: software pipeline -- a batch's granules are loaded in one iteration
+// and rated in the next, before that iteration's wait, so the rating math
+// overlaps the next batch's load latency.
 // 0 = the production path.  TELE: K8 fused telemetry compiled in (the plain
 // rating launch leaves it out, which frees the registers its code pins).
 template <int K, int G, int V, bool TELE>
@@ -125,7 +139,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
   // chunks held per wave: kHeld, or 2V for the A/B variants V >= 3 (ANA_RATE_VARIANT)
-  constexpr int kH = V >= 3 ? 2 * V : kHeld;
+  constexpr int kH = V >= 3 && V != 5 ? 2 * V : kHeld;
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
   __shared__ int32_t lrec[kWavesPerBlock][kH][kChunk * R];
@@ -165,6 +179,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     need[h] = 0u;
   }
   bool exhausted = false, tk_pending = false;
+  Batch carry;  // V5: the batch loaded last iteration, rated this one (none yet)
   unsigned tk = 0;                 // ticket returned to lane 0
   uint32_t spins = 0, iter = 0;
   // K8 fused mode: telemetry tiles fill the time a wave would spend waiting
@@ -287,31 +302,32 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     const bool worked = nassigned > 0;
 
     // ---------------------------------------------- (4) this group's loads
-    int64_t m = 0;
-    int mode = 0, n0 = 0, n1 = 0, rank0 = 1, rank1 = 1, first = j, prevdup = -1;
-    int32_t id = -1;
-    bool inr = false, islast = false, own = false;
-    uint32_t lk0 = kNoMatch;  // schedule link (common.h): next match | has-earlier
-    bool any_dup = false;     // wave-uniform: a match of this batch names a player twice
-    v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
-    float4 at4 = make_float4(NAN, NAN, NAN, 0.f);
+    Batch nb;  // any_dup is wave-uniform: a match of this batch names a player twice
+    nb.my_h = my_h;
+    nb.my_bit = my_bit;
+    nb.first = j;
     if (my_h >= 0) {
       int64_t cb = 0;
 #pragma unroll
       for (int h = 0; h < kH; ++h) if (h == my_h) cb = cbase[h];
-      m = cb + my_bit;
+      const int64_t m = cb + my_bit;
+      nb.m = m;
       const int32_t* lr = &lrec[wv][my_h][my_bit * R];
       const uint32_t m0 = (uint32_t)lr[S], m1 = (uint32_t)lr[S + 1];
-      mode = meta_mode(m0);
-      n0 = meta_n0(m0);
-      n1 = meta_n1(m0);
-      rank0 = meta_winner0(m1) ? 0 : 1;
-      rank1 = meta_winner1(m1) ? 0 : 1;
-      inr = j < S && rpos < (r0 ? n0 : n1);
-      id = inr ? lr[j] : -1;
-      islast = true;
-      any_dup = __ballot((m1 >> 3) & 1u) != 0ull;
-      if (any_dup) {  // some match of this batch repeats a player
+      const int mode = meta_mode(m0);
+      nb.mode = mode;
+      nb.n0 = meta_n0(m0);
+      nb.n1 = meta_n1(m0);
+      nb.rank0 = meta_winner0(m1) ? 0 : 1;
+      nb.rank1 = meta_winner1(m1) ? 0 : 1;
+      const bool inr = j < S && rpos < (r0 ? nb.n0 : nb.n1);
+      nb.inr = inr;
+      const int32_t id = inr ? lr[j] : -1;
+      nb.id = id;
+      bool islast = true;
+      int first = j, prevdup = -1;
+      nb.any_dup = __ballot((m1 >> 3) & 1u) != 0ull;
+      if (nb.any_dup) {  // some match of this batch repeats a player
 #pragma unroll
         for (int q = 0; q < S; ++q) {
           const int32_t oid = __shfl(id, gbase + q);
@@ -324,91 +340,33 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           }
         }
       }
-      own = inr && first == j;
+      nb.islast = islast;
+      nb.first = first;
+      nb.prevdup = prevdup;
+      const bool own = inr && first == j;
+      nb.own = own;
       if (inr) {
-        lk0 = link[m * S + j];
+        nb.lk0 = link[m * S + j];
       }
       if (own) {
         const int off = id * (kRowFloats * 4);
-        gs = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
-        gm = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * (1 + mode), 0, 16);
+        nb.gs = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+        nb.gm = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * (1 + mode), 0, 16);
       }
     }
 
-    // ---------------------------------------------- (5) next iteration's counter polls
-    ++iter;
-#pragma unroll
-    for (int h = 0; h < kH; ++h)
-      if (((pend[h] >> lane) & 1ull) && (!(prm.debug_flags & 4) || (iter & 1u)))
-        dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-
-    // ---------------------------------------------- (6) next ticket if a ring slot is free
-    {
-      bool free_slot = false;
-#pragma unroll
-      for (int h = 0; h < kH; ++h) free_slot |= cbase[h] < 0;
-      if (free_slot && !exhausted) {
-        if (lane == 0)
-          tk = __hip_atomic_fetch_add((gu32*)&ctrl[4 + head], 1u, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-        tk_pending = true;
-      }
-    }
-
-    // ---------------------------------------------- (7) the one wait of the iteration
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    // ---------------------------------------------- (9) install the staged chunk
-    if (staging >= 0) {
-      int64_t cb = 0;
-#pragma unroll
-      for (int h = 0; h < kH; ++h) if (h == staging) cb = cbase[h];
-      const int64_t mm = cb + lane;
-      // flag matches that name one player twice (bit 3 of meta1, free in the
-      // stream layout) so processing skips the duplicate scan for the rest; the
-      // match is ready once every distinct player with an earlier occurrence
-      // (kLinkHasPred on its first slot) has been published: that many
-      // increments of its completion counter
-      uint32_t nd = 0u;
-      {
-        const uint32_t m0s = (uint32_t)r[S];
-        bool dup = false;
-#pragma unroll
-        for (int a = 0; a < S; ++a) {
-          const bool ina = (a < K ? a : a - K) < (a < K ? meta_n0(m0s) : meta_n1(m0s));
-          bool firsto = ina;
-#pragma unroll
-          for (int b = 0; b < a; ++b) {
-            const bool inb = (b < K ? b : b - K) < (b < K ? meta_n0(m0s) : meta_n1(m0s));
-            dup |= r[a] >= 0 && r[a] == r[b];
-            if (inb && r[b] == r[a]) firsto = false;
-          }
-          if (firsto && (lks[a] & kLinkHasPred)) ++nd;
-        }
-        r[S + 1] = dup ? (r[S + 1] | 8) : (r[S + 1] & ~8);
-      }
-#pragma unroll
-      for (int k = 0; k < R; ++k) lrec[wv][staging][lane * R + k] = r[k];
-      const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
-      if (mm < M && est != kRated) {  // no state, no dependencies: finish it now
-#pragma unroll
-        for (int q = 0; q < 5 * S; ++q) orows[mm * orow + q] = NAN;
-        orows[mm * orow + 5 * S] = (est == kAfk || est == kInvalidRosters) ? 0.f : NAN;
-        reinterpret_cast<uint8_t*>(orows + mm * orow + 5 * S + 1)[0] = est;
-      }
-      const uint64_t pm = __ballot(mm < M && est == kRated);
-#pragma unroll
-      for (int h = 0; h < kH; ++h)
-        if (h == staging) {
-          pend[h] = pm;
-          dval[h] = kNone;  // first poll next iteration
-          need[h] = nd;
-          if (pm == 0ull) cbase[h] = -1;
-        }
-    }
-
-    // ---------------------------------------------- (10) rate this batch
+    // ---------------------------------------------- (10) rate a batch
+    auto rate_batch = [&](const Batch& bt) {
+    int my_h = bt.my_h;
+    const int my_bit = bt.my_bit;
+    const int64_t m = bt.m;
+    const int mode = bt.mode, n0 = bt.n0, n1 = bt.n1, rank0 = bt.rank0, rank1 = bt.rank1;
+    const int first = bt.first, prevdup = bt.prevdup;
+    const int32_t id = bt.id;
+    const bool inr = bt.inr, islast = bt.islast, own = bt.own, any_dup = bt.any_dup;
+    const uint32_t lk0 = bt.lk0;
+    const v4i gs = bt.gs, gm = bt.gm;
+    float4 at4 = make_float4(NAN, NAN, NAN, 0.f);
     // A counter can reach its count before the writes it announces have landed
     // (notifications do not wait for store acknowledgements): a group whose
     // granules do not carry the tags of their last writers retries next iteration.
@@ -565,13 +523,97 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         reinterpret_cast<uint8_t*>(orm + 5 * S + 1)[0] = gst;
       }
     }
+    };
+
+    // ---------------------------------------------- (5) next iteration's counter polls
+    ++iter;
+#pragma unroll
+    for (int h = 0; h < kH; ++h)
+      if (((pend[h] >> lane) & 1ull) && (!(prm.debug_flags & 4) || (iter & 1u)))
+        dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+
+    // ---------------------------------------------- (6) next ticket if a ring slot is free
+    {
+      bool free_slot = false;
+#pragma unroll
+      for (int h = 0; h < kH; ++h) free_slot |= cbase[h] < 0;
+      if (free_slot && !exhausted) {
+        if (lane == 0)
+          tk = __hip_atomic_fetch_add((gu32*)&ctrl[4 + head], 1u, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+        tk_pending = true;
+      }
+    }
+
+    if constexpr (V == 5) rate_batch(carry);
+    // ---------------------------------------------- (7) the one wait of the iteration
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    // ---------------------------------------------- (9) install the staged chunk
+    if (staging >= 0) {
+      int64_t cb = 0;
+#pragma unroll
+      for (int h = 0; h < kH; ++h) if (h == staging) cb = cbase[h];
+      const int64_t mm = cb + lane;
+      // flag matches that name one player twice (bit 3 of meta1, free in the
+      // stream layout) so processing skips the duplicate scan for the rest; the
+      // match is ready once every distinct player with an earlier occurrence
+      // (kLinkHasPred on its first slot) has been published: that many
+      // increments of its completion counter
+      uint32_t nd = 0u;
+      {
+        const uint32_t m0s = (uint32_t)r[S];
+        bool dup = false;
+#pragma unroll
+        for (int a = 0; a < S; ++a) {
+          const bool ina = (a < K ? a : a - K) < (a < K ? meta_n0(m0s) : meta_n1(m0s));
+          bool firsto = ina;
+#pragma unroll
+          for (int b = 0; b < a; ++b) {
+            const bool inb = (b < K ? b : b - K) < (b < K ? meta_n0(m0s) : meta_n1(m0s));
+            dup |= r[a] >= 0 && r[a] == r[b];
+            if (inb && r[b] == r[a]) firsto = false;
+          }
+          if (firsto && (lks[a] & kLinkHasPred)) ++nd;
+        }
+        r[S + 1] = dup ? (r[S + 1] | 8) : (r[S + 1] & ~8);
+      }
+#pragma unroll
+      for (int k = 0; k < R; ++k) lrec[wv][staging][lane * R + k] = r[k];
+      const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
+      if (mm < M && est != kRated) {  // no state, no dependencies: finish it now
+#pragma unroll
+        for (int q = 0; q < 5 * S; ++q) orows[mm * orow + q] = NAN;
+        orows[mm * orow + 5 * S] = (est == kAfk || est == kInvalidRosters) ? 0.f : NAN;
+        reinterpret_cast<uint8_t*>(orows + mm * orow + 5 * S + 1)[0] = est;
+      }
+      const uint64_t pm = __ballot(mm < M && est == kRated);
+#pragma unroll
+      for (int h = 0; h < kH; ++h)
+        if (h == staging) {
+          pend[h] = pm;
+          dval[h] = kNone;  // first poll next iteration
+          need[h] = nd;
+          if (pm == 0ull) cbase[h] = -1;
+        }
+    }
+
+    if constexpr (V == 5) {
+      // the compiler cannot see the explicit wait above: re-define the loaded values
+      // so the next iteration's use of them carries no vmcnt wait on newer loads
+      asm volatile("" : "+v"(nb.gs), "+v"(nb.gm), "+v"(nb.lk0));
+      carry = nb;
+    } else {
+      rate_batch(nb);
+    }
 
     // ---------------------------------------------- (11) retire finished chunks
     {
       uint32_t retired = 0;
 #pragma unroll
       for (int h = 0; h < kH; ++h)
-        if (cbase[h] >= 0 && pend[h] == 0ull) {
+        if (cbase[h] >= 0 && pend[h] == 0ull && (V != 5 || __ballot(carry.my_h == h) == 0ull)) {
           cbase[h] = -1;
           ++retired;
         }
@@ -680,10 +722,15 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
       else if (prm.variant == 1) ANA_RATE_LAUNCH_V(3, 8, 1);
       else if (prm.variant == 3) ANA_RATE_LAUNCH_V(3, 8, 3);  // 6 held chunks per wave
       else if (prm.variant == 4) ANA_RATE_LAUNCH_V(3, 8, 4);  // 8 held chunks per wave
+      else if (prm.variant == 5) ANA_RATE_LAUNCH_V(3, 8, 5);  // software-pipelined rating
       else ANA_RATE_LAUNCH(3, 8);
       break;
     case 4: ANA_RATE_LAUNCH(4, 8); break;
-    case 5: if (tight) ANA_RATE_LAUNCH(5, 10); else ANA_RATE_LAUNCH(5, 16); break;
+    case 5:
+      if (tight) ANA_RATE_LAUNCH(5, 10);
+      else if (prm.variant == 5) ANA_RATE_LAUNCH_V(5, 16, 5);
+      else ANA_RATE_LAUNCH(5, 16);
+      break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef ANA_RATE_LAUNCH

@@ -116,6 +116,28 @@ def test_device_repeat_launch_deterministic(gpu_device):
     assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32))
 
 
+@pytest.mark.parametrize("K,P,M", [(3, 16, 4000), (3, 100000, 1000000), (5, 2000, 200000)])
+def test_pipelined_executor_bit_identical(gpu_device, monkeypatch, K, P, M):
+    """ANA_RATE_VARIANT=5 (each batch rated one iteration after its loads, under the
+    next batch's load latency) must give the production executor's exact bits."""
+    rs = RosterSpec(num_players=P, seed=P + 3)
+    rec = make_stream(StreamSpec(team_size=K, seed=M + 1), M, P, K=K, device=gpu_device)
+    outs = []
+    for variant in ("0", "5"):
+        monkeypatch.setenv("ANA_RATE_VARIANT", variant)
+        ro = make_roster(rs, device=gpu_device)
+        rater = R.BatchRater()
+        res = rater.rate(ro, rec, K)
+        assert int(rater.error_flags(gpu_device).sum()) == 0
+        outs.append((ro.state.cpu(), res.s_mu.cpu(), res.status.cpu(), res.quality.cpu()))
+    a, b = outs
+    assert torch.equal(a[0][:, 0::2].contiguous().view(torch.int32),
+                       b[0][:, 0::2].contiguous().view(torch.int32))
+    assert torch.equal(a[1].view(torch.int32), b[1].view(torch.int32))
+    assert torch.equal(a[2], b[2])
+    assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32))
+
+
 @pytest.mark.parametrize("n,bits", [(1, 8), (4095, 20), (4097, 12), (1_000_003, 20), (300_000, 32)])
 def test_radix_sort_pairs_stable(gpu_device, n, bits):
     from analyzer_amd.ops.native import native
