@@ -185,6 +185,11 @@ class Worker:
         try:
             with trace_range("load", ids=len(ids)):
                 matches = list(session.load_matches(ids, self.cfg.chunksize))
+            if self.cfg.skip_rated:
+                fresh = [m for m in matches if m.trueskill_quality is None]
+                if len(fresh) != len(matches):
+                    counts["skipped_rated"] = len(matches) - len(fresh)
+                matches = fresh
             with trace_range("rate", matches=len(matches), engine=self.cfg.engine):
                 if self.cfg.engine == "native" and self._batched().supports(matches):
                     quarantined = self._rate_native(session, matches, counts)

@@ -179,6 +179,30 @@ def test_channel_death_redelivers_unacked():
     assert got2 == [(True, b"1"), (True, b"2")]
 
 
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_redelivery_after_commit_is_idempotent_with_skip_rated(engine):
+    """A batch commits, the consumer dies before the ack, the broker redelivers: the
+    reference rates those matches a second time; SKIP_RATED=true leaves them alone."""
+    w, matches, clock = make_worker(n=6, players=40, batch=6, engine=engine, skip_rated=True)
+    ids = [m.api_id for m in matches]
+    publish(w.channel, "analyze", ids)
+    w.rabbit.process_data_events()
+    assert w.stats.batches == 1
+    once = ratings(matches)
+    publish(w.channel, "analyze", ids)  # the redelivery
+    w.rabbit.process_data_events()
+    assert w.stats.batches == 2 and w.channel.acked == 12
+    assert ratings(matches) == once
+    # the reference behaviour (flag off): the second delivery moves the ratings again
+    w2, matches2, _ = make_worker(n=6, players=40, batch=6, engine=engine)
+    publish(w2.channel, "analyze", [m.api_id for m in matches2])
+    w2.rabbit.process_data_events()
+    first = ratings(matches2)
+    publish(w2.channel, "analyze", [m.api_id for m in matches2])
+    w2.rabbit.process_data_events()
+    assert ratings(matches2) != first
+
+
 def test_native_engine_matches_python_engine():
     wp, mp, _ = make_worker(n=60, players=25, batch=16, engine="python", seed=7)
     wn, mn, _ = make_worker(n=60, players=25, batch=16, engine="native", seed=7)
