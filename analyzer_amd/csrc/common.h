@@ -73,7 +73,7 @@ struct RateParams {
   const int32_t* epoch_ptr;    // device: read the epoch here instead (graph replays bump it)
   const float* vst;            // vst_points[tier + 1], kVstTiers entries (device/host memory)
   int32_t idle_spins;          // dataflow: max s_sleep(2) rounds of an idle wave (0 = default)
-  int32_t debug_flags;         // experiments only (ANA_RATE_DEBUG): 2 skip slot outputs
+  int32_t debug_flags;         // experiments only (ANA_RATE_DEBUG): 2 skip slot outputs, 16/32 NT record/link loads
   int32_t spec;                // dataflow: speculative one-dependency matches per wave iteration
   int32_t tight_groups;        // dataflow: 2K lanes per match instead of the next power of two
                                // (-1 auto, 0 off, 1 on)

@@ -49,6 +49,7 @@ namespace ana {
 
 typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
 
 constexpr uint64_t kTimeoutTicks = 500000000ull;  // 5 s of the 100 MHz s_memrealtime clock
 constexpr uint64_t kProgressTicks = 50000000ull;  // re-read the progress counter every 0.5 s
@@ -229,20 +230,24 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         const int64_t m = c * kChunk + lane;
         if (m < M) {
           const int32_t* src = rec + m * R;
+          // experiment flags: 16 = records, 32 = links through non-temporal loads
+          // (read once per window: keep them out of the Infinity Cache)
           if constexpr (R % 4 == 0) {
 #pragma unroll
             for (int k = 0; k < R / 4; ++k) {
-              const int4 v = reinterpret_cast<const int4*>(src)[k];
+              const v4i* q = reinterpret_cast<const v4i*>(src) + k;
+              const v4i v = (prm.debug_flags & 16) ? __builtin_nontemporal_load(q) : *q;
               r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
             }
           } else {
 #pragma unroll
-            for (int k = 0; k < R; ++k) r[k] = src[k];
+            for (int k = 0; k < R; ++k)
+              r[k] = (prm.debug_flags & 16) ? __builtin_nontemporal_load(src + k) : src[k];
           }
-          const uint2* ls = reinterpret_cast<const uint2*>(link + m * S);  // S even: 8-B aligned
+          const v2u* ls = reinterpret_cast<const v2u*>(link + m * S);  // S even: 8-B aligned
 #pragma unroll
           for (int k = 0; k < S / 2; ++k) {
-            const uint2 v = ls[k];
+            const v2u v = (prm.debug_flags & 32) ? __builtin_nontemporal_load(ls + k) : ls[k];
             lks[2 * k] = v.x;
             lks[2 * k + 1] = v.y;
           }
