@@ -166,6 +166,38 @@ def test_sweep_merge_overlapping_sums_messages(tmp_path):
         assert torch.equal(r["merged"].nan_to_num(-7), merged.nan_to_num(-7))
 
 
+def _sweep_buckets(rank, size, P, M, K, seed, comm_dtype, bucket_rows):
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.parallel.sweep import SweepMerger
+
+    roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.5))
+    rec = make_stream(StreamSpec(team_size=K, seed=seed + 1 + rank, p_afk=0.0), M, P, K=K)
+    out = {}
+    for rows in (None, bucket_rows):
+        merger = SweepMerger(P, "cpu", comm_dtype=comm_dtype,
+                             bucket_rows=P if rows is None else rows)
+        local = roster.clone()
+        merger.begin(local)
+        BatchRater().rate(local, rec, K)
+        merger.merge(local)
+        out["whole" if rows is None else "bucketed"] = local.state
+        out["n_buckets_%s" % ("whole" if rows is None else "bucketed")] = len(merger.buckets())
+    return out
+
+
+@pytest.mark.parametrize("comm_dtype", ["fp32", "fp16"])
+def test_sweep_merge_bucketed_pipeline_matches_single_bucket(tmp_path, comm_dtype):
+    """The pipelined merge (messages / async all-reduce / apply per row bucket,
+    ragged last bucket) gives the one-bucket result bit for bit: every stage is
+    per player, and two-rank sums do not depend on the reduction order."""
+    P, M, K, seed, size = 101, 300, 3, 9, 2
+    res = run_ranks(_sweep_buckets, size, tmp_path, P, M, K, seed, comm_dtype, 16)
+    for r in res:
+        assert r["n_buckets_whole"] == 1 and r["n_buckets_bucketed"] == 7
+        assert torch.equal(r["whole"].nan_to_num(-7), r["bucketed"].nan_to_num(-7))
+    assert torch.equal(res[0]["bucketed"].nan_to_num(-7), res[1]["bucketed"].nan_to_num(-7))
+
+
 @pytest.mark.parametrize("dtype,tol_mu", [("fp16", 1.0), ("bf16", 8.0)])
 def test_sweep_merge_compressed_messages(tmp_path, dtype, tol_mu):
     """COMM_DTYPE fp16/bf16: base-relative messages survive the compressed
