@@ -12,6 +12,8 @@
 // engine replaces is /root/reference/worker.py:176-192 (ORDER BY created_at).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "gen_core.h"
 #include "kernels.h"
@@ -211,15 +213,98 @@ sched_small_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, ui
   }
 }
 
+// Micro-batch schedule without a sort (default; ANA_SCHED_SMALL=bitonic selects the
+// kernel above for A/B).  A link only needs, per slot, the next slot of the same
+// player and whether an earlier one exists -- not a total order.  So: key every
+// slot into LDS, push each keyed slot onto an LDS list per hash bucket (one
+// ds atomic swap: the lists are unordered), then every slot walks its bucket's
+// list and keeps the smallest later slot with its key (its successor) and
+// whether any earlier slot has it (its predecessor flag) -- the same links as
+// the stable sort.  4096 buckets for <= 8192 slots: lists of ~1-2 slots, three
+// barriers instead of the bitonic network's ~80 dependent exchange stages.
+// LDS: 16 KB heads + 16 KB u16 list links + 32 KB keys.
+constexpr int kHashBuckets = 4096;
+
+template <int K>
+__global__ void __launch_bounds__(kSmallThreads)
+sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uint32_t* __restrict__ link,
+                  int32_t* __restrict__ deps, uint32_t* __restrict__ overflow) {
+  constexpr int S = 2 * K, R = S + 2;
+  __shared__ uint32_t head[kHashBuckets];
+  __shared__ uint16_t nxt[kSmallSched];
+  __shared__ uint32_t skey[kSmallSched];
+  const int tid = threadIdx.x;
+  const int n = (int)(M * S);
+  for (int b = tid; b < kHashBuckets; b += kSmallThreads) head[b] = 0xffffffffu;
+  for (int m = tid; m < (int)M; m += kSmallThreads) {
+    int32_t r[R];
+    const int32_t* src = rec + (int64_t)m * R;
+    if constexpr (R % 4 == 0) {
+#pragma unroll
+      for (int k = 0; k < R / 4; ++k) {
+        const int4 v = reinterpret_cast<const int4*>(src)[k];
+        r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < R; ++k) r[k] = src[k];
+    }
+    const bool rates = early_status<K>(r, (int64_t)kend) == kRated;
+    const uint32_t m0 = (uint32_t)r[S];
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      const int pos = j < K ? j : j - K;
+      const bool in_roster = pos < (j < K ? meta_n0(m0) : meta_n1(m0));
+      skey[m * S + j] = rates && in_roster ? (uint32_t)r[j] : kend;
+    }
+    deps[m] = 0;
+  }
+  if (tid == 0) *overflow = 0u;
+  __syncthreads();
+  for (int i = tid; i < n; i += kSmallThreads) {
+    const uint32_t key = skey[i];
+    if (key < kend) {
+      const uint32_t h = (key * 0x9E3779B1u) >> (32 - 12);
+      nxt[i] = (uint16_t)atomicExch(&head[h], (uint32_t)i);  // 0xffff: end of list
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += kSmallThreads) {
+    const uint32_t key = skey[i];
+    uint32_t w = kNoMatch;
+    if (key < kend) {
+      uint32_t succ = 0xffffffffu;
+      bool pred = false;
+      for (uint32_t t = head[(key * 0x9E3779B1u) >> (32 - 12)]; t < (uint32_t)kSmallSched;) {
+        if (t != (uint32_t)i && skey[t] == key) {
+          if (t > (uint32_t)i) succ = t < succ ? t : succ;
+          else pred = true;
+        }
+        t = nxt[t];  // 0xffff ends the walk (>= kSmallSched)
+      }
+      if (succ != 0xffffffffu) w = succ / (uint32_t)S;
+      if (pred) w |= kLinkHasPred;
+    }
+    link[i] = w;
+  }
+}
+
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s) {
   const int64_t n = M * 2 * K;
   if (n > 0 && n <= kSmallSched && P < 0x7fffffffLL && K >= 1 && K <= 5) {
     const int e = n <= 2048 ? 2 : n <= 4096 ? 4 : 8;  // elements per thread
+    static const bool bitonic = [] {
+      const char* v = getenv("ANA_SCHED_SMALL");
+      return v && v[0] == 'b';
+    }();
     switch (K) {
 #define ANA_SMALL_CASE(k)                                                                            \
   case k:                                                                                            \
-    if (e == 2)                                                                                      \
+    if (!bitonic)                                                                                    \
+      hipLaunchKernelGGL((sched_hash_kernel<k>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,         \
+                         (uint32_t)P, link, deps, overflow);                                         \
+    else if (e == 2)                                                                                      \
       hipLaunchKernelGGL((sched_small_kernel<k, 2>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
                          (uint32_t)P, link, deps, overflow);                                         \
     else if (e == 4)                                                                                 \
