@@ -220,7 +220,8 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
           Tensor delta, Tensor m_mu, Tensor m_sig, Tensor ctrl, Tensor vst, double beta2,
           double tau2, double unknown_sigma, bool record_first_prior, int64_t blocks,
           int64_t epoch, bool host_fp64, Tensor tele_evoff, Tensor tele_events, Tensor tele_stats,
-          int64_t progress, int64_t progress_value, int64_t progress_at, int64_t epoch_ptr) {
+          int64_t progress, int64_t progress_value, int64_t progress_at, int64_t epoch_ptr,
+          int64_t chunk_len) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
@@ -274,6 +275,8 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   prm.progress = reinterpret_cast<uint64_t*>((intptr_t)progress);
   prm.progress_value = (uint64_t)progress_value;
   prm.progress_at = progress_at;
+  TORCH_CHECK(chunk_len >= 1 && chunk_len <= 64, "chunk_len must be 1..64");
+  prm.chunk_len = (int32_t)chunk_len;
   const ana::TelemetryParams tp = telemetry_params(tele_evoff, tele_events, tele_stats, M, K, dev);
   if (dev.is_cuda()) {
     check(link, "link", torch::kInt32, dev);

@@ -84,7 +84,10 @@ struct RateParams {
   // hipStreamWaitValue64 before the next window's prepass).  null = off.
   uint64_t* progress;
   uint64_t progress_value;
-  int64_t progress_at;         // chunk index (64 matches per chunk)
+  int64_t progress_at;         // chunk index (chunk_len matches per chunk)
+  // matches per ticket, 8..64 (lanes >= chunk_len idle): 64 for windows; micro-batches
+  // use short chunks so their few matches spread over more waves (fewer iterations each)
+  int32_t chunk_len;
 };
 
 // Per-match outputs.  The participant record of the reference

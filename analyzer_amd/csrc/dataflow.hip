@@ -194,6 +194,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     return (int64_t)t < tele_tiles ? (int64_t)t : -1;
   };
   const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : 8u;
+  const int cl = prm.chunk_len;  // matches per ticket (<= kChunk lanes)
 
   for (;;) {
     // ---------------------------------------------- (1) a ticket came back: stage its chunk
@@ -212,13 +213,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       const int64_t c = (int64_t)t * kHeads + head;
       // tail signal: the first ticket of each shard at or past progress_at, and its
       // first ticket past the end (so a threshold beyond the window still fires)
-      const int64_t nchunks = (M + kChunk - 1) / kChunk;
+      const int64_t nchunks = (M + cl - 1) / cl;
       if (prm.progress && lane == 0 &&
           ((c >= prm.progress_at && c < prm.progress_at + kHeads) ||
            (c >= nchunks && c < nchunks + kHeads)))
         __hip_atomic_store(prm.progress, prm.progress_value, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-      if (c * kChunk >= M) {
+      if (c * cl >= M) {
         exhausted = true;
       } else {
 #pragma unroll
@@ -226,9 +227,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           if (cbase[h] < 0) staging = h;
 #pragma unroll
         for (int h = 0; h < kH; ++h)
-          if (h == staging) cbase[h] = c * kChunk;
-        const int64_t m = c * kChunk + lane;
-        if (m < M) {
+          if (h == staging) cbase[h] = c * cl;
+        const int64_t m = c * cl + lane;
+        if (lane < cl && m < M) {
           const int32_t* src = rec + m * R;
           // experiment flags: 16 = records, 32 = links through non-temporal loads
           // (read once per window: keep them out of the Infinity Cache)
@@ -560,7 +561,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       int64_t cb = 0;
 #pragma unroll
       for (int h = 0; h < kH; ++h) if (h == staging) cb = cbase[h];
-      const int64_t mm = cb + lane;
+      const int64_t mm = lane < cl ? cb + lane : M;  // idle lanes of a short chunk
       // flag matches that name one player twice (bit 3 of meta1, free in the
       // stream layout) so processing skips the duplicate scan for the rest; the
       // match is ready once every distinct player with an earlier occurrence
@@ -699,6 +700,7 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
   hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, 15);
   if (M <= 0) return 0;
+  if (prm.chunk_len < 1 || prm.chunk_len > kChunk) return (int)hipErrorInvalidValue;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
   if (!prm.epoch_ptr && (prm.epoch < 1 || prm.epoch > 255)) return (int)hipErrorInvalidValue;
   // the executor writes one packed row per match (ops/rate.py RateResult.allocate)

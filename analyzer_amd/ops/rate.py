@@ -178,15 +178,29 @@ class BatchRater:
         self._vst: Dict[str, torch.Tensor] = {}
         self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
 
+    def chunk_len(self, M: int, telemetry: bool = False) -> int:
+        """Matches per executor ticket: 64 (one per lane) for windows, shorter
+        (8-32, a power of two) when 64-match chunks would leave the full grid
+        (``4 * self.blocks`` waves) short of work.  A wave rates 64/G matches per
+        iteration, so a 500-match micro-batch in 64-match chunks runs 8 waves x 8
+        dependent iterations; in 8-match chunks it runs 63 waves x 1."""
+        if telemetry:
+            return 64
+        need = -(-M // (4 * self.blocks))  # matches per wave at the full grid
+        cl = 8
+        while cl < need and cl < 64:
+            cl *= 2
+        return cl
+
     def grid_blocks(self, M: int, telemetry: bool = False) -> int:
         """Persistent-grid size for a window of M matches: ``self.blocks`` (512,
         measured best for 10M-match windows), but no more than one wave per
-        64-match chunk -- a micro-batch of 500 matches needs 8 waves, not 2048
-        (the extra workgroups only cost launch and exit time).  Fused telemetry
-        keeps the full grid (its tiles need the waves)."""
+        chunk (``chunk_len``) -- a micro-batch of 500 matches needs 63 waves, not
+        2048 (the extra workgroups only cost launch and exit time).  Fused
+        telemetry keeps the full grid (its tiles need the waves)."""
         if telemetry:
             return self.blocks
-        chunks = -(-M // 64)
+        chunks = -(-M // self.chunk_len(M))
         return max(1, min(self.blocks, -(-chunks // 4)))
 
     # ------------------------------------------------------------- buffers
@@ -270,7 +284,8 @@ class BatchRater:
                       record, self.grid_blocks(M, telemetry[0].numel() > 0), epoch,
                       self.host_fp64, *telemetry,
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
-                      epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0)
+                      epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
+                      self.chunk_len(M, telemetry[0].numel() > 0))
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out

@@ -35,7 +35,7 @@ import torch
 from ..ops.rate import BatchRater, RateResult, Roster, Schedule
 from ..utils.trace import trace_range
 
-CHUNK = 64  # matches per executor ticket (csrc/dataflow.hip kChunk)
+CHUNK = 64  # matches per executor ticket of a window (csrc/dataflow.hip kChunk; BatchRater.chunk_len)
 
 
 @dataclass
@@ -127,7 +127,8 @@ class WindowPipeline:
         if self._signal:
             self._seq += 1
             M = int(prep.rec.shape[0])
-            at = int(self.tail * ((M + CHUNK - 1) // CHUNK))
+            cl = self.rater.chunk_len(M, telemetry is not None)
+            at = int(self.tail * ((M + cl - 1) // cl))
             progress = (self._signal, self._seq, at)
         with trace_range("rate", window=self.windows_rated, matches=int(prep.rec.shape[0])):
             res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,

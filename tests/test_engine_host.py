@@ -126,8 +126,11 @@ def test_noop_padding_records_touch_nothing():
 
 def test_grid_blocks_scale_with_the_window():
     br = R.BatchRater(blocks=512)
-    assert br.grid_blocks(500) == 2          # 8 chunks of 64 -> 8 waves
+    assert br.chunk_len(500) == 8 and br.grid_blocks(500) == 16   # 63 chunks of 8 -> 63 waves
+    assert br.chunk_len(500, telemetry=True) == 64
+    assert br.chunk_len(20_000) == 16 and br.chunk_len(10_000_000) == 64
     assert br.grid_blocks(1) == 1
-    assert br.grid_blocks(64 * 4 * 100) == 100
+    assert br.chunk_len(25_600) == 16 and br.grid_blocks(25_600) == 400  # 1600 chunks of 16
+    assert br.chunk_len(64 * 2048 * 2) == 64 and br.grid_blocks(64 * 2048 * 2) == 512
     assert br.grid_blocks(10_000_000) == 512
     assert br.grid_blocks(500, telemetry=True) == 512
