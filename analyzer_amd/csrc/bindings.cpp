@@ -163,7 +163,7 @@ std::tuple<Tensor, int64_t> levels(Tensor rec, int64_t K, int64_t num_players) {
 }
 
 void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
-              Tensor workspace, Tensor ctrl) {
+              Tensor workspace, Tensor ctrl, bool zero_ctrl) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(link, "link", torch::kInt32, dev);
@@ -186,7 +186,7 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
                                    deps.data_ptr<int32_t>(), workspace.data_ptr<uint8_t>(),
                                    (size_t)workspace.numel(),
                                    reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()),
-                                   stream_of(rec)), "schedule");
+                                   stream_of(rec), zero_ctrl), "schedule");
   } else {
     TORCH_CHECK(ana::host_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
                                    reinterpret_cast<uint32_t*>(link.data_ptr<int32_t>()),
@@ -221,7 +221,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
           double tau2, double unknown_sigma, bool record_first_prior, int64_t blocks,
           int64_t epoch, bool host_fp64, Tensor tele_evoff, Tensor tele_events, Tensor tele_stats,
           int64_t progress, int64_t progress_value, int64_t progress_at, int64_t epoch_ptr,
-          int64_t chunk_len) {
+          int64_t chunk_len, bool ctrl_ready) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
@@ -277,6 +277,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   prm.progress_at = progress_at;
   TORCH_CHECK(chunk_len >= 1 && chunk_len <= 64, "chunk_len must be 1..64");
   prm.chunk_len = (int32_t)chunk_len;
+  prm.ctrl_ready = ctrl_ready ? 1 : 0;
   const ana::TelemetryParams tp = telemetry_params(tele_evoff, tele_events, tele_stats, M, K, dev);
   if (dev.is_cuda()) {
     check(link, "link", torch::kInt32, dev);

@@ -88,6 +88,9 @@ struct RateParams {
   // matches per ticket, 8..64 (lanes >= chunk_len idle): 64 for windows; micro-batches
   // use short chunks so their few matches spread over more waves (fewer iterations each)
   int32_t chunk_len;
+  // 1: ctrl[1..15] were zeroed by the schedule launched just before on this stream
+  // (launch_schedule zero_ctrl), so the launch skips its own zeroing dispatch
+  int32_t ctrl_ready;
 };
 
 // Per-match outputs.  The participant record of the reference

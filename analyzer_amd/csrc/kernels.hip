@@ -228,7 +228,7 @@ constexpr int kHashBuckets = 4096;
 template <int K>
 __global__ void __launch_bounds__(kSmallThreads)
 sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uint32_t* __restrict__ link,
-                  int32_t* __restrict__ deps, uint32_t* __restrict__ overflow) {
+                  int32_t* __restrict__ deps, uint32_t* __restrict__ overflow, int nz) {
   constexpr int S = 2 * K, R = S + 2;
   __shared__ uint32_t head[kHashBuckets];
   __shared__ uint16_t nxt[kSmallSched];
@@ -259,7 +259,7 @@ sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uin
     }
     deps[m] = 0;
   }
-  if (tid == 0) *overflow = 0u;
+  if (tid < nz) overflow[tid] = 0u;
   __syncthreads();
   for (int i = tid; i < n; i += kSmallThreads) {
     const uint32_t key = skey[i];
@@ -290,7 +290,11 @@ sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uin
 }
 
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
-                    int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s) {
+                    int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s,
+                    bool zero_ctrl) {
+  // zero_ctrl: also zero the executor's control words (overflow = ctrl[0], ctrl[1..15]) for
+  // a rate launch that follows on this stream and then skips its own zeroing dispatch
+  const int nz = zero_ctrl ? 16 : 1;
   const int64_t n = M * 2 * K;
   if (n > 0 && n <= kSmallSched && P < 0x7fffffffLL && K >= 1 && K <= 5) {
     const int e = n <= 2048 ? 2 : n <= 4096 ? 4 : 8;  // elements per thread
@@ -303,7 +307,7 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
   case k:                                                                                            \
     if (!bitonic)                                                                                    \
       hipLaunchKernelGGL((sched_hash_kernel<k>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,         \
-                         (uint32_t)P, link, deps, overflow);                                         \
+                         (uint32_t)P, link, deps, overflow, nz);                                     \
     else if (e == 2)                                                                                      \
       hipLaunchKernelGGL((sched_small_kernel<k, 2>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
                          (uint32_t)P, link, deps, overflow);                                         \
@@ -317,9 +321,10 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
       ANA_SMALL_CASE(1) ANA_SMALL_CASE(2) ANA_SMALL_CASE(3) ANA_SMALL_CASE(4) ANA_SMALL_CASE(5)
 #undef ANA_SMALL_CASE
     }
+    if (bitonic && zero_ctrl) ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 64, s));
     return (int)hipGetLastError();
   }
-  ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 4, s));
+  ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 4 * (size_t)nz, s));
   if (n <= 0) return 0;
   if (n > kMaxSlots || P >= 0x7fffffffLL || K < 1 || K > 5) return (int)hipErrorInvalidValue;
   if (ws_bytes < schedule_workspace_bytes(n, P)) return (int)hipErrorInvalidValue;

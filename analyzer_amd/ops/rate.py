@@ -220,13 +220,16 @@ class BatchRater:
 
     # ------------------------------------------------------------- schedule
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
-                 tag: str = "") -> Schedule:
+                 tag: str = "", zero_ctrl: bool = False) -> Schedule:
         """Dependency structure of a window (K5): per slot the match of its
         player's next occurrence and whether it occurred earlier (``link``), and
         per match the completion counter ``deps`` (see ``Schedule``).  The device
         rate launch counts ``deps`` up, so a schedule is single-use there.
         ``tag`` selects a separate buffer set (to prepare the next window while the
-        current one is being rated)."""
+        current one is being rated).  ``zero_ctrl`` (used by ``rate`` only): the
+        schedule also zeroes the executor's control words for the launch that
+        follows it on the same stream -- never from a side stream, where a rate
+        launch may be using them."""
         M = rec.shape[0]
         dev = rec.device
         link = self._buffer(dev, "link" + tag, M * 2 * K, torch.int32).view(M, 2 * K)
@@ -238,7 +241,7 @@ class BatchRater:
         else:
             ws = torch.empty(0, dtype=torch.uint8)
             ctrl = torch.empty(0, dtype=torch.int32)
-        native().schedule(rec, K, num_players, link, deps, ws, ctrl)
+        native().schedule(rec, K, num_players, link, deps, ws, ctrl, bool(zero_ctrl and rec.is_cuda))
         return Schedule(link, deps)
 
     # ----------------------------------------------------------------- rate
@@ -267,14 +270,16 @@ class BatchRater:
         record = first_prior is not None
         fp = first_prior if record else torch.empty(0, dtype=torch.float32, device=dev)
         if dev.type == "cuda":
+            ctrl_ready = schedule is None  # the schedule below zeroes ctrl on this stream
             if schedule is None:
-                schedule = self.schedule(rec, K, P)
+                schedule = self.schedule(rec, K, P, zero_ctrl=True)
             link, deps = schedule
             ctrl = self._buffer(dev, "ctrl", 16, torch.int32)
             epoch = roster.next_epoch() if epoch_dev is None else 1
         else:
             link = deps = ctrl = torch.empty(0, dtype=torch.int32)
             epoch = 1
+            ctrl_ready = False
         if telemetry is None:
             none = torch.empty(0, dtype=torch.int64, device=dev)
             telemetry = (none, none.to(torch.int32), none.to(torch.float32))
@@ -285,7 +290,7 @@ class BatchRater:
                       self.host_fp64, *telemetry,
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
                       epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
-                      self.chunk_len(M, telemetry[0].numel() > 0))
+                      self.chunk_len(M, telemetry[0].numel() > 0), ctrl_ready)
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out
