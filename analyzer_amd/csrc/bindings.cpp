@@ -163,7 +163,7 @@ std::tuple<Tensor, int64_t> levels(Tensor rec, int64_t K, int64_t num_players) {
 }
 
 void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
-              Tensor workspace, Tensor ctrl, bool zero_ctrl) {
+              Tensor workspace, Tensor ctrl, bool zero_ctrl, int64_t epoch_bump_ptr) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(link, "link", torch::kInt32, dev);
@@ -186,7 +186,9 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
                                    deps.data_ptr<int32_t>(), workspace.data_ptr<uint8_t>(),
                                    (size_t)workspace.numel(),
                                    reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()),
-                                   stream_of(rec), zero_ctrl), "schedule");
+                                   stream_of(rec), zero_ctrl,
+                                   reinterpret_cast<int32_t*>((intptr_t)epoch_bump_ptr)),
+              "schedule");
   } else {
     TORCH_CHECK(ana::host_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
                                    reinterpret_cast<uint32_t*>(link.data_ptr<int32_t>()),

@@ -42,7 +42,7 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
 // overflow: zeroed (reserved for schedule error reporting)
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s,
-                    bool zero_ctrl = false);
+                    bool zero_ctrl = false, int32_t* epoch_bump = nullptr);
 
 // out must be the packed layout (one row per match: [s_mu | s_sig | delta |
 // m_mu | m_sig][2K], quality, status byte), else hipErrorInvalidValue.

@@ -228,7 +228,8 @@ constexpr int kHashBuckets = 4096;
 template <int K>
 __global__ void __launch_bounds__(kSmallThreads)
 sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uint32_t* __restrict__ link,
-                  int32_t* __restrict__ deps, uint32_t* __restrict__ overflow, int nz) {
+                  int32_t* __restrict__ deps, uint32_t* __restrict__ overflow, int nz,
+                  int32_t* __restrict__ epoch_bump) {
   constexpr int S = 2 * K, R = S + 2;
   __shared__ uint32_t head[kHashBuckets];
   __shared__ uint16_t nxt[kSmallSched];
@@ -260,6 +261,7 @@ sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uin
     deps[m] = 0;
   }
   if (tid < nz) overflow[tid] = 0u;
+  if (epoch_bump && tid == 0) epoch_bump[0] += 1;  // graph replays: the launch epoch (epoch_bump_kernel)
   __syncthreads();
   for (int i = tid; i < n; i += kSmallThreads) {
     const uint32_t key = skey[i];
@@ -291,7 +293,7 @@ sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uin
 
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s,
-                    bool zero_ctrl) {
+                    bool zero_ctrl, int32_t* epoch_bump) {
   // zero_ctrl: also zero the executor's control words (overflow = ctrl[0], ctrl[1..15]) for
   // a rate launch that follows on this stream and then skips its own zeroing dispatch
   const int nz = zero_ctrl ? 16 : 1;
@@ -307,7 +309,7 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
   case k:                                                                                            \
     if (!bitonic)                                                                                    \
       hipLaunchKernelGGL((sched_hash_kernel<k>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,         \
-                         (uint32_t)P, link, deps, overflow, nz);                                     \
+                         (uint32_t)P, link, deps, overflow, nz, epoch_bump);                         \
     else if (e == 2)                                                                                      \
       hipLaunchKernelGGL((sched_small_kernel<k, 2>), dim3(1), dim3(kSmallThreads), 0, s, rec, M,     \
                          (uint32_t)P, link, deps, overflow);                                         \
@@ -322,9 +324,11 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
 #undef ANA_SMALL_CASE
     }
     if (bitonic && zero_ctrl) ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 64, s));
+    if (bitonic && epoch_bump) hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(1), 0, s, epoch_bump);
     return (int)hipGetLastError();
   }
   ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 4 * (size_t)nz, s));
+  if (epoch_bump) hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(1), 0, s, epoch_bump);
   if (n <= 0) return 0;
   if (n > kMaxSlots || P >= 0x7fffffffLL || K < 1 || K > 5) return (int)hipErrorInvalidValue;
   if (ws_bytes < schedule_workspace_bytes(n, P)) return (int)hipErrorInvalidValue;

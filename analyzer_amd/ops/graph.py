@@ -14,7 +14,7 @@ one graph replay:
   schedule keys them past the last player), so any batch size up to the
   capacity replays the same graph;
 * the dataflow launch reads its tag epoch from device memory
-  (``RateParams::epoch_ptr``); a one-thread kernel inside the graph bumps it
+  (``RateParams::epoch_ptr``); the graph's schedule kernel bumps it
   before every launch, so replays never see each other's granule tags.  Before
   the epoch would pass 255 the host resets the roster's tags and the counter
   (eagerly, outside the graph), exactly like ``Roster.next_epoch``;
@@ -77,7 +77,7 @@ class GraphRater:
             self._body()
 
     def _body(self) -> None:
-        native().epoch_bump(self.epoch)
+        # rate() bumps the device epoch before its launch reads it (inside the schedule)
         self.rater.rate(self.roster, self.rec, self.K, out=self.out, check=False,
                         epoch_dev=self.epoch)
 

@@ -220,7 +220,8 @@ class BatchRater:
 
     # ------------------------------------------------------------- schedule
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
-                 tag: str = "", zero_ctrl: bool = False) -> Schedule:
+                 tag: str = "", zero_ctrl: bool = False,
+                 epoch_bump: Optional[torch.Tensor] = None) -> Schedule:
         """Dependency structure of a window (K5): per slot the match of its
         player's next occurrence and whether it occurred earlier (``link``), and
         per match the completion counter ``deps`` (see ``Schedule``).  The device
@@ -229,7 +230,8 @@ class BatchRater:
         current one is being rated).  ``zero_ctrl`` (used by ``rate`` only): the
         schedule also zeroes the executor's control words for the launch that
         follows it on the same stream -- never from a side stream, where a rate
-        launch may be using them."""
+        launch may be using them.  ``epoch_bump``: a device int32 launch epoch
+        (graph replays) the schedule increments, saving the bump its own dispatch."""
         M = rec.shape[0]
         dev = rec.device
         link = self._buffer(dev, "link" + tag, M * 2 * K, torch.int32).view(M, 2 * K)
@@ -241,7 +243,9 @@ class BatchRater:
         else:
             ws = torch.empty(0, dtype=torch.uint8)
             ctrl = torch.empty(0, dtype=torch.int32)
-        native().schedule(rec, K, num_players, link, deps, ws, ctrl, bool(zero_ctrl and rec.is_cuda))
+        bump = epoch_bump.data_ptr() if epoch_bump is not None and rec.is_cuda else 0
+        native().schedule(rec, K, num_players, link, deps, ws, ctrl, bool(zero_ctrl and rec.is_cuda),
+                          bump)
         return Schedule(link, deps)
 
     # ----------------------------------------------------------------- rate
@@ -256,8 +260,9 @@ class BatchRater:
         (K8 fused streaming mode: idle dataflow waves take telemetry tiles).
         ``progress`` = (signal address, launch number, chunk index): the tail
         signal of runtime/engine.py (device only).  ``epoch_dev``: a device int32
-        tensor holding the launch epoch (graph replays, ops/graph.py); the
-        roster's host-side epoch is then left alone."""
+        tensor holding the launch epoch (graph replays, ops/graph.py), bumped by
+        one on the device before the launch reads it; the roster's host-side
+        epoch is then left alone."""
         K = int(K or (rec.shape[1] - 2) // 2)
         M = int(rec.shape[0])
         dev = rec.device
@@ -271,8 +276,10 @@ class BatchRater:
         fp = first_prior if record else torch.empty(0, dtype=torch.float32, device=dev)
         if dev.type == "cuda":
             ctrl_ready = schedule is None  # the schedule below zeroes ctrl on this stream
-            if schedule is None:
-                schedule = self.schedule(rec, K, P, zero_ctrl=True)
+            if schedule is None:  # ... and bumps a device epoch
+                schedule = self.schedule(rec, K, P, zero_ctrl=True, epoch_bump=epoch_dev)
+            elif epoch_dev is not None:
+                native().epoch_bump(epoch_dev)
             link, deps = schedule
             ctrl = self._buffer(dev, "ctrl", 16, torch.int32)
             epoch = roster.next_epoch() if epoch_dev is None else 1
