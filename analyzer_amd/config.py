@@ -74,6 +74,8 @@ class WorkerConfig:
     # new: aggregate per-participant telemetry (participant_stats) in the rating launch
     dotelemetry: bool = False
     telemetry_events: str = "100,300"
+    # new: the run is a benchmark -- synthetic telemetry may be persisted (worker.connect)
+    synthetic_telemetry: bool = False
     # new: skip matches that already carry a rating (trueskill_quality set), so a
     # redelivery after commit-but-before-ack does not rate a match twice.  Off by
     # default: the reference re-rates redelivered matches (worker.py:122-129,194)
@@ -98,6 +100,7 @@ class WorkerConfig:
             quarantine=(env.get("QUARANTINE") or "true") == "true",
             dotelemetry=env.get("DOTELEMETRY") == "true",
             telemetry_events=_env(env, "TELEMETRY_EVENTS") or "100,300",
+            synthetic_telemetry=env.get("SYNTHETIC_TELEMETRY") == "true",
             skip_rated=env.get("SKIP_RATED") == "true",
         )
 

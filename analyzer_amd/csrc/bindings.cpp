@@ -93,7 +93,7 @@ void gen_roster(Tensor state, Tensor attrs, int64_t seed, int64_t p_tier_null, i
 void gen_stream(Tensor rec, int64_t K, int64_t seed, int64_t base, int64_t num_players,
                 int64_t team_size, std::vector<int64_t> mode_cdf, int64_t p_uneven,
                 int64_t p_bad_rosters, int64_t p_tie, int64_t p_afk, int64_t p_hot,
-                int64_t hot_players) {
+                int64_t hot_players, int64_t skew) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   TORCH_CHECK(K >= 1 && K <= 5, "K (players per roster slot block) must be 1..5");
@@ -102,11 +102,13 @@ void gen_stream(Tensor rec, int64_t K, int64_t seed, int64_t base, int64_t num_p
   TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
   TORCH_CHECK(hot_players >= 1 && hot_players <= num_players, "hot_players must be 1..num_players");
   TORCH_CHECK(mode_cdf.size() == 7, "mode_cdf must have 7 thresholds");
+  TORCH_CHECK(skew >= 1 && skew <= 8, "skew must be 1..8");
   ana::GenStreamParams g{};
   g.seed = (uint64_t)seed;
   g.base = base;
   g.num_players = num_players;
   g.team_size = (int32_t)team_size;
+  g.skew = (int32_t)skew;
   for (int k = 0; k < 7; ++k) g.mode_cdf[k] = u32(mode_cdf[k], "mode_cdf");
   g.p_uneven = u32(p_uneven, "p_uneven");
   g.p_bad_rosters = u32(p_bad_rosters, "p_bad_rosters");
@@ -178,7 +180,7 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   if (dev.is_cuda()) {
     check(workspace, "workspace", torch::kUInt8, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
-    TORCH_CHECK(ctrl.numel() >= 16, "ctrl must have 16 entries");
+    TORCH_CHECK(ctrl.numel() >= 32, "ctrl must have 32 entries");
     const size_t need = ana::schedule_workspace_bytes(M * 2 * K, num_players);
     TORCH_CHECK((size_t)workspace.numel() >= need, "workspace too small: need ", need, " bytes");
     check_hip(ana::launch_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
@@ -287,7 +289,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
     check(ctrl, "ctrl", torch::kInt32, dev);
     TORCH_CHECK(link.numel() == M * S * ana::kLinkWords, "link must be [M, 2K]");
     TORCH_CHECK(deps.numel() == M, "deps must have M entries");
-    TORCH_CHECK(ctrl.numel() >= 16, "ctrl must have 16 entries");
+    TORCH_CHECK(ctrl.numel() >= 32, "ctrl must have 32 entries");
     TORCH_CHECK(blocks >= 1 && blocks <= 65535, "blocks must be 1..65535");
     // the executor writes packed rows; other layouts go through a packed buffer
     const bool packed = out.s_sig == out.s_mu + S && out.delta == out.s_mu + 2 * S &&
@@ -388,45 +390,56 @@ void check_rows(const Tensor& t, const char* name, int64_t P, int64_t cols, cons
   TORCH_CHECK(t.dim() == 2 && t.size(0) == P && t.size(1) == cols, name, " must be [P, ", cols, "]");
 }
 
-void sweep_delta(Tensor s0, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma, bool scaled,
-                 Tensor buf) {
+// s0: common window start, prior: this rank's prior of the sweep (s0 itself in
+// the first sweep), s: the posterior after the local shard
+void sweep_delta(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma,
+                 bool scaled, Tensor buf) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
   check_rows(s0, "s0", P, ana::kRowFloats, dev);
+  check_rows(prior, "prior", P, ana::kRowFloats, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
   check_rows(attrs, "attrs", P, 4, dev);
   check_rows(buf, "buf", P, 16, dev);
   check(vst, "vst", torch::kFloat32, dev);
   TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
   if (dev.is_cuda()) {
-    check_hip(ana::launch_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(),
-                                      attrs.data_ptr<float>(), vst.data_ptr<float>(),
-                                      (float)unknown_sigma, scaled ? 1 : 0, buf.data_ptr<float>(), P,
-                                      stream_of(s)), "sweep_delta");
+    check_hip(ana::launch_sweep_delta(s0.data_ptr<float>(), prior.data_ptr<float>(),
+                                      s.data_ptr<float>(), attrs.data_ptr<float>(),
+                                      vst.data_ptr<float>(), (float)unknown_sigma, scaled ? 1 : 0,
+                                      buf.data_ptr<float>(), P, stream_of(s)), "sweep_delta");
   } else {
-    ana::host_sweep_delta(s0.data_ptr<float>(), s.data_ptr<float>(), attrs.data_ptr<float>(),
-                          vst.data_ptr<float>(), (float)unknown_sigma, scaled, buf.data_ptr<float>(), P);
+    ana::host_sweep_delta(s0.data_ptr<float>(), prior.data_ptr<float>(), s.data_ptr<float>(),
+                          attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma,
+                          scaled, buf.data_ptr<float>(), P);
   }
 }
 
-void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor vst, double unknown_sigma,
-                 bool scaled) {
+// decoded rows to s and, if s2 is non-empty, also to s2
+void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor s2, Tensor vst,
+                 double unknown_sigma, bool scaled) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
   check_rows(s0, "s0", P, ana::kRowFloats, dev);
   check_rows(buf, "buf", P, 16, dev);
   check_rows(attrs, "attrs", P, 4, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
+  float* p2 = nullptr;
+  if (s2.numel()) {
+    check_rows(s2, "s2", P, ana::kRowFloats, dev);
+    p2 = s2.data_ptr<float>();
+  }
   check(vst, "vst", torch::kFloat32, dev);
   TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
   if (dev.is_cuda()) {
     check_hip(ana::launch_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(),
-                                      attrs.data_ptr<float>(), s.data_ptr<float>(),
+                                      attrs.data_ptr<float>(), s.data_ptr<float>(), p2,
                                       vst.data_ptr<float>(), (float)unknown_sigma, scaled ? 1 : 0, P,
                                       stream_of(s)), "sweep_apply");
   } else {
     ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
-                          s.data_ptr<float>(), scaled, vst.data_ptr<float>(), (float)unknown_sigma, P);
+                          s.data_ptr<float>(), p2, scaled, vst.data_ptr<float>(),
+                          (float)unknown_sigma, P);
   }
 }
 
@@ -538,7 +551,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("telemetry", &telemetry, "K8: per-participant telemetry aggregation [M, 2K, 8]");
   m.attr("STAT_FEATURES") = ana::kStatFeatures;
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
-  m.def("sweep_apply", &sweep_apply, "K9: apply all-reduced messages to the replicated roster");
+  m.def("sweep_apply", &sweep_apply, "K9: decode summed messages against the common start (-> s, s2)");
   m.def("write_record_file", &write_record_file, "P3: write a match-record file (ANAREC01)");
   py::class_<ana::RecordReader>(m, "RecordReader")
       .def(py::init<const std::string&, int64_t, int, bool>(), py::arg("path"), py::arg("window"),

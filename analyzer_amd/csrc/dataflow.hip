@@ -393,7 +393,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         own && (((lk0 & kLinkHasPred) && s_this && (uint32_t)gs.w != kNoMatch &&
                  (uint32_t)gs.w > (uint32_t)m) ||
                 (shared_ok && gm.y == epoch && (uint32_t)gm.w == cnt % 15u + 1u));
-    if (__ballot(overtaken) != 0ull && lane == 0) atomicOr(&ctrl[2], 1u);
+    if (__ballot(overtaken) != 0ull && lane == 0) {
+      atomicOr(&ctrl[2], 1u);
+      atomicOr(&ctrl[18], 1u);  // sticky copy (never zeroed by a launch)
+    }
     const uint64_t stale_lanes = __ballot(!fresh);
     if (stale_lanes) {
       if (lane == 0)  // diagnostics: stale reads retried (ctrl[14])
@@ -658,7 +661,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         }
       }
       if (now - t0 > kTimeoutTicks) {
-        if (lane == 0) atomicOr(&ctrl[1], 1u);
+        if (lane == 0) {
+          atomicOr(&ctrl[1], 1u);
+          atomicOr(&ctrl[17], 1u);  // sticky copy
+        }
 #pragma unroll
         for (int h = 0; h < kH; ++h)
           if (cbase[h] >= 0 && ((pend[h] >> lane) & 1ull))
@@ -695,7 +701,7 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   const int64_t M = prm.num_matches;
   // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] retired chunks, [4..11] tickets,
   // [12] telemetry tile ticket, [13] malformed telemetry events, [14] stale reads retried,
-  // [15] wave iterations
+  // [15] wave iterations; [16..18] sticky OR of [0..2] over launches (host clears)
   // one-wave kernel rather than hipMemsetAsync: a 60-B fill at a 4-B offset becomes two
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
   if (!prm.ctrl_ready) hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, 15);

@@ -30,7 +30,7 @@ struct GenStreamParams {
   int64_t base;           // global index of match 0 of this window/shard
   int64_t num_players;
   int32_t team_size;      // players per roster (<= K)
-  int32_t pad;
+  int32_t skew;           // activity skew: player = floor(u^skew * P), 1 = uniform
   uint32_t mode_cdf[7];   // cumulative thresholds: modes 0..5, then "unsupported"
   uint32_t p_uneven;      // roster 1 one player short
   uint32_t p_bad_rosters; // nrosters = 3
@@ -103,7 +103,13 @@ ANA_HD void gen_match(const GenStreamParams& g, int64_t m, int32_t* rec) {
       const uint64_t h = rng_u64(s, idx, 16 + j);
       const bool hot = (uint32_t)h < g.p_hot;
       const uint64_t range = hot ? (uint64_t)g.hot_players : (uint64_t)g.num_players;
-      rec[j] = (int32_t)mulhi_range((uint32_t)(h >> 32), range);
+      // power-law activity: u^skew in 32-bit fixed point (integer products only,
+      // so host and device agree bit for bit); player 0 is the most active, with
+      // probability P^(-1/skew) per slot (skew 3 = SURVEY App. C.5 "cubic")
+      uint32_t u = (uint32_t)(h >> 32);
+      const uint32_t u1 = u;
+      for (int k = 1; k < g.skew; ++k) u = (uint32_t)(((uint64_t)u * u1) >> 32);
+      rec[j] = (int32_t)mulhi_range(u, range);
     } else {
       rec[j] = -1;
     }

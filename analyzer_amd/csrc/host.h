@@ -28,8 +28,8 @@ int host_rate(int K, bool fp64, const int32_t* rec, float* state, const float* a
 }  // namespace ana
 
 namespace ana {
-void host_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
-                      float unknown_sigma, bool scaled, float* buf, int64_t P);
-void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, bool scaled,
-                      const float* vst, float unknown_sigma, int64_t P);
+void host_sweep_delta(const float* s0, const float* a, const float* s, const float* attrs,
+                      const float* vst, float unknown_sigma, bool scaled, float* buf, int64_t P);
+void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
+                      bool scaled, const float* vst, float unknown_sigma, int64_t P);
 }  // namespace ana

@@ -54,45 +54,59 @@ RecordReader::RecordReader(const std::string& path, int64_t window, int slots, b
   if (window <= 0 || slots < 2) throw std::invalid_argument("window > 0 and slots >= 2 required");
   file_ = fopen(path.c_str(), "rb");
   if (!file_) throw std::runtime_error("cannot open " + path);
-  RecordFileHeader h{};
-  if (fread(&h, sizeof(h), 1, file_) != 1 || memcmp(h.magic, kMagic, 8) != 0) {
-    fclose(file_);
-    throw std::runtime_error(path + " is not an ANAREC01 record file");
-  }
-  K_ = h.K;
-  M_ = h.M;
-  if (K_ < 1 || K_ > 5 || M_ < 0) {
-    fclose(file_);
-    throw std::runtime_error(path + ": bad header");
-  }
-  const size_t bytes = (size_t)window_ * (size_t)(2 * K_ + 2) * sizeof(int32_t);
-  buf_.resize(slots_, nullptr);
-  n_.assign(slots_, 0);
-  base_.assign(slots_, 0);
-  for (int s = 0; s < slots_; ++s) {
-    void* p = nullptr;
-    if (pinned && hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) {
-      pinned_ = true;
-    } else {
-      (void)hipGetLastError();
-      p = malloc(bytes);
-      pinned_ = false;
+  try {
+    RecordFileHeader h{};
+    if (fread(&h, sizeof(h), 1, file_) != 1 || memcmp(h.magic, kMagic, 8) != 0)
+      throw std::runtime_error(path + " is not an ANAREC01 record file");
+    K_ = h.K;
+    M_ = h.M;
+    if (K_ < 1 || K_ > 5 || M_ < 0) throw std::runtime_error(path + ": bad header");
+    const size_t bytes = (size_t)window_ * (size_t)(2 * K_ + 2) * sizeof(int32_t);
+    buf_.assign(slots_, nullptr);
+    slot_pinned_.assign(slots_, false);
+    n_.assign(slots_, 0);
+    base_.assign(slots_, 0);
+    for (int s = 0; s < slots_; ++s) {
+      // each slot remembers its own allocator: under pinned-memory pressure some
+      // slots may be pinned and later ones plain malloc
+      void* p = nullptr;
+      if (pinned && hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess) {
+        slot_pinned_[s] = true;
+      } else {
+        (void)hipGetLastError();
+        p = malloc(bytes);
+        if (!p) throw std::bad_alloc();
+      }
+      buf_[s] = static_cast<int32_t*>(p);
     }
-    if (!p) throw std::bad_alloc();
-    buf_[s] = static_cast<int32_t*>(p);
+    producer_ = std::thread(&RecordReader::run, this);
+  } catch (...) {
+    release_buffers();
+    throw;
   }
-  producer_ = std::thread(&RecordReader::run, this);
+}
+
+void RecordReader::release_buffers() {
+  for (size_t s = 0; s < buf_.size(); ++s) {
+    if (!buf_[s]) continue;
+    if (slot_pinned_[s]) (void)hipHostFree(buf_[s]);
+    else free(buf_[s]);
+    buf_[s] = nullptr;
+  }
+  if (file_) fclose(file_);
+  file_ = nullptr;
+}
+
+bool RecordReader::pinned() const {
+  for (bool b : slot_pinned_)
+    if (!b) return false;
+  return !slot_pinned_.empty();
 }
 
 RecordReader::~RecordReader() {
   stop_.store(true, std::memory_order_release);
   if (producer_.joinable()) producer_.join();
-  for (int32_t* p : buf_) {
-    if (!p) continue;
-    if (pinned_) (void)hipHostFree(p);
-    else free(p);
-  }
-  if (file_) fclose(file_);
+  release_buffers();
 }
 
 int64_t RecordReader::num_windows() const { return (M_ + window_ - 1) / window_; }
@@ -111,7 +125,7 @@ void RecordReader::run() {
     const int s = (int)(head % (uint64_t)slots_);
     const int64_t base = w * window_;
     const int64_t n = (M_ - base) < window_ ? (M_ - base) : window_;
-    if (fseek(file_, (long)(sizeof(RecordFileHeader) + (size_t)base * R * sizeof(int32_t)), SEEK_SET) != 0 ||
+    if (fseeko(file_, (off_t)(sizeof(RecordFileHeader) + (size_t)base * R * sizeof(int32_t)), SEEK_SET) != 0 ||
         fread(buf_[s], R * sizeof(int32_t), (size_t)n, file_) != (size_t)n) {
       error_.store(true, std::memory_order_release);
       head_.store(head + 1, std::memory_order_release);  // wake the consumer

@@ -25,7 +25,8 @@ class RecordReader {
   int64_t num_matches() const { return M_; }
   int64_t window() const { return window_; }
   int64_t num_windows() const;
-  bool pinned() const { return pinned_; }
+  // every slot is pinned host memory (slots fall back to malloc one by one)
+  bool pinned() const;
   int32_t* slot_data(int slot) const { return buf_[slot]; }
 
   // blocks until the next window is filled; false at end of file
@@ -35,6 +36,7 @@ class RecordReader {
 
  private:
   void run();
+  void release_buffers();
 
   std::string path_;
   int64_t window_;
@@ -42,8 +44,8 @@ class RecordReader {
   int K_ = 0;
   int64_t M_ = 0;
   FILE* file_ = nullptr;
-  bool pinned_ = false;
   std::vector<int32_t*> buf_;
+  std::vector<bool> slot_pinned_;
   std::vector<int64_t> n_, base_;
   std::atomic<uint64_t> head_{0}, tail_{0};
   uint64_t next_ = 0;  // consumer-only cursor

@@ -65,8 +65,11 @@ int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_
 }  // namespace ana
 
 namespace ana {
-int launch_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
-                       float unknown_sigma, int scaled, float* buf, int64_t P, hipStream_t st);
-int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,
+// s0: common window start, a: the rank's prior of this sweep (may be s0), s: posterior
+int launch_sweep_delta(const float* s0, const float* a, const float* s, const float* attrs,
+                       const float* vst, float unknown_sigma, int scaled, float* buf, int64_t P,
+                       hipStream_t st);
+// decoded rows to s and (s2 != nullptr) s2
+int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                        const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st);
 }  // namespace ana

@@ -8,9 +8,12 @@
 // and the merged posterior is  nat(prior) + sum_g delta_g  -- one dense
 // all-reduce (SUM) of a [P][8][2] fp32 buffer over RCCL/xGMI.
 //
-// Every rank measures its message against the SAME base (sweep_core.h
+// Every rank's message is decoded against the SAME base (sweep_core.h
 // track_base): the window-start value, or for a track NULL at window start the
-// prior the reference would assign (seed / window-start shared).  A track only
+// prior the reference would assign (seed / window-start shared).  Causal
+// re-sweeps (parallel/sweep.py) re-rate rank r's shard from the start plus the
+// messages of ranks < r (an exclusive prefix over ranks); the message is then
+// measured from that prior, so the prefix telescopes to rank r-1's posterior.  A track only
 // one rank touched therefore merges to exactly that rank's posterior; tracks
 // several ranks touched combine as independent evidence (the sweep-mode
 // approximation of concurrent shards).  Slot 7 of each player's buffer row
@@ -36,25 +39,34 @@ __device__ __forceinline__ void load_row(const float4* __restrict__ src, int64_t
   }
 }
 
-__global__ void sweep_delta_kernel(const float4* __restrict__ s0, const float4* __restrict__ s,
-                                   const float4* __restrict__ attrs, const float* __restrict__ vst,
-                                   float unknown_sigma, int scaled, float4* __restrict__ buf,
-                                   int64_t P) {
+// s0: common window start, a: this rank's prior of the sweep (may alias s0),
+// s: posterior after the local window; buf: [P][16] messages
+__global__ void sweep_delta_kernel(const float4* __restrict__ s0, const float4* a0,
+                                   const float4* __restrict__ s, const float4* __restrict__ attrs,
+                                   const float* __restrict__ vst, float unknown_sigma, int scaled,
+                                   float4* __restrict__ buf, int64_t P) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  float a[kRowFloats], b[kRowFloats], o[16];
-  load_row(s0, p, a);
+  float c[kRowFloats], a[kRowFloats], b[kRowFloats], o[16];
+  load_row(s0, p, c);
+  if (a0 != s0) load_row(a0, p, a);
+  else
+#pragma unroll
+    for (int k = 0; k < kRowFloats; ++k) a[k] = c[k];
   load_row(s, p, b);
   const float4 at = attrs[p];
   const float attr[4] = {at.x, at.y, at.z, at.w};
-  sweep_delta_player(a, b, attr, vst, unknown_sigma, scaled != 0, o);
+  sweep_delta_player(c, a, b, attr, vst, unknown_sigma, scaled != 0, o);
 #pragma unroll
   for (int k = 0; k < 4; ++k)
     buf[p * 4 + k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
 }
 
+// decoded rows go to s and, when given, also to s2: the final merge of a window
+// writes the next window's common start there (no per-window snapshot copy),
+// a causal re-sweep writes the rank's prior for the next message
 __global__ void sweep_apply_kernel(const float4* __restrict__ s0, const float4* __restrict__ buf,
-                                   const float4* __restrict__ attrs, float4* __restrict__ s,
+                                   const float4* __restrict__ attrs, float4* s, float4* s2,
                                    const float* __restrict__ vst, float unknown_sigma, int scaled,
                                    int64_t P) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -70,27 +82,31 @@ __global__ void sweep_apply_kernel(const float4* __restrict__ s0, const float4* 
   const float attr[4] = {at.x, at.y, at.z, at.w};
   sweep_apply_player(a, d, attr, vst, unknown_sigma, scaled != 0, o);
 #pragma unroll
-  for (int k = 0; k < kRowVec; ++k)
-    s[p * kRowVec + k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+  for (int k = 0; k < kRowVec; ++k) {
+    const float4 v = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    s[p * kRowVec + k] = v;
+    if (s2) s2[p * kRowVec + k] = v;
+  }
 }
 
-int launch_sweep_delta(const float* s0, const float* s, const float* attrs, const float* vst,
-                       float unknown_sigma, int scaled, float* buf, int64_t P, hipStream_t st) {
+int launch_sweep_delta(const float* s0, const float* a, const float* s, const float* attrs,
+                       const float* vst, float unknown_sigma, int scaled, float* buf, int64_t P,
+                       hipStream_t st) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(sweep_delta_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(s0), reinterpret_cast<const float4*>(s),
-                     reinterpret_cast<const float4*>(attrs), vst, unknown_sigma, scaled,
-                     reinterpret_cast<float4*>(buf), P);
+                     reinterpret_cast<const float4*>(s0), reinterpret_cast<const float4*>(a),
+                     reinterpret_cast<const float4*>(s), reinterpret_cast<const float4*>(attrs), vst,
+                     unknown_sigma, scaled, reinterpret_cast<float4*>(buf), P);
   return (int)hipGetLastError();
 }
 
-int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s,
+int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                        const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(sweep_apply_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
                      reinterpret_cast<const float4*>(s0), reinterpret_cast<const float4*>(buf),
-                     reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s), vst,
-                     unknown_sigma, scaled, P);
+                     reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
+                     reinterpret_cast<float4*>(s2), vst, unknown_sigma, scaled, P);
   return (int)hipGetLastError();
 }
 

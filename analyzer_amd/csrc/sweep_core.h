@@ -37,40 +37,51 @@ ANA_HD bool track_base(const float* a, int t, bool seeded, float seed_mu, float 
   return seeded;
 }
 
-// Message encodings (both linear, so the all-reduce SUM stays exact in algebra):
+// Message encodings (both linear in the natural parameters, so sums over ranks
+// -- the all-reduce, and the exclusive prefix of the causal sweeps -- stay exact
+// in algebra):
 //  raw    (d_pi, d_tau)
-//  scaled (d_pi / pi_b, (d_tau - mu_b d_pi) / pi_b): dimensionless precision ratio and
+//  scaled (d_pi / pi_B, (d_tau - mu_B d_pi) / pi_B): dimensionless precision ratio and
 //         a rating-point-sized mean shift -- small, well-conditioned numbers that
-//         survive an fp16 / bf16 all-reduce (COMM_DTYPE), decoded against the same base.
+//         survive an fp16 / bf16 all-reduce (COMM_DTYPE), decoded against the same base B.
 //
-// a: window-start row, b: row after the local window, attr/vst/unknown_sigma:
-// seed inputs.  o: 16 floats = message per track + touch fields for tracks
-// that were NULL at window start and are rated now (base-16 counters, exact in
-// fp32 for <= 15 ranks).
-ANA_HD void sweep_delta_player(const float* a, const float* b, const float* attr, const float* vst,
-                               float unknown_sigma, bool scaled, float* o) {
+// s: the COMMON window-start row (identical on every rank; it defines the base B
+// of each track), a: the prior this rank rated its shard from in this sweep
+// (== s in the first sweep; the start plus the earlier ranks' messages in a
+// causal re-sweep, parallel/sweep.py), b: the row after the local window.  The
+// message is nat(b) - nat(a), measured against a's value where a has one and
+// against B where the track is NULL in a: prefix sums then telescope, so the
+// start + the messages of ranks 0..r-1 is exactly rank r-1's posterior once
+// every earlier rank rated from its exact prior.  attr/vst/unknown_sigma: seed
+// inputs.  o: 16 floats = message per track + touch fields for tracks that are
+// NULL in a and rated now (base-16 counters, exact in fp32 for <= 15 ranks).
+ANA_HD void sweep_delta_player(const float* s, const float* a, const float* b, const float* attr,
+                               const float* vst, float unknown_sigma, bool scaled, float* o) {
   float seed_mu = NAN, seed_sig = NAN;
   const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
   float touch_lo = 0.f, touch_hi = 0.f;
   for (int t = 0; t < kTracks; ++t) {
     const float mu0 = a[4 * t], sg0 = a[4 * t + 2], mu = b[4 * t], sg = b[4 * t + 2];
     float dp = 0.f, dt = 0.f;
-    const bool changed = mu0 == mu0 ? (mu != mu0 || sg != sg0) : mu == mu;
+    const bool had = mu0 == mu0;
+    const bool changed = had ? (mu != mu0 || sg != sg0) : mu == mu;
     float bm, bs;
-    if (changed && track_base(a, t, seeded, seed_mu, seed_sig, bm, bs)) {
-      if (scaled) {  // (pi/pi_b - 1, (pi/pi_b)(mu - mu_b)): no cancellation
-        const float r = bs / sg;
-        dp = r * r - 1.f;
-        dt = r * r * (mu - bm);
+    if (changed && track_base(s, t, seeded, seed_mu, seed_sig, bm, bs)) {
+      if (scaled) {  // (pi/pi_B - pi0/pi_B, (pi/pi_B)(mu - mu_B) - (pi0/pi_B)(mu0 - mu_B))
+        const float r1 = bs / sg;
+        const float r0 = had ? bs / sg0 : 1.f;
+        dp = r1 * r1 - r0 * r0;
+        dt = r1 * r1 * (mu - bm) - (had ? r0 * r0 * (mu0 - bm) : 0.f);
       } else {
         float p1, t1, p0, t0;
         nat_params(mu, sg, p1, t1);
-        nat_params(bm, bs, p0, t0);
+        if (had) nat_params(mu0, sg0, p0, t0);
+        else nat_params(bm, bs, p0, t0);
         dp = p1 - p0;
         dt = t1 - t0;
       }
     }
-    if (mu0 != mu0 && mu == mu) {
+    if (!had && mu == mu) {
       if (t < 4) touch_lo += (float)(1 << (4 * t));
       else touch_hi += (float)(1 << (4 * (t - 4)));
     }
@@ -81,8 +92,9 @@ ANA_HD void sweep_delta_player(const float* a, const float* b, const float* attr
   o[15] = touch_hi;
 }
 
-// a: window-start row, d: all-reduced messages, attr: player attributes,
-// o: merged row (tags reset to 0; spare floats copied).
+// a: common window-start row, d: summed messages (all ranks: the merged window;
+// ranks < r: rank r's prior for a causal re-sweep), attr: player attributes,
+// o: decoded row (tags reset to 0; spare floats copied).
 ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr,
                                const float* vst, float unknown_sigma, bool scaled, float* o) {
   float seed_mu = NAN, seed_sig = NAN;

@@ -30,6 +30,7 @@ from .native import native
 RATED, AFK, INVALID_ROSTERS, UNSUPPORTED_MODE = 0, 1, 2, 3
 ERR_SEED, ERR_SIGMA, ERR_EMPTY_ROSTER, ERR_NUMERIC, ERR_BAD_RECORD = 4, 5, 6, 7, 8
 NOT_PROCESSED = 255
+CTRL_WORDS = 32  # executor control words (csrc/dataflow.hip launch_rate)
 STATUS_NAMES = {RATED: "rated", AFK: "afk", INVALID_ROSTERS: "invalid_rosters",
                 UNSUPPORTED_MODE: "unsupported_mode", ERR_SEED: "error_seed",
                 ERR_SIGMA: "error_sigma", ERR_EMPTY_ROSTER: "error_empty_roster",
@@ -178,6 +179,12 @@ class BatchRater:
         self._vst: Dict[str, torch.Tensor] = {}
         self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
 
+    @staticmethod
+    def has_telemetry(telemetry) -> bool:
+        """One definition of "this launch aggregates telemetry" for every caller
+        that sizes chunks (rate(), runtime/engine.py's tail signal)."""
+        return telemetry is not None and telemetry[0].numel() > 0
+
     def chunk_len(self, M: int, telemetry: bool = False) -> int:
         """Matches per executor ticket: 64 (one per lane) for windows, shorter
         (8-32, a power of two) when 64-match chunks would leave the full grid
@@ -218,6 +225,17 @@ class BatchRater:
             self._ws[key] = buf
         return buf[:numel]
 
+    def _ctrl(self, device) -> torch.Tensor:
+        """The executor's control words (csrc/dataflow.hip launch_rate): [0..15]
+        per launch (zeroed before each), [16..18] sticky OR of the error flags
+        over every launch since ``clear_sticky``."""
+        key = (str(device), "ctrl")
+        buf = self._ws.get(key)
+        if buf is None:
+            buf = torch.zeros(CTRL_WORDS, dtype=torch.int32, device=device)
+            self._ws[key] = buf
+        return buf
+
     # ------------------------------------------------------------- schedule
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
                  tag: str = "", zero_ctrl: bool = False,
@@ -239,7 +257,7 @@ class BatchRater:
         if rec.is_cuda:
             nbytes = native().schedule_workspace_bytes(M * 2 * K, num_players)
             ws = self._buffer(dev, "sched_ws", nbytes, torch.uint8)
-            ctrl = self._buffer(dev, "ctrl", 16, torch.int32)
+            ctrl = self._ctrl(dev)
         else:
             ws = torch.empty(0, dtype=torch.uint8)
             ctrl = torch.empty(0, dtype=torch.int32)
@@ -281,23 +299,24 @@ class BatchRater:
             elif epoch_dev is not None:
                 native().epoch_bump(epoch_dev)
             link, deps = schedule
-            ctrl = self._buffer(dev, "ctrl", 16, torch.int32)
+            ctrl = self._ctrl(dev)
             epoch = roster.next_epoch() if epoch_dev is None else 1
         else:
             link = deps = ctrl = torch.empty(0, dtype=torch.int32)
             epoch = 1
             ctrl_ready = False
-        if telemetry is None:
+        tele = self.has_telemetry(telemetry)
+        if not tele:
             none = torch.empty(0, dtype=torch.int64, device=dev)
             telemetry = (none, none.to(torch.int32), none.to(torch.float32))
         native().rate(rec, K, link, deps, roster.state, roster.attrs, fp, out.quality, out.status,
                       out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
                       float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
-                      record, self.grid_blocks(M, telemetry[0].numel() > 0), epoch,
+                      record, self.grid_blocks(M, tele), epoch,
                       self.host_fp64, *telemetry,
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
                       epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
-                      self.chunk_len(M, telemetry[0].numel() > 0), ctrl_ready)
+                      self.chunk_len(M, tele), ctrl_ready)
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out
@@ -305,22 +324,31 @@ class BatchRater:
     def stale_retries(self, device) -> int:
         """Granule reads of the last launch that found their predecessor's write not
         yet landed and were retried (diagnostics; syncs)."""
-        return int(self._buffer(device, "ctrl", 16, torch.int32)[14].item())
+        return int(self._ctrl(device)[14].item())
 
     def iterations(self, device) -> int:
         """Wave iterations of the last executor launch (diagnostics; syncs)."""
-        return int(self._buffer(device, "ctrl", 16, torch.int32)[15].item())
+        return int(self._ctrl(device)[15].item())
 
     def telemetry_errors(self, device) -> int:
         """Malformed telemetry events seen by the last fused launch (syncs)."""
-        return int(self._buffer(device, "ctrl", 16, torch.int32)[13].item())
+        return int(self._ctrl(device)[13].item())
 
     def error_flags(self, device) -> torch.Tensor:
         """Device tensor [schedule overflow, timeout, protocol] of the last launch (no sync)."""
-        return self._buffer(device, "ctrl", 16, torch.int32)[0:3]
+        return self._ctrl(device)[0:3]
 
-    def check_errors(self, device) -> None:
-        flags = self.error_flags(device).cpu()
+    def sticky_flags(self, device) -> torch.Tensor:
+        """Device tensor [schedule, timeout, protocol]: OR over every launch since
+        the last ``clear_sticky`` (no sync) -- a window pipeline checks this once
+        instead of after each launch, without losing a middle window's failure."""
+        return self._ctrl(device)[16:19]
+
+    def clear_sticky(self, device) -> None:
+        self._ctrl(device)[16:19].zero_()
+
+    def check_errors(self, device, sticky: bool = False) -> None:
+        flags = (self.sticky_flags(device) if sticky else self.error_flags(device)).cpu()
         if int(flags[0]):
             raise NativeRateError("schedule prepass failed (flag %d)" % int(flags[0]))
         if int(flags[1]):

@@ -53,6 +53,7 @@ class StreamSpec:
     p_afk: float = 0.02            # somebody went AFK
     p_hot: float = 0.0             # probability a slot draws from the hot set
     hot_fraction: float = 0.01     # hot set = first fraction of the roster
+    skew: int = 1                  # power-law activity: player = floor(u^skew * P) (1 = uniform)
 
     def mode_cdf(self):
         weights = [float(self.modes.get(m, 0.0)) for m in MODES]
@@ -96,5 +97,5 @@ def make_stream(spec: StreamSpec, num_matches: int, num_players: int, K: Optiona
     native().gen_stream(out, K, int(spec.seed), int(base), int(num_players), int(spec.team_size),
                         spec.mode_cdf(), prob_u32(spec.p_uneven), prob_u32(spec.p_bad_rosters),
                         prob_u32(spec.p_tie), prob_u32(spec.p_afk), prob_u32(spec.p_hot),
-                        min(hot, num_players))
+                        min(hot, num_players), int(spec.skew))
     return out

@@ -9,6 +9,8 @@ messages through RabbitMQ (/root/reference/worker.py:44-46,85-92).
 * ``broadcast_roster`` (C3) -- the initial replicated roster from one rank.
 * ``reduce_counts`` (C4) -- status counters and timings summed / maxed over ranks.
 * ``shard`` -- contiguous block partition of a range (time-axis sharding, P1/P4).
+* ``exclusive_scan`` (C1') -- per-row prefix sum over ranks (causal re-sweeps of
+  parallel/sweep.py) as two all-to-alls.
 """
 from __future__ import annotations
 
@@ -19,10 +21,65 @@ import torch
 import torch.distributed as dist
 
 
-def world() -> Tuple[int, int]:
+def world(group=None) -> Tuple[int, int]:
     if dist.is_available() and dist.is_initialized():
-        return dist.get_rank(), dist.get_world_size()
+        return dist.get_rank(group), dist.get_world_size(group)
     return 0, 1
+
+
+def _staged(t: torch.Tensor, group=None) -> bool:
+    """gloo moves host memory only: device tensors are staged through the host
+    (the 1-GPU multi-rank rehearsal; RCCL takes device tensors directly)."""
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_to_all_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """``all_to_all_single`` over equal row blocks (one per rank)."""
+    if _staged(inp, group):
+        o = torch.empty_like(out, device="cpu")
+        dist.all_to_all_single(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, group=group)
+
+
+def exclusive_scan(t: torch.Tensor, group=None) -> torch.Tensor:
+    """Row-wise exclusive prefix sum over ranks: rank r gets sum_{q<r} t_q
+    (zeros on rank 0), summed in rank order.
+
+    Two all-to-alls instead of a chain: rank b owns row block b, receives block b
+    of every rank, prefix-sums it in rank order and sends each rank its prefix
+    back.  Each rank moves 2(N-1)/N of the buffer -- an all-reduce's volume --
+    and on xGMI's full mesh every block travels its own point-to-point link, so
+    the scan costs about one all-reduce rather than log2(N) dependent hops."""
+    _, size = world(group)
+    if size <= 1:
+        return torch.zeros_like(t)
+    P = t.shape[0]
+    C = t[0].numel() if P else 1
+    blk = -(-P // size)
+    send = t.new_zeros((size * blk, C))
+    send[:P] = t.reshape(P, C)
+    recv = torch.empty_like(send)
+    all_to_all_rows(recv, send, group)  # recv block q = rank q's rows of my block
+    r3 = recv.view(size, blk, C)
+    ex = torch.zeros_like(r3)
+    if size > 1:
+        torch.cumsum(r3[:-1], 0, out=ex[1:])
+    back = torch.empty_like(send)
+    all_to_all_rows(back, ex.view(size * blk, C), group)  # block b = my prefix of block b
+    return back[:P].view_as(t)
+
+
+def all_reduce_sum(t: torch.Tensor, group=None, async_op: bool = False):
+    """SUM all-reduce in place; gloo + device tensor goes through the host.
+    Returns a work handle (``async_op``) or None."""
+    if _staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        t.copy_(h)
+        return None
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
 
 
 def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, torch.device]:

@@ -5,21 +5,37 @@ replication is the right call on 288 GB devices), rates its shard of every
 window exactly and in order, and then all ranks merge what they learned with
 ONE dense all-reduce of natural-parameter messages (csrc/sweep.hip):
 
-    begin(roster)   -> snapshot the window-start roster
+    begin(roster)   -> the common window start (kept by the last merge: no copy)
     <rate the local shard exactly>
-    merge(roster)   -> messages against a common base -> all_reduce(SUM) over
-                       RCCL/xGMI -> apply (csrc/sweep_core.h)
+    merge(roster)   -> messages against the start -> all_reduce(SUM) over
+                       RCCL/xGMI -> decode into the roster AND the next start
 
 ``merge`` runs the three stages bucketed over player rows and pipelined: the
 all-reduce of bucket b (asynchronous, on the collective's own stream) runs
-while the main stream computes the messages of bucket b+1 and applies bucket
+while the main stream computes the messages of bucket b+1 and decodes bucket
 b-1, so on xGMI only the first bucket's message kernel and the last bucket's
-apply stay exposed.  Buckets default to 64 MB of messages (ANA_MERGE_BUCKET_MB;
-0 = one bucket): a 1M-player roster (64 MB) stays one all-reduce, whose ring
-keeps every link at full bandwidth and whose two kernels (~40 us each) are not
-worth smaller, slower messages; a 10M-player re-rate roster (640 MB) becomes ten
-64-MB reduces that hide ~0.8 ms of message/apply kernels.  Every stage is
-per player, so bucketing is exact.
+decode stay exposed.  Buckets default to 64 MB of messages (ANA_MERGE_BUCKET_MB;
+0 = one bucket): a 1M-player roster (64 MB) stays one all-reduce; a 10M-player
+re-rate roster (640 MB) becomes ten 64-MB reduces that hide the kernels.
+Every stage is per player, so bucketing is exact.
+
+**Causal re-sweeps (``sweeps`` > 1).**  Rank r's shard is the r-th time slice
+of the global window (bench.py, runtime/rerate.py), so under the reference's
+exact semantics (ORDER BY created_at + a sequential loop,
+/root/reference/worker.py:176,191-192) rank r's matches must see the
+posteriors of ranks 0..r-1.  One sweep rates every shard from the window start
+(the approximation).  A re-sweep re-rates shard r from
+
+    prior_r = start + sum_{q<r} message_q      (exclusive prefix over ranks,
+                                                 comm.exclusive_scan)
+
+and measures the new message from that prior (sweep_core.h), so the prefix
+telescopes: after sweep s, ranks 0..s-1 hold their exact posteriors, and
+``sweeps == world`` reproduces the sequential result up to fp32 rounding of the
+natural-parameter round trip.  ``parallel/accuracy.py`` measures the error per
+sweep count.  This is deliberately a prefix, not the EP cavity (merged / own
+message): the cavity would feed later ranks' evidence into earlier matches,
+which converges to a smoother, not to the reference's filter.
 
 With one rank the merge is skipped (the exact single-GPU result stands).
 Backend: ``nccl`` (RCCL on ROCm) for device tensors, ``gloo`` for CPU tests.
@@ -28,9 +44,8 @@ replicas racing on MySQL rows (/root/reference/worker.py:91,174-194).
 """
 from __future__ import annotations
 
-from typing import Optional
-
 import os
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -38,6 +53,7 @@ import torch.distributed as dist
 from ..config import RaterConfig
 from ..models.tiers import vst_table
 from ..ops.native import native
+from .comm import all_reduce_sum, exclusive_scan, world
 
 MAX_RANKS = 15  # touch counts are base-16 fields in fp32 (see csrc/sweep_core.h)
 COMM_DTYPES = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
@@ -45,24 +61,28 @@ COMM_DTYPES = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloa
 
 class SweepMerger:
     def __init__(self, num_players: int, device, cfg: Optional[RaterConfig] = None,
-                 group=None, comm_dtype: str = "fp32", bucket_rows: Optional[int] = None):
+                 group=None, comm_dtype: str = "fp32", bucket_rows: Optional[int] = None,
+                 sweeps: int = 1, world_size: Optional[int] = None):
         self.P = int(num_players)
         self.device = torch.device(device)
         self.cfg = cfg or RaterConfig.from_env()
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.world = int(world_size) if world_size is not None else world(group)[1]
         if self.world > MAX_RANKS:
             raise ValueError("sweep merge supports at most %d ranks per group" % MAX_RANKS)
         if comm_dtype not in COMM_DTYPES:
             raise ValueError("comm_dtype must be one of %s" % sorted(COMM_DTYPES))
+        self.sweeps = max(1, int(sweeps))
         # fp16/bf16: messages use the base-relative encoding (sweep_core.h) and
         # travel compressed; the touch counters travel separately as int32
         self.comm_dtype = comm_dtype
         self.scaled = comm_dtype != "fp32"
         f = dict(dtype=torch.float32, device=self.device)
-        self.start = torch.empty((self.P, 32), **f)
+        self.start = torch.empty((self.P, 32), **f)   # common window start
+        self.prior = None                            # this rank's prior (re-sweeps only)
         self.buf = torch.empty((self.P, 16), **f)
         self.vst = torch.tensor(vst_table(), **f)
+        self._none = torch.empty(0, **f)
         self.comm_bytes = self.P * (16 * 4 if not self.scaled else
                                     14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4)
         if bucket_rows is None:
@@ -70,37 +90,77 @@ class SweepMerger:
             bucket_rows = int(mb * (1 << 20)) // (16 * 4) if mb > 0 else self.P
         self.bucket_rows = max(1, min(int(bucket_rows), max(self.P, 1)))
         self.windows = 0
+        self._synced = False   # start == the roster as the last merge left it
+        self._sweep = 0        # sweeps rated in the current window
+        self.timing = False    # record per-stage CUDA events (profile())
+        self._events: List[tuple] = []
 
+    # ----------------------------------------------------------- stages
     def buckets(self):
         """Row ranges [lo, hi) of the pipelined merge."""
         return [(lo, min(lo + self.bucket_rows, self.P)) for lo in range(0, self.P, self.bucket_rows)]
 
     def begin(self, roster) -> None:
-        self.start.copy_(roster.state)
+        """Start a window.  The common start is the roster the last merge wrote
+        (the merge decodes into both), so only the first window -- or one after
+        ``invalidate()`` -- copies it."""
+        if not self._synced:
+            self.start.copy_(roster.state)
+            self._synced = True
+        self._sweep = 0
+
+    def invalidate(self) -> None:
+        """The roster was changed outside the merger: re-snapshot at the next begin."""
+        self._synced = False
 
     def messages(self, roster, lo: int = 0, hi: Optional[int] = None) -> torch.Tensor:
+        """Messages of rows [lo, hi): posterior (roster) against this sweep's prior."""
         hi = self.P if hi is None else hi
-        native().sweep_delta(self.start[lo:hi], roster.state[lo:hi], roster.attrs[lo:hi], self.vst,
-                             float(self.cfg.unknown_player_sigma), self.scaled, self.buf[lo:hi])
+        prior = self.start if self._sweep <= 1 or self.prior is None else self.prior
+        native().sweep_delta(self.start[lo:hi], prior[lo:hi], roster.state[lo:hi], roster.attrs[lo:hi],
+                             self.vst, float(self.cfg.unknown_player_sigma), self.scaled, self.buf[lo:hi])
         return self.buf
+
+    def decode(self, roster, lo: int = 0, hi: Optional[int] = None, into=None) -> None:
+        """roster.state[lo:hi] (and ``into``[lo:hi]) := start + summed messages in buf."""
+        hi = self.P if hi is None else hi
+        s2 = into[lo:hi] if into is not None else self._none
+        native().sweep_apply(self.start[lo:hi], self.buf[lo:hi], roster.attrs[lo:hi],
+                             roster.state[lo:hi], s2, self.vst, float(self.cfg.unknown_player_sigma),
+                             self.scaled)
+        roster.epoch = roster.epoch if roster.epoch is not None else 0  # decode wrote tag 0
+
+    # legacy name: decode the all-reduced messages into the roster only
+    def apply(self, roster, lo: int = 0, hi: Optional[int] = None) -> None:
+        self.decode(roster, lo, hi)
+
+    def rated(self) -> None:
+        """The local shard was rated once more (the engine calls this after each sweep)."""
+        self._sweep += 1
+
+    # ------------------------------------------------------ collectives
+    def _split(self, buf):
+        if not self.scaled:
+            return [buf]
+        return [buf[:, :14].to(COMM_DTYPES[self.comm_dtype]), buf[:, 14:].to(torch.int32)]
+
+    def _join(self, buf, parts) -> None:
+        if self.scaled:
+            buf[:, :14].copy_(parts[0])
+            buf[:, 14:].copy_(parts[1])
 
     def _launch_reduce(self, lo: int, hi: int):
         """Start the all-reduce of rows [lo, hi); returns a finisher that waits
         for it (stream-ordered, the host does not block on RCCL) and unpacks."""
         buf = self.buf[lo:hi]
-        if not self.scaled:
-            work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            return work.wait
-        msg = buf[:, :14].to(COMM_DTYPES[self.comm_dtype])
-        touch = buf[:, 14:].to(torch.int32)
-        w_msg = dist.all_reduce(msg, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-        w_touch = dist.all_reduce(touch, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        parts = self._split(buf)
+        works = [all_reduce_sum(t, group=self.group, async_op=True) for t in parts]
 
         def finish():
-            w_msg.wait()
-            w_touch.wait()
-            buf[:, :14].copy_(msg)
-            buf[:, 14:].copy_(touch)
+            for w in works:
+                if w is not None:
+                    w.wait()
+            self._join(buf, parts)
         return finish
 
     def reduce(self, lo: int = 0, hi: Optional[int] = None) -> None:
@@ -108,38 +168,94 @@ class SweepMerger:
             return
         self._launch_reduce(lo, self.P if hi is None else hi)()
 
-    def apply(self, roster, lo: int = 0, hi: Optional[int] = None) -> None:
-        hi = self.P if hi is None else hi
-        native().sweep_apply(self.start[lo:hi], self.buf[lo:hi], roster.attrs[lo:hi],
-                             roster.state[lo:hi], self.vst, float(self.cfg.unknown_player_sigma),
-                             self.scaled)
-        roster.epoch = roster.epoch if roster.epoch is not None else 0  # apply wrote tag 0
+    def scan(self) -> None:
+        """buf := sum of the messages of the ranks before this one (exclusive prefix)."""
+        parts = [exclusive_scan(t, group=self.group) for t in self._split(self.buf)]
+        if self.scaled:
+            self._join(self.buf, parts)
+        else:
+            self.buf.copy_(parts[0])
+
+    # ------------------------------------------------------------ drivers
+    def needs_resweep(self) -> bool:
+        return self.world > 1 and self._sweep < self.sweeps
+
+    def resweep(self, roster) -> None:
+        """Between sweeps: roster := this rank's causal prior (start + messages of
+        the earlier ranks), kept in ``prior`` to measure the next message from."""
+        if self.prior is None:
+            self.prior = torch.empty_like(self.start)
+        self.messages(roster)
+        self.scan()
+        self.decode(roster, into=self.prior)
+
+    def _ev(self, name):
+        if self.timing and self.device.type == "cuda":
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._events.append((name, e))
 
     def merge(self, roster) -> None:
         """Combine every rank's window into the replicated roster (in place):
-        messages -> all-reduce -> apply, pipelined over row buckets."""
+        messages -> all-reduce -> decode, pipelined over row buckets; the decode
+        also writes the next window's common start."""
         if self.world <= 1:
             self.windows += 1
             return
         pending = None  # (lo, hi, finisher) of the bucket whose reduce is in flight
+        self._ev("begin")
         for lo, hi in self.buckets():
             self.messages(roster, lo, hi)
+            self._ev("messages")
             fin = self._launch_reduce(lo, hi)
             if pending is not None:
                 plo, phi, pfin = pending
                 pfin()
-                self.apply(roster, plo, phi)
+                self._ev("allreduce")
+                self.decode(roster, plo, phi, into=self.start)
+                self._ev("apply")
             pending = (lo, hi, fin)
         if pending is not None:
             plo, phi, pfin = pending
             pfin()
-            self.apply(roster, plo, phi)
+            self._ev("allreduce")
+            self.decode(roster, plo, phi, into=self.start)
+            self._ev("apply")
+        self._synced = True
         self.windows += 1
 
+    def stage_ms(self) -> Dict[str, float]:
+        """Per-stage main-stream time of the recorded merges (syncs; ``timing``):
+        each event's time since the previous one, summed by stage name."""
+        if not self._events:
+            return {}
+        torch.cuda.synchronize(self.device)
+        out: Dict[str, float] = {}
+        prev = None
+        for name, e in self._events:
+            if name != "begin" and prev is not None:
+                out[name] = out.get(name, 0.0) + prev.elapsed_time(e)
+            prev = e
+        self._events.clear()
+        return out
 
-def rate_window_dp(rater, merger: SweepMerger, roster, rec, K=None, out=None, check=True):
-    """One DP step: exact local rating of this rank's shard + posterior merge."""
+
+def rate_window_dp(rater, merger: SweepMerger, roster, rec, K=None, out=None, check=True,
+                   schedule=None):
+    """One DP step: exact local rating of this rank's shard (``merger.sweeps``
+    causal sweeps) + posterior merge."""
     merger.begin(roster)
-    res = rater.rate(roster, rec, K, out=out, check=check)
+    K = int(K or (rec.shape[1] - 2) // 2)
+    if schedule is None and rec.is_cuda and merger.sweeps > 1:
+        schedule = rater.schedule(rec, K, roster.num_players, tag="_dp")
+    while True:
+        res = rater.rate(roster, rec, K, out=out, check=check, schedule=schedule)
+        merger.rated()
+        if not merger.needs_resweep():
+            break
+        merger.resweep(roster)
+        if schedule is not None:
+            schedule.deps.zero_()  # the executor counted them up; links are reusable
+        out = res
     merger.merge(roster)
     return res

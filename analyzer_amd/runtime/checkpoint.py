@@ -9,7 +9,9 @@ source) checkpoints
     roster state + attributes (safetensors) + {next window, stream offset,
     stream/roster specs, epoch, metrics} (JSON)
 
-atomically (write to a temp name, fsync, rename).  Resuming loads the roster and
+atomically (write to a temp name, fsync, rename, fsync the parent).  A crash
+between the two renames of a replacement leaves only ``<name>.old``, which
+``CheckpointManager.latest`` falls back to.  Resuming loads the roster and
 replays from the recorded offset, so the result is bit-identical to an
 uninterrupted run: exactly-once rating by construction.
 """
@@ -29,6 +31,14 @@ META = "meta.json"
 TENSORS = "roster.safetensors"
 
 
+def _fsync_dir(path: str) -> None:
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
 def _atomic_dir_write(final: str, writer) -> None:
     parent = os.path.dirname(os.path.abspath(final)) or "."
     os.makedirs(parent, exist_ok=True)
@@ -37,15 +47,19 @@ def _atomic_dir_write(final: str, writer) -> None:
     for name in os.listdir(tmp):
         with open(os.path.join(tmp, name), "rb") as f:
             os.fsync(f.fileno())
+    _fsync_dir(tmp)
     if os.path.exists(final):
         old = final + ".old"
         if os.path.exists(old):
             _rmtree(old)
         os.replace(final, old)
+        _fsync_dir(parent)       # from here on, a crash leaves only <final>.old
         os.replace(tmp, final)
+        _fsync_dir(parent)
         _rmtree(old)
     else:
         os.replace(tmp, final)
+        _fsync_dir(parent)
 
 
 def _rmtree(path: str) -> None:
@@ -103,7 +117,12 @@ class CheckpointManager:
         return True
 
     def latest(self, device="cpu") -> Optional[Tuple[Roster, Dict[str, Any]]]:
+        """The newest complete checkpoint: ``latest``, or ``latest.old`` when a
+        crash hit between the renames of a replacement."""
         p = self.path
-        if p and os.path.exists(os.path.join(p, META)):
-            return load(p, device)
+        if not p:
+            return None
+        for cand in (p, p + ".old"):
+            if os.path.exists(os.path.join(cand, META)) and os.path.exists(os.path.join(cand, TENSORS)):
+                return load(cand, device)
         return None

@@ -127,12 +127,24 @@ class WindowPipeline:
         if self._signal:
             self._seq += 1
             M = int(prep.rec.shape[0])
-            cl = self.rater.chunk_len(M, telemetry is not None)
+            cl = self.rater.chunk_len(M, self.rater.has_telemetry(telemetry))
             at = int(self.tail * ((M + cl - 1) // cl))
             progress = (self._signal, self._seq, at)
         with trace_range("rate", window=self.windows_rated, matches=int(prep.rec.shape[0])):
             res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
                                   schedule=prep.schedule, telemetry=telemetry, progress=progress)
+        if self.merger is not None:
+            # causal re-sweeps (parallel/sweep.py): re-rate from the prefix of the
+            # earlier ranks' messages, reusing the links (only the counters reset)
+            self.merger.rated()
+            while self.merger.needs_resweep():
+                with trace_range("resweep", window=self.windows_rated):
+                    self.merger.resweep(self.roster)
+                    if prep.schedule is not None:
+                        prep.schedule.deps.zero_()
+                    res = self.rater.rate(self.roster, prep.rec, self.K, out=res, check=check,
+                                          schedule=prep.schedule)
+                self.merger.rated()
         if self.cuda:
             done = torch.cuda.Event()
             done.record(main)

@@ -80,56 +80,92 @@ class FileSource:
 
 
 class OutputSink:
-    """Asynchronous D2H of per-window results into pinned host memory."""
+    """Asynchronous D2H of per-window results into a ring of pinned host buffers.
+
+    ``push(base, res)`` enqueues the copy of ``res`` on a copy stream behind
+    everything already on the main stream and returns at once;
+    ``on_ready(base, host)`` runs (on the host, from ``push``/``poll``/``flush``)
+    once that copy has landed, with views into the pinned slot that stay valid
+    until the callback returns.  ``copied(res)`` is the event to make the main
+    stream wait on before it overwrites ``res`` (double-buffered outputs).
+    Pinned slots are allocated once (``slots`` of them, grown to the largest
+    window) and recycled: pinning a 2-GB window per push would cost more than
+    the copy."""
 
     FIELDS = ("quality", "status", "s_mu", "s_sig", "delta", "m_mu", "m_sig")
 
-    def __init__(self, device, on_ready: Callable[[int, dict], None]):
+    def __init__(self, device, on_ready: Callable[[int, dict], None], slots: int = 2):
         self.device = torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.on_ready = on_ready
         self.copy_stream = torch.cuda.Stream(self.device) if self.cuda else None
-        self._pending: Deque[Tuple[int, dict, Optional[torch.cuda.Event]]] = collections.deque()
+        self._slots = [None] * max(1, int(slots))
+        self._next = 0
+        self._pending: Deque[Tuple[int, dict, Optional[torch.cuda.Event], int]] = collections.deque()
+        self._copied = {}
+        self.bytes = 0
+
+    def _slot(self, i: int, shape, dtype) -> torch.Tensor:
+        buf = self._slots[i]
+        n = 1
+        for d in shape:
+            n *= int(d)
+        if buf is None or buf.numel() < n or buf.dtype != dtype:
+            buf = torch.empty(n, dtype=dtype, pin_memory=True)
+            self._slots[i] = buf
+        return buf[:n].view(shape)
 
     def push(self, base: int, res: RateResult) -> None:
         if not self.cuda:
             self.on_ready(base, {f: getattr(res, f).clone() for f in self.FIELDS})
             return
+        # the ring slot we are about to reuse must have been delivered
+        while len(self._pending) >= len(self._slots):
+            self.poll(block=True, limit=1)
+        i = self._next
+        self._next = (self._next + 1) % len(self._slots)
         main = torch.cuda.current_stream(self.device)
         done = torch.cuda.Event()
         done.record(main)
-        host = {}
         with torch.cuda.stream(self.copy_stream):
             self.copy_stream.wait_event(done)
             if res.packed is not None:  # one DMA of the packed rows, host views rebuilt
-                buf = torch.empty(res.packed.shape, dtype=torch.float32, pin_memory=True)
+                buf = self._slot(i, res.packed.shape, torch.float32)
                 buf.copy_(res.packed, non_blocking=True)
-                res.packed.record_stream(self.copy_stream)
                 S = res.s_mu.shape[1]
                 host = {"quality": buf[:, 5 * S], "status": buf.view(torch.uint8)[:, 4 * (5 * S + 1)]}
-                for i, f in enumerate(("s_mu", "s_sig", "delta", "m_mu", "m_sig")):
-                    host[f] = buf[:, i * S:(i + 1) * S]
+                for k, f in enumerate(("s_mu", "s_sig", "delta", "m_mu", "m_sig")):
+                    host[f] = buf[:, k * S:(k + 1) * S]
+                self.bytes += res.packed.numel() * 4
             else:
+                host = {}
                 for f in self.FIELDS:
                     src = getattr(res, f)
                     dst = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
                     dst.copy_(src, non_blocking=True)
-                    src.record_stream(self.copy_stream)
                     host[f] = dst
+                    self.bytes += src.numel() * src.element_size()
             ev = torch.cuda.Event()
             ev.record(self.copy_stream)
-        self._pending.append((base, host, ev))
+        self._copied[id(res.packed if res.packed is not None else res.s_mu)] = ev
+        self._pending.append((base, host, ev, i))
         self.poll()
 
-    def poll(self, block: bool = False) -> None:
-        while self._pending:
-            base, host, ev = self._pending[0]
+    def copied(self, res: RateResult) -> Optional[torch.cuda.Event]:
+        """Event after which ``res`` may be overwritten (None: never pushed)."""
+        return self._copied.get(id(res.packed if res.packed is not None else res.s_mu))
+
+    def poll(self, block: bool = False, limit: Optional[int] = None) -> None:
+        n = 0
+        while self._pending and (limit is None or n < limit):
+            base, host, ev, _ = self._pending[0]
             if not block and ev is not None and not ev.query():
                 return
             if ev is not None:
                 ev.synchronize()
             self.on_ready(base, host)
             self._pending.popleft()
+            n += 1
 
     def flush(self) -> None:
         self.poll(block=True)

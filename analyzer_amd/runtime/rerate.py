@@ -16,7 +16,16 @@ streams a long synthetic history through the engine window by window:
 * every ``checkpoint_every`` windows the replicated roster and the stream
   position are checkpointed atomically; a restarted run resumes from there and
   produces the same roster as an uninterrupted run (exactly-once);
-* status counters are accumulated on the device and reduced over ranks (C4).
+* every window's per-participant output records (the reference writes them per
+  match, /root/reference/rater.py:151-169, committed per batch at
+  worker.py:194) are accounted for: ``records="digest"`` reduces them on the
+  device to a count + fp64 column sums per window (a resumed run reproduces the
+  digests of the windows it re-rates); ``records="host"`` streams them D2H into
+  a ring of pinned buffers on a copy stream, overlapped with the next windows
+  (double-buffered device outputs), and hands them to ``on_records``;
+* status counters are accumulated on the device and reduced over ranks (C4);
+  the executor's error flags are sticky over windows and checked before every
+  checkpoint, so a failed middle window is never checkpointed over.
 
     python -m analyzer_amd.runtime.rerate --matches 1000000000 --players 10000000 \\
         --window 16000000 --team-size 3 --checkpoint-dir /tmp/ck
@@ -41,6 +50,7 @@ from ..parallel.sweep import SweepMerger
 from ..utils.trace import trace_range
 from .checkpoint import CheckpointManager
 from .engine import WindowPipeline
+from .ingest import OutputSink
 
 
 class InjectedFault(SystemExit):
@@ -76,11 +86,34 @@ def window_slice(spec: RerateSpec, g: int, rank: int, size: int):
     return lo, max(lo, hi)
 
 
+def window_digest(res: R.RateResult) -> torch.Tensor:
+    """[2 + 5*2K + 1] fp64 on the device: matches with records (rated / AFK /
+    invalid), participant records written (non-NULL shared mu), then the column
+    sums of the five per-slot outputs and quality over written values."""
+    S = res.s_mu.shape[1]
+    st = res.status
+    wrote = (st == R.RATED) | (st == R.AFK) | (st == R.INVALID_ROSTERS)
+    parts = [wrote.sum().to(torch.float64).view(1),
+             (~torch.isnan(res.s_mu)).sum().to(torch.float64).view(1)]
+    for t in (res.s_mu, res.s_sig, res.delta, res.m_mu, res.m_sig):
+        parts.append(torch.nansum(t, dim=0, dtype=torch.float64).view(S))
+    parts.append(torch.nansum(res.quality, dtype=torch.float64).view(1))
+    return torch.cat(parts)
+
+
 def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
         checkpoint_every: int = 1, fault_kill_after: Optional[int] = None,
         on_window: Optional[Callable[[int, R.RateResult], None]] = None,
-        rater: Optional[R.BatchRater] = None, comm_dtype: str = "fp32"):
-    """Rate the whole history; returns (metrics reduced over ranks, final roster)."""
+        rater: Optional[R.BatchRater] = None, comm_dtype: str = "fp32",
+        records: str = "digest", on_records: Optional[Callable[[int, dict], None]] = None,
+        sweeps: int = 1):
+    """Rate the whole history; returns (metrics reduced over ranks, final roster).
+
+    ``records``: "digest" (device reduction per window, in the metrics as
+    ``window_digests``), "host" (pinned D2H ring; ``on_records(base, host_dict)``
+    gets every window's rows) or "none"."""
+    if records not in ("digest", "host", "none"):
+        raise ValueError("records must be digest, host or none")
     rank, size = world()
     dev = torch.device(device) if device is not None else (
         torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
@@ -97,12 +130,25 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
     else:
         roster = make_roster(spec.roster_spec(), device=dev)
         broadcast_roster(roster)  # C3 (identical by construction; keeps replicas honest)
-    merger = SweepMerger(spec.players, dev, rater.cfg, comm_dtype=comm_dtype) if size > 1 else None
+    merger = (SweepMerger(spec.players, dev, rater.cfg, comm_dtype=comm_dtype, sweeps=sweeps)
+              if size > 1 else None)
     pipe = WindowPipeline(rater, roster, K, merger=merger)
     total = n_windows(spec, size)
     counts = torch.zeros(256, dtype=torch.int64, device=dev)
+    digests = {}
     sspec = spec.stream_spec()
-    out = None
+    outs = [None, None]  # double-buffered: the sink copies one while the next is rated
+    host_stats = {"windows": 0, "participant_records": 0}
+
+    def took(base, host):
+        host_stats["windows"] += 1
+        host_stats["participant_records"] += int((~torch.isnan(host["s_mu"])).sum())
+        if on_records is not None:
+            on_records(base, host)
+
+    sink = OutputSink(dev, took) if records == "host" else None
+    if dev.type == "cuda":
+        rater.clear_sticky(dev)
 
     def window_rec(g):
         lo, hi = window_slice(spec, g, rank, size)
@@ -114,34 +160,56 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
     for g in range(start_window, total):
         cur = nxt
         M = cur.rec.shape[0]
-        if out is None or out.quality.shape[0] != M:
-            out = R.RateResult.allocate(M, K, dev)
+        b = g & 1
+        if outs[b] is None or outs[b].quality.shape[0] != M:
+            outs[b] = R.RateResult.allocate(M, K, dev)
+        elif sink is not None and sink.copied(outs[b]) is not None:
+            torch.cuda.current_stream(dev).wait_event(sink.copied(outs[b]))
         # window g+1 is generated before rate(g) is enqueued; its prepass waits for the tail
-        res, nxt = pipe.step(cur, window_rec(g + 1) if g + 1 < total else None, out=out)
+        res, nxt = pipe.step(cur, window_rec(g + 1) if g + 1 < total else None, out=outs[b])
         counts += torch.bincount(res.status.to(torch.int64), minlength=256)
+        if records == "digest":
+            digests[g] = window_digest(res)
+        elif sink is not None:
+            sink.push(window_slice(spec, g, rank, size)[0], res)
         rated += M
         if on_window is not None:
             on_window(g, res)
-        if rank == 0 and ck.due(g + 1):
-            with trace_range("checkpoint", window=g + 1):
-                ck.maybe_save(g + 1, roster, {"spec": asdict(spec), "world": size,
-                                              "next_offset": window_slice(spec, g + 1, 0, size)[0]})
+        if ck.due(g + 1):
+            if dev.type == "cuda":  # never checkpoint over a failed window
+                rater.check_errors(dev, sticky=True)
+            if rank == 0:
+                with trace_range("checkpoint", window=g + 1):
+                    ck.maybe_save(g + 1, roster, {"spec": asdict(spec), "world": size,
+                                                  "next_offset": window_slice(spec, g + 1, 0, size)[0]})
         if fault_kill_after is not None and g + 1 >= fault_kill_after:
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             raise InjectedFault(17)
+    if sink is not None:
+        sink.flush()
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    rater.check_errors(dev) if dev.type == "cuda" else None
+    if dev.type == "cuda":
+        rater.check_errors(dev, sticky=True)
     c = counts.cpu()
     local = {R.STATUS_NAMES.get(i, str(i)): float(c[i]) for i in range(256) if int(c[i])}
     local["matches"] = float(rated)
+    if records == "digest" and digests:
+        d = torch.stack([digests[g] for g in sorted(digests)]).cpu()
+        local["match_records"] = float(d[:, 0].sum())
+        local["participant_records"] = float(d[:, 1].sum())
+    elif records == "host":
+        local["participant_records"] = float(host_stats["participant_records"])
+        local["egress_bytes"] = float(sink.bytes)
     summed = reduce_counts(local, dev)
     summed["seconds"] = reduce_counts({"seconds": dt}, dev, op="max")["seconds"]
     summed["windows"] = float(total - start_window)
     summed["resumed_from_window"] = float(start_window)
     summed["matches_per_s"] = summed["matches"] / summed["seconds"] if summed["seconds"] > 0 else 0.0
+    if records == "digest":
+        summed["window_digests"] = {g: digests[g].cpu().tolist() for g in sorted(digests)}
     return summed, roster
 
 
@@ -159,13 +227,32 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default=None)
     ap.add_argument("--comm-dtype", default=os.environ.get("COMM_DTYPE") or "fp32",
                     choices=["fp32", "fp16", "bf16"], help="sweep-merge message precision")
+    ap.add_argument("--records", default="digest", choices=["digest", "host", "none"],
+                    help="output records: device digest per window, pinned D2H stream, or dropped")
+    ap.add_argument("--sweeps", type=int, default=1, help="causal sweeps per window (N ranks)")
+    ap.add_argument("--digests", action="store_true", help="print every window's digest")
     args = ap.parse_args(argv)
     rank, size, dev = init_from_env()
     spec = RerateSpec(total_matches=int(args.matches), players=int(args.players),
                       team_size=args.team_size, window=int(args.window), seed=args.seed)
-    res, _ = run(spec, args.device or dev, args.checkpoint_dir, args.checkpoint_every,
-                 args.fault_kill_after, comm_dtype=args.comm_dtype)
+    try:
+        res, roster = run(spec, args.device or dev, args.checkpoint_dir, args.checkpoint_every,
+                          args.fault_kill_after, comm_dtype=args.comm_dtype, records=args.records,
+                          sweeps=args.sweeps)
+    except InjectedFault:
+        if rank == 0:
+            print(json.dumps({"fault_injected_after_windows": args.fault_kill_after}), flush=True)
+        raise
     if rank == 0:
+        digs = res.pop("window_digests", None)
+        if digs is not None and not args.digests:  # a compact fingerprint instead of every window
+            res["digest_fingerprint"] = float(sum(sum(v) for v in digs.values()))
+        elif digs is not None:
+            res["window_digests"] = digs
+        import hashlib  # bit-exact: sha256 of every (mu, sigma) of the final roster
+
+        res["roster_sha256"] = hashlib.sha256(
+            roster.state[:, 0::2].contiguous().cpu().numpy().tobytes()).hexdigest()
         print(json.dumps(dict(res, n_ranks=size, spec=asdict(spec))), flush=True)
     return 0
 

@@ -35,6 +35,10 @@ Deliberate, documented differences:
   into ``participant_stats`` in the same launch as the rating (K8 fused mode,
   BASELINE config 4).  Telemetry is synthetic here: the reference only forwards
   asset URLs (worker.py:148-161) and this image has no network to fetch them.
+  Synthetic stats are therefore never persisted into a real database: with a
+  ``DATABASE_URI`` other than the in-process ``memory://`` store, ``connect``
+  refuses ``DOTELEMETRY`` unless ``SYNTHETIC_TELEMETRY=true`` says the run is a
+  benchmark.
 
 Per-batch counters (matches rated/afk/invalid/unsupported/quarantined, timing)
 are kept in ``stats`` and logged as one JSON line per batch (SURVEY §5 metrics).
@@ -95,6 +99,12 @@ class Worker:
 
     # ------------------------------------------------------------ connect (W3/W4)
     def connect(self) -> "Worker":
+        if self.cfg.dotelemetry and not self.cfg.synthetic_telemetry:
+            uri = self.cfg.database_uri or ""
+            if uri and not uri.startswith("memory:"):
+                raise ValueError("DOTELEMETRY aggregates SYNTHETIC telemetry (no real event source "
+                                 "exists yet): refusing to write it into %s; set "
+                                 "SYNTHETIC_TELEMETRY=true for a benchmark run" % uri)
         if self.store is None:
             self.store = open_store(self.cfg.database_uri)
         if self.rabbit is None:

@@ -12,6 +12,12 @@ config 3 / north star).  Weak scaling: per-GPU work is fixed as N grows.
     python bench.py --gpus N --steps K --warmup W
     torchrun --nproc-per-node N bench.py --gpus N ...   (driver launches N>1)
 
+``python bench.py --gpus N`` (N > 1) without a torchrun environment starts its
+own N ranks: child processes, one per GPU, before this process touches the
+GPU; rank 0 prints the JSON line and the exit status is the worst child's.
+``ANA_DIST_BACKEND=gloo`` rehearses N ranks on fewer GPUs (ranks share
+devices; the merge goes through the host).
+
 Synthetic data: roster and streams come from the on-device counter RNG
 (random-init ratings), generated before the timed region like a prefetched
 data loader; the timed region contains all rating work of every step.
@@ -21,6 +27,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,7 +44,8 @@ BASELINE_5V5_MATCHES_PER_S = 2112.0
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (default: WORLD_SIZE, else 1); N > 1 without torchrun spawns N ranks")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--players", type=int, default=1_000_000)
@@ -45,11 +54,17 @@ def parse(argv=None):
     ap.add_argument("--ring", type=int, default=4, help="distinct pre-generated windows per rank")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--check", action="store_true", help="also validate statuses after timing")
+    ap.add_argument("--verify", action="store_true",
+                    help="after timing, rate window 0 again on the device and on the fp64 host "
+                         "mirror and report the deviations (ops/verify.py) in the JSON line")
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5],
                     help="BASELINE config: 2 = 10M 3v3/GPU (headline), 3 = 12.5M 5v5/GPU (100M at DP=8), "
                          "4 = streaming: rating + per-event telemetry aggregation, "
                          "5 = full-history re-rate windows: 16M 3v3/GPU over a 10M-player roster, "
                          "fp16 merge messages")
+    ap.add_argument("--skew", type=int, default=1,
+                    help="player activity: floor(u^skew * P); 1 = uniform (headline), 2 = quadratic, "
+                         "3 = cubic (SURVEY H1: ~585k dependency levels per 10M window)")
     ap.add_argument("--events", default="20,60", help="config 4: min,max telemetry events per match")
     ap.add_argument("--telemetry-mode", default="separate", choices=["overlap", "fused", "separate"],
                     help="config 4: overlap = the MFMA aggregation kernel co-runs with the rating "
@@ -57,6 +72,9 @@ def parse(argv=None):
                          "time; separate = aggregation after the rating on the same stream")
     ap.add_argument("--comm-dtype", default=os.environ.get("COMM_DTYPE") or "fp32",
                     choices=["fp32", "fp16", "bf16"], help="sweep-merge message precision (N > 1)")
+    ap.add_argument("--sweeps", type=int, default=int(os.environ.get("SWEEPS", "1")),
+                    help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
+                         "N = exact sequential semantics (parallel/sweep.py)")
     args = ap.parse_args(argv)
     if args.config == 3:
         args.team_size = 5
@@ -75,14 +93,58 @@ def parse(argv=None):
     return args
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start ``n`` ranks of this benchmark as child processes (torchrun's
+    environment contract, rendezvous on 127.0.0.1).  Nothing here touches the
+    GPU: each child initialises its own device.  Returns the worst exit code."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        failed = [c for c in codes if c not in (None, 0)]
+        if failed:  # one rank died: the others would hang in a collective
+            time.sleep(5)
+            for i, p in enumerate(procs):
+                if p.poll() is None:
+                    p.kill()
+                codes[i] = p.wait()
+            break
+        time.sleep(0.2)
+    bad = [c for c in codes if c != 0]
+    if bad:
+        print("bench: rank exit codes %s" % codes, file=sys.stderr)
+        return max(abs(c) for c in bad) or 1
+    return 0
+
+
 def main(argv=None) -> int:
-    args = parse(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    raw = list(sys.argv[1:] if argv is None else argv)
+    args = parse(raw)
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.gpus is None:
+        args.gpus = int(env_world or 1)
+    if args.gpus > 1 and env_world is None:
+        return spawn_ranks(args.gpus, raw)
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print("warning: --gpus %d but WORLD_SIZE=%d; using WORLD_SIZE" % (args.gpus, world),
-              file=sys.stderr)
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     # one rank per GPU; ANA_DIST_BACKEND=gloo lets several ranks share one GPU to
     # rehearse the multi-process path on a 1-GPU box (production: nccl = RCCL)
     backend = os.environ.get("ANA_DIST_BACKEND", "nccl")
@@ -95,6 +157,7 @@ def main(argv=None) -> int:
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
     from analyzer_amd.ops.rate import BatchRater, RateResult, NOT_PROCESSED
     from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
@@ -103,7 +166,7 @@ def main(argv=None) -> int:
 
     P, M, K = args.players, args.matches_per_gpu, args.team_size
     roster = make_roster(RosterSpec(num_players=P, seed=args.seed), device=dev)
-    spec = StreamSpec(team_size=K, seed=args.seed + 1)
+    spec = StreamSpec(team_size=K, seed=args.seed + 1, skew=args.skew)
     n_windows = max(1, min(args.ring, args.steps + args.warmup))
     total_windows = args.steps + args.warmup
     windows = [make_stream(spec, M, P, K=K, base=(w * world + rank) * M, device=dev)
@@ -118,9 +181,9 @@ def main(argv=None) -> int:
         tele = [make_telemetry(tspec, windows[w], K, base=(w * world + rank) * M) for w in range(n_windows)]
         stats = allocate_stats(M, K, dev)
         n_events = sum(t.num_events for t in tele) / n_windows
-    merger = SweepMerger(P, dev, comm_dtype=args.comm_dtype) if world > 1 else None
+    merger = SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps) if world > 1 else None
     pipe = WindowPipeline(rater, roster, K, merger=merger)
-    err = torch.zeros(3, dtype=torch.int32, device=dev)
+    rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     torch.cuda.synchronize()
     prepared = {0: pipe.prepare(windows[0])}
 
@@ -146,7 +209,6 @@ def main(argv=None) -> int:
             t = tele[i % n_windows]
             _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out,
                                            telemetry=(t.evoff, t.events, stats))
-        err.bitwise_or_(rater.error_flags(dev))
 
     for i in range(args.warmup):
         step(i)
@@ -154,6 +216,8 @@ def main(argv=None) -> int:
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if merger is not None:
+        merger.timing = True  # stage events on the main stream (no syncs)
     t0 = time.perf_counter()
     for i in range(args.warmup, total_windows):
         step(i)
@@ -163,11 +227,24 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     ms = elapsed * 1000.0 / args.steps
-    t = torch.tensor([ms], dtype=torch.float64, device=dev)
+    merge = {}
+    if merger is not None:
+        merger.timing = False
+        merge = {k: v / args.steps for k, v in merger.stage_ms().items()}
+    vals = [ms] + [merge.get(k, 0.0) for k in ("messages", "allreduce", "apply")]
+    t = torch.tensor(vals, dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    ms = float(t.item())
-    flags = err.cpu()
+    ms = float(t[0].item())
+    merge_ms = None
+    if merger is not None:
+        mm = [float(x) for x in t[1:].tolist()]
+        # snapshot: 0 -- the merge decodes into the roster and the next window's
+        # start in one pass, so no per-window copy of the roster is taken
+        merge_ms = {"snapshot": 0.0, "messages": mm[0], "allreduce": mm[1], "apply": mm[2],
+                    "total": sum(mm), "bytes_per_rank": merger.comm_bytes,
+                    "buckets": len(merger.buckets())}
+    flags = rater.sticky_flags(dev).cpu()
     if int(flags.sum()):
         raise RuntimeError("dataflow error flags set during the benchmark: %s" % flags.tolist())
     if args.check:
@@ -175,6 +252,14 @@ def main(argv=None) -> int:
         assert NOT_PROCESSED not in out.status.unique().tolist(), counts
         if rank == 0:
             print("status counts (last window):", counts, file=sys.stderr)
+    verify = None
+    if args.verify and rank == 0:  # untimed: a fresh roster and window 0, device vs fp64 host
+        from analyzer_amd.ops.verify import verify_window
+
+        verify = verify_window(make_roster(RosterSpec(num_players=P, seed=args.seed), device=dev),
+                               windows[0], K)
+        if tele is not None:
+            verify["note"] = "rating only (telemetry is checked by tests/test_telemetry.py)"
     value = world * M / (ms / 1000.0)
     metric = "matches/sec rated (whole node), 3v3 TrueSkill, 1M-player roster"
     extra = {}
@@ -203,6 +288,10 @@ def main(argv=None) -> int:
                                     else BASELINE_MATCHES_PER_S),
             "dtype": "fp32",
             "data": "synthetic (on-device counter RNG stream, random-init %d-player roster)" % P,
+            "merge_ms": merge_ms,
+            "verify": verify,
+            "rccl_world": dist.get_world_size() if world > 1 else None,
+            "dist_backend": backend if world > 1 else None,
             "config": {
                 "model": "TrueSkill 2-team EP (beta=1000, tau=10, draw_probability=0), "
                          "shared + per-mode tracks",
@@ -212,9 +301,13 @@ def main(argv=None) -> int:
                 "matches_per_gpu": M,
                 "team_size": K,
                 "parallelism": "dp%d" % world,
-                "mode": "exact" if world == 1 else "sweep (exact per rank + RCCL posterior merge)",
+                "mode": ("exact" if world == 1 else
+                         "sweep (exact per rank + RCCL posterior merge, %d causal sweep%s)"
+                         % (args.sweeps, "s" if args.sweeps > 1 else "")),
                 "bench_config": args.config,
+                "skew": args.skew,
                 "comm_dtype": args.comm_dtype if world > 1 else None,
+                "sweeps": args.sweeps if world > 1 else None,
                 **extra,
             },
         }), flush=True)

@@ -1,0 +1,120 @@
+#!/bin/bash
+# One entry point for the GPU-box runs (replaces the round-1 one-off scripts).
+#
+#   scripts/gpu.sh TASK [TASK ...]      e.g.  scripts/gpu.sh tests bench dp accuracy
+#
+# Every GPU step runs under its own `timeout -k 10`, output goes under
+# gpurun_out/<task>/, and the script stops at the first failing step (no GPU
+# work after a fault, abort or time limit).
+#
+# tasks:
+#   tests      pytest -m gpu (+ smoke)                    gpurun_out/tests/
+#   bench      bench.py config 2, 20 steps, --verify      gpurun_out/bench/
+#   configs    bench.py configs 3, 4 (fused + separate), 5
+#   skew       bench.py --skew 2 and 3
+#   dp         bench.py --gpus 2 and 4 on this one GPU (gloo rehearsal of the spawn path)
+#   accuracy   sweep-DP accuracy, 8 ranks x 10M matches over 1M players, sweeps 1,2,4,8
+#   prof       rocprofv3 --kernel-trace --stats of config 2
+#   pmc        rocprofv3 --pmc passes over the executor (bench config 2, 3 steps)
+#   rerate     config 5 end to end: 1B matches / 10M players, checkpoint + kill + resume
+#   worker     streaming worker on the device (ENGINE=native), memory + sqlite stores
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+export TMPDIR=/tmp
+PY=python3
+
+run() {  # run NAME SECONDS CMD...: one bounded step, output to gpurun_out/NAME.log
+  local name=$1 secs=$2; shift 2
+  mkdir -p "$ROOT/gpurun_out/$(dirname "$name")"
+  echo "== $name: $*"
+  timeout -k 10 "$secs" "$@" > "$ROOT/gpurun_out/$name.log" 2>&1
+  local rc=$?
+  tail -3 "$ROOT/gpurun_out/$name.log" | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "!! $name failed rc=$rc"; exit $rc; fi
+}
+
+for task in "$@"; do
+  case $task in
+    tests)
+      run tests/pytest 900 $PY -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+      run tests/smoke 300 $PY -c "import __graft_entry__ as g; g.smoke()"
+      ;;
+    bench)
+      run bench/config2 400 $PY bench.py --steps 20 --warmup 3 --check --verify
+      ;;
+    configs)
+      run bench/config3 400 $PY bench.py --config 3 --steps 10 --warmup 2 --check
+      run bench/config4_fused 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode fused
+      run bench/config4_separate 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode separate
+      run bench/config5 400 $PY bench.py --config 5 --steps 10 --warmup 2 --check
+      ;;
+    skew)
+      run bench/skew2 600 $PY bench.py --skew 2 --steps 3 --warmup 1 --check
+      run bench/skew3 900 $PY bench.py --skew 3 --steps 2 --warmup 1 --check
+      ;;
+    dp)
+      run dp/gloo2 600 env ANA_DIST_BACKEND=gloo $PY bench.py --gpus 2 --steps 5 --warmup 2
+      run dp/gloo4 900 env ANA_DIST_BACKEND=gloo $PY bench.py --gpus 4 --steps 3 --warmup 1
+      run dp/gloo2_sweeps2 600 env ANA_DIST_BACKEND=gloo $PY bench.py --gpus 2 --steps 3 --warmup 1 --sweeps 2
+      ;;
+    accuracy)
+      run accuracy/dp8 900 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 8 \
+          --players 1e6 --matches-per-rank 1e7 --windows 1 --warm-windows 1 --sweeps 1,2,4,8
+      run accuracy/dp4_skew 900 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 4 \
+          --players 2e4 --matches-per-rank 2e5 --windows 8 --warm-windows 1 --sweeps 1,2,3,4
+      ;;
+    prof)
+      mkdir -p gpurun_out/prof
+      (cd /tmp && run prof/config2 400 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof/config2" \
+          -o run --output-format csv -- $PY "$ROOT/bench.py" --steps 5 --warmup 2) || exit $?
+      ;;
+    pmc)
+      for set in "FETCH_SIZE WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
+                 "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
+                 "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM" \
+                 "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+        name=$(echo $set | cut -d' ' -f1)
+        (cd /tmp && run pmc/$name 120 rocprofv3 --pmc $set --kernel-trace --stats \
+            -d "$ROOT/gpurun_out/pmc/$name" -o run --output-format csv -- $PY "$ROOT/bench.py" --steps 3 --warmup 1) \
+            || exit $?
+        $PY scripts/pmc_kernel.py "gpurun_out/pmc/$name/*" rate_dataflow >> gpurun_out/pmc/executor.txt
+      done
+      cat gpurun_out/pmc/executor.txt
+      ;;
+    rerate)
+      rm -rf /tmp/ck5
+      rm -rf /tmp/ck5_full
+      run rerate/full 900 $PY -m analyzer_amd.runtime.rerate --matches 1e9 --players 1e7 --window 1.6e7 \
+          --checkpoint-dir /tmp/ck5_full --checkpoint-every 8 --digests
+      # injected crash after 20 windows, then resume from the checkpoint of window 16
+      mkdir -p gpurun_out/rerate
+      echo "== rerate/kill"
+      timeout -k 10 600 $PY -m analyzer_amd.runtime.rerate --matches 1e9 --players 1e7 --window 1.6e7 \
+          --checkpoint-dir /tmp/ck5 --checkpoint-every 8 --fault-kill-after 20 > gpurun_out/rerate/kill.log 2>&1
+      rc=$?; tail -2 gpurun_out/rerate/kill.log
+      if [ $rc -ne 17 ]; then echo "!! expected exit 17 from the injected fault, got $rc"; exit 1; fi
+      run rerate/resume 900 $PY -m analyzer_amd.runtime.rerate --matches 1e9 --players 1e7 --window 1.6e7 \
+          --checkpoint-dir /tmp/ck5 --checkpoint-every 8 --digests
+      $PY - <<'EOF'
+import json
+full = json.loads(open("gpurun_out/rerate/full.log").read().strip().splitlines()[-1])
+res = json.loads(open("gpurun_out/rerate/resume.log").read().strip().splitlines()[-1])
+g0 = int(res["resumed_from_window"])
+same = all(full["window_digests"][g] == d for g, d in res["window_digests"].items())
+print("resumed from window", g0, "| roster bit-identical:", full["roster_sha256"] == res["roster_sha256"],
+      "| re-rated windows' records identical:", same, "| participant records (full run):",
+      full["participant_records"])
+EOF
+      run rerate/host_egress 900 $PY -m analyzer_amd.runtime.rerate --matches 2e8 --players 1e7 \
+          --window 1.6e7 --records host
+      ;;
+    worker)
+      run worker/memory 600 env ENGINE=native BATCHSIZE=500 IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 200000
+      run worker/python 600 env ENGINE=python BATCHSIZE=500 IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 5000
+      run worker/sqlite 600 env ENGINE=native BATCHSIZE=500 IDLE_TIMEOUT=0.01 \
+          DATABASE_URI=sqlite:////tmp/worker.db $PY worker.py --synthetic 50000
+      ;;
+    *) echo "unknown task $task"; exit 2 ;;
+  esac
+done

@@ -100,9 +100,12 @@ static void run(int K, int64_t P, int64_t M, uint64_t seed) {
   // DP merge round trip (raw and base-relative encodings): messages of "after"
   // against "before", then apply, reproduces "after"
   for (int scaled = 0; scaled < 2; ++scaled) {
-    std::vector<float> buf((size_t)P * 16), merged(state.size());
-    host_sweep_delta(state.data(), st64.data(), attrs.data(), vst.data(), 500.f, scaled, buf.data(), P);
-    host_sweep_apply(state.data(), buf.data(), attrs.data(), merged.data(), scaled, vst.data(), 500.f, P);
+    std::vector<float> buf((size_t)P * 16), merged(state.size()), copy(state.size());
+    host_sweep_delta(state.data(), state.data(), st64.data(), attrs.data(), vst.data(), 500.f, scaled,
+                     buf.data(), P);
+    host_sweep_apply(state.data(), buf.data(), attrs.data(), merged.data(), copy.data(), scaled,
+                     vst.data(), 500.f, P);
+    CHECK(memcmp(merged.data(), copy.data(), merged.size() * sizeof(float)) == 0);
     for (int64_t p = 0; p < P; ++p)
       for (int t = 0; t < kTracks; ++t) {
         const float a = st64[p * kRowFloats + 4 * t], b = merged[p * kRowFloats + 4 * t];

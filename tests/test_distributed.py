@@ -215,3 +215,89 @@ def test_sweep_merge_compressed_messages(tmp_path, dtype, tol_mu):
     sg_a, sg_b = a[:, 2::4][ok], b[:, 2::4][ok]
     assert float(((sg_a - sg_b).abs() / sg_a).max()) < 2e-2
     assert torch.equal(got[0]["merged"].nan_to_num(-7), got[1]["merged"].nan_to_num(-7))
+
+
+# ------------------------------------------------ causal re-sweeps (K9 + C1')
+def _scan(rank, size):
+    from analyzer_amd.parallel.comm import exclusive_scan
+
+    t = torch.arange(7 * 3, dtype=torch.float32).view(7, 3) * (rank + 1)
+    return {"ex": exclusive_scan(t)}
+
+
+def test_exclusive_scan_over_ranks(tmp_path):
+    size = 3
+    res = run_ranks(_scan, size, tmp_path)
+    base = torch.arange(7 * 3, dtype=torch.float32).view(7, 3)
+    for r, out in enumerate(res):
+        assert torch.equal(out["ex"], base * sum(q + 1 for q in range(r)))
+
+
+def _resweep(rank, size, P, M, K, seed, sweeps, comm_dtype):
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.parallel.sweep import SweepMerger, rate_window_dp
+
+    roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
+    spec = StreamSpec(team_size=K, seed=seed + 1)
+    merger = SweepMerger(P, "cpu", comm_dtype=comm_dtype, sweeps=sweeps)
+    outs = []
+    for w in range(2):  # two windows: the second starts from the merge's own start copy
+        rec = make_stream(spec, M, P, K=K, base=(w * size + rank) * M)
+        outs.append(rate_window_dp(BatchRater(), merger, roster, rec, K).s_mu.clone())
+    return {"state": roster.state, "s_mu": outs[-1]}
+
+
+@pytest.mark.parametrize("sweeps", [1, 2, 3])
+def test_causal_resweeps_converge_to_exact(tmp_path, sweeps):
+    """N gloo ranks rate consecutive time slices; ``sweeps`` causal re-sweeps
+    (exclusive prefix of the earlier ranks' messages) converge to the exact
+    sequential result: at sweeps == N it is reproduced up to fp32 rounding, and
+    the distributed run equals the one-process simulation (parallel/accuracy.py)."""
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.parallel.accuracy import compare, simulate_sweep_dp
+
+    P, M, K, seed, size = 300, 700, 3, 21, 3
+    res = run_ranks(_resweep, size, tmp_path, P, M, K, seed, sweeps, "fp32")
+    spec = StreamSpec(team_size=K, seed=seed + 1)
+    start = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
+    exact, sim = start.clone(), start.clone()
+    for w in range(2):
+        shards = [make_stream(spec, M, P, K=K, base=(w * size + r) * M) for r in range(size)]
+        ref_out = [BatchRater().rate(exact, sh, K) for sh in shards]
+        simulate_sweep_dp(BatchRater(), sim, shards, K, sweeps=sweeps)
+    for r in res[1:]:  # replicas agree
+        assert torch.equal(r["state"].nan_to_num(-7), res[0]["state"].nan_to_num(-7))
+    got = res[0]["state"]
+    # distributed == simulation (sums of 3 fp32 messages may round differently)
+    ok = ~torch.isnan(sim.state[:, 0::4])
+    assert torch.equal(torch.isnan(got[:, 0::4]), ~ok)
+    assert float((got[:, 0::4][ok] - sim.state[:, 0::4][ok]).abs().max()) < 1e-2
+    from analyzer_amd.ops.rate import Roster
+
+    stats = compare(Roster(got, start.attrs), exact)
+    sh = stats["tracks"]["shared"]
+    assert sh["null_mismatch"] == 0
+    bound = {1: None, 2: None, 3: 0.02}[sweeps]
+    if bound is not None:
+        assert sh["dmu_max"] < bound, sh
+        # the last rank's records are exact too
+        last = ref_out[-1].s_mu
+        d = (res[-1]["s_mu"] - last).abs()
+        assert float(d[~torch.isnan(d)].max()) < bound
+
+
+def test_resweep_error_falls_per_sweep():
+    """One-process simulation, 4 ranks: each causal re-sweep cuts the deviation
+    from exact by more than 5x, and sweeps == ranks is exact to fp32 rounding."""
+    from analyzer_amd.parallel.accuracy import run
+
+    t = run(ranks=4, players=1500, matches_per_rank=3000, windows=2, sweeps=[1, 2, 3, 4],
+            warm_windows=1)
+    errs = [t["sweeps"][str(s)]["tracks"]["shared"] for s in (1, 2, 3, 4)]
+    for a, b in zip(errs, errs[1:]):
+        assert b["dmu_p99"] < a["dmu_p99"] / 5, (a, b)
+    assert errs[-1]["dmu_max"] < 5e-3
+    assert errs[0]["dmu_median"] > 1.0  # one sweep is a real approximation at this density
+    for e in errs:
+        assert e["null_mismatch"] == 0
+    assert t["sweeps"]["4"]["records_shared_mu"]["dmu_max"] < 5e-3

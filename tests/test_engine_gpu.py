@@ -25,8 +25,8 @@ def test_generators_bit_identical(gpu_device):
     a, b = make_roster(rs), make_roster(rs, device=gpu_device)
     assert torch.equal(a.state.view(torch.int32), b.state.cpu().view(torch.int32))
     assert torch.equal(a.attrs.view(torch.int32), b.attrs.cpu().view(torch.int32))
-    for K in (1, 3, 5):
-        ss = StreamSpec(team_size=K, seed=33, p_afk=0.1, p_tie=0.1, p_hot=0.3, p_uneven=0.1)
+    for K, skew in ((1, 1), (3, 1), (5, 1), (3, 2), (3, 3)):
+        ss = StreamSpec(team_size=K, seed=33, p_afk=0.1, p_tie=0.1, p_hot=0.3, p_uneven=0.1, skew=skew)
         ra = make_stream(ss, 20000, 5000, base=123)
         rb = make_stream(ss, 20000, 5000, base=123, device=gpu_device)
         assert torch.equal(ra, rb.cpu())
@@ -159,33 +159,40 @@ def test_radix_sort_pairs_stable(gpu_device, n, bits):
 
 
 @pytest.mark.parametrize("scaled", [False, True])
-def test_sweep_kernels_match_host(gpu_device, scaled):
-    """K9 device kernels (messages + apply) == C++ host mirror on 128-B rows."""
+@pytest.mark.parametrize("resweep", [False, True])
+def test_sweep_kernels_match_host(gpu_device, scaled, resweep):
+    """K9 device kernels (messages + decode, dual write) == C++ host mirror on
+    128-B rows; ``resweep``: messages measured from a prior != the start."""
     from analyzer_amd.ops.native import native
     from analyzer_amd.models.tiers import vst_table
 
     P = 5000
     start = make_roster(RosterSpec(num_players=P, seed=3, p_rated=0.5))
-    after = start.clone()
+    prior = start.clone()
+    if resweep:  # a prior that moved on from the start (touches NULL tracks too)
+        R.BatchRater().rate(prior, make_stream(StreamSpec(team_size=3, seed=14), 8000, P), 3)
+    after = prior.clone()
     rec = make_stream(StreamSpec(team_size=3, seed=4), 20000, P)
     R.BatchRater().rate(after, rec, 3)
     vst = torch.tensor(vst_table(), dtype=torch.float32)
+    g = lambda t: t.to(gpu_device)
     bh = torch.empty((P, 16))
-    native().sweep_delta(start.state, after.state, start.attrs, vst, 500.0, scaled, bh)
+    native().sweep_delta(start.state, prior.state, after.state, start.attrs, vst, 500.0, scaled, bh)
     bd = torch.empty((P, 16), device=gpu_device)
-    native().sweep_delta(start.state.to(gpu_device), after.state.to(gpu_device),
-                         start.attrs.to(gpu_device), vst.to(gpu_device), 500.0, scaled, bd)
-    # scaled messages are (pi/pi_b - 1, ...): a 1-ulp difference in pi/pi_b near 1 is a
-    # large relative one in the message (they travel as fp16/bf16 anyway)
+    native().sweep_delta(g(start.state), g(prior.state), g(after.state), g(start.attrs), g(vst), 500.0,
+                         scaled, bd)
+    # scaled messages are (pi/pi_b - pi0/pi_b, ...): a 1-ulp difference in a ratio near 1
+    # is a large relative one in the message (they travel as fp16/bf16 anyway)
     np.testing.assert_allclose(bd.cpu().numpy(), bh.numpy(), rtol=1e-3 if scaled else 1e-6,
                                atol=1e-5 if scaled else 1e-9)
-    sh = start.state.clone()
-    native().sweep_apply(start.state, bh * 2, start.attrs, sh, vst, 500.0, scaled)
-    sd = start.state.to(gpu_device).clone()
-    native().sweep_apply(start.state.to(gpu_device), (bh * 2).to(gpu_device),
-                         start.attrs.to(gpu_device), sd, vst.to(gpu_device), 500.0, scaled)
+    sh, sh2 = start.state.clone(), torch.zeros_like(start.state)
+    native().sweep_apply(start.state, bh * 2, start.attrs, sh, sh2, vst, 500.0, scaled)
+    sd, sd2 = g(start.state).clone(), torch.zeros_like(g(start.state))
+    native().sweep_apply(g(start.state), g(bh * 2), g(start.attrs), sd, sd2, g(vst), 500.0, scaled)
     # fp32 (tau / pi, 1 / sqrt(pi)): device fma contraction vs host rounding
     np.testing.assert_allclose(sd.cpu().numpy(), sh.numpy(), rtol=5e-5, atol=1e-6, equal_nan=True)
+    assert torch.equal(sd.nan_to_num(-7), sd2.nan_to_num(-7))
+    assert torch.equal(sh.nan_to_num(-7), sh2.nan_to_num(-7))
 
 
 def test_telemetry_device_generator_and_aggregation(gpu_device):

@@ -134,3 +134,16 @@ def test_grid_blocks_scale_with_the_window():
     assert br.chunk_len(64 * 2048 * 2) == 64 and br.grid_blocks(64 * 2048 * 2) == 512
     assert br.grid_blocks(10_000_000) == 512
     assert br.grid_blocks(500, telemetry=True) == 512
+
+
+@pytest.mark.parametrize("skew", [1, 2, 3])
+def test_skewed_activity_draw(skew):
+    """``StreamSpec.skew``: player = floor(u^skew * P), so P(player < x) = (x/P)^(1/skew)."""
+    from analyzer_amd.ops.synth import StreamSpec, make_stream
+
+    P, M = 100_000, 40_000
+    rec = make_stream(StreamSpec(team_size=3, seed=5, p_afk=0.0, skew=skew), M, P)
+    ids = rec[:, :6].reshape(-1).double()
+    for x in (100, 10_000):
+        frac = float((ids < x).double().mean())
+        assert abs(frac - (x / P) ** (1.0 / skew)) < 0.01, (x, frac)

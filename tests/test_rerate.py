@@ -40,6 +40,36 @@ def test_checkpoint_resume_after_injected_crash(tmp_path):
     assert summary["resumed_from_window"] == 2 and summary["matches"] == 1250 - 600
     ref, _ = _sequential(SPEC)
     assert torch.equal(roster.state.nan_to_num(-7), ref.state.nan_to_num(-7))  # exactly once
+    # the re-rated windows reproduce the uninterrupted run's output records
+    full, _ = run(SPEC, "cpu")
+    assert sorted(summary["window_digests"]) == [2, 3, 4]
+    for g in (2, 3, 4):
+        assert summary["window_digests"][g] == full["window_digests"][g]
+
+
+def test_output_records_accounted_for():
+    """Every participant record of every window reaches the host sink, and the
+    device digest counts the same records."""
+    seen = []
+    host, _ = run(SPEC, "cpu", records="host", on_records=lambda base, h: seen.append(
+        (base, int(h["s_mu"].shape[0]), int((~torch.isnan(h["s_mu"])).sum()))))
+    dig, _ = run(SPEC, "cpu")
+    assert [b for b, _, _ in seen] == [0, 300, 600, 900, 1200]
+    assert sum(m for _, m, _ in seen) == SPEC.total_matches
+    assert host["participant_records"] == dig["participant_records"] == sum(p for _, _, p in seen)
+    _, res = _sequential(SPEC)
+    assert dig["participant_records"] == float((~torch.isnan(res.s_mu)).sum())
+    assert dig["match_records"] == float(((res.status <= 2)).sum())
+
+
+def test_checkpoint_falls_back_to_old_after_torn_replace(tmp_path):
+    d = str(tmp_path / "ck")
+    run(SPEC, "cpu", checkpoint_dir=d, checkpoint_every=2)
+    latest = os.path.join(d, "latest")
+    os.replace(latest, latest + ".old")  # crash between the two renames of a replace
+    mgr = checkpoint.CheckpointManager(d)
+    got = mgr.latest()
+    assert got is not None and got[1]["windows_done"] == 4
 
 
 def test_checkpoint_rejects_foreign_run(tmp_path):
@@ -60,19 +90,23 @@ def test_checkpoint_roundtrip_is_safetensors(tmp_path):
     assert sorted(os.listdir(str(tmp_path))) == ["c"]
 
 
-def _dp_rerate(rank, size, spec):
-    summary, roster = run(spec, "cpu")
+def _dp_rerate(rank, size, spec, sweeps):
+    summary, roster = run(spec, "cpu", sweeps=sweeps)
     return {"state": roster.state, "summary": summary}
 
 
-def test_time_axis_sharded_rerate_two_ranks(tmp_path):
+@pytest.mark.parametrize("sweeps", [1, 2])
+def test_time_axis_sharded_rerate_two_ranks(tmp_path, sweeps):
     spec = RerateSpec(total_matches=1200, players=500, team_size=3, window=200, seed=5)
-    res = run_ranks(_dp_rerate, 2, tmp_path, spec)
+    res = run_ranks(_dp_rerate, 2, tmp_path, spec, sweeps)
     assert torch.equal(res[0]["state"].nan_to_num(-7), res[1]["state"].nan_to_num(-7))
     assert res[0]["summary"]["matches"] == 1200 and res[0]["summary"]["windows"] == 3
-    # sweep merge stays close to the exact sequential result on a sparse history
     ref, _ = _sequential(spec)
     mu, rmu = res[0]["state"][:, 0], ref.state[:, 0]
     ok = ~torch.isnan(rmu)
     assert torch.equal(ok, ~torch.isnan(mu))
-    assert float((mu[ok] - rmu[ok]).abs().median()) < 25.0
+    err = (mu[ok] - rmu[ok]).abs()
+    if sweeps == 1:  # one merge: an approximation (parallel/accuracy.py quantifies it)
+        assert float(err.median()) < 25.0
+    else:  # sweeps == ranks: the exact sequential result up to fp32 rounding
+        assert float(err.max()) < 0.05

@@ -297,3 +297,14 @@ def test_streaming_worker_telemetry_into_participant_stats(tmp_path):
             for p in m.participants:
                 total += s.participant_stats(p.api_id)["events"]
     assert 5 * 10 <= total <= 9 * 10  # every event lands on exactly one participant
+
+
+def test_synthetic_telemetry_never_persisted_to_a_real_database(tmp_path):
+    """DOTELEMETRY generates synthetic events: refused against a real DATABASE_URI
+    unless the run declares itself a benchmark (SYNTHETIC_TELEMETRY=true)."""
+    uri = "sqlite:///" + str(tmp_path / "real.db")
+    with pytest.raises(ValueError, match="SYNTHETIC"):
+        make_worker(n=2, engine="native", database_uri=uri, dotelemetry=True)
+    w, _, _ = make_worker(n=2, engine="native", database_uri=uri, dotelemetry=True,
+                          synthetic_telemetry=True)
+    assert w.channel is not None
