@@ -90,7 +90,8 @@ class OutputSink:
     stream wait on before it overwrites ``res`` (double-buffered outputs).
     Pinned slots are allocated once (``slots`` of them, grown to the largest
     window) and recycled: pinning a 2-GB window per push would cost more than
-    the copy."""
+    the copy.  ``slots=0``: no ring -- every window gets fresh pinned buffers
+    that the callback may keep (small windows, tests)."""
 
     FIELDS = ("quality", "status", "s_mu", "s_sig", "delta", "m_mu", "m_sig")
 
@@ -99,6 +100,7 @@ class OutputSink:
         self.cuda = self.device.type == "cuda"
         self.on_ready = on_ready
         self.copy_stream = torch.cuda.Stream(self.device) if self.cuda else None
+        self.ring = int(slots) > 0
         self._slots = [None] * max(1, int(slots))
         self._next = 0
         self._pending: Deque[Tuple[int, dict, Optional[torch.cuda.Event], int]] = collections.deque()
@@ -106,7 +108,7 @@ class OutputSink:
         self.bytes = 0
 
     def _slot(self, i: int, shape, dtype) -> torch.Tensor:
-        buf = self._slots[i]
+        buf = self._slots[i] if self.ring else None
         n = 1
         for d in shape:
             n *= int(d)
@@ -120,7 +122,7 @@ class OutputSink:
             self.on_ready(base, {f: getattr(res, f).clone() for f in self.FIELDS})
             return
         # the ring slot we are about to reuse must have been delivered
-        while len(self._pending) >= len(self._slots):
+        while self.ring and len(self._pending) >= len(self._slots):
             self.poll(block=True, limit=1)
         i = self._next
         self._next = (self._next + 1) % len(self._slots)
@@ -179,7 +181,7 @@ def rate_file(path: str, roster, window: int, rater=None, on_result=None) -> int
 
     src = FileSource(path, window, roster.device)
     pipe = WindowPipeline(rater or BatchRater(), roster, src.K)
-    sink = OutputSink(roster.device, on_result) if on_result is not None else None
+    sink = OutputSink(roster.device, on_result, slots=0) if on_result is not None else None
     bases = []
 
     def windows():
