@@ -74,6 +74,8 @@ class WorkerConfig:
     # new: aggregate per-participant telemetry (participant_stats) in the rating launch
     dotelemetry: bool = False
     telemetry_events: str = "100,300"
+    # new: ENGINE=native keeps the player table resident on the device across batches
+    resident: bool = True
     # new: the run is a benchmark -- synthetic telemetry may be persisted (worker.connect)
     synthetic_telemetry: bool = False
     # new: skip matches that already carry a rating (trueskill_quality set), so a
@@ -101,6 +103,7 @@ class WorkerConfig:
             dotelemetry=env.get("DOTELEMETRY") == "true",
             telemetry_events=_env(env, "TELEMETRY_EVENTS") or "100,300",
             synthetic_telemetry=env.get("SYNTHETIC_TELEMETRY") == "true",
+            resident=(env.get("RESIDENT") or "true") == "true",
             skip_rated=env.get("SKIP_RATED") == "true",
         )
 

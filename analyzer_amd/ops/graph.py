@@ -44,12 +44,44 @@ def noop_records(n: int, K: int, device) -> torch.Tensor:
     return rec
 
 
-class GraphRater:
-    """Rate batches of up to ``capacity`` matches against ``roster`` by graph replay."""
+class EpochClock:
+    """The device launch epoch of every graph that rates one roster.
+
+    Granule tags are only unambiguous if no two launches since the last tag
+    reset used the same epoch, so graphs of different team sizes (or
+    capacities) over one roster must share ONE counter: each replay bumps it on
+    the device, and before it would pass 255 the host resets the roster's tags
+    and the counter (eagerly, outside the graphs)."""
 
     MAX_EPOCH = 255
 
-    def __init__(self, roster: Roster, K: int, capacity: int, rater: Optional[BatchRater] = None):
+    def __init__(self, roster: Roster):
+        self.roster = roster
+        self.epoch = torch.zeros(1, dtype=torch.int32, device=roster.device)
+        self.bumps = 0
+        # the graphs own the roster's tags from here on: start from a clean slate, and
+        # make any later eager launch (Roster.next_epoch) reset them first
+        native().reset_tags(roster.state)
+        roster.epoch = None
+
+    def before_launch(self) -> None:
+        if self.bumps + 1 >= self.MAX_EPOCH:  # the next bump would reuse a live epoch
+            native().reset_tags(self.roster.state)
+            self.epoch.zero_()
+            self.bumps = 0
+            self.roster.epoch = None
+
+    def launched(self) -> None:
+        self.bumps += 1
+
+
+class GraphRater:
+    """Rate batches of up to ``capacity`` matches against ``roster`` by graph replay."""
+
+    MAX_EPOCH = EpochClock.MAX_EPOCH
+
+    def __init__(self, roster: Roster, K: int, capacity: int, rater: Optional[BatchRater] = None,
+                 clock: Optional[EpochClock] = None):
         dev = roster.device
         if dev.type != "cuda":
             raise ValueError("GraphRater needs a device roster")
@@ -57,24 +89,25 @@ class GraphRater:
         self.rater = rater or BatchRater()
         self.rec = noop_records(self.capacity, self.K, dev)
         self.out = RateResult.allocate(self.capacity, self.K, dev)
-        self.epoch = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.clock = clock if clock is not None else EpochClock(roster)
+        self.epoch = self.clock.epoch
         self._filled = 0  # records of the last batch (the rest are no-ops)
-        # the graph owns the roster's tags from here on: start from a clean slate, and
-        # make any later eager launch (Roster.next_epoch) reset them first
-        native().reset_tags(roster.state)
-        roster.epoch = None
-        self._bumps = 0
         # warm-up outside capture (allocates the schedule workspaces), then capture
+        self.clock.before_launch()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             self._body()
         torch.cuda.current_stream(dev).wait_stream(side)
         torch.cuda.synchronize(dev)
-        self._bumps += 1
+        self.clock.launched()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self._body()
+
+    @property
+    def _bumps(self) -> int:
+        return self.clock.bumps
 
     def _body(self) -> None:
         # rate() bumps the device epoch before its launch reads it (inside the schedule)
@@ -93,12 +126,9 @@ class GraphRater:
         if m < self._filled:
             self.rec[m:self._filled].copy_(noop_records(self._filled - m, self.K, rec.device))
         self._filled = m
-        if self._bumps + 1 >= self.MAX_EPOCH:  # the next bump would reuse a live epoch range
-            native().reset_tags(self.roster.state)
-            self.epoch.zero_()
-            self._bumps = 0
+        self.clock.before_launch()
         self.graph.replay()
-        self._bumps += 1
+        self.clock.launched()
         o = self.out
         return RateResult(o.quality[:m], o.status[:m], o.s_mu[:m], o.s_sig[:m], o.delta[:m],
                           o.m_mu[:m], o.m_sig[:m], packed=o.packed[:m])
@@ -108,4 +138,4 @@ class GraphRater:
         self.rater.check_errors(self.roster.device)
 
 
-__all__ = ["GraphRater", "noop_records"]
+__all__ = ["EpochClock", "GraphRater", "noop_records"]

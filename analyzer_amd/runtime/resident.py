@@ -1,0 +1,328 @@
+"""The worker's GPU path: a device-resident roster + per-batch graph replay.
+
+The reference rates each batch of <= BATCHSIZE matches by loading the players
+from MySQL, rating match after match in Python and committing the player rows
+back (/root/reference/worker.py:169-199, rater.py:108-169).  Rebuilding a
+device roster from those objects for every batch costs more than the rating
+itself, so ``ENGINE=native`` keeps the player table ON THE DEVICE across
+batches:
+
+* ``ResidentRoster``: the ``Roster`` tensors (128 B per player) plus an
+  ``api_id -> row`` map that grows when a batch brings players it has not seen
+  (their stored ratings are uploaded once, with one H2D copy per batch;
+  capacity doubles when full).  The worker is then the owner of the ratings it
+  writes: rows are never re-read from the store (``RESIDENT=false`` restores
+  the rebuild-per-batch path for deployments that share the table with other
+  writers -- the reference's replicas race on those rows anyway,
+  worker.py:174-194);
+* each batch is encoded columnarly into the stream layout and rated by ONE
+  HIP-graph replay per team size (ops/graph.py; copy -> schedule -> executor),
+  all graphs sharing the roster's epoch clock.  ``DOTELEMETRY`` launches the
+  fused rating + telemetry executor eagerly on the same clock;
+* only the batch's outputs (one packed 128-B row per match) and the batch's
+  player rows come back to the host, and only the fields the reference writes
+  are set on the objects (rater.py:103-105,141,151-169);
+* a failed batch (exception after rating, QUARANTINE=false errors, a failed
+  commit) is rolled back on the device too: the batch's rows are snapshotted
+  before the launch and restored by ``rollback``.
+
+On the CPU the same class rates through the C++ host mirror (no graphs).
+"""
+from __future__ import annotations
+
+import math
+from operator import attrgetter
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..config import MODES, TRACK_COLUMNS
+from ..ops import rate as R
+from .objects import STAT_COLUMNS, Match, ParticipantStats
+
+RATING_COLS = tuple(c + s for c in TRACK_COLUMNS for s in ("_mu", "_sigma"))
+ATTR_COLS = ("rank_points_ranked", "rank_points_blitz", "skill_tier")
+_get_ratings = attrgetter(*RATING_COLS)
+_get_attrs = attrgetter(*ATTR_COLS)
+MODE_INDEX = {m: k for k, m in enumerate(MODES)}
+MAX_TEAM = 5
+_MU = [c + "_mu" for c in TRACK_COLUMNS]
+_SIG = [c + "_sigma" for c in TRACK_COLUMNS]
+
+
+def _f(x: float) -> Optional[float]:
+    return None if math.isnan(x) else x
+
+
+class ResidentRoster:
+    """Device roster of every player the worker has seen, keyed by api id."""
+
+    def __init__(self, device, capacity: int = 1 << 16):
+        self.device = torch.device(device)
+        self.roster = R.Roster.empty(max(1, int(capacity)), self.device)
+        self.rows: Dict[str, int] = {}
+        self.n = 0
+        self.generation = 0  # bumped when the tensors move (graphs must be re-captured)
+
+    @property
+    def capacity(self) -> int:
+        return self.roster.num_players
+
+    def rows_for(self, players: Sequence) -> List[int]:
+        """Row of every player object (uploading the ones not seen before)."""
+        rows, new = [], []
+        get = self.rows.get
+        for pl in players:
+            r = get(pl.api_id)
+            if r is None:
+                r = self.n + len(new)
+                self.rows[pl.api_id] = r
+                new.append(pl)
+            rows.append(r)
+        if new:
+            self._upload(new)
+        return rows
+
+    def _grow(self, need: int) -> None:
+        cap = self.capacity
+        while cap < need:
+            cap *= 2
+        bigger = R.Roster.empty(cap, self.device)
+        bigger.state[:self.n].copy_(self.roster.state[:self.n])
+        bigger.attrs[:self.n].copy_(self.roster.attrs[:self.n])
+        self.roster = bigger
+        self.generation += 1
+
+    def _upload(self, new: Sequence) -> None:
+        base, k = self.n, len(new)
+        if base + k > self.capacity:
+            self._grow(base + k)
+        vals = np.array([_get_ratings(pl) for pl in new], dtype=np.float64).reshape(k, len(RATING_COLS))
+        st = np.zeros((k, 32), dtype=np.float32)
+        st[:, 0::2] = np.nan
+        mu = vals[:, 0::2]
+        st[:, 0:28:4] = mu
+        st[:, 2:28:4] = np.where(np.isnan(mu), np.nan, vals[:, 1::2])
+        at = np.zeros((k, 4), dtype=np.float32)
+        at[:, :3] = np.array([_get_attrs(pl) for pl in new], dtype=np.float64).reshape(k, 3)
+        self.roster.state[base:base + k].copy_(torch.from_numpy(st))
+        self.roster.attrs[base:base + k].copy_(torch.from_numpy(at))
+        self.n = base + k
+
+
+def team_size(matches: Sequence[Match]) -> int:
+    k = 1
+    for m in matches:
+        for r in m.rosters[:2]:
+            n = len(r.participants)
+            if n > k:
+                k = n
+    return k
+
+
+def encode(matches: Sequence[Match], row_of: Dict[int, int], K: int) -> torch.Tensor:
+    """``[M, 2K+2]`` int32 records (csrc/common.h layout) from object matches;
+    ``row_of`` maps ``id(player object)`` to its roster row."""
+    S = 2 * K
+    out = np.full((len(matches), S + 2), -1, dtype=np.int64)
+    for i, m in enumerate(matches):
+        rosters = m.rosters
+        nr = len(rosters)
+        row = out[i]
+        afk = 0
+        k = 0
+        n = [0, 0]
+        for ri in range(min(nr, 2)):
+            parts = rosters[ri].participants
+            n[ri] = len(parts)
+            off = ri * K
+            for pos, p in enumerate(parts):
+                if pos < K:
+                    row[off + pos] = row_of[id(p.player[0])]
+                if p.went_afk == 1:
+                    afk |= 1 << min(k, 23)
+                k += 1
+        for ri in range(2, nr):
+            for p in rosters[ri].participants:
+                if p.went_afk == 1:
+                    afk |= 1 << 23
+        w0 = nr > 0 and bool(rosters[0].winner)
+        w1 = nr > 1 and bool(rosters[1].winner)
+        row[S] = (MODE_INDEX.get(m.game_mode, 255) | (min(n[0], 255) << 8) | (min(n[1], 255) << 16)
+                  | (min(nr, 255) << 24))
+        row[S + 1] = (1 if w0 else 0) | (2 if w1 else 0) | (4 if afk else 0) | ((afk & 0xffffff) << 8)
+    return torch.from_numpy(out.astype(np.uint32).view(np.int32))
+
+
+class ResidentBatchRater:
+    """``ENGINE=native`` batch rater over a ``ResidentRoster`` (see module doc)."""
+
+    def __init__(self, rater: Optional[R.BatchRater] = None, device=None, capacity: int = 500,
+                 roster_capacity: int = 1 << 16, graphs: bool = True):
+        self.rater = rater or R.BatchRater()
+        if device is None:
+            device = "cuda" if torch.cuda.is_available() else "cpu"
+        self.device = torch.device(device)
+        self.resident = ResidentRoster(self.device, roster_capacity)
+        self.capacity = int(capacity)
+        self.use_graphs = graphs and self.device.type == "cuda"
+        self._graphs: Dict[int, object] = {}
+        self._clock = None
+        self._generation = -1
+        self._undo = None  # (rows, saved state rows) of the last batch
+
+    def supports(self, matches: Sequence[Match]) -> bool:
+        return team_size(matches) <= MAX_TEAM
+
+    # ------------------------------------------------------------ graphs
+    def _graph(self, K: int, m: int):
+        from ..ops.graph import EpochClock, GraphRater
+
+        if self._generation != self.resident.generation:  # the roster moved
+            self._graphs.clear()
+            self._clock = EpochClock(self.resident.roster)
+            self._generation = self.resident.generation
+        if m > self.capacity:
+            return None
+        g = self._graphs.get(K)
+        if g is None:
+            g = GraphRater(self.resident.roster, K, self.capacity, self.rater, clock=self._clock)
+            self._graphs[K] = g
+        return g
+
+    # ------------------------------------------------------------ rating
+    def rate(self, matches: Sequence[Match], telemetry=None) -> List[int]:
+        if not matches:
+            return []
+        K = team_size(matches)
+        if K > MAX_TEAM:
+            raise ValueError("teams of %d players exceed the batched engine (max %d)" % (K, MAX_TEAM))
+        players, row_of = [], {}
+        for m in matches:
+            for r in m.rosters[:2]:
+                for p in r.participants:
+                    pl = p.player[0]
+                    if id(pl) not in row_of:
+                        row_of[id(pl)] = -1
+                        players.append(pl)
+        rows = self.resident.rows_for(players)
+        for pl, r in zip(players, rows):
+            row_of[id(pl)] = r
+        rec = encode(matches, row_of, K).to(self.device, non_blocking=True)
+        roster = self.resident.roster
+        idx = torch.tensor(rows, dtype=torch.int64).to(self.device, non_blocking=True)
+        self._undo = (idx, roster.state.index_select(0, idx)) if rows else None
+        stats = None
+        if telemetry is not None:
+            from ..ops.telemetry import allocate_stats, make_telemetry
+            tel = make_telemetry(telemetry, rec, K)
+            stats = allocate_stats(len(matches), K, self.device)
+            res = self._eager(rec, K, (tel.evoff, tel.events, stats))
+        else:
+            g = self._graph(K, len(matches)) if self.use_graphs else None
+            res = g.rate(rec) if g is not None else self._eager(rec, K, None)
+        packed = res.packed.cpu().numpy() if res.packed is not None else None
+        final = roster.state.index_select(0, idx).cpu().numpy() if rows else None
+        st = self._write_back(matches, res, packed, K, row_of, final, rows)
+        if stats is not None:
+            _write_stats(matches, stats, K)
+        if self.device.type == "cuda":
+            self.rater.check_errors(self.device)
+        return st
+
+    def _eager(self, rec, K, telemetry):
+        if self.device.type != "cuda":
+            return self.rater.rate(self.resident.roster, rec, K, telemetry=telemetry)
+        if self._clock is None or self._generation != self.resident.generation:
+            self._graph(K, self.capacity + 1)  # (re)creates the clock only
+        self._clock.before_launch()
+        res = self.rater.rate(self.resident.roster, rec, K, telemetry=telemetry, check=False,
+                              epoch_dev=self._clock.epoch)
+        self._clock.launched()
+        return res
+
+    def rollback(self) -> None:
+        """Undo the last batch on the device roster (the store rolled back)."""
+        if self._undo is not None:
+            idx, saved = self._undo
+            self.resident.roster.state.index_copy_(0, idx, saved)
+            self._undo = None
+
+    def commit(self) -> None:
+        self._undo = None
+
+    @staticmethod
+    def _write_back(matches, res, packed, K, row_of, final, rows) -> List[int]:
+        S = 2 * K
+        if packed is not None:
+            st = packed.view(np.uint8)[:, 4 * (5 * S + 1)]
+            q = packed[:, 5 * S].astype(np.float64).tolist()
+            s_mu = packed[:, 0:S].astype(np.float64).tolist()
+            s_sig = packed[:, S:2 * S].astype(np.float64).tolist()
+            dl = packed[:, 2 * S:3 * S].astype(np.float64).tolist()
+            m_mu = packed[:, 3 * S:4 * S].astype(np.float64).tolist()
+            m_sig = packed[:, 4 * S:5 * S].astype(np.float64).tolist()
+        else:
+            st = res.status.cpu().numpy()
+            q = res.quality.cpu().double().tolist()
+            s_mu, s_sig, dl, m_mu, m_sig = (t.cpu().double().tolist()
+                                            for t in (res.s_mu, res.s_sig, res.delta, res.m_mu, res.m_sig))
+        status = [int(x) for x in st.tolist()]
+        touched: Dict[int, set] = {}
+        skip = set(R.ERROR_STATUSES) | {R.UNSUPPORTED_MODE, R.NOT_PROCESSED}
+        for i, m in enumerate(matches):
+            s = status[i]
+            if s in skip:
+                continue
+            if s == R.AFK or s == R.INVALID_ROSTERS:
+                m.trueskill_quality = 0
+                for p in m.participants:
+                    p.participant_items[0].any_afk = True
+                continue
+            mode = MODE_INDEX[m.game_mode]
+            cmu, csig = _MU[1 + mode], _SIG[1 + mode]
+            m.trueskill_quality = q[i]
+            for p in m.participants:
+                p.participant_items[0].any_afk = False
+            smu, ssg, sdl, mmu, msg = s_mu[i], s_sig[i], dl[i], m_mu[i], m_sig[i]
+            for ri, r in enumerate(m.rosters[:2]):
+                off = ri * K
+                for pos, p in enumerate(r.participants):
+                    j = off + pos
+                    p.trueskill_mu = smu[j]
+                    p.trueskill_sigma = ssg[j]
+                    p.trueskill_delta = sdl[j]
+                    it = p.participant_items[0]
+                    setattr(it, cmu, mmu[j])
+                    setattr(it, csig, msg[j])
+                    key = id(p.player[0])
+                    t = touched.get(key)
+                    if t is None:
+                        touched[key] = t = set()
+                    t.add(0)
+                    t.add(1 + mode)
+        if final is None or not touched:
+            return status
+        fin = final.astype(np.float64)
+        by_id = {}
+        for m in matches:
+            for p in m.participants:
+                by_id[id(p.player[0])] = p.player[0]
+        pos_of = {r: k for k, r in enumerate(rows)}
+        for key, tracks in touched.items():
+            pl = by_id[key]
+            row = fin[pos_of[row_of[key]]]
+            for t in tracks:
+                setattr(pl, _MU[t], _f(float(row[4 * t])))
+                setattr(pl, _SIG[t], _f(float(row[4 * t + 2])))
+        return status
+
+
+def _write_stats(matches, stats: torch.Tensor, K: int) -> None:
+    st = stats.cpu().double().numpy()
+    for i, m in enumerate(matches):
+        for ri, r in enumerate(m.rosters[:2]):
+            for pos, p in enumerate(r.participants[:K]):
+                vals = dict(zip(STAT_COLUMNS, (float(v) for v in st[i, ri * K + pos])))
+                p.participant_stats = [ParticipantStats(p.api_id, **vals)]

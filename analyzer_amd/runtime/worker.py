@@ -22,7 +22,9 @@ Same observable protocol as the reference:
 Deliberate, documented differences:
 
 * ``ENGINE=native`` rates the whole batch with one launch of the batched
-  engine (runtime/batch.py) instead of per-object Python;
+  engine instead of per-object Python: against a device-resident roster with
+  one HIP-graph replay per batch (runtime/resident.py; ``RESIDENT=false``
+  rebuilds the roster from the batch's objects instead, runtime/batch.py);
 * ``QUARANTINE=true`` (default) isolates the matches the reference would raise
   on (tier None/30, sigma 0, empty roster, non-finite result): only their
   deliveries go to ``QUEUE_failed``; the rest of the batch commits.
@@ -207,8 +209,12 @@ class Worker:
                     quarantined = self._rate_python(session, matches, counts)
             with trace_range("commit"):
                 session.commit()
+            if self._object_rater is not None and hasattr(self._object_rater, "commit"):
+                self._object_rater.commit()
         except Exception:
             session.rollback()
+            if self._object_rater is not None and hasattr(self._object_rater, "rollback"):
+                self._object_rater.rollback()  # the device roster too
             raise
         finally:
             session.close()
@@ -238,10 +244,15 @@ class Worker:
 
     def _batched(self):
         if self._object_rater is None:
-            from .batch import ObjectBatchRater
-
             from ..ops.rate import BatchRater
-            self._object_rater = ObjectBatchRater(BatchRater(self.rater_cfg))
+
+            if self.cfg.resident:
+                from .resident import ResidentBatchRater
+                self._object_rater = ResidentBatchRater(BatchRater(self.rater_cfg),
+                                                        capacity=self.cfg.batchsize)
+            else:
+                from .batch import ObjectBatchRater
+                self._object_rater = ObjectBatchRater(BatchRater(self.rater_cfg))
         return self._object_rater
 
     def _rate_native(self, session, matches, counts) -> List[str]:

@@ -266,7 +266,7 @@ def test_graph_rater_matches_eager(gpu_device):
     off = 0
     for i, m in enumerate([500, 100, 512, 37, 400, 1, 512, 300]):
         if i == 5:
-            gr._bumps = gr.MAX_EPOCH - 2  # the next replays pass the wrap: tags reset
+            gr.clock.bumps = gr.MAX_EPOCH - 2  # the next replays pass the wrap: tags reset
         batch = stream[off:off + m]
         off += m
         got = gr.rate(batch)
