@@ -70,7 +70,7 @@ for task in "$@"; do
           -o run --output-format csv -- $PY "$ROOT/bench.py" --steps 5 --warmup 2) || exit $?
       ;;
     pmc)
-      for set in "FETCH_SIZE WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
+      for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
                  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
                  "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM" \
                  "GRBM_GUI_ACTIVE GRBM_COUNT"; do
@@ -79,6 +79,7 @@ for task in "$@"; do
             -d "$ROOT/gpurun_out/pmc/$name" -o run --output-format csv -- $PY "$ROOT/bench.py" --steps 3 --warmup 1) \
             || exit $?
         $PY scripts/pmc_kernel.py "gpurun_out/pmc/$name/*" rate_dataflow >> gpurun_out/pmc/executor.txt
+        $PY scripts/pmc_kernel.py "gpurun_out/pmc/$name/*" "" >> gpurun_out/pmc/all_kernels.txt
       done
       cat gpurun_out/pmc/executor.txt
       ;;
