@@ -269,11 +269,10 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   prm.epoch = (int32_t)epoch;
   prm.vst = vst.data_ptr<float>();
   if (const char* e = std::getenv("ANA_RATE_IDLE")) prm.idle_spins = std::atoi(e);  // tuning knob
-  if (const char* e = std::getenv("ANA_RATE_DEBUG")) prm.debug_flags = std::atoi(e);  // experiments
-  prm.spec = 0;
-  prm.variant = 0;
-  if (const char* e = std::getenv("ANA_RATE_VARIANT")) prm.variant = std::atoi(e);  // experiments
-  if (const char* e = std::getenv("ANA_RATE_SPEC")) prm.spec = std::atoi(e);
+  prm.local_handoff = 1;
+  if (const char* e = std::getenv("ANA_RATE_LOCAL")) prm.local_handoff = std::atoi(e);  // A/B knob
+  prm.diag = 0;
+  if (const char* e = std::getenv("ANA_RATE_DIAG")) prm.diag = std::atoi(e);  // timing build
   prm.tight_groups = -1;
   if (const char* e = std::getenv("ANA_RATE_TIGHT")) prm.tight_groups = std::atoi(e);
   prm.progress = reinterpret_cast<uint64_t*>((intptr_t)progress);

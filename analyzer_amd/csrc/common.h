@@ -73,11 +73,12 @@ struct RateParams {
   const int32_t* epoch_ptr;    // device: read the epoch here instead (graph replays bump it)
   const float* vst;            // vst_points[tier + 1], kVstTiers entries (device/host memory)
   int32_t idle_spins;          // dataflow: max s_sleep(2) rounds of an idle wave (0 = default)
-  int32_t debug_flags;         // experiments only (ANA_RATE_DEBUG): 2 skip slot outputs, 16/32 NT record/link loads
-  int32_t spec;                // dataflow: speculative one-dependency matches per wave iteration
   int32_t tight_groups;        // dataflow: 2K lanes per match instead of the next power of two
                                // (-1 auto, 0 off, 1 on)
-  int32_t variant;             // dataflow: executor variant for A/B experiments (0 = production)
+  int32_t local_handoff;       // dataflow: a successor held by the producing wave is released
+                               // through an LDS counter, not the global one (ANA_RATE_LOCAL, default 1)
+  int32_t diag;                // dataflow: 1 = the timing build (ANA_RATE_DIAG): wait/iteration
+                               // clocks in ctrl[20..27]
   // Tail signal: once chunks from progress_at on are being claimed (every
   // earlier chunk is claimed, the launch is in its tail), waves store
   // progress_value to *progress (signal memory a side stream waits on with

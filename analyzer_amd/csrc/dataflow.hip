@@ -29,6 +29,12 @@
 //  * Software pipeline, one memory round trip per iteration: this iteration's
 //    granule/link/attribute loads, the next iteration's counter polls and the
 //    next chunk ticket retire in ONE vmcnt(0) wait.
+//  * Local hand-off: when the successor of a published player lies in a chunk
+//    the SAME wave holds, the producer bumps that match's counter in LDS
+//    instead of the global one.  Readiness = polled global count + LDS count,
+//    so the successor is assigned in the very next iteration -- no poll round
+//    trip -- which is what a hot player's chain (consecutive matches of one
+//    player in one chunk: skewed activity) runs on.
 //
 // Claims are monotone per ticket shard and every claimed match is held by a
 // running wave, so the oldest unfinished match is always ready: no deadlock
@@ -124,13 +130,11 @@ struct Batch {
   v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
 };
 
-// V: executor variant for same-process A/B experiments (ANA_RATE_VARIANT);
-// V == 5: software pipeline -- a batch's granules are loaded in one iteration
-// and rated in the next, before that iteration's wait, so the rating math
-// overlaps the next batch's load latency.
-// 0 = the production path.  TELE: K8 fused telemetry compiled in (the plain
-// rating launch leaves it out, which frees the registers its code pins).
-template <int K, int G, int V, bool TELE>
+// TELE: K8 fused telemetry compiled in (the plain rating launch leaves it out,
+// which frees the registers its code pins).  DIAG: the timing build
+// (ANA_RATE_DIAG=1) -- every wave clocks its iterations and its wait with
+// s_memrealtime and adds them to ctrl[20..27] at exit (launch_rate).
+template <int K, int G, bool TELE, bool DIAG>
 __global__ void __launch_bounds__(256)
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
@@ -139,11 +143,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
                      RateParams prm, TelemetryParams tp) {
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
-  // chunks held per wave: kHeld, or 2V for the A/B variants V >= 3 (ANA_RATE_VARIANT)
-  constexpr int kH = V >= 3 && V != 5 ? 2 * V : kHeld;
+  constexpr int kH = kHeld;
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
   __shared__ int32_t lrec[kWavesPerBlock][kH][kChunk * R];
+  // local hand-off counters: increments of each held match's completion count
+  // by publishes of THIS wave (never also added to the global counter)
+  __shared__ uint32_t lloc[kWavesPerBlock][kH][kChunk];
   __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -165,8 +171,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // (ctrl[3] counts retired chunks), so long dependency chains never trip it
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_progress = 0;
-  // experiment: issue priority over co-running kernels (the next window's prepass)
-  if (prm.debug_flags & 8) __builtin_amdgcn_s_setprio(3);
+  const bool local_ok = prm.local_handoff != 0;
+  // hand-off statistics (wave-uniform counts, added to ctrl[26..27] at exit)
+  uint32_t n_local = 0, n_global = 0;
+  uint64_t d_wait = 0, d_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint32_t d_worked = 0, d_groups = 0;
 
   int64_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
   uint64_t pend[kH];   // wave-uniform: stateful matches not yet handed to a group
@@ -180,7 +189,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     need[h] = 0u;
   }
   bool exhausted = false, tk_pending = false;
-  Batch carry;  // V5: the batch loaded last iteration, rated this one (none yet)
   unsigned tk = 0;                 // ticket returned to lane 0
   uint32_t spins = 0, iter = 0;
   // K8 fused mode: telemetry tiles fill the time a wave would spend waiting
@@ -231,24 +239,20 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         const int64_t m = c * cl + lane;
         if (lane < cl && m < M) {
           const int32_t* src = rec + m * R;
-          // experiment flags: 16 = records, 32 = links through non-temporal loads
-          // (read once per window: keep them out of the Infinity Cache)
           if constexpr (R % 4 == 0) {
 #pragma unroll
             for (int k = 0; k < R / 4; ++k) {
-              const v4i* q = reinterpret_cast<const v4i*>(src) + k;
-              const v4i v = (prm.debug_flags & 16) ? __builtin_nontemporal_load(q) : *q;
+              const v4i v = reinterpret_cast<const v4i*>(src)[k];
               r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
             }
           } else {
 #pragma unroll
-            for (int k = 0; k < R; ++k)
-              r[k] = (prm.debug_flags & 16) ? __builtin_nontemporal_load(src + k) : src[k];
+            for (int k = 0; k < R; ++k) r[k] = src[k];
           }
           const v2u* ls = reinterpret_cast<const v2u*>(link + m * S);  // S even: 8-B aligned
 #pragma unroll
           for (int k = 0; k < S / 2; ++k) {
-            const v2u v = (prm.debug_flags & 32) ? __builtin_nontemporal_load(ls + k) : ls[k];
+            const v2u v = ls[k];
             lks[2 * k] = v.x;
             lks[2 * k + 1] = v.y;
           }
@@ -259,13 +263,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // ---------------------------------------------- (2) readiness from the last poll
     uint64_t ready[kH];
 #pragma unroll
-    for (int h = 0; h < kH; ++h) ready[h] = __ballot(dval[h] == need[h]) & pend[h];
+    for (int h = 0; h < kH; ++h) {
+      const uint32_t loc = local_ok && cbase[h] >= 0 ? lloc[wv][h][lane] : 0u;
+      ready[h] = __ballot(dval[h] != kNone && dval[h] + loc == need[h]) & pend[h];
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
 
     // ---------------------------------------------- (3) oldest ready matches -> groups
-    // then, in spare groups, up to prm.spec matches still waiting on ONE
-    // predecessor: their loads race the predecessor's stores and the tag check
-    // accepts them if the stores won (saves the poll round trip on the hop)
     int my_h = -1, my_bit = 0, nassigned = 0;
     // scalar: the sets, chunk bases and counts are wave-uniform; group g of
     // the wave takes the g-th pick (s_ff1 over the set of the oldest chunk)
@@ -298,14 +302,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
     };
     assign(ready, NG);
-    if (prm.spec > 0 && nassigned < NG) {
-      uint64_t cand[kH];
-#pragma unroll
-      for (int h = 0; h < kH; ++h) cand[h] = __ballot(dval[h] + 1u == need[h]) & pend[h];
-      const int lim = nassigned + prm.spec < NG ? nassigned + prm.spec : NG;
-      assign(cand, lim);
-    }
     const bool worked = nassigned > 0;
+    if constexpr (DIAG) {
+      d_worked += worked ? 1u : 0u;
+      d_groups += (uint32_t)nassigned;
+    }
 
     // ---------------------------------------------- (4) this group's loads
     Batch nb;  // any_dup is wave-uniform: a match of this batch names a player twice
@@ -507,9 +508,25 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         __builtin_amdgcn_raw_buffer_store_b128(
             ok ? granule(nsm, stag, nss, succ) : granule(rsmu, stag, rssg, succ),
             rs, off, 0, 16);
-        if (succ != kNoMatch)  // the successor verifies the tags, so no store wait
-          __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+        if (succ != kNoMatch) {  // the successor verifies the tags, so no store wait
+          int lh = -1;
+          if (local_ok) {
+#pragma unroll
+            for (int h = 0; h < kH; ++h)
+              if (cbase[h] >= 0 && (int64_t)succ >= cbase[h] && (int64_t)succ < cbase[h] + cl) lh = h;
+          }
+          if (lh >= 0) {  // held by this wave: release it through LDS, next iteration
+#pragma unroll
+            for (int h = 0; h < kH; ++h)
+              if (h == lh) atomicAdd(&lloc[wv][h][(int)((int64_t)succ - cbase[h])], 1u);
+          } else {
+            __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+          }
+          const uint64_t lb = __ballot(lh >= 0);
+          n_local += (uint32_t)__popcll(lb);
+          n_global += (uint32_t)__popcll(__ballot(true) & ~lb);
+        }
       }
       if (ok && prm.record_first_prior && own) {
         float* fp = first_prior + (int64_t)id * kRowFloats;
@@ -520,7 +537,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       // match's packed 128-B row (ops/rate.py RateResult) keep them from competing
       // with the roster for cache (-6%) and make each match one line (-3%)
       float* const orm = orows + m * orow;  // [s_mu | s_sig | delta | m_mu | m_sig][S], quality, status
-      if (j < S && !(prm.debug_flags & 2)) {
+      if (j < S) {
         __builtin_nontemporal_store(ok ? nsm : NAN, orm + j);
         __builtin_nontemporal_store(ok ? nss : NAN, orm + S + j);
         __builtin_nontemporal_store(ok ? dl : NAN, orm + 2 * S + j);
@@ -538,7 +555,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     ++iter;
 #pragma unroll
     for (int h = 0; h < kH; ++h)
-      if (((pend[h] >> lane) & 1ull) && (!(prm.debug_flags & 4) || (iter & 1u)))
+      if ((pend[h] >> lane) & 1ull)
         dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
 
@@ -555,9 +572,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
     }
 
-    if constexpr (V == 5) rate_batch(carry);
     // ---------------------------------------------- (7) the one wait of the iteration
+    uint64_t d_w0 = 0;
+    if constexpr (DIAG) d_w0 = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (DIAG) d_wait += __builtin_amdgcn_s_memrealtime() - d_w0;
 
     // ---------------------------------------------- (9) install the staged chunk
     if (staging >= 0) {
@@ -590,6 +609,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
 #pragma unroll
       for (int k = 0; k < R; ++k) lrec[wv][staging][lane * R + k] = r[k];
+#pragma unroll
+      for (int h = 0; h < kH; ++h)
+        if (h == staging) lloc[wv][h][lane] = 0u;
       const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
       if (mm < M && est != kRated) {  // no state, no dependencies: finish it now
 #pragma unroll
@@ -608,21 +630,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         }
     }
 
-    if constexpr (V == 5) {
-      // the compiler cannot see the explicit wait above: re-define the loaded values
-      // so the next iteration's use of them carries no vmcnt wait on newer loads
-      asm volatile("" : "+v"(nb.gs), "+v"(nb.gm), "+v"(nb.lk0));
-      carry = nb;
-    } else {
-      rate_batch(nb);
-    }
+    rate_batch(nb);
 
     // ---------------------------------------------- (11) retire finished chunks
     {
       uint32_t retired = 0;
 #pragma unroll
       for (int h = 0; h < kH; ++h)
-        if (cbase[h] >= 0 && pend[h] == 0ull && (V != 5 || __ballot(carry.my_h == h) == 0ull)) {
+        if (cbase[h] >= 0 && pend[h] == 0ull) {
           cbase[h] = -1;
           ++retired;
         }
@@ -635,8 +650,20 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
     for (int h = 0; h < kH; ++h) held |= cbase[h] >= 0;
     if (exhausted && !held && !tk_pending) {
-      if (lane == 0)  // diagnostics: wave iterations (ctrl[15])
+      if (lane == 0) {  // diagnostics: wave iterations (ctrl[15]), hand-offs (ctrl[26..27])
         __hip_atomic_fetch_add((gu32*)&ctrl[15], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((gu32*)&ctrl[26], n_local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add((gu32*)&ctrl[27], n_global, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (DIAG) {
+          // [20] worked iterations, [21] groups assigned, [22..23] wait ticks,
+          // [24..25] wave lifetime ticks (100 MHz s_memrealtime)
+          __hip_atomic_fetch_add((gu32*)&ctrl[20], d_worked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add((gu32*)&ctrl[21], d_groups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[22]), (unsigned long long)d_wait);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[24]),
+                    (unsigned long long)(__builtin_amdgcn_s_memrealtime() - d_start));
+        }
+      }
       if constexpr (TELE) {
         while (!tele_done) {  // leftover telemetry tiles
           const int64_t t = tele_claim();
@@ -673,8 +700,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       if constexpr (TELE) {
         // nothing ready for a while: aggregate a telemetry tile instead of sleeping
-        // (V1: only after 4 idle iterations, so the hand-off path keeps polling)
-        if (!tele_done && (V != 1 || spins >= 4) && (!tp.fused_tail || !held)) {
+        if (!tele_done && (!tp.fused_tail || !held)) {
           const int64_t t = tele_claim();
           if (t >= 0) {
             if (tp.impl) telemetry_tile_mfma<K>(tp, t, lane, tele[wv], &ctrl[13]);
@@ -701,10 +727,13 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   const int64_t M = prm.num_matches;
   // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] retired chunks, [4..11] tickets,
   // [12] telemetry tile ticket, [13] malformed telemetry events, [14] stale reads retried,
-  // [15] wave iterations; [16..18] sticky OR of [0..2] over launches (host clears)
+  // [15] wave iterations; [16..18] sticky OR of [0..2] over launches (host clears);
+  // [20..25] timing build (see the kernel), [26] local / [27] global hand-offs
   // one-wave kernel rather than hipMemsetAsync: a 60-B fill at a 4-B offset becomes two
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
   if (!prm.ctrl_ready) hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, 15);
+  // the diagnostic words are zeroed by every launch (not by the schedule's zeroing)
+  hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 8);
   if (M <= 0) return 0;
   if (prm.chunk_len < 1 || prm.chunk_len > kChunk) return (int)hipErrorInvalidValue;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
@@ -721,39 +750,31 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // with the scalar-bookkeeping executor: 3v3 8 lanes, 5v5 16 lanes (20.0 vs
   // 21.2 ms for 12.5M matches with 10) -> auto = off.
   const bool tight = prm.tight_groups > 0;
-#define ANA_RATE_LAUNCH_V(k, g, v)                                                                 \
-  do {                                                                                             \
-    if (tp.evoff)                                                                                  \
-      hipLaunchKernelGGL((rate_dataflow_kernel<k, g, v, true>), dim3((unsigned)blocks), dim3(256), 0, \
-                         s, rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, \
-                         tp);                                                                      \
-    else                                                                                           \
-      hipLaunchKernelGGL((rate_dataflow_kernel<k, g, v, false>), dim3((unsigned)blocks), dim3(256), 0, \
-                         s, rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, \
-                         tp);                                                                      \
+#define ANA_RATE_LAUNCH_D(k, g, tele, diag)                                                        \
+  hipLaunchKernelGGL((rate_dataflow_kernel<k, g, tele, diag>), dim3((unsigned)blocks), dim3(256), 0, s, \
+                     rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, tp)
+#define ANA_RATE_LAUNCH(k, g)                                      \
+  do {                                                             \
+    if (tp.evoff) ANA_RATE_LAUNCH_D(k, g, true, false);            \
+    else if (prm.diag) ANA_RATE_LAUNCH_D(k, g, false, true);       \
+    else ANA_RATE_LAUNCH_D(k, g, false, false);                    \
   } while (0)
-#define ANA_RATE_LAUNCH(k, g) ANA_RATE_LAUNCH_V(k, g, 0)
   switch (K) {
     case 1: ANA_RATE_LAUNCH(1, 2); break;
     case 2: ANA_RATE_LAUNCH(2, 4); break;
     case 3:
       if (tight) ANA_RATE_LAUNCH(3, 6);
-      else if (prm.variant == 1) ANA_RATE_LAUNCH_V(3, 8, 1);
-      else if (prm.variant == 3) ANA_RATE_LAUNCH_V(3, 8, 3);  // 6 held chunks per wave
-      else if (prm.variant == 4) ANA_RATE_LAUNCH_V(3, 8, 4);  // 8 held chunks per wave
-      else if (prm.variant == 5) ANA_RATE_LAUNCH_V(3, 8, 5);  // software-pipelined rating
       else ANA_RATE_LAUNCH(3, 8);
       break;
     case 4: ANA_RATE_LAUNCH(4, 8); break;
     case 5:
       if (tight) ANA_RATE_LAUNCH(5, 10);
-      else if (prm.variant == 5) ANA_RATE_LAUNCH_V(5, 16, 5);
       else ANA_RATE_LAUNCH(5, 16);
       break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef ANA_RATE_LAUNCH
-#undef ANA_RATE_LAUNCH_V
+#undef ANA_RATE_LAUNCH_D
   return (int)hipGetLastError();
 }
 

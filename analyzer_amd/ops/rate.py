@@ -330,6 +330,28 @@ class BatchRater:
         """Wave iterations of the last executor launch (diagnostics; syncs)."""
         return int(self._ctrl(device)[15].item())
 
+    def handoffs(self, device) -> Tuple[int, int]:
+        """(local, global) dependency hand-offs of the last launch: successors
+        released through the producing wave's LDS counters vs the global ones."""
+        c = self._ctrl(device)[26:28].cpu()
+        return int(c[0]), int(c[1])
+
+    def diag(self, device) -> Dict[str, float]:
+        """Timing-build statistics of the last launch (ANA_RATE_DIAG=1; syncs):
+        wave iterations, the share spent in the iteration's one wait, and the
+        mean iteration time."""
+        c = self._ctrl(device).cpu()
+        u64 = lambda i: int(c[i].item() & 0xffffffff) | (int(c[i + 1].item() & 0xffffffff) << 32)
+        iters = int(c[15]) & 0xffffffff
+        wait, life = u64(22), u64(24)  # 100 MHz ticks, summed over waves
+        loc, glob = int(c[26]) & 0xffffffff, int(c[27]) & 0xffffffff
+        return {"wave_iterations": iters, "worked_iterations": int(c[20]) & 0xffffffff,
+                "groups_assigned": int(c[21]) & 0xffffffff,
+                "wait_fraction": wait / life if life else 0.0,
+                "iteration_us": (life * 0.01 / iters) if iters else 0.0,
+                "wait_us_per_iteration": (wait * 0.01 / iters) if iters else 0.0,
+                "local_handoffs": loc, "global_handoffs": glob}
+
     def telemetry_errors(self, device) -> int:
         """Malformed telemetry events seen by the last fused launch (syncs)."""
         return int(self._ctrl(device)[13].item())

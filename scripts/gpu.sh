@@ -14,8 +14,11 @@
 #   skew       bench.py --skew 2 and 3
 #   dp         bench.py --gpus 2 and 4 on this one GPU (gloo rehearsal of the spawn path)
 #   accuracy   sweep-DP accuracy, 8 ranks x 10M matches over 1M players, sweeps 1,2,4,8
+#   micro      executor hop latency A/B (scripts/tune_rate.py: serial / uniform / skewed, timing build)
 #   prof       rocprofv3 --kernel-trace --stats of config 2
-#   pmc        rocprofv3 --pmc passes over the executor (bench config 2, 3 steps)
+#   pmc        rocprofv3 --pmc passes over the executor (10M-match window, tune_rate.py: one
+#              process, no side-stream waits -- counter collection serialises dispatches, and a
+#              stream wait on the executor's tail signal then never returns)
 #   rerate     config 5 end to end: 1B matches / 10M players, checkpoint + kill + resume
 #   worker     streaming worker on the device (ENGINE=native), memory + sqlite stores
 set -o pipefail
@@ -64,6 +67,14 @@ for task in "$@"; do
       run accuracy/dp4_skew 900 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 4 \
           --players 2e4 --matches-per-rank 2e5 --windows 8 --warm-windows 1 --sweeps 1,2,3,4
       ;;
+    micro)  # executor hop latency: serial chain, uniform window, skewed window (timing build A/B)
+      run micro/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 \
+          --rounds 2 --local 0,1 --diag 0,1
+      run micro/random 300 $PY scripts/tune_rate.py --pattern random --rounds 2 --local 0,1 --diag 0,1
+      run micro/skew2 300 $PY scripts/tune_rate.py --pattern random --skew 2 --rounds 1 --local 0,1 --diag 0,1
+      run micro/skew3 600 $PY scripts/tune_rate.py --pattern random --skew 3 --matches 2000000 --rounds 1 \
+          --local 0,1 --diag 0,1
+      ;;
     prof)
       mkdir -p gpurun_out/prof
       (cd /tmp && run prof/config2 400 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof/config2" \
@@ -76,7 +87,7 @@ for task in "$@"; do
                  "GRBM_GUI_ACTIVE GRBM_COUNT"; do
         name=$(echo $set | cut -d' ' -f1)
         (cd /tmp && run pmc/$name 120 rocprofv3 --pmc $set --kernel-trace --stats \
-            -d "$ROOT/gpurun_out/pmc/$name" -o run --output-format csv -- $PY "$ROOT/bench.py" --steps 3 --warmup 1) \
+            -d "$ROOT/gpurun_out/pmc/$name" -o run --output-format csv -- $PY "$ROOT/scripts/tune_rate.py" --rounds 1) \
             || exit $?
         $PY scripts/pmc_kernel.py "gpurun_out/pmc/$name/*" rate_dataflow >> gpurun_out/pmc/executor.txt
         $PY scripts/pmc_kernel.py "gpurun_out/pmc/$name/*" "" >> gpurun_out/pmc/all_kernels.txt

@@ -1,6 +1,15 @@
 #!/usr/bin/env python3
-"""Time the schedule prepass and the dataflow launch separately for several
-persistent-grid sizes, interleaved in one process (guide §5.4 rule 24)."""
+"""Time the schedule prepass and the dataflow launch separately, A/B-ing
+executor knobs interleaved in one process (guide §5.4 rule 24).
+
+    python scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 \\
+        --local 0,1 --diag 1
+
+patterns: random (uniform players, or ``--skew`` power law), serial (every
+match has the same 2K players: chain depth = M, the pure hop latency), disjoint
+(no player repeats: nothing ever waits).  ``--diag 1`` runs the timing build
+(ANA_RATE_DIAG) and prints the per-iteration wait/iteration clocks.
+"""
 import argparse
 import json
 import os
@@ -16,47 +25,42 @@ from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_str
 
 
 def main():
-    ap = argparse.ArgumentParser()
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--players", type=int, default=1_000_000)
     ap.add_argument("--matches", type=int, default=10_000_000)
     ap.add_argument("--team-size", type=int, default=3)
-    ap.add_argument("--blocks", default="128,256,512,1024,2048")
+    ap.add_argument("--blocks", default="512")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--idle", default="8", help="ANA_RATE_IDLE values (max idle sleep rounds)")
-    ap.add_argument("--debug", default="0", help="ANA_RATE_DEBUG values (experiments)")
-    ap.add_argument("--spec", default="0", help="ANA_RATE_SPEC values (speculative matches/iteration)")
     ap.add_argument("--tight", default="-1", help="ANA_RATE_TIGHT values (2K lanes per match; -1 auto)")
-    ap.add_argument("--variant", default="0", help="ANA_RATE_VARIANT values (executor A/B variants)")
-    ap.add_argument("--packed", default="1", help="output layout: 1 packed rows, 0 separate arrays")
-    ap.add_argument("--hot", type=float, default=0.0)
+    ap.add_argument("--local", default="1", help="ANA_RATE_LOCAL values (LDS local hand-off)")
+    ap.add_argument("--diag", default="0", help="ANA_RATE_DIAG values (timing build)")
+    ap.add_argument("--skew", type=int, default=1)
     ap.add_argument("--rated", type=float, default=1.0,
                     help="fraction of players with stored ratings (1.0 = steady state, no seeding)")
     ap.add_argument("--pattern", default="random", choices=["random", "serial", "disjoint"])
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     P, M, K = args.players, args.matches, args.team_size
-    rec = make_stream(StreamSpec(team_size=K, seed=5, p_hot=args.hot, p_afk=0.0), M, P, device=dev)
+    rec = make_stream(StreamSpec(team_size=K, seed=5, p_afk=0.0, skew=args.skew), M, P, device=dev)
     if args.pattern == "serial":      # every match has the same 2K players: chain depth = M
         rec[:, :2 * K] = torch.arange(2 * K, dtype=torch.int32, device=dev)
     elif args.pattern == "disjoint":  # no player repeats: nothing ever waits
         assert P >= 2 * K * M, "disjoint pattern needs players >= 2K * matches"
         rec[:, :2 * K] = (torch.arange(M, dtype=torch.int32, device=dev)[:, None] * (2 * K)
                           + torch.arange(2 * K, dtype=torch.int32, device=dev)[None, :])
-    outs = {1: RateResult.allocate(M, K, dev), 0: RateResult.allocate(M, K, dev, packed=False)}
+    out = RateResult.allocate(M, K, dev)
     results = {}
+    combos = [(int(b), int(i), int(t), int(lo), int(d)) for b in args.blocks.split(",")
+              for i in args.idle.split(",") for t in args.tight.split(",")
+              for lo in args.local.split(",") for d in args.diag.split(",")]
     for rnd in range(args.rounds):
-        for b, idle, dbg, sp, tg, pk, va in [(int(x), int(y), int(z), int(w), int(v), int(u), int(t))
-                                             for x in args.blocks.split(",") for y in args.idle.split(",")
-                                             for z in args.debug.split(",") for w in args.spec.split(",")
-                                             for v in args.tight.split(",") for u in args.packed.split(",")
-                                             for t in args.variant.split(",")]:
-            out = outs[pk]
+        for b, idle, tg, loc, dg in combos:
             os.environ["ANA_RATE_TIGHT"] = str(tg)
             os.environ["ANA_RATE_IDLE"] = str(idle)
-            os.environ["ANA_RATE_DEBUG"] = str(dbg)
-            os.environ["ANA_RATE_SPEC"] = str(sp)
-            os.environ["ANA_RATE_VARIANT"] = str(va)
-            key = "b%d/i%d/d%d/s%d/t%d/p%d/v%d" % (b, idle, dbg, sp, tg, pk, va)
+            os.environ["ANA_RATE_LOCAL"] = str(loc)
+            os.environ["ANA_RATE_DIAG"] = str(dg)
+            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg)
             roster = make_roster(RosterSpec(num_players=P, seed=1, p_rated=args.rated,
                                             p_mode_rated=args.rated), device=dev)
             br = BatchRater(blocks=b)
@@ -71,15 +75,23 @@ def main():
             t2 = time.perf_counter()
             br.check_errors(dev)
             stale = br.stale_retries(dev)
-            iters = br.iterations(dev)
-            results.setdefault(key, []).append(((t1 - t0) * 1e3, (t2 - t1) * 1e3))
-            print("round %d %s schedule %7.2f ms rate %8.2f ms stale retries %d iterations %d "
-                  "(%.2f matches/iteration)" % (rnd, key, (t1 - t0) * 1e3, (t2 - t1) * 1e3, stale,
-                                                iters, M / max(iters, 1)), flush=True)
-    summary = {b: {"schedule_ms_min": min(x[0] for x in v), "rate_ms_min": min(x[1] for x in v),
-                   "rate_ms_median": sorted(x[1] for x in v)[len(v) // 2]} for b, v in results.items()}
-    print(json.dumps({"pattern": args.pattern, "players": P, "matches": M, "team_size": K, "hot": args.hot,
-                      "by_blocks": summary}))
+            d = br.diag(dev)
+            results.setdefault(key, []).append(((t1 - t0) * 1e3, (t2 - t1) * 1e3, d))
+            line = ("round %d %s schedule %7.2f ms rate %8.2f ms stale %d iterations %d (%.2f matches/it)"
+                    " hand-offs local %d global %d" % (rnd, key, (t1 - t0) * 1e3, (t2 - t1) * 1e3, stale,
+                                                       d["wave_iterations"], M / max(d["wave_iterations"], 1),
+                                                       d["local_handoffs"], d["global_handoffs"]))
+            if dg:
+                line += " | iteration %.3f us, wait %.3f us (%.0f%%)" % (
+                    d["iteration_us"], d["wait_us_per_iteration"], 100 * d["wait_fraction"])
+            if args.pattern == "serial":
+                line += " | %.3f us per hop" % ((t2 - t1) * 1e6 / M)
+            print(line, flush=True)
+    summary = {k: {"schedule_ms_min": min(x[0] for x in v), "rate_ms_min": min(x[1] for x in v),
+                   "rate_ms_median": sorted(x[1] for x in v)[len(v) // 2], "diag_last": v[-1][2]}
+               for k, v in results.items()}
+    print(json.dumps({"pattern": args.pattern, "players": P, "matches": M, "team_size": K,
+                      "skew": args.skew, "by_config": summary}))
 
 
 if __name__ == "__main__":

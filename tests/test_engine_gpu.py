@@ -116,26 +116,39 @@ def test_device_repeat_launch_deterministic(gpu_device):
     assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32))
 
 
-@pytest.mark.parametrize("K,P,M", [(3, 16, 4000), (3, 100000, 1000000), (5, 2000, 200000)])
-def test_pipelined_executor_bit_identical(gpu_device, monkeypatch, K, P, M):
-    """ANA_RATE_VARIANT=5 (each batch rated one iteration after its loads, under the
-    next batch's load latency) must give the production executor's exact bits."""
+@pytest.mark.parametrize("K,P,M,skew", [(3, 16, 4000, 1), (3, 100000, 1000000, 1), (5, 2000, 200000, 1),
+                                        (3, 100000, 300000, 3)])
+def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K, P, M, skew):
+    """The LDS local hand-off (ANA_RATE_LOCAL) and the timing build
+    (ANA_RATE_DIAG) change only WHEN a match runs, never its result: all three
+    executors give the same bits, and hot chains (16 players, skewed activity)
+    actually take the local path."""
     rs = RosterSpec(num_players=P, seed=P + 3)
-    rec = make_stream(StreamSpec(team_size=K, seed=M + 1), M, P, K=K, device=gpu_device)
+    rec = make_stream(StreamSpec(team_size=K, seed=M + 1, skew=skew), M, P, K=K, device=gpu_device)
     outs = []
-    for variant in ("0", "5"):
-        monkeypatch.setenv("ANA_RATE_VARIANT", variant)
+    for local, diag in (("0", "0"), ("1", "0"), ("1", "1")):
+        monkeypatch.setenv("ANA_RATE_LOCAL", local)
+        monkeypatch.setenv("ANA_RATE_DIAG", diag)
         ro = make_roster(rs, device=gpu_device)
         rater = R.BatchRater()
         res = rater.rate(ro, rec, K)
         assert int(rater.error_flags(gpu_device).sum()) == 0
+        nl, ng = rater.handoffs(gpu_device)
+        if local == "0":
+            assert nl == 0
+        elif P <= 16 or skew > 1:
+            assert nl > 0, (nl, ng)
+        if diag == "1":
+            d = rater.diag(gpu_device)
+            assert d["wave_iterations"] > 0 and 0.0 < d["wait_fraction"] < 1.0, d
         outs.append((ro.state.cpu(), res.s_mu.cpu(), res.status.cpu(), res.quality.cpu()))
-    a, b = outs
-    assert torch.equal(a[0][:, 0::2].contiguous().view(torch.int32),
-                       b[0][:, 0::2].contiguous().view(torch.int32))
-    assert torch.equal(a[1].view(torch.int32), b[1].view(torch.int32))
-    assert torch.equal(a[2], b[2])
-    assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32))
+    for b in outs[1:]:
+        a = outs[0]
+        assert torch.equal(a[0][:, 0::2].contiguous().view(torch.int32),
+                           b[0][:, 0::2].contiguous().view(torch.int32))
+        assert torch.equal(a[1].view(torch.int32), b[1].view(torch.int32))
+        assert torch.equal(a[2], b[2])
+        assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32))
 
 
 @pytest.mark.parametrize("n,bits", [(1, 8), (4095, 20), (4097, 12), (1_000_003, 20), (300_000, 32)])
