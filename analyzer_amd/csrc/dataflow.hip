@@ -174,7 +174,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   const bool local_ok = prm.local_handoff != 0;
   // hand-off statistics (wave-uniform counts, added to ctrl[26..27] at exit)
   uint32_t n_local = 0, n_global = 0;
-  uint64_t d_wait = 0, d_start = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+  // timing build: clocks of the iterations that rated something, split at the wait
+  uint64_t d_issue = 0, d_wait = 0, d_after = 0, d_it0 = 0;
   uint32_t d_worked = 0, d_groups = 0;
 
   int64_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
@@ -205,6 +206,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   const int cl = prm.chunk_len;  // matches per ticket (<= kChunk lanes)
 
   for (;;) {
+    if constexpr (DIAG) d_it0 = __builtin_amdgcn_s_memrealtime();
     // ---------------------------------------------- (1) a ticket came back: stage its chunk
     int staging = -1;
     int32_t r[R];
@@ -573,10 +575,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
 
     // ---------------------------------------------- (7) the one wait of the iteration
-    uint64_t d_w0 = 0;
+    uint64_t d_w0 = 0, d_w1 = 0;
     if constexpr (DIAG) d_w0 = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (DIAG) d_wait += __builtin_amdgcn_s_memrealtime() - d_w0;
+    if constexpr (DIAG) d_w1 = __builtin_amdgcn_s_memrealtime();
 
     // ---------------------------------------------- (9) install the staged chunk
     if (staging >= 0) {
@@ -631,6 +633,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
 
     rate_batch(nb);
+    if constexpr (DIAG) {
+      if (worked) {
+        d_issue += d_w0 - d_it0;
+        d_wait += d_w1 - d_w0;
+        d_after += __builtin_amdgcn_s_memrealtime() - d_w1;
+      }
+    }
 
     // ---------------------------------------------- (11) retire finished chunks
     {
@@ -655,13 +664,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         __hip_atomic_fetch_add((gu32*)&ctrl[26], n_local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add((gu32*)&ctrl[27], n_global, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (DIAG) {
-          // [20] worked iterations, [21] groups assigned, [22..23] wait ticks,
-          // [24..25] wave lifetime ticks (100 MHz s_memrealtime)
+          // iterations that rated something: [20] count, [21] groups assigned, and
+          // 100 MHz s_memrealtime ticks [22..23] issue (top of the loop -> the wait),
+          // [24..25] the wait, [28..29] after it (rating, publish, bookkeeping)
           __hip_atomic_fetch_add((gu32*)&ctrl[20], d_worked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_fetch_add((gu32*)&ctrl[21], d_groups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[22]), (unsigned long long)d_wait);
-          atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[24]),
-                    (unsigned long long)(__builtin_amdgcn_s_memrealtime() - d_start));
+          atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[22]), (unsigned long long)d_issue);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[24]), (unsigned long long)d_wait);
+          atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[28]), (unsigned long long)d_after);
         }
       }
       if constexpr (TELE) {
@@ -728,12 +738,12 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] retired chunks, [4..11] tickets,
   // [12] telemetry tile ticket, [13] malformed telemetry events, [14] stale reads retried,
   // [15] wave iterations; [16..18] sticky OR of [0..2] over launches (host clears);
-  // [20..25] timing build (see the kernel), [26] local / [27] global hand-offs
+  // [20..25], [28..29] timing build (see the kernel), [26] local / [27] global hand-offs
   // one-wave kernel rather than hipMemsetAsync: a 60-B fill at a 4-B offset becomes two
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
   if (!prm.ctrl_ready) hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, 15);
   // the diagnostic words are zeroed by every launch (not by the schedule's zeroing)
-  hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 8);
+  hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 12);
   if (M <= 0) return 0;
   if (prm.chunk_len < 1 || prm.chunk_len > kChunk) return (int)hipErrorInvalidValue;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;

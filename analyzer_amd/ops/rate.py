@@ -337,20 +337,18 @@ class BatchRater:
         return int(c[0]), int(c[1])
 
     def diag(self, device) -> Dict[str, float]:
-        """Timing-build statistics of the last launch (ANA_RATE_DIAG=1; syncs):
-        wave iterations, the share spent in the iteration's one wait, and the
-        mean iteration time."""
-        c = self._ctrl(device).cpu()
-        u64 = lambda i: int(c[i].item() & 0xffffffff) | (int(c[i + 1].item() & 0xffffffff) << 32)
-        iters = int(c[15]) & 0xffffffff
-        wait, life = u64(22), u64(24)  # 100 MHz ticks, summed over waves
-        loc, glob = int(c[26]) & 0xffffffff, int(c[27]) & 0xffffffff
-        return {"wave_iterations": iters, "worked_iterations": int(c[20]) & 0xffffffff,
-                "groups_assigned": int(c[21]) & 0xffffffff,
-                "wait_fraction": wait / life if life else 0.0,
-                "iteration_us": (life * 0.01 / iters) if iters else 0.0,
-                "wait_us_per_iteration": (wait * 0.01 / iters) if iters else 0.0,
-                "local_handoffs": loc, "global_handoffs": glob}
+        """Timing-build statistics of the last launch (ANA_RATE_DIAG=1; syncs).
+        Over the wave iterations that rated something: the mean time from the
+        top of the loop to the iteration's one wait (issue), in the wait, and
+        after it (rating, publish, bookkeeping), in microseconds."""
+        c = [int(x) & 0xffffffff for x in self._ctrl(device).cpu().tolist()]
+        u64 = lambda i: c[i] | (c[i + 1] << 32)
+        worked = c[20]
+        per = (lambda t: t * 0.01 / worked) if worked else (lambda t: 0.0)  # 100 MHz ticks -> us
+        return {"wave_iterations": c[15], "worked_iterations": worked, "groups_assigned": c[21],
+                "matches_per_worked_iteration": c[21] / worked if worked else 0.0,
+                "issue_us": per(u64(22)), "wait_us": per(u64(24)), "after_us": per(u64(28)),
+                "local_handoffs": c[26], "global_handoffs": c[27]}
 
     def telemetry_errors(self, device) -> int:
         """Malformed telemetry events seen by the last fused launch (syncs)."""

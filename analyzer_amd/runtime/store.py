@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import sqlite3
 from dataclasses import dataclass
+from operator import attrgetter
 from typing import Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 from ..config import TRACK_COLUMNS
@@ -73,10 +74,16 @@ SCHEMA = [
 
 
 # ---------------------------------------------------------------- snapshots
+# attrgetter: one C call per object instead of a Python generator per column
+_get_part = attrgetter(*PARTICIPANT_WRITE_COLS)
+_get_item = attrgetter(*ITEM_WRITE_COLS)
+_get_player = attrgetter(*PLAYER_RATING_COLS)
+
+
 def _snap_match(m: Match) -> tuple:
-    return (m.trueskill_quality,
-            [tuple(getattr(p, c) for c in PARTICIPANT_WRITE_COLS) for p in m.participants],
-            [tuple(getattr(p.participant_items[0], c) for c in ITEM_WRITE_COLS) for p in m.participants])
+    parts = m.participants
+    return (m.trueskill_quality, [_get_part(p) for p in parts],
+            [_get_item(p.participant_items[0]) for p in parts])
 
 
 def _restore_match(m: Match, snap: tuple) -> None:
@@ -91,7 +98,7 @@ def _restore_match(m: Match, snap: tuple) -> None:
 
 
 def _snap_player(pl: Player) -> tuple:
-    return tuple(getattr(pl, c) for c in PLAYER_RATING_COLS)
+    return _get_player(pl)
 
 
 def _restore_player(pl: Player, snap: tuple) -> None:
@@ -108,10 +115,14 @@ class _SessionBase:
         self.closed = False
 
     def _track(self, m: Match) -> None:
-        self._match_snaps.setdefault(id(m), (m, _snap_match(m)))
+        ms = self._match_snaps
+        if id(m) not in ms:
+            ms[id(m)] = (m, _snap_match(m))
+        ps = self._player_snaps
         for p in m.participants:
             pl = p.player[0]
-            self._player_snaps.setdefault(id(pl), (pl, _snap_player(pl)))
+            if id(pl) not in ps:
+                ps[id(pl)] = (pl, _get_player(pl))
 
     def savepoint(self, m: Match) -> tuple:
         """Snapshot of one match and its players (for per-match quarantine)."""

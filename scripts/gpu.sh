@@ -69,11 +69,10 @@ for task in "$@"; do
       ;;
     micro)  # executor hop latency: serial chain, uniform window, skewed window (timing build A/B)
       run micro/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 \
-          --rounds 2 --local 0,1 --diag 0,1
-      run micro/random 300 $PY scripts/tune_rate.py --pattern random --rounds 2 --local 0,1 --diag 0,1
-      run micro/skew2 300 $PY scripts/tune_rate.py --pattern random --skew 2 --rounds 1 --local 0,1 --diag 0,1
+          --rounds 2 --blocks ${MICRO_BLOCKS:-8,512} --local ${MICRO_LOCAL:-0,1} --diag 0,1
+      run micro/random 300 $PY scripts/tune_rate.py --pattern random --rounds 2 --local ${MICRO_LOCAL:-0,1} --diag 0,1
       run micro/skew3 600 $PY scripts/tune_rate.py --pattern random --skew 3 --matches 2000000 --rounds 1 \
-          --local 0,1 --diag 0,1
+          --blocks ${MICRO_BLOCKS:-8,512} --local 1 --diag 0,1
       ;;
     prof)
       mkdir -p gpurun_out/prof

@@ -82,8 +82,9 @@ def main():
                                                        d["wave_iterations"], M / max(d["wave_iterations"], 1),
                                                        d["local_handoffs"], d["global_handoffs"]))
             if dg:
-                line += " | iteration %.3f us, wait %.3f us (%.0f%%)" % (
-                    d["iteration_us"], d["wait_us_per_iteration"], 100 * d["wait_fraction"])
+                line += " | worked iterations %d (%.2f matches each): issue %.3f + wait %.3f + after %.3f us" % (
+                    d["worked_iterations"], d["matches_per_worked_iteration"], d["issue_us"], d["wait_us"],
+                    d["after_us"])
             if args.pattern == "serial":
                 line += " | %.3f us per hop" % ((t2 - t1) * 1e6 / M)
             print(line, flush=True)
