@@ -122,7 +122,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 // One wave iteration's assignment: per lane, its group's match and the
 // participant's slot facts and granules (section 4 of the executor loop).
 struct Batch {
-  int64_t m = 0;
+  int32_t m = 0;
   int my_h = -1, my_bit = 0, mode = 0, n0 = 0, n1 = 0, rank0 = 1, rank1 = 1, first = 0, prevdup = -1;
   int32_t id = -1;
   bool inr = false, islast = false, own = false, any_dup = false;
@@ -150,6 +150,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // local hand-off counters: increments of each held match's completion count
   // by publishes of THIS wave (never also added to the global counter)
   __shared__ uint32_t lloc[kWavesPerBlock][kH][kChunk];
+  // this iteration's pick per group: {match index, slot << 8 | lane in chunk}
+  __shared__ uint2 lpick[kWavesPerBlock][NG];
   __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -178,7 +180,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   uint64_t d_issue = 0, d_wait = 0, d_after = 0, d_it0 = 0;
   uint32_t d_worked = 0, d_groups = 0;
 
-  int64_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
+  int32_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
+                       // (a window has < 2^28 slots, so match indices fit int32)
   uint64_t pend[kH];   // wave-uniform: stateful matches not yet handed to a group
   uint32_t dval[kH];   // per lane: completion counter of match cbase+lane, as last polled
   uint32_t need[kH];   // per lane: the count at which that match is ready
@@ -237,7 +240,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           if (cbase[h] < 0) staging = h;
 #pragma unroll
         for (int h = 0; h < kH; ++h)
-          if (h == staging) cbase[h] = c * cl;
+          if (h == staging) cbase[h] = (int32_t)(c * cl);
         const int64_t m = c * cl + lane;
         if (lane < cl && m < M) {
           const int32_t* src = rec + m * R;
@@ -271,39 +274,37 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
 
-    // ---------------------------------------------- (3) oldest ready matches -> groups
+    // ---------------------------------------------- (3) ready matches -> groups
+    // Within a chunk, lane b's rank among the ready bits below it (mbcnt) is the
+    // group it goes to: lane b writes its match into the wave's LDS pick list at
+    // nassigned + rank, and group g reads entry g.  A handful of instructions
+    // per chunk, where a scalar loop per picked match (~600 static instructions,
+    // oldest chunk first) sat on every hop.  Chunks go in slot order: a wave
+    // rarely has more ready matches than groups (2-3.4 per iteration on the
+    // bench), so age order buys nothing measurable.
     int my_h = -1, my_bit = 0, nassigned = 0;
-    // scalar: the sets, chunk bases and counts are wave-uniform; group g of
-    // the wave takes the g-th pick (s_ff1 over the set of the oldest chunk)
-    auto assign = [&](uint64_t (&sets)[kH], int limit) {
 #pragma unroll
-      for (int pass = 0; pass < kH; ++pass) {
-        int best = -1;
-        int64_t bb = 0;
-#pragma unroll
-        for (int h = 0; h < kH; ++h)
-          if (sets[h] && (best < 0 || cbase[h] < bb)) { best = h; bb = cbase[h]; }
-        if (best < 0 || nassigned >= limit) break;
-        uint64_t rdy = 0;
-#pragma unroll
-        for (int h = 0; h < kH; ++h) if (h == best) rdy = sets[h];
-        uint64_t taken = 0;
-        while (rdy != 0ull && nassigned < limit) {
-          const int b = __builtin_ctzll(rdy);
-          rdy &= rdy - 1ull;
-          taken |= 1ull << b;
-          if (g == nassigned) {
-            my_h = best;
-            my_bit = b;
-          }
-          ++nassigned;
-        }
-#pragma unroll
-        for (int h = 0; h < kH; ++h)
-          if (h == best) { pend[h] &= ~taken; sets[h] = 0ull; }
+    for (int h = 0; h < kH; ++h) {
+      const uint64_t rdy = ready[h];
+      if (rdy != 0ull && nassigned < NG) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(rdy >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rdy, 0u));
+        const bool mine = ((rdy >> lane) & 1ull) && nassigned + (int)below < NG;
+        if (mine)
+          lpick[wv][nassigned + (int)below] =
+              make_uint2((uint32_t)(cbase[h] + lane), ((uint32_t)h << 8) | (uint32_t)lane);
+        const uint64_t taken = __ballot(mine);
+        pend[h] &= ~taken;
+        nassigned += __popcll(taken);
       }
-    };
-    assign(ready, NG);
+    }
+    int32_t my_m = 0;
+    if (g < nassigned) {
+      const uint2 pk = lpick[wv][g];
+      my_m = (int32_t)pk.x;
+      my_h = (int)(pk.y >> 8);
+      my_bit = (int)(pk.y & 255u);
+    }
     const bool worked = nassigned > 0;
     if constexpr (DIAG) {
       d_worked += worked ? 1u : 0u;
@@ -316,10 +317,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     nb.my_bit = my_bit;
     nb.first = j;
     if (my_h >= 0) {
-      int64_t cb = 0;
-#pragma unroll
-      for (int h = 0; h < kH; ++h) if (h == my_h) cb = cbase[h];
-      const int64_t m = cb + my_bit;
+      const int32_t m = my_m;
       nb.m = m;
       const int32_t* lr = &lrec[wv][my_h][my_bit * R];
       const uint32_t m0 = (uint32_t)lr[S], m1 = (uint32_t)lr[S + 1];
@@ -368,7 +366,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     auto rate_batch = [&](const Batch& bt) {
     int my_h = bt.my_h;
     const int my_bit = bt.my_bit;
-    const int64_t m = bt.m;
+    const int32_t m = bt.m;
     const int mode = bt.mode, n0 = bt.n0, n1 = bt.n1, rank0 = bt.rank0, rank1 = bt.rank1;
     const int first = bt.first, prevdup = bt.prevdup;
     const int32_t id = bt.id;
@@ -515,12 +513,12 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           if (local_ok) {
 #pragma unroll
             for (int h = 0; h < kH; ++h)
-              if (cbase[h] >= 0 && (int64_t)succ >= cbase[h] && (int64_t)succ < cbase[h] + cl) lh = h;
+              if (cbase[h] >= 0 && (int32_t)succ >= cbase[h] && (int32_t)succ < cbase[h] + cl) lh = h;
           }
           if (lh >= 0) {  // held by this wave: release it through LDS, next iteration
 #pragma unroll
             for (int h = 0; h < kH; ++h)
-              if (h == lh) atomicAdd(&lloc[wv][h][(int)((int64_t)succ - cbase[h])], 1u);
+              if (h == lh) atomicAdd(&lloc[wv][h][(int32_t)succ - cbase[h]], 1u);
           } else {
             __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -538,7 +536,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       // output records are a write-once stream: non-temporal stores into the
       // match's packed 128-B row (ops/rate.py RateResult) keep them from competing
       // with the roster for cache (-6%) and make each match one line (-3%)
-      float* const orm = orows + m * orow;  // [s_mu | s_sig | delta | m_mu | m_sig][S], quality, status
+      float* const orm = orows + (int64_t)m * orow;  // [s_mu | s_sig | delta | m_mu | m_sig][S], quality, status
       if (j < S) {
         __builtin_nontemporal_store(ok ? nsm : NAN, orm + j);
         __builtin_nontemporal_store(ok ? nss : NAN, orm + S + j);
@@ -705,7 +703,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
         for (int h = 0; h < kH; ++h)
           if (cbase[h] >= 0 && ((pend[h] >> lane) & 1ull))
-            reinterpret_cast<uint8_t*>(orows + (cbase[h] + lane) * orow + 5 * S + 1)[0] = kNotProcessed;
+            reinterpret_cast<uint8_t*>(orows + (int64_t)(cbase[h] + lane) * orow + 5 * S + 1)[0] = kNotProcessed;
         return;  // give up: the host sees ctrl[1] and raises
       }
       if constexpr (TELE) {
