@@ -510,15 +510,17 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
             rs, off, 0, 16);
         if (succ != kNoMatch) {  // the successor verifies the tags, so no store wait
           int lh = -1;
+          int32_t lcb = 0;
           if (local_ok) {
 #pragma unroll
             for (int h = 0; h < kH; ++h)
-              if (cbase[h] >= 0 && (int32_t)succ >= cbase[h] && (int32_t)succ < cbase[h] + cl) lh = h;
+              if (cbase[h] >= 0 && (int32_t)succ >= cbase[h] && (int32_t)succ < cbase[h] + cl) {
+                lh = h;
+                lcb = cbase[h];
+              }
           }
           if (lh >= 0) {  // held by this wave: release it through LDS, next iteration
-#pragma unroll
-            for (int h = 0; h < kH; ++h)
-              if (h == lh) atomicAdd(&lloc[wv][h][(int32_t)succ - cbase[h]], 1u);
+            atomicAdd(&lloc[wv][0][0] + lh * kChunk + ((int32_t)succ - lcb), 1u);
           } else {
             __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
