@@ -62,8 +62,47 @@ class ResidentRoster:
         self.device = torch.device(device)
         self.roster = R.Roster.empty(max(1, int(capacity)), self.device)
         self.rows: Dict[str, int] = {}
+        self.by_key = np.full(0, -1, dtype=np.int64)  # integer store key -> row (columnar stores)
         self.n = 0
         self.generation = 0  # bumped when the tensors move (graphs must be re-captured)
+
+    def rows_for_keys(self, keys: np.ndarray, fetch) -> np.ndarray:
+        """Rows of integer store keys (unique); ``fetch(new_keys)`` returns the
+        stored (ratings [n, 14], attributes [n, 3]) of keys not seen before."""
+        keys = np.asarray(keys, dtype=np.int64)
+        if keys.size == 0:
+            return keys
+        top = int(keys.max()) + 1
+        if top > self.by_key.size:
+            grown = np.full(max(top, 2 * self.by_key.size), -1, dtype=np.int64)
+            grown[:self.by_key.size] = self.by_key
+            self.by_key = grown
+        rows = self.by_key[keys]
+        new = rows < 0
+        if new.any():
+            nk = keys[new]
+            nr = self.n + np.arange(nk.size)
+            self.by_key[nk] = nr
+            rows[new] = nr
+            ratings, attrs = fetch(nk)
+            self._upload_arrays(np.asarray(ratings, dtype=np.float64), np.asarray(attrs, dtype=np.float64))
+        return rows
+
+    def _upload_arrays(self, vals: np.ndarray, attrs: np.ndarray) -> None:
+        """Append rows from stored ratings [k, 14] (NaN = NULL) and attributes [k, 3]."""
+        base, k = self.n, vals.shape[0]
+        if base + k > self.capacity:
+            self._grow(base + k)
+        st = np.zeros((k, 32), dtype=np.float32)
+        st[:, 0::2] = np.nan
+        mu = vals[:, 0::2]
+        st[:, 0:28:4] = mu
+        st[:, 2:28:4] = np.where(np.isnan(mu), np.nan, vals[:, 1::2])
+        at = np.zeros((k, 4), dtype=np.float32)
+        at[:, :3] = attrs
+        self.roster.state[base:base + k].copy_(torch.from_numpy(st))
+        self.roster.attrs[base:base + k].copy_(torch.from_numpy(at))
+        self.n = base + k
 
     @property
     def capacity(self) -> int:
@@ -95,20 +134,10 @@ class ResidentRoster:
         self.generation += 1
 
     def _upload(self, new: Sequence) -> None:
-        base, k = self.n, len(new)
-        if base + k > self.capacity:
-            self._grow(base + k)
+        k = len(new)
         vals = np.array([_get_ratings(pl) for pl in new], dtype=np.float64).reshape(k, len(RATING_COLS))
-        st = np.zeros((k, 32), dtype=np.float32)
-        st[:, 0::2] = np.nan
-        mu = vals[:, 0::2]
-        st[:, 0:28:4] = mu
-        st[:, 2:28:4] = np.where(np.isnan(mu), np.nan, vals[:, 1::2])
-        at = np.zeros((k, 4), dtype=np.float32)
-        at[:, :3] = np.array([_get_attrs(pl) for pl in new], dtype=np.float64).reshape(k, 3)
-        self.roster.state[base:base + k].copy_(torch.from_numpy(st))
-        self.roster.attrs[base:base + k].copy_(torch.from_numpy(at))
-        self.n = base + k
+        attrs = np.array([_get_attrs(pl) for pl in new], dtype=np.float64).reshape(k, 3)
+        self._upload_arrays(vals, attrs)
 
 
 def team_size(matches: Sequence[Match]) -> int:
@@ -230,6 +259,78 @@ class ResidentBatchRater:
         if self.device.type == "cuda":
             self.rater.check_errors(self.device)
         return st
+
+    def rate_batch(self, batch, fetch, telemetry=None) -> np.ndarray:
+        """Rate a columnar ``MatchBatch`` (runtime/columnar.py) in order and fill
+        its result columns; ``fetch(keys)`` gives the stored ratings of players
+        the resident roster has not seen.  Returns the status per match."""
+        from .columnar import RATED
+
+        M, K = len(batch), batch.K
+        if M == 0:
+            batch.status = np.zeros(0, dtype=np.uint8)
+            return batch.status
+        if K > MAX_TEAM:
+            raise ValueError("teams of %d players exceed the batched engine (max %d)" % (K, MAX_TEAM))
+        keys = batch.player
+        valid = keys >= 0
+        uniq, inv = np.unique(keys[valid], return_inverse=True)
+        rows_u = self.resident.rows_for_keys(uniq, fetch)
+        slot = np.full(keys.shape, -1, dtype=np.int64)
+        slot[valid] = rows_u[inv]
+        S = 2 * K
+        rec = np.empty((M, S + 2), dtype=np.int64)
+        rec[:, :S] = slot.reshape(M, S)
+        rec[:, S], rec[:, S + 1] = batch.record_meta()
+        rec_t = torch.from_numpy(rec.astype(np.uint32).view(np.int32)).to(self.device, non_blocking=True)
+        roster = self.resident.roster
+        idx = torch.from_numpy(rows_u).to(self.device, non_blocking=True)
+        self._undo = (idx, roster.state.index_select(0, idx)) if rows_u.size else None
+        stats = None
+        if telemetry is not None:
+            from ..ops.telemetry import allocate_stats, make_telemetry
+            tel = make_telemetry(telemetry, rec_t, K)
+            stats = allocate_stats(M, K, self.device)
+            res = self._eager(rec_t, K, (tel.evoff, tel.events, stats))
+        else:
+            g = self._graph(K, M) if self.use_graphs else None
+            res = g.rate(rec_t) if g is not None else self._eager(rec_t, K, None)
+        packed = res.packed.cpu().numpy()
+        final = roster.state.index_select(0, idx).cpu().numpy() if rows_u.size else None
+        if self.device.type == "cuda":
+            self.rater.check_errors(self.device)
+        status = packed.view(np.uint8)[:, 4 * (5 * S + 1)].copy()
+        batch.status = status
+        batch.quality = packed[:, 5 * S].astype(np.float64)
+        shape = (M, 2, K)
+        batch.s_mu, batch.s_sig, batch.delta, batch.m_mu, batch.m_sig = (
+            packed[:, f * S:(f + 1) * S].astype(np.float64).reshape(shape) for f in range(5))
+        if stats is not None:
+            batch.stats = stats.cpu().double().numpy().reshape(M, 2, K, -1)
+        # final ratings of the players of rated matches, on the tracks those matches touched
+        rated = status == RATED
+        touched = np.zeros((uniq.size, 7), dtype=bool)
+        if rated.any():
+            pos = np.full(keys.shape, -1, dtype=np.int64)
+            pos[valid] = inv
+            pr = pos[rated]                                   # [R, 2, K]
+            md = np.broadcast_to(batch.mode[rated][:, None, None], pr.shape)
+            ok = pr >= 0
+            touched[pr[ok], 0] = True
+            touched[pr[ok], 1 + md[ok]] = True
+        has = touched.any(axis=1)
+        batch.final_keys = uniq[has]
+        if final is not None and has.any():
+            f = final[has].astype(np.float64)
+            vals = np.empty((f.shape[0], 14))
+            vals[:, 0::2] = f[:, 0:28:4]
+            vals[:, 1::2] = f[:, 2:28:4]
+            batch.final = vals
+            batch.final_tracks = touched[has]
+        else:
+            batch.final = np.zeros((0, 14))
+            batch.final_tracks = np.zeros((0, 7), dtype=bool)
+        return status
 
     def _eager(self, rec, K, telemetry):
         if self.device.type != "cuda":

@@ -215,6 +215,169 @@ class SqliteSession(_SessionBase):
         self.store = store
         self.conn = store.conn
         self._players: Dict[str, Player] = {}  # identity map
+        self._batches: List = []
+
+    # ------------------------------------------------------------- columnar batches
+    def load_batch(self, ids: Iterable[str], chunksize: int = 100):
+        """The batch as columns (runtime/columnar.MatchBatch) from three SELECTs;
+        player keys are the store's integer keys of their api ids."""
+        import numpy as np
+
+        from .columnar import MODE_INDEX, UNSUPPORTED, MatchBatch, afk_mask
+
+        ids = list(set(ids))
+        heads: List[tuple] = []
+        for chunk in _chunks(ids, 500):
+            heads += self.conn.execute(
+                "SELECT api_id, game_mode, created_at FROM match WHERE api_id IN (%s)"
+                % ", ".join("?" * len(chunk)), chunk).fetchall()
+        heads.sort(key=lambda r: (r[2] is None, r[2]))
+        mids = [h[0] for h in heads]
+        pos = {m: i for i, m in enumerate(mids)}
+        rosters: List[List[tuple]] = [[] for _ in mids]
+        parts: Dict[str, List[tuple]] = {}
+        for chunk in _chunks(mids, 500):
+            ph = ", ".join("?" * len(chunk))
+            for r in self.conn.execute("SELECT api_id, match_api_id, winner FROM roster WHERE "
+                                       "match_api_id IN (%s) ORDER BY rowid" % ph, chunk):
+                rosters[pos[r[1]]].append(r)
+            for p in self.conn.execute(
+                    "SELECT p.api_id, p.roster_api_id, p.player_api_id, p.went_afk, p.rowid, i.rowid "
+                    "FROM participant p LEFT JOIN participant_items i ON i.participant_api_id = p.api_id "
+                    "WHERE p.match_api_id IN (%s) ORDER BY p.rowid" % ph, chunk):
+                parts.setdefault(p[1], []).append(p)
+        M = len(mids)
+        nr = np.array([len(r) for r in rosters], dtype=np.int64)
+        n = np.zeros((M, 2), dtype=np.int64)
+        for i, rs in enumerate(rosters):
+            for ri in range(min(2, len(rs))):
+                n[i, ri] = len(parts.get(rs[ri][0], ()))
+        K = int(max(1, n.max() if M else 1))
+        player = np.full((M, 2, K), -1, dtype=np.int64)
+        part = np.full((M, 2, K), -1, dtype=np.int64)
+        afk = np.zeros((M, 2, K), dtype=bool)
+        winner = np.zeros((M, 2), dtype=bool)
+        keys = self.store.player_keys
+        pnames: List[str] = []
+        prow: List[int] = []  # participant rowids (integer-key UPDATEs)
+        irow: List[int] = []  # their participant_items rowids
+        extra: Dict[int, List[int]] = {}
+        afk23 = np.zeros(M, dtype=bool)
+        for i, rs in enumerate(rosters):
+            for ri, r in enumerate(rs):
+                ps = parts.get(r[0], ())
+                if ri >= 2:
+                    ext = extra.setdefault(i, [])
+                    for p in ps:
+                        ext.append(len(pnames))
+                        pnames.append(p[0])
+                        prow.append(p[4])
+                        irow.append(p[5])
+                        afk23[i] |= p[3] == 1
+                    continue
+                winner[i, ri] = r[2] is not None and bool(r[2])
+                for k, p in enumerate(ps):
+                    k_ = keys.get(p[2])
+                    if k_ is None:
+                        k_ = keys[p[2]] = len(self.store.player_names)
+                        self.store.player_names.append(p[2])
+                    player[i, ri, k] = k_
+                    part[i, ri, k] = len(pnames)
+                    pnames.append(p[0])
+                    prow.append(p[4])
+                    irow.append(p[5])
+                    afk[i, ri, k] = p[3] == 1
+        mask = afk_mask(n, afk[:, 0], afk[:, 1]) | np.where(afk23, np.int64(1) << 23, 0)
+        mode = np.array([MODE_INDEX.get(h[1], UNSUPPORTED) for h in heads], dtype=np.int64)
+        b = MatchBatch(ids=mids, mode=mode, nrosters=nr, n=n, winner=winner, afk=mask, player=player,
+                       part=part, player_names=pnames, extra_parts=extra)
+        b.part_rowids = prow
+        b.item_rowids = irow
+        self._batches.append(b)
+        return b
+
+    def fetch_players(self, keys):
+        """Stored (ratings [n,14], attributes [n,3]) of integer player keys."""
+        import numpy as np
+
+        names = [self.store.player_names[int(k)] for k in keys]
+        cols = ("api_id", "rowid", "rank_points_ranked", "rank_points_blitz", "skill_tier") + PLAYER_RATING_COLS
+        got = {}
+        for chunk in _chunks(names, 500):
+            for row in self.conn.execute("SELECT %s FROM player WHERE api_id IN (%s)"
+                                         % (", ".join(_q(c) for c in cols), ", ".join("?" * len(chunk))),
+                                         chunk):
+                got[row[0]] = row[2:]
+                self.store.player_rowid[row[0]] = row[1]
+        nan = float("nan")
+        att = np.full((len(names), 3), nan)
+        rat = np.full((len(names), 14), nan)
+        for i, a in enumerate(names):
+            row = got.get(a)
+            if row is not None:
+                att[i] = [nan if v is None else float(v) for v in row[:3]]
+                rat[i] = [nan if v is None else float(v) for v in row[3:]]
+        return rat, att
+
+    def _write_batch(self, b) -> None:
+        import numpy as np
+
+        from .columnar import AFK, INVALID, RATED
+
+        if b.status is None:
+            return
+        c = self.conn
+        st = b.status
+        rated = st == RATED
+        afkm = (st == AFK) | (st == INVALID)
+        c.executemany("UPDATE match SET trueskill_quality=? WHERE api_id=?",
+                      [(float(b.quality[i]), b.ids[i]) for i in np.nonzero(rated)[0]] +
+                      [(0.0, b.ids[i]) for i in np.nonzero(afkm)[0]])
+        names = b.player_names
+        irow, rid = b.item_rowids, b.part_rowids
+        sel = rated[:, None, None] & (b.part >= 0)
+        # AFK / invalid: any_afk on every participant (incl. rosters beyond the second)
+        flag = []
+        for i in np.nonzero(afkm)[0]:
+            for p in b.part[i][b.part[i] >= 0].tolist() + b.extra_parts.get(int(i), []):
+                flag.append((1, irow[p]))
+        c.executemany("UPDATE participant_items SET any_afk=? WHERE rowid=?", flag)
+        extra = [(0, irow[p]) for i in np.nonzero(rated)[0] for p in b.extra_parts.get(int(i), [])]
+        if extra:
+            c.executemany("UPDATE participant_items SET any_afk=? WHERE rowid=?", extra)
+        ps = b.part[sel].tolist()
+        mu, sg, dl = b.s_mu[sel].tolist(), b.s_sig[sel].tolist(), b.delta[sel].tolist()
+        c.executemany("UPDATE participant SET trueskill_mu=?, trueskill_sigma=?, trueskill_delta=? "
+                      "WHERE rowid=?", [(a, s_, d, rid[p]) for a, s_, d, p in zip(mu, sg, dl, ps)])
+        mode = np.broadcast_to(b.mode[:, None, None], b.part.shape)[sel].tolist()
+        mm, ms = b.m_mu[sel].tolist(), b.m_sig[sel].tolist()
+        by_mode: Dict[int, list] = {}
+        for md, a, s_, p in zip(mode, mm, ms, ps):  # any_afk = False and the mode rating at once
+            by_mode.setdefault(md, []).append((a, s_, irow[p]))
+        for md, rows in by_mode.items():
+            col = TRACK_COLUMNS[1 + md]
+            c.executemany("UPDATE participant_items SET any_afk=0, %s=?, %s=? WHERE rowid=?"
+                          % (_q(col + "_mu"), _q(col + "_sigma")), rows)
+        if b.stats is not None:
+            st8 = b.stats[sel].tolist()
+            c.executemany("INSERT OR REPLACE INTO participant_stats VALUES (?, ?, %s)"
+                          % ", ".join("?" * len(STAT_COLUMNS)),
+                          [[names[p], names[p]] + v for p, v in zip(ps, st8)])
+        if b.final_keys is not None and len(b.final_keys):
+            pn, prow_of = self.store.player_names, self.store.player_rowid
+            f = b.final
+            groups: Dict[tuple, list] = {}  # one UPDATE per set of touched tracks
+            for u, k in enumerate(b.final_keys.tolist()):
+                tracks = tuple(np.nonzero(b.final_tracks[u])[0].tolist())
+                vals = []
+                for t in tracks:
+                    vals += [None if f[u, 2 * t] != f[u, 2 * t] else float(f[u, 2 * t]),
+                             None if f[u, 2 * t + 1] != f[u, 2 * t + 1] else float(f[u, 2 * t + 1])]
+                groups.setdefault(tracks, []).append(vals + [prow_of[pn[int(k)]]])
+            for tracks, rows in groups.items():
+                sets = ", ".join("%s=?, %s=?" % (_q(TRACK_COLUMNS[t] + "_mu"), _q(TRACK_COLUMNS[t] + "_sigma"))
+                                 for t in tracks)
+                c.executemany("UPDATE player SET %s WHERE rowid=?" % sets, rows)
 
     def _load_players(self, api_ids: Sequence[str]) -> None:
         need = [a for a in set(api_ids) if a not in self._players]
@@ -290,6 +453,9 @@ class SqliteSession(_SessionBase):
 
     def commit(self) -> None:
         c = self.conn
+        for b in self._batches:
+            self._write_batch(b)
+        self._batches.clear()
         for m, _ in self._match_snaps.values():
             c.execute("UPDATE match SET trueskill_quality=? WHERE api_id=?", (m.trueskill_quality, m.api_id))
             for p in m.participants:
@@ -314,6 +480,7 @@ class SqliteSession(_SessionBase):
 
     def rollback(self) -> None:
         super().rollback()
+        self._batches.clear()
         self.conn.rollback()
 
     def participant_stats(self, participant_api_id: str):
@@ -330,10 +497,19 @@ class SqliteStore:
     def __init__(self, path: str = ":memory:"):
         self.path = path
         self.conn = sqlite3.connect(path)
+        if path != ":memory:":
+            # write-ahead log: a commit appends to the log instead of rewriting pages +
+            # journal; NORMAL sync keeps every committed batch across a process crash
+            self.conn.execute("PRAGMA journal_mode=WAL")
+            self.conn.execute("PRAGMA synchronous=NORMAL")
         for ddl in SCHEMA:
             self.conn.execute(ddl)
         self.conn.commit()
         self.commits = 0
+        # integer keys of player api ids (columnar batches, resident roster rows)
+        self.player_keys: Dict[str, int] = {}
+        self.player_names: List[str] = []
+        self.player_rowid: Dict[str, int] = {}
 
     def session(self) -> SqliteSession:
         return SqliteSession(self)
@@ -368,8 +544,13 @@ class SqliteStore:
         c.commit()
 
     def add_asset(self, match_api_id: str, url: str) -> None:
+        self.add_assets([(match_api_id, url)])
+
+    def add_assets(self, pairs) -> None:
+        pairs = list(pairs)
         n = self.conn.execute("SELECT COUNT(*) FROM asset").fetchone()[0]
-        self.conn.execute("INSERT INTO asset VALUES (?, ?, ?)", ("a%d" % n, match_api_id, url))
+        self.conn.executemany("INSERT INTO asset VALUES (?, ?, ?)",
+                              [("a%d" % (n + i), m, u) for i, (m, u) in enumerate(pairs)])
         self.conn.commit()
 
     def close(self) -> None:
@@ -383,10 +564,15 @@ def _chunks(seq: Sequence, n: int):
 
 
 def open_store(uri: Optional[str]):
-    """Store for a ``DATABASE_URI``: None / ``memory://`` -> MemoryStore,
-    ``sqlite:///path`` (or ``sqlite://`` for an in-memory database) -> SqliteStore."""
+    """Store for a ``DATABASE_URI``: None / ``memory://`` -> MemoryStore (object
+    graph), ``columnar://`` -> ColumnarStore (numpy columns, the worker's fast
+    native path), ``sqlite:///path`` (or ``sqlite://`` for an in-memory
+    database) -> SqliteStore."""
     if not uri or uri.startswith("memory:"):
         return MemoryStore()
+    if uri.startswith("columnar:"):
+        from .columnar import ColumnarStore
+        return ColumnarStore()
     if uri.startswith("sqlite://"):
         path = uri[len("sqlite://"):]
         path = path[1:] if path.startswith("/") else path

@@ -49,6 +49,8 @@ from __future__ import annotations
 
 import json
 import time
+
+import numpy as np
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Tuple
 
@@ -195,18 +197,27 @@ class Worker:
         quarantined: List[str] = []
         counts: Dict[str, int] = {}
         try:
-            with trace_range("load", ids=len(ids)):
-                matches = list(session.load_matches(ids, self.cfg.chunksize))
-            if self.cfg.skip_rated:
-                fresh = [m for m in matches if m.trueskill_quality is None]
-                if len(fresh) != len(matches):
-                    counts["skipped_rated"] = len(matches) - len(fresh)
-                matches = fresh
-            with trace_range("rate", matches=len(matches), engine=self.cfg.engine):
-                if self.cfg.engine == "native" and self._batched().supports(matches):
-                    quarantined = self._rate_native(session, matches, counts)
-                else:
-                    quarantined = self._rate_python(session, matches, counts)
+            if (self.cfg.engine == "native" and self.cfg.resident and not self.cfg.skip_rated
+                    and hasattr(session, "load_batch")):
+                # columnar path: no per-object work (runtime/columnar.py)
+                with trace_range("load", ids=len(ids)):
+                    batch = session.load_batch(ids, self.cfg.chunksize)
+                with trace_range("rate", matches=len(batch), engine="native"):
+                    quarantined = self._rate_batch(batch, session, counts)
+                matches = batch.ids
+            else:
+                with trace_range("load", ids=len(ids)):
+                    matches = list(session.load_matches(ids, self.cfg.chunksize))
+                if self.cfg.skip_rated:
+                    fresh = [m for m in matches if m.trueskill_quality is None]
+                    if len(fresh) != len(matches):
+                        counts["skipped_rated"] = len(matches) - len(fresh)
+                    matches = fresh
+                with trace_range("rate", matches=len(matches), engine=self.cfg.engine):
+                    if self.cfg.engine == "native" and self._batched().supports(matches):
+                        quarantined = self._rate_native(session, matches, counts)
+                    else:
+                        quarantined = self._rate_python(session, matches, counts)
             with trace_range("commit"):
                 session.commit()
             if self._object_rater is not None and hasattr(self._object_rater, "commit"):
@@ -255,15 +266,33 @@ class Worker:
                 self._object_rater = ObjectBatchRater(BatchRater(self.rater_cfg))
         return self._object_rater
 
+    def _telemetry_spec(self):
+        if not self.cfg.dotelemetry:
+            return None
+        from ..ops.telemetry import TelemetrySpec
+        lo, hi = (int(x) for x in self.cfg.telemetry_events.split(","))
+        return TelemetrySpec(seed=self.stats.batches + 1, min_events=lo, max_events=hi)
+
+    def _rate_batch(self, batch, session, counts) -> List[str]:
+        from ..ops import rate as R
+
+        if len(batch) == 0:
+            return []
+        status = self._batched().rate_batch(batch, session.fetch_players, telemetry=self._telemetry_spec())
+        vals, num = np.unique(status, return_counts=True)
+        for v, c in zip(vals.tolist(), num.tolist()):
+            name = R.STATUS_NAMES.get(v, str(v))
+            counts[name] = counts.get(name, 0) + c
+        badmask = np.isin(status, list(R.ERROR_STATUSES) + [R.NOT_PROCESSED])
+        bad = [batch.ids[i] for i in np.nonzero(badmask)[0].tolist()]
+        if bad and not self.cfg.quarantine:
+            raise MatchError("%d match(es) failed to rate (first: %s)" % (len(bad), bad[0]))
+        return bad
+
     def _rate_native(self, session, matches, counts) -> List[str]:
         from ..ops import rate as R
 
-        spec = None
-        if self.cfg.dotelemetry:
-            from ..ops.telemetry import TelemetrySpec
-            lo, hi = (int(x) for x in self.cfg.telemetry_events.split(","))
-            spec = TelemetrySpec(seed=self.stats.batches + 1, min_events=lo, max_events=hi)
-        status = self._batched().rate(matches, telemetry=spec)
+        status = self._batched().rate(matches, telemetry=self._telemetry_spec())
         bad = []
         for m, s in zip(matches, status):
             name = R.STATUS_NAMES.get(s, str(s))

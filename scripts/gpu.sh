@@ -120,11 +120,17 @@ EOF
       run rerate/host_egress 900 $PY -m analyzer_amd.runtime.rerate --matches 2e8 --players 1e7 \
           --window 1.6e7 --records host
       ;;
-    worker)
-      run worker/memory 600 env ENGINE=native BATCHSIZE=500 IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 200000
-      run worker/python 600 env ENGINE=python BATCHSIZE=500 IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 5000
-      run worker/sqlite 600 env ENGINE=native BATCHSIZE=500 IDLE_TIMEOUT=0.01 \
-          DATABASE_URI=sqlite:////tmp/worker.db $PY worker.py --synthetic 50000
+    worker)  # the streaming worker, BATCHSIZE=500: columnar / object / SQLite stores, native vs python
+      run worker/columnar_native 600 env DATABASE_URI=columnar:// ENGINE=native BATCHSIZE=500 \
+          IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 200000
+      run worker/columnar_native_telemetry 600 env DATABASE_URI=columnar:// ENGINE=native DOTELEMETRY=true \
+          BATCHSIZE=500 IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 200000
+      run worker/memory_native 600 env ENGINE=native BATCHSIZE=500 IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 50000
+      run worker/memory_python 600 env ENGINE=python BATCHSIZE=500 IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 20000
+      run worker/sqlite_native 600 env DATABASE_URI=sqlite:////tmp/wn.db ENGINE=native BATCHSIZE=500 \
+          IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 50000
+      run worker/sqlite_python 600 env DATABASE_URI=sqlite:////tmp/wp.db ENGINE=python BATCHSIZE=500 \
+          IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 20000
       ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
