@@ -1,0 +1,198 @@
+"""Reflected SQLAlchemy store: the reference's persistence layer.
+
+The reference reflects whatever schema ``DATABASE_URI`` holds with
+``automap_base`` and wires list-valued relationships on the ``api_id`` columns
+by hand (/root/reference/worker.py:38-83), then loads each batch with one
+ordered query, ``load_only`` column lists and chained ``selectinload``s,
+``yield_per(CHUNKSIZE)`` (worker.py:176-191).  ``SqlAlchemyStore`` does the
+same with SQLAlchemy 2.0 (the reference pins 1.2.0b1, whose string
+``load_only("api_id")`` form 2.0 rejects -- SURVEY H7 -- so the column lists
+are attribute objects here), for any URL a SQLAlchemy dialect + driver is
+installed for: ``mysql+cymysql://`` in production (driver absent in this
+image), ``sqlite:///file`` here.  The ORM objects carry the reference's column
+names, so ``models.match_rater`` (ENGINE=python) and the resident-roster batch
+rater (ENGINE=native) rate them unchanged.
+
+Selected by ``STORE_BACKEND=sqlalchemy`` (with a sqlite URL), a
+``sqlalchemy+<url>`` URI, or any URL scheme other than memory/columnar/sqlite
+(runtime/store.open_store).
+"""
+from __future__ import annotations
+
+from typing import Iterable, Iterator, List, Optional
+
+from sqlalchemy import create_engine, insert, select, text
+from sqlalchemy.ext.automap import automap_base
+from sqlalchemy.orm import load_only, relationship, selectinload, sessionmaker
+
+from ..config import TRACK_COLUMNS
+from .objects import STAT_COLUMNS
+from .store import (ITEM_WRITE_COLS, PARTICIPANT_WRITE_COLS, PLAYER_RATING_COLS, SCHEMA, Asset,
+                    _restore_match, _restore_player, _snap_match, _snap_player)
+
+# the player columns the reference's batch query loads (worker.py:184-190); the
+# 5v5 tracks and skill_tier are lazy-loaded on first access there, and here
+PLAYER_LOAD = ("api_id", "rank_points_ranked", "rank_points_blitz") + tuple(
+    c + s for c in TRACK_COLUMNS[:5] for s in ("_sigma", "_mu"))
+
+
+class SqlAlchemyStore:
+    def __init__(self, uri: str, create_schema: bool = False):
+        self.uri = uri
+        kw = {"pool_recycle": 3600}
+        if not uri.startswith("sqlite"):
+            kw["pool_size"] = 1  # worker.py:44
+        self.engine = create_engine(uri, **kw)
+        if create_schema:
+            with self.engine.begin() as c:
+                for ddl in SCHEMA:
+                    c.execute(text(ddl))
+        Base = automap_base()
+        Base.prepare(autoload_with=self.engine)
+        C = Base.classes
+        self.Asset, self.Match, self.Roster = C.asset, C.match, C.roster
+        self.Participant, self.Player = C.participant, C.player
+        self.ParticipantStats, self.ParticipantItems = C.participant_stats, C.participant_items
+        # the reference's hand-wired, list-valued relationships (worker.py:52-82);
+        # read-only here: the rater writes columns, never the links
+        rel = lambda target, fk, join: relationship(target, foreign_keys=fk, primaryjoin=join, viewonly=True)
+        self.Match.rosters = rel("roster", "roster.match_api_id", "match.api_id == roster.match_api_id")
+        self.Match.participants = rel("participant", "participant.match_api_id",
+                                      "match.api_id == participant.match_api_id")
+        self.Roster.match = rel("match", "match.api_id", "match.api_id == roster.match_api_id")
+        self.Roster.participants = rel("participant", "participant.roster_api_id",
+                                       "roster.api_id == participant.roster_api_id")
+        self.Participant.roster = rel("roster", "roster.api_id", "roster.api_id == participant.roster_api_id")
+        self.Participant.match = rel("match", "match.api_id", "match.api_id == participant.match_api_id")
+        self.Participant.player = rel("player", "player.api_id", "player.api_id == participant.player_api_id")
+        self.Participant.participant_stats = rel(
+            "participant_stats", "participant_stats.participant_api_id",
+            "participant_stats.participant_api_id == participant.api_id")
+        self.Participant.participant_items = rel(
+            "participant_items", "participant_items.participant_api_id",
+            "participant_items.participant_api_id == participant.api_id")
+        Base.registry.configure()
+        self.tables = Base.metadata.tables
+        self.Session = sessionmaker(bind=self.engine, autoflush=False)
+        self.commits = 0
+
+    # ------------------------------------------------------------- loading (synthetic data)
+    def _insert(self, table: str, rows: List[dict]) -> None:
+        if rows:
+            with self.engine.begin() as c:
+                c.execute(insert(self.tables[table]), rows)
+
+    def add_players(self, players) -> None:
+        cols = ("api_id", "skill_tier", "rank_points_ranked", "rank_points_blitz") + PLAYER_RATING_COLS
+        self._insert("player", [{c: getattr(p, c) for c in cols} for p in players])
+
+    def add_matches(self, matches) -> None:
+        ms, rs, ps, its = [], [], [], []
+        for m in matches:
+            ms.append({"api_id": m.api_id, "game_mode": m.game_mode, "created_at": m.created_at,
+                       "trueskill_quality": m.trueskill_quality})
+            for r in m.rosters:
+                rs.append({"api_id": r.api_id, "match_api_id": m.api_id,
+                           "winner": None if r.winner is None else int(bool(r.winner))})
+                for p in r.participants:
+                    ps.append({"api_id": p.api_id, "match_api_id": m.api_id, "roster_api_id": r.api_id,
+                               "player_api_id": p.player[0].api_id, "skill_tier": p.skill_tier,
+                               "went_afk": p.went_afk, "trueskill_mu": p.trueskill_mu,
+                               "trueskill_sigma": p.trueskill_sigma, "trueskill_delta": p.trueskill_delta})
+                    it = p.participant_items[0]
+                    row = {"api_id": it.api_id or p.api_id, "participant_api_id": p.api_id}
+                    row.update({c: getattr(it, c) for c in ITEM_WRITE_COLS})
+                    row["any_afk"] = None if row["any_afk"] is None else int(bool(row["any_afk"]))
+                    its.append(row)
+        for t, rows in (("match", ms), ("roster", rs), ("participant", ps), ("participant_items", its)):
+            self._insert(t, rows)
+
+    def add_assets(self, pairs) -> None:
+        with self.engine.begin() as c:
+            n = c.execute(text("SELECT COUNT(*) FROM asset")).scalar()
+        self._insert("asset", [{"api_id": "a%d" % (n + i), "match_api_id": m, "url": u}
+                               for i, (m, u) in enumerate(pairs)])
+
+    def add_asset(self, match_api_id: str, url: str) -> None:
+        self.add_assets([(match_api_id, url)])
+
+    def session(self) -> "SqlAlchemySession":
+        return SqlAlchemySession(self)
+
+    def close(self) -> None:
+        self.engine.dispose()
+
+
+class SqlAlchemySession:
+    """The worker's session interface over one ORM session."""
+
+    def __init__(self, store: SqlAlchemyStore):
+        self.store = store
+        self.db = store.Session()
+        self._snaps = {}  # id(match) -> snapshot for rollback of the in-memory objects
+        self._players = {}
+        self.closed = False
+
+    def load_matches(self, ids: Iterable[str], chunksize: int = 100) -> Iterator:
+        """The reference's batch query (worker.py:176-191), SQLAlchemy 2.0 spelling."""
+        s = self.store
+        M, R, P, PL = s.Match, s.Roster, s.Participant, s.Player
+        q = (select(M).where(M.api_id.in_(list(set(ids)))).order_by(M.created_at.asc())
+             .options(load_only(M.api_id, M.game_mode, M.created_at),
+                      selectinload(M.rosters).load_only(R.api_id, R.match_api_id, R.winner)
+                      .selectinload(R.participants)
+                      .load_only(P.api_id, P.match_api_id, P.roster_api_id, P.player_api_id,
+                                 P.skill_tier, P.went_afk)
+                      .selectinload(P.player).load_only(*(getattr(PL, c) for c in PLAYER_LOAD)))
+             .execution_options(yield_per=max(1, int(chunksize))))
+        for m in self.db.scalars(q):
+            self._snaps.setdefault(id(m), (m, _snap_match(m)))
+            for p in m.participants:
+                pl = p.player[0]
+                self._players.setdefault(id(pl), (pl, _snap_player(pl)))
+            yield m
+
+    def savepoint(self, m) -> tuple:
+        return (_snap_match(m), [(p.player[0], _snap_player(p.player[0])) for p in m.participants])
+
+    def restore(self, m, sp: tuple) -> None:
+        _restore_match(m, sp[0])
+        for pl, snap in sp[1]:
+            _restore_player(pl, snap)
+
+    def commit(self) -> None:
+        self.db.commit()
+        self.store.commits += 1
+        self._snaps.clear()
+        self._players.clear()
+
+    def rollback(self) -> None:
+        self.db.rollback()
+        for m, snap in self._snaps.values():
+            _restore_match(m, snap)
+        for pl, snap in self._players.values():
+            _restore_player(pl, snap)
+
+    def assets(self, match_api_id: str) -> List[Asset]:
+        A = self.store.Asset
+        return [Asset(a.url, a.match_api_id) for a in
+                self.db.scalars(select(A).where(A.match_api_id == match_api_id))]
+
+    def participant_stats(self, participant_api_id: str):
+        S = self.store.ParticipantStats
+        row = self.db.scalars(select(S).where(S.participant_api_id == participant_api_id)).first()
+        return None if row is None else {c: getattr(row, c) for c in STAT_COLUMNS}
+
+    def close(self) -> None:
+        self.db.close()
+        self.closed = True
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+
+__all__ = ["SqlAlchemyStore", "SqlAlchemySession", "PARTICIPANT_WRITE_COLS"]

@@ -3,8 +3,9 @@
 The reference reflects ``match, roster, participant, participant_items,
 participant_stats, player, asset`` with SQLAlchemy automap and wires list-valued
 relationships on the ``api_id`` foreign keys (/root/reference/worker.py:38-83).
-Neither SQLAlchemy nor a MySQL driver exists in this image, so the
-store is pluggable behind one small session interface:
+That store is runtime/sqla.py (SQLAlchemy 2.0 is installed; the MySQL driver
+the reference uses is not).  Every store sits behind one small session
+interface:
 
     with store.session() as s:
         for match in s.load_matches(ids, chunksize):   # ORDER BY created_at ASC
@@ -563,11 +564,23 @@ def _chunks(seq: Sequence, n: int):
         yield seq[i:i + n]
 
 
-def open_store(uri: Optional[str]):
+def open_store(uri: Optional[str], backend: Optional[str] = None):
     """Store for a ``DATABASE_URI``: None / ``memory://`` -> MemoryStore (object
     graph), ``columnar://`` -> ColumnarStore (numpy columns, the worker's fast
     native path), ``sqlite:///path`` (or ``sqlite://`` for an in-memory
-    database) -> SqliteStore."""
+    database) -> SqliteStore (stdlib sqlite3, columnar batches), and any other
+    SQLAlchemy URL (``mysql+cymysql://...``), a ``sqlalchemy+<url>`` URI or
+    ``STORE_BACKEND=sqlalchemy`` -> SqlAlchemyStore (automap reflection, the
+    reference's relationships and batch query; runtime/sqla.py)."""
+    import os
+
+    backend = backend or os.environ.get("STORE_BACKEND") or ""
+    if uri and uri.startswith("sqlalchemy+"):
+        backend, uri = "sqlalchemy", uri[len("sqlalchemy+"):]
+    if backend == "sqlalchemy" or (uri and not uri.startswith(("memory:", "columnar:", "sqlite:"))):
+        from .sqla import SqlAlchemyStore
+        # a sqlite file gets the reference's tables on first use; other servers must have them
+        return SqlAlchemyStore(uri, create_schema=uri.startswith("sqlite"))
     if not uri or uri.startswith("memory:"):
         return MemoryStore()
     if uri.startswith("columnar:"):
@@ -577,7 +590,4 @@ def open_store(uri: Optional[str]):
         path = uri[len("sqlite://"):]
         path = path[1:] if path.startswith("/") else path
         return SqliteStore(path or ":memory:")
-    if uri.startswith("mysql"):
-        raise RuntimeError("DATABASE_URI=%s needs a MySQL driver (cymysql/SQLAlchemy), which this "
-                           "image does not ship; use sqlite:///path or memory://" % uri)
     raise ValueError("unsupported DATABASE_URI %r" % uri)

@@ -38,7 +38,7 @@ Deliberate, documented differences:
   BASELINE config 4).  Telemetry is synthetic here: the reference only forwards
   asset URLs (worker.py:148-161) and this image has no network to fetch them.
   Synthetic stats are therefore never persisted into a real database: with a
-  ``DATABASE_URI`` other than the in-process ``memory://`` store, ``connect``
+  ``DATABASE_URI`` other than the in-process ``memory://`` / ``columnar://`` stores, ``connect``
   refuses ``DOTELEMETRY`` unless ``SYNTHETIC_TELEMETRY=true`` says the run is a
   benchmark.
 
@@ -105,12 +105,15 @@ class Worker:
     def connect(self) -> "Worker":
         if self.cfg.dotelemetry and not self.cfg.synthetic_telemetry:
             uri = self.cfg.database_uri or ""
-            if uri and not uri.startswith("memory:"):
+            if uri and not uri.startswith(("memory:", "columnar:")):  # in-process stores only
                 raise ValueError("DOTELEMETRY aggregates SYNTHETIC telemetry (no real event source "
                                  "exists yet): refusing to write it into %s; set "
                                  "SYNTHETIC_TELEMETRY=true for a benchmark run" % uri)
         if self.store is None:
             self.store = open_store(self.cfg.database_uri)
+        if self.cfg.dotelemetry and type(self.store).__name__ == "SqlAlchemyStore":
+            raise ValueError("DOTELEMETRY writes participant_stats through the memory, columnar and "
+                             "sqlite stores only")
         if self.rabbit is None:
             self.rabbit = B.connect(self.cfg.rabbitmq_uri, clock=self.clock)
         ch = self.rabbit.channel()

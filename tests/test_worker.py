@@ -308,3 +308,79 @@ def test_synthetic_telemetry_never_persisted_to_a_real_database(tmp_path):
     w, _, _ = make_worker(n=2, engine="native", database_uri=uri, dotelemetry=True,
                           synthetic_telemetry=True)
     assert w.channel is not None
+
+
+# ------------------------------------------------------------------ SQLAlchemy store (W3, W7)
+def _sqla(tmp_path, name="sa.db"):
+    return open_store("sqlite:///" + str(tmp_path / name), backend="sqlalchemy")
+
+
+def test_sqlalchemy_store_reflects_and_wires_relationships(tmp_path):
+    """automap reflection of the reference's tables + the hand-wired api_id
+    relationships (/root/reference/worker.py:43-83), list-valued as the rater
+    expects (participant.player[0], participant.participant_items[0])."""
+    store = _sqla(tmp_path)
+    ms = populate(store, 4, 10, team_size=3, seed=5)
+    s = store.session()
+    got = list(s.load_matches([m.api_id for m in ms][::-1] + [ms[0].api_id]))
+    assert [m.api_id for m in got] == [m.api_id for m in ms]  # ORDER BY created_at, deduped
+    m = got[0]
+    assert len(m.rosters) == 2 and all(len(r.participants) == 3 for r in m.rosters)
+    p = m.rosters[0].participants[0]
+    assert p.player[0].api_id == p.player_api_id and p.participant_items[0].participant_api_id == p.api_id
+    assert [q.api_id for q in m.participants] == [q.api_id for r in m.rosters for q in r.participants]
+    assert p.roster[0].api_id == m.rosters[0].api_id and p.match[0].api_id == m.api_id
+    assert s.assets(m.api_id)[0].url.startswith("https://telemetry.invalid/")
+    s.close()
+
+
+@pytest.mark.parametrize("engine", ["python", "native"])
+def test_sqlalchemy_store_worker_matches_memory_store(tmp_path, engine):
+    """The whole worker over the reflected store writes what it writes over the
+    in-process store (python: bit for bit; native: fp32 state)."""
+    ref, mref, _ = make_worker(n=40, players=20, batch=16, engine="python", seed=9)
+    publish(ref.channel, "analyze", [m.api_id for m in mref])
+    ref.start_consuming()
+    store = _sqla(tmp_path)
+    w, ms, _ = make_worker(n=40, players=20, batch=16, engine=engine, seed=9, store=store)
+    publish(w.channel, "analyze", [m.api_id for m in ms])
+    w.start_consuming()
+    assert w.stats.acked == 40 and w.stats.failed_batches == 0
+    s = store.session()
+    got = {m.api_id: m for m in s.load_matches([m.api_id for m in ms])}
+    tol = 0.0 if engine == "python" else 2e-3
+    for m in mref:
+        g = got[m.api_id]
+        assert (m.trueskill_quality is None) == (g.trueskill_quality is None)
+        if m.trueskill_quality is not None:
+            assert abs(m.trueskill_quality - g.trueskill_quality) <= max(tol, 1e-6 if tol else 0.0)
+        for p, q in zip(m.participants, g.participants):
+            assert bool(p.participant_items[0].any_afk) == bool(q.participant_items[0].any_afk)
+            for c in ("trueskill_mu", "trueskill_sigma", "trueskill_delta"):
+                a, b = getattr(p, c), getattr(q, c)
+                assert (a is None) == (b is None)
+                if a is not None:
+                    assert abs(a - b) <= tol
+            pa, pb = p.player[0], q.player[0]
+            for c in ("trueskill_mu", "trueskill_ranked_mu", "trueskill_casual_sigma"):
+                a, b = getattr(pa, c), getattr(pb, c)
+                assert (a is None) == (b is None)
+                if a is not None:
+                    assert abs(a - b) <= tol
+    s.close()
+
+
+def test_sqlalchemy_store_rollback_and_quarantine(tmp_path):
+    store = _sqla(tmp_path)
+    w, ms, _ = make_worker(n=8, batch=8, quarantine=False, store=store)
+    with store.engine.begin() as c:  # a player the reference raises KeyError on
+        from sqlalchemy import text
+        pid = ms[3].rosters[0].participants[0].player[0].api_id
+        c.execute(text("UPDATE player SET trueskill_mu=NULL, trueskill_sigma=NULL, skill_tier=30, "
+                       "rank_points_ranked=NULL, rank_points_blitz=NULL WHERE api_id=:p"), {"p": pid})
+    publish(w.channel, "analyze", [m.api_id for m in ms])
+    w.start_consuming()
+    assert w.stats.failed_batches == 1 and w.channel.nacked == 8
+    s = store.session()
+    assert all(m.trueskill_quality is None for m in s.load_matches([m.api_id for m in ms]))  # rolled back
+    s.close()
