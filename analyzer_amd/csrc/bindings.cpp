@@ -180,7 +180,7 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   if (dev.is_cuda()) {
     check(workspace, "workspace", torch::kUInt8, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
-    TORCH_CHECK(ctrl.numel() >= 32, "ctrl must have 32 entries");
+    TORCH_CHECK(ctrl.numel() >= 48, "ctrl must have 48 entries");
     const size_t need = ana::schedule_workspace_bytes(M * 2 * K, num_players);
     TORCH_CHECK((size_t)workspace.numel() >= need, "workspace too small: need ", need, " bytes");
     check_hip(ana::launch_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
@@ -288,7 +288,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
     check(ctrl, "ctrl", torch::kInt32, dev);
     TORCH_CHECK(link.numel() == M * S * ana::kLinkWords, "link must be [M, 2K]");
     TORCH_CHECK(deps.numel() == M, "deps must have M entries");
-    TORCH_CHECK(ctrl.numel() >= 32, "ctrl must have 32 entries");
+    TORCH_CHECK(ctrl.numel() >= 48, "ctrl must have 48 entries");
     TORCH_CHECK(blocks >= 1 && blocks <= 65535, "blocks must be 1..65535");
     // the executor writes packed rows; other layouts go through a packed buffer
     const bool packed = out.s_sig == out.s_mu + S && out.delta == out.s_mu + 2 * S &&

@@ -178,6 +178,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   uint32_t n_local = 0, n_global = 0;
   // timing build: clocks of the iterations that rated something, split at the wait
   uint64_t d_issue = 0, d_wait = 0, d_after = 0, d_it0 = 0;
+  uint64_t d_t[4] = {0, 0, 0, 0}, d_p[5] = {0, 0, 0, 0, 0};  // after-phase split (timing build)
   uint32_t d_worked = 0, d_groups = 0;
 
   int32_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
@@ -453,6 +454,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       if (gst == kRated && (n0 == 0 || n1 == 0)) gst = kErrEmptyRoster;
       float nsm = NAN, nss = NAN, nmm = NAN, nms = NAN, dl = NAN, q = NAN;
       if (gst == kRated) {
+        if constexpr (DIAG) d_p[1] = __builtin_amdgcn_s_memrealtime();
         const float sgn = r0 ? 1.f : -1.f;
         const float s_c2 = group_sum<G>(inr ? pss * pss + tau2 : 0.f, j, gbase);
         const float s_d = group_sum<G>(inr ? sgn * pms : 0.f, j, gbase);
@@ -494,6 +496,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         else dl = 0.f;
       }
       const bool ok = gst == kRated && inr;
+      if constexpr (DIAG) d_p[2] = __builtin_amdgcn_s_memrealtime();
       if (inr && islast) {  // publish: new values, or the untouched ones on error
         const int off = id * (kRowFloats * 4);
         // shared granule: tagged with the next reader + bumped mode counter;
@@ -530,6 +533,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           n_global += (uint32_t)__popcll(__ballot(true) & ~lb);
         }
       }
+      if constexpr (DIAG) d_p[3] = __builtin_amdgcn_s_memrealtime();
       if (ok && prm.record_first_prior && own) {
         float* fp = first_prior + (int64_t)id * kRowFloats;
         if (pflags & 2u) { fp[0] = pms; fp[2] = pss; }
@@ -632,12 +636,27 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         }
     }
 
+    if constexpr (DIAG) d_p[0] = d_p[1] = d_p[2] = d_p[3] = d_w1;
     rate_batch(nb);
     if constexpr (DIAG) {
       if (worked) {
+        const uint64_t end = __builtin_amdgcn_s_memrealtime();
         d_issue += d_w0 - d_it0;
         d_wait += d_w1 - d_w0;
-        d_after += __builtin_amdgcn_s_memrealtime() - d_w1;
+        d_after += end - d_w1;
+        // the markers are per lane (the rating ran in the assigned groups): take lane 0's group
+        const uint64_t p1 = __builtin_amdgcn_readfirstlane((uint32_t)d_p[1]) |
+                            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d_p[1] >> 32)) << 32);
+        const uint64_t p2 = __builtin_amdgcn_readfirstlane((uint32_t)d_p[2]) |
+                            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d_p[2] >> 32)) << 32);
+        const uint64_t p3 = __builtin_amdgcn_readfirstlane((uint32_t)d_p[3]) |
+                            ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d_p[3] >> 32)) << 32);
+        if (p1 >= d_w1 && p2 >= p1 && p3 >= p2 && end >= p3) {
+          d_t[0] += p1 - d_w1;
+          d_t[1] += p2 - p1;
+          d_t[2] += p3 - p2;
+          d_t[3] += end - p3;
+        }
       }
     }
 
@@ -672,6 +691,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[22]), (unsigned long long)d_issue);
           atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[24]), (unsigned long long)d_wait);
           atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[28]), (unsigned long long)d_after);
+          // [32..39] the after phase split: prior + sums, update, publish, outputs + rest
+          for (int q = 0; q < 4; ++q)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[32 + 2 * q]), (unsigned long long)d_t[q]);
         }
       }
       if constexpr (TELE) {
@@ -743,7 +765,7 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
   if (!prm.ctrl_ready) hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, 15);
   // the diagnostic words are zeroed by every launch (not by the schedule's zeroing)
-  hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 12);
+  hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 28);
   if (M <= 0) return 0;
   if (prm.chunk_len < 1 || prm.chunk_len > kChunk) return (int)hipErrorInvalidValue;
   if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;

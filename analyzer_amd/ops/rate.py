@@ -30,7 +30,7 @@ from .native import native
 RATED, AFK, INVALID_ROSTERS, UNSUPPORTED_MODE = 0, 1, 2, 3
 ERR_SEED, ERR_SIGMA, ERR_EMPTY_ROSTER, ERR_NUMERIC, ERR_BAD_RECORD = 4, 5, 6, 7, 8
 NOT_PROCESSED = 255
-CTRL_WORDS = 32  # executor control words (csrc/dataflow.hip launch_rate)
+CTRL_WORDS = 48  # executor control words (csrc/dataflow.hip launch_rate)
 STATUS_NAMES = {RATED: "rated", AFK: "afk", INVALID_ROSTERS: "invalid_rosters",
                 UNSUPPORTED_MODE: "unsupported_mode", ERR_SEED: "error_seed",
                 ERR_SIGMA: "error_sigma", ERR_EMPTY_ROSTER: "error_empty_roster",
@@ -348,6 +348,10 @@ class BatchRater:
         return {"wave_iterations": c[15], "worked_iterations": worked, "groups_assigned": c[21],
                 "matches_per_worked_iteration": c[21] / worked if worked else 0.0,
                 "issue_us": per(u64(22)), "wait_us": per(u64(24)), "after_us": per(u64(28)),
+                # the after phase split: priors + team sums, coefficients + update,
+                # publish (granules + hand-off), output records + bookkeeping
+                "after_prior_us": per(u64(32)), "after_update_us": per(u64(34)),
+                "after_publish_us": per(u64(36)), "after_rest_us": per(u64(38)),
                 "local_handoffs": c[26], "global_handoffs": c[27]}
 
     def telemetry_errors(self, device) -> int:

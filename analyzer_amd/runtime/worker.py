@@ -110,7 +110,10 @@ class Worker:
                                  "exists yet): refusing to write it into %s; set "
                                  "SYNTHETIC_TELEMETRY=true for a benchmark run" % uri)
         if self.store is None:
-            self.store = open_store(self.cfg.database_uri)
+            # no DATABASE_URI: an in-process store -- columnar for the native engine
+            # (no per-object work at all), the object graph for the Python engine
+            uri = self.cfg.database_uri or ("columnar://" if self.cfg.engine == "native" else None)
+            self.store = open_store(uri)
         if self.cfg.dotelemetry and type(self.store).__name__ == "SqlAlchemyStore":
             raise ValueError("DOTELEMETRY writes participant_stats through the memory, columnar and "
                              "sqlite stores only")

@@ -85,6 +85,8 @@ def main():
                 line += " | worked iterations %d (%.2f matches each): issue %.3f + wait %.3f + after %.3f us" % (
                     d["worked_iterations"], d["matches_per_worked_iteration"], d["issue_us"], d["wait_us"],
                     d["after_us"])
+                line += " [prior %.3f update %.3f publish %.3f rest %.3f]" % (
+                    d["after_prior_us"], d["after_update_us"], d["after_publish_us"], d["after_rest_us"])
             if args.pattern == "serial":
                 line += " | %.3f us per hop" % ((t2 - t1) * 1e6 / M)
             print(line, flush=True)
