@@ -14,10 +14,12 @@ ONE dense all-reduce of natural-parameter messages (csrc/sweep.hip):
 all-reduce of bucket b (asynchronous, on the collective's own stream) runs
 while the main stream computes the messages of bucket b+1 and decodes bucket
 b-1, so on xGMI only the first bucket's message kernel and the last bucket's
-decode stay exposed.  Buckets default to 64 MB of messages (ANA_MERGE_BUCKET_MB;
-0 = one bucket): a 1M-player roster (64 MB) stays one all-reduce; a 10M-player
-re-rate roster (640 MB) becomes ten 64-MB reduces that hide the kernels.
-Every stage is per player, so bucketing is exact.
+decode stay exposed.  Buckets default to 16 MB of messages (ANA_MERGE_BUCKET_MB;
+0 = one bucket): a 1M-player roster (64 MB) becomes four all-reduces, each big
+enough to run the xGMI links at bandwidth, so the message kernel of bucket b+1
+and the decode of bucket b-1 (~0.1 ms each per 16 MB) hide behind the
+collective; a 10M-player re-rate roster (640 MB) becomes forty.  Every stage
+is per player, so bucketing is exact.
 
 **Causal re-sweeps (``sweeps`` > 1).**  Rank r's shard is the r-th time slice
 of the global window (bench.py, runtime/rerate.py), so under the reference's
@@ -86,7 +88,7 @@ class SweepMerger:
         self.comm_bytes = self.P * (16 * 4 if not self.scaled else
                                     14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4)
         if bucket_rows is None:
-            mb = float(os.environ.get("ANA_MERGE_BUCKET_MB", "64"))
+            mb = float(os.environ.get("ANA_MERGE_BUCKET_MB", "16"))
             bucket_rows = int(mb * (1 << 20)) // (16 * 4) if mb > 0 else self.P
         self.bucket_rows = max(1, min(int(bucket_rows), max(self.P, 1)))
         self.windows = 0
