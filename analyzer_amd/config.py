@@ -114,23 +114,63 @@ class WorkerConfig:
 
 @dataclass(frozen=True)
 class EngineConfig:
-    """Knobs of the MI355X rating engine (new; no reference counterpart)."""
+    """Knobs of the MI355X rating engine (new; no reference counterpart), read
+    once from the environment.  The Python-side consumers take their defaults
+    from here (``EngineConfig.from_env()``); the knobs the native extension reads
+    at launch time are listed in ``NATIVE_KNOBS`` with what they do.
 
-    num_gpus: int = 1
-    mode: str = "exact"           # exact | sweep
-    window: int = 0               # matches per GPU per merge window (sweep mode); 0 = all
-    comm_dtype: str = "fp32"      # fp32 | fp16 | bf16 compression of merge deltas
-    checkpoint_every: int = 0     # windows between checkpoints (0 = off)
+    ======================  ========  =============================================
+    variable                default   consumer
+    ======================  ========  =============================================
+    ANA_RATE_BLOCKS         512       persistent grid of a window launch (ops/rate.py)
+    ANA_PREPASS_AT          0.8       tail overlap point of the next prepass (runtime/engine.py)
+    ANA_PREPASS_CUS         0         CU-masked prepass stream, 0 = off (runtime/engine.py)
+    ANA_PREPASS_SERIAL      0         prepass on the main stream (A/B, runtime/engine.py)
+    ANA_MERGE_BUCKET_MB     16        sweep-merge bucket size (parallel/sweep.py)
+    COMM_DTYPE              fp32      sweep-merge message precision (bench.py, rerate)
+    SWEEPS                  1         causal sweeps per window (bench.py, rerate)
+    ANA_DIST_BACKEND        nccl      process group backend (gloo: N ranks on one GPU)
+    CHECKPOINT_DIR / _EVERY -- / 1    re-rate checkpoints (runtime/rerate.py)
+    ANA_TRACE               0         roctx ranges + Chrome trace (utils/trace.py)
+    ======================  ========  =============================================
+    """
+
+    rate_blocks: int = 512
+    prepass_at: float = 0.8
+    prepass_cus: int = 0
+    prepass_serial: bool = False
+    merge_bucket_mb: float = 16.0
+    comm_dtype: str = "fp32"
+    sweeps: int = 1
+    dist_backend: str = "nccl"
+    checkpoint_every: int = 1
     checkpoint_dir: Optional[str] = None
-    extra: Mapping[str, str] = field(default_factory=dict)
+    trace: bool = False
+
+    # read by the native extension itself (csrc/bindings.cpp, kernels), per launch
+    NATIVE_KNOBS = {
+        "ANA_RATE_IDLE": "max s_sleep rounds of an idle executor wave (default 8)",
+        "ANA_RATE_TIGHT": "2K lanes per match instead of the next power of two (-1 auto)",
+        "ANA_RATE_LOCAL": "LDS local hand-off of successors held by the producing wave (default 1)",
+        "ANA_RATE_DIAG": "timing build of the executor: per-phase clocks in ctrl[20..39] (default 0)",
+        "ANA_TELE_IMPL": "telemetry aggregation: 1 one-hot MFMA GEMM (default), 0 LDS atomics",
+        "ANA_TELE_FUSED_TAIL": "fused telemetry only after the executor's chunks are drained",
+        "ANA_SCHED_SMALL": "micro-batch schedule: hash lists (default) or bitonic sort",
+        "ANA_SORT_RB / ANA_SORT_NT": "radix-sort tile rows / non-temporal loads (tuning)",
+    }
 
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "EngineConfig":
         return EngineConfig(
-            num_gpus=int(_env(env, "NUM_GPUS") or 1),
-            mode=_env(env, "MODE") or "exact",
-            window=int(_env(env, "WINDOW") or 0),
+            rate_blocks=int(_env(env, "ANA_RATE_BLOCKS") or 512),
+            prepass_at=float(_env(env, "ANA_PREPASS_AT") or 0.8) if env.get("ANA_PREPASS_AT") != "0" else 0.0,
+            prepass_cus=int(_env(env, "ANA_PREPASS_CUS") or 0),
+            prepass_serial=(env.get("ANA_PREPASS_SERIAL") or "0") not in ("", "0"),
+            merge_bucket_mb=float(_env(env, "ANA_MERGE_BUCKET_MB") or 16),
             comm_dtype=_env(env, "COMM_DTYPE") or "fp32",
-            checkpoint_every=int(_env(env, "CHECKPOINT_EVERY") or 0),
+            sweeps=int(_env(env, "SWEEPS") or 1),
+            dist_backend=_env(env, "ANA_DIST_BACKEND") or "nccl",
+            checkpoint_every=int(_env(env, "CHECKPOINT_EVERY") or 1),
             checkpoint_dir=_env(env, "CHECKPOINT_DIR"),
+            trace=(env.get("ANA_TRACE") or "0") not in ("", "0"),
         )

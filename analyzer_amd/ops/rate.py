@@ -22,7 +22,7 @@ from typing import Dict, NamedTuple, Optional, Tuple
 
 import torch
 
-from ..config import MODES, N_TRACKS, RaterConfig
+from ..config import MODES, N_TRACKS, EngineConfig, RaterConfig
 from ..models.tiers import vst_table
 from .native import native
 
@@ -175,7 +175,7 @@ class BatchRater:
         self.cfg = cfg or RaterConfig.from_env()
         self.host_fp64 = host_fp64
         # persistent-grid size of the dataflow launch (4 waves per block)
-        self.blocks = int(blocks or os.environ.get("ANA_RATE_BLOCKS", 512))
+        self.blocks = int(blocks or EngineConfig.from_env().rate_blocks)
         self._vst: Dict[str, torch.Tensor] = {}
         self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
 

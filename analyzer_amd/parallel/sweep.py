@@ -52,7 +52,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
-from ..config import RaterConfig
+from ..config import EngineConfig, RaterConfig
 from ..models.tiers import vst_table
 from ..ops.native import native
 from .comm import all_reduce_sum, exclusive_scan, world
@@ -88,7 +88,7 @@ class SweepMerger:
         self.comm_bytes = self.P * (16 * 4 if not self.scaled else
                                     14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4)
         if bucket_rows is None:
-            mb = float(os.environ.get("ANA_MERGE_BUCKET_MB", "16"))
+            mb = EngineConfig.from_env().merge_bucket_mb
             bucket_rows = int(mb * (1 << 20)) // (16 * 4) if mb > 0 else self.P
         self.bucket_rows = max(1, min(int(bucket_rows), max(self.P, 1)))
         self.windows = 0

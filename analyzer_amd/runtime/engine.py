@@ -32,6 +32,7 @@ import os
 
 import torch
 
+from ..config import EngineConfig
 from ..ops.rate import BatchRater, RateResult, Roster, Schedule
 from ..utils.trace import trace_range
 
@@ -61,7 +62,8 @@ class WindowPipeline:
         self._free: List[Optional[torch.cuda.Event]] = [None, None]
         self.windows_rated = 0
         # tail overlap: signal word + number of the last enqueued rate launch
-        self.tail = float(os.environ.get("ANA_PREPASS_AT", "0.8") or 0)
+        self.ecfg = EngineConfig.from_env()
+        self.tail = self.ecfg.prepass_at
         self._signal = 0
         self._seq = 0
         if self.cuda and self.tail > 0:
@@ -76,9 +78,10 @@ class WindowPipeline:
         (HIP CU mask) so it trickles alongside the executor instead of bursting."""
         import os
 
-        if os.environ.get("ANA_PREPASS_SERIAL", "") not in ("", "0"):
+        ecfg = EngineConfig.from_env()
+        if ecfg.prepass_serial:
             return torch.cuda.current_stream(self.device)  # no overlap (A/B)
-        n = int(os.environ.get("ANA_PREPASS_CUS", "0") or 0)
+        n = ecfg.prepass_cus
         if n > 0:
             from ..ops.native import native
 

@@ -42,7 +42,7 @@ from typing import Callable, Dict, Optional
 
 import torch
 
-from ..config import RaterConfig
+from ..config import EngineConfig, RaterConfig
 from ..ops import rate as R
 from ..ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
 from ..parallel.comm import broadcast_roster, init_from_env, reduce_counts, world
@@ -220,16 +220,17 @@ def main(argv=None) -> int:
     ap.add_argument("--team-size", type=int, default=3)
     ap.add_argument("--window", type=float, default=1e6)
     ap.add_argument("--seed", type=int, default=2024)
-    ap.add_argument("--checkpoint-dir", default=os.environ.get("CHECKPOINT_DIR"))
-    ap.add_argument("--checkpoint-every", type=int, default=int(os.environ.get("CHECKPOINT_EVERY") or 1))
+    ecfg = EngineConfig.from_env()
+    ap.add_argument("--checkpoint-dir", default=ecfg.checkpoint_dir)
+    ap.add_argument("--checkpoint-every", type=int, default=ecfg.checkpoint_every)
     ap.add_argument("--fault-kill-after", type=int, default=None,
                     help="fault injection: exit(17) after this many windows")
     ap.add_argument("--device", default=None)
-    ap.add_argument("--comm-dtype", default=os.environ.get("COMM_DTYPE") or "fp32",
+    ap.add_argument("--comm-dtype", default=ecfg.comm_dtype,
                     choices=["fp32", "fp16", "bf16"], help="sweep-merge message precision")
     ap.add_argument("--records", default="digest", choices=["digest", "host", "none"],
                     help="output records: device digest per window, pinned D2H stream, or dropped")
-    ap.add_argument("--sweeps", type=int, default=1, help="causal sweeps per window (N ranks)")
+    ap.add_argument("--sweeps", type=int, default=ecfg.sweeps, help="causal sweeps per window (N ranks)")
     ap.add_argument("--digests", action="store_true", help="print every window's digest")
     args = ap.parse_args(argv)
     rank, size, dev = init_from_env()

@@ -25,7 +25,8 @@ _lock = threading.Lock()
 
 
 def enabled() -> bool:
-    return os.environ.get("ANA_TRACE", "") not in ("", "0")
+    from ..config import EngineConfig
+    return EngineConfig.from_env().trace
 
 
 def _roctx():

@@ -35,6 +35,8 @@ import time
 import torch
 import torch.distributed as dist
 
+from analyzer_amd.config import EngineConfig
+
 # reference rate: ~354 3v3 matches/s per CPU core for rater.rate_match
 # (measured); the whole-node bound is 8 cores x 354 = 2832/s.
 BASELINE_MATCHES_PER_S = 2832.0
@@ -70,9 +72,9 @@ def parse(argv=None):
                     help="config 4: overlap = the MFMA aggregation kernel co-runs with the rating "
                          "launch on its own stream; fused = executor waves aggregate in their idle "
                          "time; separate = aggregation after the rating on the same stream")
-    ap.add_argument("--comm-dtype", default=os.environ.get("COMM_DTYPE") or "fp32",
+    ap.add_argument("--comm-dtype", default=EngineConfig.from_env().comm_dtype,
                     choices=["fp32", "fp16", "bf16"], help="sweep-merge message precision (N > 1)")
-    ap.add_argument("--sweeps", type=int, default=int(os.environ.get("SWEEPS", "1")),
+    ap.add_argument("--sweeps", type=int, default=EngineConfig.from_env().sweeps,
                     help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
                          "N = exact sequential semantics (parallel/sweep.py)")
     args = ap.parse_args(argv)
@@ -147,7 +149,7 @@ def main(argv=None) -> int:
         raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     # one rank per GPU; ANA_DIST_BACKEND=gloo lets several ranks share one GPU to
     # rehearse the multi-process path on a 1-GPU box (production: nccl = RCCL)
-    backend = os.environ.get("ANA_DIST_BACKEND", "nccl")
+    backend = EngineConfig.from_env().dist_backend
     ngpu = torch.cuda.device_count()
     local = local % ngpu if backend != "nccl" and ngpu else local
     torch.cuda.set_device(local)
