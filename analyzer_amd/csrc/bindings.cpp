@@ -442,6 +442,69 @@ void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor s2, Tenso
   }
 }
 
+// ------------------------------------------------------------- C2 exchange
+// rec: the rank's slice of one round [m, 2K+2]; status: its per-match status
+// (any row stride); out: [cap, 33] float entries, cap >= m * 2K
+void pack_rows(Tensor rec, int64_t K, Tensor status, Tensor state, Tensor out) {
+  const auto dev = state.device();
+  check(rec, "rec", torch::kInt32, dev);
+  check(state, "state", torch::kFloat32, dev);
+  check(out, "out", torch::kFloat32, dev);
+  TORCH_CHECK(K >= 1 && K <= 5 && rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [m, 2K+2]");
+  const int64_t m = rec.size(0);
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == ana::kRowFloats, "state must be [P, 32]");
+  TORCH_CHECK(out.dim() == 2 && out.size(1) == 33 && out.size(0) >= m * 2 * K, "out must be [cap >= m*2K, 33]");
+  const int64_t sstride = check_rows_view(status, "status", torch::kUInt8, dev, m, 1);
+  const int64_t P = state.size(0);
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_pack_rows(rec.data_ptr<int32_t>(), (int)K, m, status.data_ptr<uint8_t>(), sstride,
+                                    state.data_ptr<float>(), out.data_ptr<float>(), out.size(0),
+                                    stream_of(state)), "pack_rows");
+    return;
+  }
+  const int S = 2 * (int)K;
+  const int32_t* r = rec.data_ptr<int32_t>();
+  const uint8_t* st = status.data_ptr<uint8_t>();
+  const float* sp = state.data_ptr<float>();
+  float* o = out.data_ptr<float>();
+  for (int64_t e = 0; e < out.size(0); ++e) {
+    int32_t id = -1;
+    if (e < m * S) {
+      const int64_t i = e / S;
+      const int j = (int)(e % S);
+      const uint32_t m0 = (uint32_t)r[i * (S + 2) + S];
+      const int n = j < K ? (int)ana::meta_n0(m0) : (int)ana::meta_n1(m0);
+      const int32_t v = r[i * (S + 2) + j];
+      if (st[i * sstride] == ana::kRated && (j < K ? j : j - K) < n && v >= 0 && v < P) id = v;
+    }
+    if (id >= 0)
+      for (int k = 0; k < ana::kRowFloats; ++k) o[e * 33 + k] = sp[(int64_t)id * ana::kRowFloats + k];
+    int32_t* oi = reinterpret_cast<int32_t*>(o + e * 33 + 32);
+    *oi = id;
+  }
+}
+
+void unpack_rows(Tensor buf, Tensor state) {
+  const auto dev = state.device();
+  check(buf, "buf", torch::kFloat32, dev);
+  check(state, "state", torch::kFloat32, dev);
+  TORCH_CHECK(buf.dim() == 2 && buf.size(1) == 33, "buf must be [n, 33]");
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == ana::kRowFloats, "state must be [P, 32]");
+  const int64_t n = buf.size(0), P = state.size(0);
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_unpack_rows(buf.data_ptr<float>(), n, state.data_ptr<float>(), stream_of(state)),
+              "unpack_rows");
+    return;
+  }
+  const float* b = buf.data_ptr<float>();
+  float* sp = state.data_ptr<float>();
+  for (int64_t e = 0; e < n; ++e) {
+    const int32_t id = *reinterpret_cast<const int32_t*>(b + e * 33 + 32);
+    if (id < 0 || id >= P) continue;
+    for (int k = 0; k < ana::kRowFloats; ++k) sp[(int64_t)id * ana::kRowFloats + k] = (k & 1) ? 0.f : b[e * 33 + k];
+  }
+}
+
 // A HIP stream restricted to ``num_cus`` compute units, spread evenly over the
 // device's CUs (and so over its XCDs).  Used for the schedule prepass so its
 // bandwidth-bound kernels trickle alongside the latency-bound executor instead
@@ -551,6 +614,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("STAT_FEATURES") = ana::kStatFeatures;
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
   m.def("sweep_apply", &sweep_apply, "K9: decode summed messages against the common start (-> s, s2)");
+  m.def("pack_rows", &pack_rows, "C2: changed rows of a round slice -> fixed-capacity [cap, 33] entries");
+  m.def("unpack_rows", &unpack_rows, "C2: write gathered entries (id >= 0) into the roster, tags zeroed");
   m.def("write_record_file", &write_record_file, "P3: write a match-record file (ANAREC01)");
   py::class_<ana::RecordReader>(m, "RecordReader")
       .def(py::init<const std::string&, int64_t, int, bool>(), py::arg("path"), py::arg("window"),

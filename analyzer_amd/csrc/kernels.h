@@ -72,4 +72,8 @@ int launch_sweep_delta(const float* s0, const float* a, const float* s, const fl
 // decoded rows to s and (s2 != nullptr) s2
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                        const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st);
+// C2 exact-DP exchange (sweep.hip): fixed-capacity [cap][33] entries of changed rows
+int launch_pack_rows(const int32_t* rec, int K, int64_t m, const uint8_t* status, int64_t sstride,
+                     const float* state, float* out, int64_t cap, hipStream_t st);
+int launch_unpack_rows(const float* buf, int64_t n, float* state, hipStream_t st);
 }  // namespace ana

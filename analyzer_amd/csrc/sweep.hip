@@ -110,4 +110,65 @@ int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, fl
   return (int)hipGetLastError();
 }
 
+// ------------------------------------------------------------ C2 exact DP exchange
+// One round of exact DP (parallel/exact_dp.py): every rank rated a disjoint
+// slice of a conflict-free round, so each player changed on at most one rank.
+// pack: one 33-float entry per slot of the slice -- the player's 128-B row,
+// then its id (as float bits; -1 = no entry: unrated match or empty slot);
+// entries past the slice are -1, so the buffer has the fixed capacity the
+// all-gather needs and nothing is counted on the host.
+__global__ void pack_rows_kernel(const int32_t* __restrict__ rec, int S, int64_t m,
+                                 const uint8_t* __restrict__ status, int64_t sstride,
+                                 const float4* __restrict__ state, float* __restrict__ out,
+                                 int64_t cap) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= cap) return;
+  const int K = S / 2;
+  int32_t id = -1;
+  if (e < m * S) {
+    const int64_t i = e / S;
+    const int j = (int)(e % S);
+    const int32_t* r = rec + i * (S + 2);
+    const uint32_t m0 = (uint32_t)r[S];
+    const int n = j < K ? (int)meta_n0(m0) : (int)meta_n1(m0);
+    if (status[i * sstride] == kRated && (j < K ? j : j - K) < n) id = r[j];
+  }
+  float* o = out + e * 33;
+  if (id >= 0) {
+#pragma unroll
+    for (int k = 0; k < kRowVec; ++k) {
+      const float4 v = state[(int64_t)id * kRowVec + k];
+      o[4 * k] = v.x; o[4 * k + 1] = v.y; o[4 * k + 2] = v.z; o[4 * k + 3] = v.w;
+    }
+  }
+  o[32] = __int_as_float(id);
+}
+
+// unpack: write every entry with an id into the roster; tag words are zeroed
+// (they belong to another rank's launch epochs)
+__global__ void unpack_rows_kernel(const float* __restrict__ buf, int64_t n, float* __restrict__ state) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float* b = buf + e * 33;
+  const int32_t id = __float_as_int(b[32]);
+  if (id < 0) return;
+#pragma unroll
+  for (int k = 0; k < kRowFloats; ++k) state[(int64_t)id * kRowFloats + k] = (k & 1) ? 0.f : b[k];
+}
+
+int launch_pack_rows(const int32_t* rec, int K, int64_t m, const uint8_t* status, int64_t sstride,
+                     const float* state, float* out, int64_t cap, hipStream_t st) {
+  if (cap <= 0) return 0;
+  hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)((cap + 255) / 256)), dim3(256), 0, st, rec, 2 * K,
+                     m, status, sstride, reinterpret_cast<const float4*>(state), out, cap);
+  return (int)hipGetLastError();
+}
+
+int launch_unpack_rows(const float* buf, int64_t n, float* state, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(unpack_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, buf, n,
+                     state);
+  return (int)hipGetLastError();
+}
+
 }  // namespace ana

@@ -1,23 +1,38 @@
 """Exact data-parallel rating by conflict-free rounds.
 
 Exact chronological semantics (/root/reference/worker.py:176,191-192) allow
-parallelism only between matches that share no player.  The host levelizer
-(K5, ``native().levels``) assigns every match its round: 1 + the latest round
-of any of its players.  Matches of one round are disjoint, so ranks split each
-round, rate their share against their replica, and exchange ONLY the rows they
-changed: one variable-size all-gather of (player id, 128-B row) per round.
-The result is bit-identical to one process rating the window in order.
+parallelism only between matches that share no player.  The levelizer (K5,
+``native().levels``, C++) gives every match its round: 1 + the latest round of
+any of its players, 0 for matches that touch no state (they go with round 1).
+Matches of one round are disjoint, so ranks split each round into contiguous
+slices, rate their slice against their replica, and exchange ONLY the rows
+they changed.  The result is bit-identical to one process rating the window in
+order (ratings; the tag words of exchanged rows are reset).
 
-This mode is latency-bound -- one collective per round, ~900 rounds for a 10M
-3v3 window over 1M players -- which is why the throughput path on one node is
-the single-GPU dataflow engine plus the sweep merge (parallel/sweep.py); exact
-DP is the correctness-preserving way to spread one window over several
-devices (e.g. when its outputs do not fit one GPU).
+Everything about the window's shape is known on the host before the first
+launch -- rounds, slice bounds, the largest slice -- so the round loop never
+waits for the device: a rank's slices are gathered once into round order, and
+per round it launches the rating, one pack kernel (csrc/sweep.hip: the rows of
+its rated players + their ids into a fixed-capacity buffer, -1 padded), ONE
+``all_gather_into_tensor`` and one unpack kernel.  No ``.item()``, no
+variable-size collectives.
+
+How far this scales is set by the DAG, not by the implementation: a 10M 3v3
+window over 1M uniform players has ~900 rounds of ~11k matches, so exact DP
+needs ~900 exchanges per window.  Grouping g rounds per exchange stays exact
+only if no dependency crosses ranks inside the group, i.e. if whole connected
+components of the g-round sub-DAG go to one rank; a player there has
+~0.066 g occurrences, so at 5 x 0.066 g > 1 (g > 3) a giant component forms and
+grouping stops paying.  Exact mode is therefore the way to spread one window's
+outputs over several devices; throughput scaling is sweep DP
+(parallel/sweep.py), whose causal re-sweeps reach exact results with
+``sweeps == world`` in ``2 * world`` collectives (at ``world``x the rating work).
 """
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import Optional
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -32,25 +47,20 @@ def rounds(rec: torch.Tensor, K: int, num_players: int):
     return level, int(depth)
 
 
-def _gather_rows(ids: torch.Tensor, rows: torch.Tensor, group=None):
-    """All-gather variable-size (ids, rows) from every rank (padded to the max)."""
-    _, size = world()
-    n = torch.tensor([ids.numel()], dtype=torch.int64, device=ids.device)
-    sizes = [torch.zeros_like(n) for _ in range(size)]
-    dist.all_gather(sizes, n, group=group)
-    cap = int(max(int(s.item()) for s in sizes))
-    if cap == 0:
-        return [], []
-    pid = torch.full((cap,), -1, dtype=ids.dtype, device=ids.device)
-    pid[:ids.numel()] = ids
-    prow = torch.zeros((cap, rows.shape[1]), dtype=rows.dtype, device=rows.device)
-    prow[:rows.shape[0]] = rows
-    all_ids = [torch.empty_like(pid) for _ in range(size)]
-    all_rows = [torch.empty_like(prow) for _ in range(size)]
-    dist.all_gather(all_ids, pid, group=group)
-    dist.all_gather(all_rows, prow, group=group)
-    return ([a[:int(s.item())] for a, s in zip(all_ids, sizes)],
-            [r[:int(s.item())] for r, s in zip(all_rows, sizes)])
+class RoundPlan:
+    """Host-side plan of a window: round order, per-rank slice bounds, capacity."""
+
+    def __init__(self, level: torch.Tensor, size: int):
+        lv = np.maximum(level.numpy().astype(np.int64), 1)  # stateless matches go with round 1
+        M = lv.size
+        self.order = np.argsort(lv, kind="stable")             # round order, stable in time
+        counts = np.bincount(lv, minlength=int(lv.max()) + 1 if M else 2)[1:]
+        self.n_rounds = int(counts.size)
+        starts = np.concatenate([[0], np.cumsum(counts)])
+        # slice q of round r: [starts[r] + r_q, starts[r] + r_{q+1}) with sizes differing by <= 1
+        q = np.arange(size + 1)
+        self.bounds = starts[:-1, None] + (counts[:, None] * q[None, :]) // size   # [R, size+1]
+        self.max_slice = int((self.bounds[:, 1:] - self.bounds[:, :-1]).max()) if M else 0
 
 
 def rate_exact_dp(rater: BatchRater, roster: Roster, rec: torch.Tensor, K: int,
@@ -59,44 +69,57 @@ def rate_exact_dp(rater: BatchRater, roster: Roster, rec: torch.Tensor, K: int,
 
     Every rank returns the full-window outputs for the matches IT rated and
     NaN / status 255 elsewhere (outputs stay sharded; gather them if needed)."""
-    rank, size = world()
+    rank, size = world(group)
     M = rec.shape[0]
     dev = roster.device
     out = RateResult.allocate(M, K, dev)
-    out.quality.fill_(float("nan"))
+    out.packed.fill_(float("nan"))
     out.status.fill_(255)
-    for t in (out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig):
-        t.fill_(float("nan"))
+    if M == 0:
+        return out
     if level is None:
         level, _ = rounds(rec, K, roster.num_players)
-    level = level.to(torch.int64)
-    # stateless matches (level 0) go with round 1; ranks take every size-th match of a round
-    order = torch.argsort(level.clamp(min=1) * (M + 1) + torch.arange(M), stable=True)
-    lv = level.clamp(min=1)[order]
-    bounds = torch.searchsorted(lv, torch.arange(1, int(lv.max().item()) + 2 if M else 2))
+    plan = RoundPlan(level, size)
     S = 2 * K
-    for r in range(len(bounds) - 1):
-        idx = order[int(bounds[r]):int(bounds[r + 1])]
-        mine = idx[rank::size]
-        if mine.numel():
-            mine_d = mine.to(dev)
-            sub = rec.index_select(0, mine_d) if rec.device == dev else rec.index_select(0, mine).to(dev)
-            res = rater.rate(roster, sub, K)
-            out.quality[mine_d] = res.quality
-            out.status[mine_d] = res.status
-            for a, b in ((out.s_mu, res.s_mu), (out.s_sig, res.s_sig), (out.delta, res.delta),
-                         (out.m_mu, res.m_mu), (out.m_sig, res.m_sig)):
-                a[mine_d] = b
-            # only rated matches change rows; the players of stateless matches (AFK,
-            # unsupported, errors) may be updated by another rank in this round
-            ids = sub[res.status == 0][:, :S].reshape(-1)
-            ids = torch.unique(ids[ids >= 0])
+    # this rank's matches, in round order, gathered once
+    mine = np.concatenate([np.arange(plan.bounds[r, rank], plan.bounds[r, rank + 1])
+                           for r in range(plan.n_rounds)]).astype(np.int64)
+    idx = torch.from_numpy(plan.order[mine]).to(dev)
+    my_rec = rec.index_select(0, idx) if rec.device == dev else rec.index_select(0, idx.cpu()).to(dev)
+    my_out = RateResult.allocate(int(idx.numel()), K, dev)
+    offs = np.concatenate([[0], np.cumsum(plan.bounds[:, rank + 1] - plan.bounds[:, rank])])
+    cap = max(1, plan.max_slice * S)
+    f = dict(dtype=torch.float32, device=dev)
+    send = torch.empty((cap, 33), **f)
+    recv = torch.empty((size * cap, 33), **f)
+    staged = dev.type == "cuda" and size > 1 and dist.get_backend(group) == "gloo"
+    if dev.type == "cuda":
+        rater.clear_sticky(dev)
+    for r in range(plan.n_rounds):
+        lo, hi = int(offs[r]), int(offs[r + 1])
+        if hi > lo:
+            sub = my_rec[lo:hi]
+            res = rater.rate(roster, sub, K, out=RateResult(
+                my_out.quality[lo:hi], my_out.status[lo:hi], my_out.s_mu[lo:hi], my_out.s_sig[lo:hi],
+                my_out.delta[lo:hi], my_out.m_mu[lo:hi], my_out.m_sig[lo:hi],
+                packed=my_out.packed[lo:hi]), check=False)
+        if size <= 1:
+            continue
+        if hi > lo:
+            native().pack_rows(sub, K, res.status, roster.state, send)
         else:
-            ids = torch.empty(0, dtype=torch.int32, device=dev)
-        if size > 1:
-            all_ids, all_rows = _gather_rows(ids.to(torch.int64), roster.state.index_select(0, ids.long()),
-                                             group)
-            for q, (i, rw) in enumerate(zip(all_ids, all_rows)):
-                if q != rank and i.numel():
-                    roster.state[i] = rw
+            send[:, 32].view(torch.int32).fill_(-1)
+        if staged:  # gloo moves host memory only
+            h = torch.empty((size * cap, 33))
+            dist.all_gather_into_tensor(h, send.cpu(), group=group)
+            recv.copy_(h)
+        else:
+            dist.all_gather_into_tensor(recv, send, group=group)
+        # every rank's changed rows (this rank's own are rewritten unchanged, tags reset)
+        native().unpack_rows(recv, roster.state)
+    roster.epoch = None  # foreign rows carry reset tags; re-zero before the next eager launch
+    if dev.type == "cuda":
+        rater.check_errors(dev, sticky=True)  # every round's launch, one sync
+    # scatter this rank's outputs back to window order
+    out.packed.index_copy_(0, idx, my_out.packed)
     return out

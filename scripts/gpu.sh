@@ -80,18 +80,20 @@ for task in "$@"; do
           -o run --output-format csv -- $PY "$ROOT/bench.py" --steps 5 --warmup 2) || exit $?
       ;;
     pmc)
+      # PMC_TAG / PMC_ARGS select the workload (default: the 10M-match bench window)
+      tag=${PMC_TAG:-window}
       for set in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" \
                  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
                  "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM" \
+                 "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_INST_LEVEL_VMEM SQ_LDS_BANK_CONFLICT" \
                  "GRBM_GUI_ACTIVE GRBM_COUNT"; do
         name=$(echo $set | cut -d' ' -f1)
-        (cd /tmp && run pmc/$name 120 rocprofv3 --pmc $set --kernel-trace --stats \
-            -d "$ROOT/gpurun_out/pmc/$name" -o run --output-format csv -- $PY "$ROOT/scripts/tune_rate.py" --rounds 1) \
-            || exit $?
-        $PY scripts/pmc_kernel.py "gpurun_out/pmc/$name/*" rate_dataflow >> gpurun_out/pmc/executor.txt
-        $PY scripts/pmc_kernel.py "gpurun_out/pmc/$name/*" "" >> gpurun_out/pmc/all_kernels.txt
+        (cd /tmp && run pmc/$tag/$name 120 rocprofv3 --pmc $set --kernel-trace --stats \
+            -d "$ROOT/gpurun_out/pmc/$tag/$name" -o run --output-format csv -- $PY "$ROOT/scripts/tune_rate.py" \
+            --rounds 1 ${PMC_ARGS:-}) || exit $?
+        $PY scripts/pmc_kernel.py "gpurun_out/pmc/$tag/$name/*" rate_dataflow >> gpurun_out/pmc/$tag/executor.txt
       done
-      cat gpurun_out/pmc/executor.txt
+      cat gpurun_out/pmc/$tag/executor.txt
       ;;
     rerate)
       rm -rf /tmp/ck5
