@@ -63,6 +63,9 @@ constexpr int kHeads = 8;                          // ticket shards
 constexpr int kChunk = 64;                         // matches per ticket = one per lane
 constexpr int kHeld = ANA_HELD;                   // chunks a wave keeps in flight
 constexpr int kWavesPerBlock = 4;
+// byte offset past every buffer the executor reads through a resource (the
+// launcher checks the roster and the links stay below it): a load there returns 0
+constexpr int kOutOfRange = 0x7fffffc0;
 
 // sum over the G lanes of a group, result in every lane of the group.
 // Power-of-two groups up to a DPP row (16 lanes): a butterfly of DPP lane moves
@@ -146,12 +149,15 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   constexpr int kH = kHeld;
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
-  __shared__ int32_t lrec[kWavesPerBlock][kH][kChunk * R];
+  static_assert(kH == 4, "readiness reads the held chunks' local counts as one uint4");
   // local hand-off counters: increments of each held match's completion count
-  // by publishes of THIS wave (never also added to the global counter)
-  __shared__ uint32_t lloc[kWavesPerBlock][kH][kChunk];
-  // this iteration's pick per group: {match index, slot << 8 | lane in chunk}
-  __shared__ uint2 lpick[kWavesPerBlock][NG];
+  // by publishes of THIS wave (never also added to the global counter); [lane][h]
+  // so a lane reads its four in one ds_read_b128
+  __shared__ uint4 lloc[kWavesPerBlock][kChunk];
+  // this iteration's pick per group, written by the lane holding the match:
+  // {match index, slot << 8 | lane in chunk, meta0, meta1, player ids...}
+  constexpr int SP = (4 + S + 3) / 4 * 4;
+  __shared__ int32_t lpick[kWavesPerBlock][NG][SP];
   __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -168,6 +174,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   const int epoch = prm.epoch_ptr ? __builtin_amdgcn_readfirstlane(*prm.epoch_ptr) : prm.epoch;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(state, 0, (int)(P * kRowFloats * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint32_t*>(link), 0, (int)(M * S * 4), 0x00020000);
   const int head = blockIdx.x % kHeads;
   // watchdog: give up only after kTimeoutTicks without ANY chunk retiring GPU-wide
   // (ctrl[3] counts retired chunks), so long dependency chains never trip it
@@ -179,8 +187,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // timing build: clocks of the iterations that rated something, split at the wait
   uint64_t d_issue = 0, d_wait = 0, d_after = 0, d_it0 = 0;
   uint64_t d_t[4] = {0, 0, 0, 0}, d_p[5] = {0, 0, 0, 0, 0};  // after-phase split (timing build)
+  uint64_t d_s[4] = {0, 0, 0, 0}, d_i[3] = {0, 0, 0};         // issue-phase split (timing build)
   uint32_t d_worked = 0, d_groups = 0;
 
+  // per lane: the record of match cbase[h] + lane (ids, meta0, meta1), kept in
+  // registers so the lane that picks a match hands the whole record to its group
+  // through one LDS slot (one round trip instead of pick -> meta -> id)
+  int32_t hrec[kH][R];
   int32_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
                        // (a window has < 2^28 slots, so match indices fit int32)
   uint64_t pend[kH];   // wave-uniform: stateful matches not yet handed to a group
@@ -190,6 +203,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   for (int h = 0; h < kH; ++h) {
     cbase[h] = -1;
     pend[h] = 0ull;
+#pragma unroll
+    for (int k = 0; k < R; ++k) hrec[h][k] = -1;
     dval[h] = kNone;
     need[h] = 0u;
   }
@@ -267,13 +282,18 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
 
     // ---------------------------------------------- (2) readiness from the last poll
+    // one unconditional LDS read: a free slot's stale count is masked by pend = 0,
+    // and without local hand-off the counts stay 0
     uint64_t ready[kH];
+    {
+      const uint4 lv = lloc[wv][lane];
+      const uint32_t loc[4] = {lv.x, lv.y, lv.z, lv.w};
 #pragma unroll
-    for (int h = 0; h < kH; ++h) {
-      const uint32_t loc = local_ok && cbase[h] >= 0 ? lloc[wv][h][lane] : 0u;
-      ready[h] = __ballot(dval[h] != kNone && dval[h] + loc == need[h]) & pend[h];
+      for (int h = 0; h < kH; ++h)
+        ready[h] = __ballot(dval[h] != kNone && dval[h] + loc[h] == need[h]) & pend[h];
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
+    if constexpr (DIAG) d_i[0] = __builtin_amdgcn_s_memrealtime();
 
     // ---------------------------------------------- (3) ready matches -> groups
     // Within a chunk, lane b's rank among the ready bits below it (mbcnt) is the
@@ -291,46 +311,62 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         const uint32_t below = __builtin_amdgcn_mbcnt_hi(
             (uint32_t)(rdy >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rdy, 0u));
         const bool mine = ((rdy >> lane) & 1ull) && nassigned + (int)below < NG;
-        if (mine)
-          lpick[wv][nassigned + (int)below] =
-              make_uint2((uint32_t)(cbase[h] + lane), ((uint32_t)h << 8) | (uint32_t)lane);
+        if (mine) {
+          int32_t w[SP];
+          w[0] = cbase[h] + lane;
+          w[1] = (h << 8) | lane;
+          w[2] = hrec[h][S];
+          w[3] = hrec[h][S + 1];
+#pragma unroll
+          for (int k = 0; k < SP - 4; ++k) w[4 + k] = k < S ? hrec[h][k] : -1;
+          v4i* dst = reinterpret_cast<v4i*>(&lpick[wv][nassigned + (int)below][0]);
+#pragma unroll
+          for (int q = 0; q < SP / 4; ++q) dst[q] = v4i{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
+        }
         const uint64_t taken = __ballot(mine);
         pend[h] &= ~taken;
         nassigned += __popcll(taken);
       }
     }
-    int32_t my_m = 0;
-    if (g < nassigned) {
-      const uint2 pk = lpick[wv][g];
-      my_m = (int32_t)pk.x;
-      my_h = (int)(pk.y >> 8);
-      my_bit = (int)(pk.y & 255u);
+    int32_t my_m = 0, my_id = -1;
+    uint32_t my_m0 = 0u, my_m1 = 0u;
+    if (g < nassigned) {  // two LDS reads, one wait
+      const v4i pk = *reinterpret_cast<const v4i*>(&lpick[wv][g][0]);
+      if (j < S) my_id = lpick[wv][g][4 + j];
+      my_m = pk.x;
+      my_h = pk.y >> 8;
+      my_bit = pk.y & 255;
+      my_m0 = (uint32_t)pk.z;
+      my_m1 = (uint32_t)pk.w;
     }
     const bool worked = nassigned > 0;
     if constexpr (DIAG) {
       d_worked += worked ? 1u : 0u;
       d_groups += (uint32_t)nassigned;
+      d_i[1] = __builtin_amdgcn_s_memrealtime();
     }
 
     // ---------------------------------------------- (4) this group's loads
+    // Straight-line for every lane (no branch around the loads): a lane without a
+    // participant loads out of range (buffer bounds check: zeros, no access), so
+    // nothing forces a copy of the loaded registers -- and with it an early wait
+    // on the loads -- at the join of a branch.
     Batch nb;  // any_dup is wave-uniform: a match of this batch names a player twice
-    nb.my_h = my_h;
-    nb.my_bit = my_bit;
-    nb.first = j;
-    if (my_h >= 0) {
+    {
       const int32_t m = my_m;
-      nb.m = m;
-      const int32_t* lr = &lrec[wv][my_h][my_bit * R];
-      const uint32_t m0 = (uint32_t)lr[S], m1 = (uint32_t)lr[S + 1];
+      const uint32_t m0 = my_m0, m1 = my_m1;  // 0 on lanes of unassigned groups: no roster
       const int mode = meta_mode(m0);
+      nb.my_h = my_h;
+      nb.my_bit = my_bit;
+      nb.m = m;
       nb.mode = mode;
       nb.n0 = meta_n0(m0);
       nb.n1 = meta_n1(m0);
       nb.rank0 = meta_winner0(m1) ? 0 : 1;
       nb.rank1 = meta_winner1(m1) ? 0 : 1;
-      const bool inr = j < S && rpos < (r0 ? nb.n0 : nb.n1);
+      const bool inr = my_h >= 0 && j < S && rpos < (r0 ? nb.n0 : nb.n1);
       nb.inr = inr;
-      const int32_t id = inr ? lr[j] : -1;
+      const int32_t id = inr ? my_id : -1;
       nb.id = id;
       bool islast = true;
       int first = j, prevdup = -1;
@@ -353,14 +389,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       nb.prevdup = prevdup;
       const bool own = inr && first == j;
       nb.own = own;
-      if (inr) {
-        nb.lk0 = link[m * S + j];
-      }
-      if (own) {
-        const int off = id * (kRowFloats * 4);
-        nb.gs = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
-        nb.gm = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * (1 + mode), 0, 16);
-      }
+      const int goff = own ? id * (kRowFloats * 4) : kOutOfRange;
+      nb.gs = __builtin_amdgcn_raw_buffer_load_b128(rs, goff, 0, 16);
+      nb.gm = __builtin_amdgcn_raw_buffer_load_b128(rs, goff + 16 * (1 + mode), 0, 16);
+      nb.lk0 = __builtin_amdgcn_raw_buffer_load_b32(rl, inr ? (m * S + j) * 4 : kOutOfRange, 0, 0);
     }
 
     // ---------------------------------------------- (10) rate a batch
@@ -374,7 +406,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     const bool inr = bt.inr, islast = bt.islast, own = bt.own, any_dup = bt.any_dup;
     const uint32_t lk0 = bt.lk0;
     const v4i gs = bt.gs, gm = bt.gm;
-    float4 at4 = make_float4(NAN, NAN, NAN, 0.f);
     // A counter can reach its count before the writes it announces have landed
     // (notifications do not wait for store acknowledgements): a group whose
     // granules do not carry the tags of their last writers retries next iteration.
@@ -394,7 +425,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     const bool overtaken =
         own && (((lk0 & kLinkHasPred) && s_this && (uint32_t)gs.w != kNoMatch &&
                  (uint32_t)gs.w > (uint32_t)m) ||
-                (shared_ok && gm.y == epoch && (uint32_t)gm.w == cnt % 15u + 1u));
+                (shared_ok && gm.y == epoch && (uint32_t)gm.w == (cnt == 15u ? 1u : cnt + 1u)));
     if (__ballot(overtaken) != 0ull && lane == 0) {
       atomicOr(&ctrl[2], 1u);
       atomicOr(&ctrl[18], 1u);  // sticky copy (never zeroed by a launch)
@@ -422,15 +453,23 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       // seed attributes only for players without a shared rating (their first
       // match): one extra round trip in the rare iterations that need it, instead
       // of a 16-B load per participant per match (-19% executor time on the bench)
-      const bool need_seed = own && smu != smu;
-      if (__ballot(need_seed) != 0ull && need_seed) at4 = reinterpret_cast<const float4*>(attrs)[id];
-      const float attr[4] = {at4.x, at4.y, at4.z, at4.w};
-      float pms = 0.f, pss = 1.f, pmm = 0.f, psm = 1.f;
-      uint32_t pflags = 0;
-      uint8_t lst = kRated;
-      if (own)
-        lst = player_prior<float>(smu, ssg, mmu, msg, attr, us, prm.vst, pms, pss, pmm, psm,
-                                  pflags);
+      // player_prior (rate_core.h) as selects: only the seeding of a player's
+      // first match (the attribute load, rare) stays a branch
+      const bool sh_null = smu != smu, md_null = mmu != mmu;
+      float pms = smu, pss = ssg;
+      bool seed_ok = true;
+      if (__ballot(own && sh_null) != 0ull && own && sh_null) {
+        const float4 at4 = reinterpret_cast<const float4*>(attrs)[id];
+        const float attr[4] = {at4.x, at4.y, at4.z, at4.w};
+        seed_ok = seed_prior<float>(attr, us, prm.vst, pms, pss);
+      }
+      const bool sh_bad = !sh_null && !(ssg == ssg && ssg != 0.f);
+      const bool md_bad = !md_null && !(msg == msg && msg != 0.f);
+      float pmm = md_null ? pms : mmu, psm = md_null ? pss : msg;
+      uint32_t pflags = own ? ((sh_null ? 2u : 1u) | (md_null ? 4u : 0u)) : 0u;
+      const uint8_t lst = !own ? (uint8_t)kRated
+                               : (sh_null && !seed_ok) ? (uint8_t)kErrSeed
+                               : (sh_bad || md_bad) ? (uint8_t)kErrSigma : (uint8_t)kRated;
       const uint64_t eb = __ballot(lst != kRated) & gmask;
       uint8_t gst = kRated;
       if (eb) gst = (uint8_t)__shfl((int)lst, (int)__builtin_ctzll(eb));
@@ -502,7 +541,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         // shared granule: tagged with the next reader + bumped mode counter;
         // mode granule: tagged with its new write count
         const uint32_t succ = lk0 & kMatchMask;
-        const uint32_t c = ((rcnt >> (4 * mode)) & 15u) % 15u + 1u;
+        const uint32_t c4 = (rcnt >> (4 * mode)) & 15u;  // write count, wraps 15 -> 1
+        const uint32_t c = c4 == 15u ? 1u : c4 + 1u;
         const uint32_t ncnt = (rcnt & ~(15u << (4 * mode))) | (c << (4 * mode));
         const uint32_t stag = (uint32_t)epoch | (ncnt << 8);
         __builtin_amdgcn_raw_buffer_store_b128(
@@ -523,7 +563,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
               }
           }
           if (lh >= 0) {  // held by this wave: release it through LDS, next iteration
-            atomicAdd(&lloc[wv][0][0] + lh * kChunk + ((int32_t)succ - lcb), 1u);
+            atomicAdd(reinterpret_cast<uint32_t*>(&lloc[wv][(int32_t)succ - lcb]) + lh, 1u);
           } else {
             __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -558,6 +598,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     };
 
     // ---------------------------------------------- (5) next iteration's counter polls
+    if constexpr (DIAG) d_i[2] = __builtin_amdgcn_s_memrealtime();
     ++iter;
 #pragma unroll
     for (int h = 0; h < kH; ++h)
@@ -614,10 +655,12 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         r[S + 1] = dup ? (r[S + 1] | 8) : (r[S + 1] & ~8);
       }
 #pragma unroll
-      for (int k = 0; k < R; ++k) lrec[wv][staging][lane * R + k] = r[k];
-#pragma unroll
       for (int h = 0; h < kH; ++h)
-        if (h == staging) lloc[wv][h][lane] = 0u;
+        if (h == staging) {
+#pragma unroll
+          for (int k = 0; k < R; ++k) hrec[h][k] = r[k];
+        }
+      reinterpret_cast<uint32_t*>(&lloc[wv][lane])[staging] = 0u;
       const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
       if (mm < M && est != kRated) {  // no state, no dependencies: finish it now
 #pragma unroll
@@ -644,6 +687,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         d_issue += d_w0 - d_it0;
         d_wait += d_w1 - d_w0;
         d_after += end - d_w1;
+        // the issue phase: staging + readiness, assignment, this batch's loads, polls + ticket
+        d_s[0] += d_i[0] - d_it0;
+        d_s[1] += d_i[1] - d_i[0];
+        d_s[2] += d_i[2] - d_i[1];
+        d_s[3] += d_w0 - d_i[2];
         // the markers are per lane (the rating ran in the assigned groups): take lane 0's group
         const uint64_t p1 = __builtin_amdgcn_readfirstlane((uint32_t)d_p[1]) |
                             ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(d_p[1] >> 32)) << 32);
@@ -694,6 +742,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           // [32..39] the after phase split: prior + sums, update, publish, outputs + rest
           for (int q = 0; q < 4; ++q)
             atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[32 + 2 * q]), (unsigned long long)d_t[q]);
+          // [40..47] the issue phase split
+          for (int q = 0; q < 4; ++q)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[40 + 2 * q]), (unsigned long long)d_s[q]);
         }
       }
       if constexpr (TELE) {
@@ -768,7 +819,8 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 28);
   if (M <= 0) return 0;
   if (prm.chunk_len < 1 || prm.chunk_len > kChunk) return (int)hipErrorInvalidValue;
-  if ((int64_t)prm.num_players * kRowFloats * 4 >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  if ((int64_t)prm.num_players * kRowFloats * 4 > kOutOfRange) return (int)hipErrorInvalidValue;
+  if (M * 2 * K * 4 > kOutOfRange) return (int)hipErrorInvalidValue;  // links, read by resource
   if (!prm.epoch_ptr && (prm.epoch < 1 || prm.epoch > 255)) return (int)hipErrorInvalidValue;
   // the executor writes one packed row per match (ops/rate.py RateResult.allocate)
   const int S = 2 * K;

@@ -352,6 +352,10 @@ class BatchRater:
                 # publish (granules + hand-off), output records + bookkeeping
                 "after_prior_us": per(u64(32)), "after_update_us": per(u64(34)),
                 "after_publish_us": per(u64(36)), "after_rest_us": per(u64(38)),
+                # the issue phase split: chunk staging + readiness, assignment (pick
+                # list), this batch's loads, next polls + ticket
+                "issue_ready_us": per(u64(40)), "issue_assign_us": per(u64(42)),
+                "issue_loads_us": per(u64(44)), "issue_polls_us": per(u64(46)),
                 "local_handoffs": c[26], "global_handoffs": c[27]}
 
     def telemetry_errors(self, device) -> int:

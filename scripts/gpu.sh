@@ -14,6 +14,8 @@
 #   skew       bench.py --skew 2 and 3
 #   dp         bench.py --gpus 2 and 4 on this one GPU (gloo rehearsal of the spawn path)
 #   accuracy   sweep-DP accuracy, 8 ranks x 10M matches over 1M players, sweeps 1,2,4,8
+#   hop        quick executor A/B (serial chain + 10M window, local hand-off, timing build)
+#   ab         in-call A/B of executor builds (AB_LIBS, scripts/ab_build.sh), interleaved rounds
 #   micro      executor hop latency A/B (scripts/tune_rate.py: serial / uniform / skewed, timing build)
 #   prof       rocprofv3 --kernel-trace --stats of config 2
 #   pmc        rocprofv3 --pmc passes over the executor (10M-match window, tune_rate.py: one
@@ -67,6 +69,25 @@ for task in "$@"; do
       run accuracy/dp4_skew 900 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 4 \
           --players 2e4 --matches-per-rank 2e5 --windows 8 --warm-windows 1 --sweeps 1,2,3,4
       ;;
+    hop)  # quick executor A/B: serial chain + 10M window, production + timing build
+      run hop/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 \
+          --rounds 2 --blocks 8 --local 1 --diag 0,1
+      run hop/random 300 $PY scripts/tune_rate.py --pattern random --rounds 3 --local 1 --diag 0,1
+      grep -h "^round" gpurun_out/hop/*.log | cut -c1-420
+      ;;
+    ab)  # in-call A/B of executor builds: AB_LIBS="name:ab/name_C.so ..." ("cur:" = the tree's),
+         # rounds interleaved so box drift hits every build alike (scripts/ab_build.sh)
+      for r in 1 2 3; do
+        for spec in ${AB_LIBS:-cur:}; do
+          name=${spec%%:*}; lib=${spec#*:}
+          ANA_NATIVE_LIB=$lib run ab/serial_${name}_$r 300 $PY scripts/tune_rate.py --pattern serial --players 1000 \
+              --matches 20000 --rounds 1 --blocks 8 --local 1 --diag 0
+          ANA_NATIVE_LIB=$lib run ab/random_${name}_$r 300 $PY scripts/tune_rate.py --pattern random --rounds 2 \
+              --local 1 --diag 0
+        done
+      done
+      for f in gpurun_out/ab/*.log; do echo "$f $(grep -h '^round' $f | sed -E 's/.*rate +([0-9.]+) ms.*/\1/' | tr '\n' ' ')"; done
+      ;;
     micro)  # executor hop latency: serial chain, uniform window, skewed window (timing build A/B)
       run micro/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 \
           --rounds 2 --blocks ${MICRO_BLOCKS:-8,512} --local ${MICRO_LOCAL:-0,1} --diag 0,1
@@ -91,7 +112,7 @@ for task in "$@"; do
         (cd /tmp && run pmc/$tag/$name 120 rocprofv3 --pmc $set --kernel-trace --stats \
             -d "$ROOT/gpurun_out/pmc/$tag/$name" -o run --output-format csv -- $PY "$ROOT/scripts/tune_rate.py" \
             --rounds 1 ${PMC_ARGS:-}) || exit $?
-        $PY scripts/pmc_kernel.py "gpurun_out/pmc/$tag/$name/*" rate_dataflow >> gpurun_out/pmc/$tag/executor.txt
+        $PY scripts/pmc_kernel.py "gpurun_out/pmc/$tag/$name" rate_dataflow >> gpurun_out/pmc/$tag/executor.txt
       done
       cat gpurun_out/pmc/$tag/executor.txt
       ;;

@@ -87,6 +87,8 @@ def main():
                     d["after_us"])
                 line += " [prior %.3f update %.3f publish %.3f rest %.3f]" % (
                     d["after_prior_us"], d["after_update_us"], d["after_publish_us"], d["after_rest_us"])
+                line += " issue [ready %.3f assign %.3f loads %.3f polls %.3f]" % (
+                    d["issue_ready_us"], d["issue_assign_us"], d["issue_loads_us"], d["issue_polls_us"])
             if args.pattern == "serial":
                 line += " | %.3f us per hop" % ((t2 - t1) * 1e6 / M)
             print(line, flush=True)
