@@ -226,61 +226,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 
   for (;;) {
     if constexpr (DIAG) d_it0 = __builtin_amdgcn_s_memrealtime();
-    // ---------------------------------------------- (1) a ticket came back: stage its chunk
-    int staging = -1;
-    int32_t r[R];
-    uint32_t lks[S];  // the staged match's links: its readiness count
-#pragma unroll
-    for (int k = 0; k < R; ++k) r[k] = -1;
-#pragma unroll
-    for (int k = 0; k < S; ++k) lks[k] = 0u;
-    if (tk_pending) {
-      // readfirstlane, not a shuffle: the compiler then knows the chunk bases and
-      // masks derived from it are wave-uniform and keeps the bookkeeping scalar
-      const unsigned t = __builtin_amdgcn_readfirstlane(tk);
-      tk_pending = false;
-      const int64_t c = (int64_t)t * kHeads + head;
-      // tail signal: the first ticket of each shard at or past progress_at, and its
-      // first ticket past the end (so a threshold beyond the window still fires)
-      const int64_t nchunks = (M + cl - 1) / cl;
-      if (prm.progress && lane == 0 &&
-          ((c >= prm.progress_at && c < prm.progress_at + kHeads) ||
-           (c >= nchunks && c < nchunks + kHeads)))
-        __hip_atomic_store(prm.progress, prm.progress_value, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      if (c * cl >= M) {
-        exhausted = true;
-      } else {
-#pragma unroll
-        for (int h = kH - 1; h >= 0; --h)
-          if (cbase[h] < 0) staging = h;
-#pragma unroll
-        for (int h = 0; h < kH; ++h)
-          if (h == staging) cbase[h] = (int32_t)(c * cl);
-        const int64_t m = c * cl + lane;
-        if (lane < cl && m < M) {
-          const int32_t* src = rec + m * R;
-          if constexpr (R % 4 == 0) {
-#pragma unroll
-            for (int k = 0; k < R / 4; ++k) {
-              const v4i v = reinterpret_cast<const v4i*>(src)[k];
-              r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
-            }
-          } else {
-#pragma unroll
-            for (int k = 0; k < R; ++k) r[k] = src[k];
-          }
-          const v2u* ls = reinterpret_cast<const v2u*>(link + m * S);  // S even: 8-B aligned
-#pragma unroll
-          for (int k = 0; k < S / 2; ++k) {
-            const v2u v = ls[k];
-            lks[2 * k] = v.x;
-            lks[2 * k + 1] = v.y;
-          }
-        }
-      }
-    }
-
     // ---------------------------------------------- (2) readiness from the last poll
     // one unconditional LDS read: a free slot's stale count is masked by pend = 0,
     // and without local hand-off the counts stay 0
@@ -393,6 +338,63 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       nb.gs = __builtin_amdgcn_raw_buffer_load_b128(rs, goff, 0, 16);
       nb.gm = __builtin_amdgcn_raw_buffer_load_b128(rs, goff + 16 * (1 + mode), 0, 16);
       nb.lk0 = __builtin_amdgcn_raw_buffer_load_b32(rl, inr ? (m * S + j) * 4 : kOutOfRange, 0, 0);
+    }
+
+    // ---------------------------------------------- (1) a ticket came back: stage its chunk
+    // (after this batch's loads: the top of the loop waits only for the polls)
+    if constexpr (DIAG) d_i[2] = __builtin_amdgcn_s_memrealtime();
+    int staging = -1;
+    int32_t r[R];
+    uint32_t lks[S];  // the staged match's links: its readiness count
+#pragma unroll
+    for (int k = 0; k < R; ++k) r[k] = -1;
+#pragma unroll
+    for (int k = 0; k < S; ++k) lks[k] = 0u;
+    if (tk_pending) {
+      // readfirstlane, not a shuffle: the compiler then knows the chunk bases and
+      // masks derived from it are wave-uniform and keeps the bookkeeping scalar
+      const unsigned t = __builtin_amdgcn_readfirstlane(tk);
+      tk_pending = false;
+      const int64_t c = (int64_t)t * kHeads + head;
+      // tail signal: the first ticket of each shard at or past progress_at, and its
+      // first ticket past the end (so a threshold beyond the window still fires)
+      const int64_t nchunks = (M + cl - 1) / cl;
+      if (prm.progress && lane == 0 &&
+          ((c >= prm.progress_at && c < prm.progress_at + kHeads) ||
+           (c >= nchunks && c < nchunks + kHeads)))
+        __hip_atomic_store(prm.progress, prm.progress_value, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      if (c * cl >= M) {
+        exhausted = true;
+      } else {
+#pragma unroll
+        for (int h = kH - 1; h >= 0; --h)
+          if (cbase[h] < 0) staging = h;
+#pragma unroll
+        for (int h = 0; h < kH; ++h)
+          if (h == staging) cbase[h] = (int32_t)(c * cl);
+        const int64_t m = c * cl + lane;
+        if (lane < cl && m < M) {
+          const int32_t* src = rec + m * R;
+          if constexpr (R % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < R / 4; ++k) {
+              const v4i v = reinterpret_cast<const v4i*>(src)[k];
+              r[4 * k] = v.x; r[4 * k + 1] = v.y; r[4 * k + 2] = v.z; r[4 * k + 3] = v.w;
+            }
+          } else {
+#pragma unroll
+            for (int k = 0; k < R; ++k) r[k] = src[k];
+          }
+          const v2u* ls = reinterpret_cast<const v2u*>(link + m * S);  // S even: 8-B aligned
+#pragma unroll
+          for (int k = 0; k < S / 2; ++k) {
+            const v2u v = ls[k];
+            lks[2 * k] = v.x;
+            lks[2 * k + 1] = v.y;
+          }
+        }
+      }
     }
 
     // ---------------------------------------------- (10) rate a batch
@@ -597,15 +599,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
     };
 
-    // ---------------------------------------------- (5) next iteration's counter polls
-    if constexpr (DIAG) d_i[2] = __builtin_amdgcn_s_memrealtime();
-    ++iter;
-#pragma unroll
-    for (int h = 0; h < kH; ++h)
-      if ((pend[h] >> lane) & 1ull)
-        dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-
     // ---------------------------------------------- (6) next ticket if a ring slot is free
     {
       bool free_slot = false;
@@ -707,6 +700,16 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         }
       }
     }
+
+    // ---------------------------------------------- (5) next iteration's counter polls, as late as possible:
+    // the readiness at the top waits for them, so what it sees is one rating
+    // phase fresher than a poll issued before the wait
+    ++iter;
+#pragma unroll
+    for (int h = 0; h < kH; ++h)
+      if ((pend[h] >> lane) & 1ull)
+        dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
 
     // ---------------------------------------------- (11) retire finished chunks
     {
