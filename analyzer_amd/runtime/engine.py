@@ -13,6 +13,12 @@ Two schedule buffer sets alternate; events order "schedule(i+1) may reuse the
 set that rate(i-1) consumed" and "rate(i) needs schedule(i)".  On the CPU the
 same API runs the host mirror sequentially.
 
+Default since round 2 (``ANA_PREPASS_SERIAL=1``): the prepass runs on the main
+stream between launches.  Measured on MI355X for config 2, the co-running
+prepass slows the latency-bound executor by more than it hides (step 7.79 ms
+serial vs 7.94-8.17 ms with tail overlap at 0.9-0.8, profiles/r2/tail_sweep.log),
+so the overlap below is opt-in (``ANA_PREPASS_SERIAL=0``).
+
 Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.8): the
 prepass of window i+1 does not start with rate(i) -- co-running the two for the
 whole launch costs the latency-bound executor about as much as the prepass
@@ -63,7 +69,8 @@ class WindowPipeline:
         self.windows_rated = 0
         # tail overlap: signal word + number of the last enqueued rate launch
         self.ecfg = EngineConfig.from_env()
-        self.tail = self.ecfg.prepass_at
+        # serial prepass (the default): nothing to overlap, no tail signal
+        self.tail = 0.0 if self.ecfg.prepass_serial else self.ecfg.prepass_at
         self._signal = 0
         self._seq = 0
         if self.cuda and self.tail > 0:
@@ -80,7 +87,7 @@ class WindowPipeline:
 
         ecfg = EngineConfig.from_env()
         if ecfg.prepass_serial:
-            return torch.cuda.current_stream(self.device)  # no overlap (A/B)
+            return torch.cuda.current_stream(self.device)  # no overlap (the default)
         n = ecfg.prepass_cus
         if n > 0:
             from ..ops.native import native

@@ -15,6 +15,7 @@
 #   dp         bench.py --gpus 2 and 4 on this one GPU (gloo rehearsal of the spawn path)
 #   accuracy   sweep-DP accuracy, 8 ranks x 10M matches over 1M players, sweeps 1,2,4,8
 #   hop        quick executor A/B (serial chain + 10M window, local hand-off, timing build)
+#   tail       prepass start point sweep for config 2 (ANA_PREPASS_AT, serial)
 #   ab         in-call A/B of executor builds (AB_LIBS, scripts/ab_build.sh), interleaved rounds
 #   micro      executor hop latency A/B (scripts/tune_rate.py: serial / uniform / skewed, timing build)
 #   prof       rocprofv3 --kernel-trace --stats of config 2
@@ -86,7 +87,18 @@ for task in "$@"; do
               --local 1 --diag 0
         done
       done
-      for f in gpurun_out/ab/*.log; do echo "$f $(grep -h '^round' $f | sed -E 's/.*rate +([0-9.]+) ms.*/\1/' | tr '\n' ' ')"; done
+      for f in gpurun_out/ab/*.log; do
+        echo "$f $(grep -h '^round' $f | sed -E 's/.*schedule +([0-9.]+) ms rate +([0-9.]+) ms.*/sched \1 rate \2 |/' | tr '\n' ' ')"
+      done
+      ;;
+    tail)  # where the next window's prepass starts (ANA_PREPASS_AT sweep, config 2; 0 = with the launch)
+      for r in 1 2; do
+        for at in ${TAIL_AT:-0.8 0.9}; do
+          ANA_PREPASS_SERIAL=0 ANA_PREPASS_AT=$at run tail/config2_at${at}_$r 400 $PY bench.py --steps 20 --warmup 3
+        done
+        ANA_PREPASS_SERIAL=1 run tail/config2_serial_$r 400 $PY bench.py --steps 20 --warmup 3
+      done
+      for f in gpurun_out/tail/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
       ;;
     micro)  # executor hop latency: serial chain, uniform window, skewed window (timing build A/B)
       run micro/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 \
@@ -98,7 +110,8 @@ for task in "$@"; do
     prof)
       mkdir -p gpurun_out/prof
       (cd /tmp && run prof/config2 400 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof/config2" \
-          -o run --output-format csv -- $PY "$ROOT/bench.py" --steps 5 --warmup 2) || exit $?
+          -o run --output-format csv -- $PY "$ROOT/bench.py" --steps 5 --warmup 2 ${PROF_ARGS:-}) || exit $?
+      $PY scripts/prof_summary.py gpurun_out/prof/config2/run_kernel_trace.csv | tee gpurun_out/prof/config2/summary.txt
       ;;
     pmc)
       # PMC_TAG / PMC_ARGS select the workload (default: the 10M-match bench window)
