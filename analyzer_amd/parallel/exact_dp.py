@@ -60,7 +60,11 @@ class RoundPlan:
         # slice q of round r: [starts[r] + r_q, starts[r] + r_{q+1}) with sizes differing by <= 1
         q = np.arange(size + 1)
         self.bounds = starts[:-1, None] + (counts[:, None] * q[None, :]) // size   # [R, size+1]
-        self.max_slice = int((self.bounds[:, 1:] - self.bounds[:, :-1]).max()) if M else 0
+        sizes = self.bounds[:, 1:] - self.bounds[:, :-1]
+        self.max_slice = int(sizes.max()) if M else 0
+        # per round: the largest slice of any rank -- the round's exchange size
+        # (every rank knows the plan, so the gathers agree without a size exchange)
+        self.round_max = sizes.max(1).astype(np.int64) if M else np.zeros(0, np.int64)
 
 
 def rate_exact_dp(rater: BatchRater, roster: Roster, rec: torch.Tensor, K: int,
@@ -90,8 +94,8 @@ def rate_exact_dp(rater: BatchRater, roster: Roster, rec: torch.Tensor, K: int,
     offs = np.concatenate([[0], np.cumsum(plan.bounds[:, rank + 1] - plan.bounds[:, rank])])
     cap = max(1, plan.max_slice * S)
     f = dict(dtype=torch.float32, device=dev)
-    send = torch.empty((cap, 33), **f)
-    recv = torch.empty((size * cap, 33), **f)
+    send_buf = torch.empty((cap, 33), **f)
+    recv_buf = torch.empty((size * cap, 33), **f)
     staged = dev.type == "cuda" and size > 1 and dist.get_backend(group) == "gloo"
     if dev.type == "cuda":
         rater.clear_sticky(dev)
@@ -105,12 +109,16 @@ def rate_exact_dp(rater: BatchRater, roster: Roster, rec: torch.Tensor, K: int,
                 packed=my_out.packed[lo:hi]), check=False)
         if size <= 1:
             continue
+        # this round's exchange: the largest slice's rows (a 10M window's rounds
+        # average ~1/20 of the largest), not the window-wide capacity
+        rc = max(1, int(plan.round_max[r]) * S)
+        send, recv = send_buf[:rc], recv_buf[:size * rc]
         if hi > lo:
             native().pack_rows(sub, K, res.status, roster.state, send)
         else:
             send[:, 32].view(torch.int32).fill_(-1)
         if staged:  # gloo moves host memory only
-            h = torch.empty((size * cap, 33))
+            h = torch.empty((size * rc, 33))
             dist.all_gather_into_tensor(h, send.cpu(), group=group)
             recv.copy_(h)
         else:

@@ -15,6 +15,8 @@
 #   dp         bench.py --gpus 2 and 4 on this one GPU (gloo rehearsal of the spawn path)
 #   accuracy   sweep-DP accuracy, 8 ranks x 10M matches over 1M players, sweeps 1,2,4,8
 #   hop        quick executor A/B (serial chain + 10M window, local hand-off, timing build)
+#   merge      sweep-merge message/decode kernels at P = 1M, 10M on one GPU
+#   exactdp    exact DP (C2) rehearsal, 2/4 gloo ranks on one GPU, rounds + time per window
 #   tail       prepass start point sweep for config 2 (ANA_PREPASS_AT, serial)
 #   ab         in-call A/B of executor builds (AB_LIBS, scripts/ab_build.sh), interleaved rounds
 #   micro      executor hop latency A/B (scripts/tune_rate.py: serial / uniform / skewed, timing build)
@@ -90,6 +92,13 @@ for task in "$@"; do
       for f in gpurun_out/ab/*.log; do
         echo "$f $(grep -h '^round' $f | sed -E 's/.*schedule +([0-9.]+) ms rate +([0-9.]+) ms.*/sched \1 rate \2 |/' | tr '\n' ' ')"
       done
+      ;;
+    merge)  # sweep-merge kernels (messages, decode) at 1M and 10M players, no collective
+      run merge/kernels 300 $PY scripts/merge_micro.py --players 1e6,1e7
+      ;;
+    exactdp)  # exact DP rehearsal: 2 and 4 gloo ranks on this one GPU, 1M-match window
+      run exactdp/r2 600 $PY scripts/exact_dp_rehearsal.py --ranks 2
+      run exactdp/r4 600 $PY scripts/exact_dp_rehearsal.py --ranks 4
       ;;
     tail)  # where the next window's prepass starts (ANA_PREPASS_AT sweep, config 2; 0 = with the launch)
       for r in 1 2; do

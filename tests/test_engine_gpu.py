@@ -379,3 +379,42 @@ def test_edge_windows_device_vs_host(gpu_device, case):
     rd = R.BatchRater().rate(dev, rec.to(gpu_device), K)
     assert torch.equal(rd.status.cpu(), rh.status)
     assert_close_to_fp64(rd, dev, rh, host)
+
+
+def _exact_dp_device(rank, size, P, M, K, seed):
+    from analyzer_amd.parallel.exact_dp import rate_exact_dp
+
+    dev = torch.device("cuda:0")
+    roster = make_roster(RosterSpec(num_players=P, seed=seed), device=dev)
+    rec = make_stream(StreamSpec(team_size=K, seed=seed + 1, p_afk=0.05, p_tie=0.05), M, P, K=K, device=dev)
+    out = rate_exact_dp(R.BatchRater(), roster, rec, K)
+    return {"state": roster.state.cpu(), "status": out.status.cpu(), "s_mu": out.s_mu.cpu(),
+            "delta": out.delta.cpu(), "m_mu": out.m_mu.cpu()}
+
+
+def test_exact_dp_two_ranks_on_device_bit_identical(gpu_device, tmp_path):
+    """C2 on the device: 2 ranks (gloo, both on this GPU) rate a window round by
+    round and exchange packed rows; replicas and sharded outputs equal one
+    device rating the window alone, bit for bit."""
+    from test_distributed import run_ranks
+
+    P, M, K, seed = 3000, 20000, 3, 17
+    res = run_ranks(_exact_dp_device, 2, tmp_path, P, M, K, seed)
+    roster = make_roster(RosterSpec(num_players=P, seed=seed), device=gpu_device)
+    rec = make_stream(StreamSpec(team_size=K, seed=seed + 1, p_afk=0.05, p_tie=0.05), M, P, K=K,
+                      device=gpu_device)
+    ref = R.BatchRater().rate(roster, rec, K)
+    want = roster.state.cpu()
+    for r in res:
+        # tag words of exchanged rows are reset; compare the rating floats
+        got, exp = r["state"].view(P, 8, 4), want.view(P, 8, 4)
+        for c in (0, 2):
+            assert torch.equal(got[..., c].nan_to_num(-7), exp[..., c].nan_to_num(-7))
+    owner = torch.stack([r["status"] != 255 for r in res]).sum(0)
+    assert bool((owner == 1).all())
+    for key in ("s_mu", "delta", "m_mu"):
+        merged = torch.full_like(getattr(ref, key).cpu(), float("nan"))
+        for r in res:
+            mine = r["status"] != 255
+            merged[mine] = r[key][mine]
+        assert torch.equal(merged.nan_to_num(-7), getattr(ref, key).cpu().nan_to_num(-7)), key
