@@ -13,9 +13,9 @@ Everything about the window's shape is known on the host before the first
 launch -- rounds, slice bounds, the largest slice -- so the round loop never
 waits for the device: a rank's slices are gathered once into round order, and
 per round it launches the rating, one pack kernel (csrc/sweep.hip: the rows of
-its rated players + their ids into a fixed-capacity buffer, -1 padded), ONE
-``all_gather_into_tensor`` and one unpack kernel.  No ``.item()``, no
-variable-size collectives.
+its rated players + their ids, -1 padded to the round's largest slice, which
+every rank reads off the shared plan), ONE ``all_gather_into_tensor`` and one
+unpack kernel.  No ``.item()``, no size exchange.
 
 How far this scales is set by the DAG, not by the implementation: a 10M 3v3
 window over 1M uniform players has ~900 rounds of ~11k matches, so exact DP
