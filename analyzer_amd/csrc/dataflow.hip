@@ -149,11 +149,12 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   constexpr int kH = kHeld;
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
-  static_assert(kH == 4, "readiness reads the held chunks' local counts as one uint4");
+  static_assert(kH == 2 || kH == 4, "readiness reads the held chunks' local counts as one vector");
+  typedef uint32_t hvec __attribute__((ext_vector_type(kH)));
   // local hand-off counters: increments of each held match's completion count
   // by publishes of THIS wave (never also added to the global counter); [lane][h]
-  // so a lane reads its four in one ds_read_b128
-  __shared__ uint4 lloc[kWavesPerBlock][kChunk];
+  // so a lane reads them in one ds_read_b64/b128
+  __shared__ hvec lloc[kWavesPerBlock][kChunk];
   // this iteration's pick per group, written by the lane holding the match:
   // {match index, slot << 8 | lane in chunk, meta0, meta1, player ids...}
   constexpr int SP = (4 + S + 3) / 4 * 4;
@@ -221,7 +222,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     t = __builtin_amdgcn_readfirstlane(t);
     return (int64_t)t < tele_tiles ? (int64_t)t : -1;
   };
-  const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : 8u;
+  const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : prm.idle_spins < 0 ? 0u : 8u;
   const int cl = prm.chunk_len;  // matches per ticket (<= kChunk lanes)
 
   for (;;) {
@@ -231,11 +232,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // and without local hand-off the counts stay 0
     uint64_t ready[kH];
     {
-      const uint4 lv = lloc[wv][lane];
-      const uint32_t loc[4] = {lv.x, lv.y, lv.z, lv.w};
+      const hvec lv = lloc[wv][lane];
 #pragma unroll
       for (int h = 0; h < kH; ++h)
-        ready[h] = __ballot(dval[h] != kNone && dval[h] + loc[h] == need[h]) & pend[h];
+        ready[h] = __ballot(dval[h] != kNone && dval[h] + lv[h] == need[h]) & pend[h];
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
     if constexpr (DIAG) d_i[0] = __builtin_amdgcn_s_memrealtime();

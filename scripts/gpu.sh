@@ -72,6 +72,12 @@ for task in "$@"; do
       run accuracy/dp4_skew 900 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 4 \
           --players 2e4 --matches-per-rank 2e5 --windows 8 --warm-windows 1 --sweeps 1,2,3,4
       ;;
+    idle)  # idle back-off and grid size sweep of the executor (10M window + serial chain)
+      run idle/random 400 $PY scripts/tune_rate.py --pattern random --rounds 2 --idle=-1,2,8,16 --blocks 512,1024
+      run idle/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 --rounds 2 \
+          --blocks 8 --idle=-1,2,8
+      grep -h "^round 1" gpurun_out/idle/*.log | cut -c1-120
+      ;;
     hop)  # quick executor A/B: serial chain + 10M window, production + timing build
       run hop/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 \
           --rounds 2 --blocks 8 --local 1 --diag 0,1
