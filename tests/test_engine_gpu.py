@@ -418,3 +418,68 @@ def test_exact_dp_two_ranks_on_device_bit_identical(gpu_device, tmp_path):
             mine = r["status"] != 255
             merged[mine] = r[key][mine]
         assert torch.equal(merged.nan_to_num(-7), getattr(ref, key).cpu().nan_to_num(-7)), key
+
+
+def _rccl_single_rank(rank, size, P, M, K, seed):
+    """One RCCL rank on the device: the collectives the DP paths issue, and the
+    bucketed sweep merge run through a real (1-rank) RCCL communicator."""
+    from analyzer_amd.parallel.comm import all_reduce_sum, all_to_all_rows, world
+    from analyzer_amd.parallel.sweep import SweepMerger
+
+    assert torch.distributed.get_backend() == "nccl" and world() == (0, 1)
+    dev = torch.device("cuda:0")
+    x = torch.arange(1000, dtype=torch.float32, device=dev)
+    all_reduce_sum(x)
+    y = torch.arange(256, dtype=torch.bfloat16, device=dev).view(64, 4)
+    z = torch.empty_like(y)
+    all_to_all_rows(z, y)
+    g = torch.empty(2000, device=dev)
+    torch.distributed.all_gather_into_tensor(g[:1000], x)
+    roster = make_roster(RosterSpec(num_players=P, seed=seed), device=dev)
+    rec = make_stream(StreamSpec(team_size=K, seed=seed + 1), M, P, K=K, device=dev)
+    # world_size=2 forces the full merge (messages -> RCCL all-reduce -> decode) on the 1-rank group
+    merger = SweepMerger(P, dev, world_size=2, bucket_rows=P // 3 + 1)
+    merger.begin(roster)
+    R.BatchRater().rate(roster, rec, K)
+    posterior = roster.state.clone()
+    merger.merge(roster)
+    torch.cuda.synchronize()
+    return {"x": x.cpu(), "z": z.float().cpu(), "y": y.float().cpu(), "g": g[:1000].cpu(),
+            "posterior": posterior.cpu(), "merged": roster.state.cpu()}
+
+
+def test_rccl_single_rank_collectives_and_merge(gpu_device, tmp_path, monkeypatch):
+    """RCCL (backend "nccl") on this box: one rank runs the comm layer and the
+    pipelined sweep merge through the communicator; with one rank the merge must
+    give back the rank's own posterior (up to the natural-parameter round trip).
+    Several ranks cannot share one GPU under RCCL -- that path runs in the
+    driver's multi-GPU bench."""
+    import torch.multiprocessing as mp
+
+    from test_distributed import _free_port
+
+    P, M, K, seed = 5000, 20000, 3, 23
+    mp.spawn(_rccl_entry, args=(_free_port(), str(tmp_path), (P, M, K, seed)), nprocs=1, join=True)
+    r = torch.load(str(tmp_path / "r0.pt"), weights_only=True)
+    assert torch.equal(r["x"], torch.arange(1000, dtype=torch.float32))
+    assert torch.equal(r["z"], r["y"]) and torch.equal(r["g"], r["x"])
+    post = r["posterior"].view(P, 8, 4)[..., 0::2]
+    got = r["merged"].view(P, 8, 4)[..., 0::2]
+    np.testing.assert_allclose(got[..., 0].numpy(), post[..., 0].numpy(), rtol=0, atol=2e-3, equal_nan=True)
+    np.testing.assert_allclose(got[..., 1].numpy(), post[..., 1].numpy(), rtol=1e-4, atol=0, equal_nan=True)
+
+
+def _rccl_entry(rank, port, outdir, args):
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        res = _rccl_single_rank(0, 1, *args)
+        torch.save(res, os.path.join(outdir, "r0.pt"))
+    finally:
+        dist.destroy_process_group()
