@@ -180,7 +180,7 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   if (dev.is_cuda()) {
     check(workspace, "workspace", torch::kUInt8, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
-    TORCH_CHECK(ctrl.numel() >= 64, "ctrl must have 64 entries");
+    TORCH_CHECK(ctrl.numel() >= 48, "ctrl must have 48 entries");
     const size_t need = ana::schedule_workspace_bytes(M * 2 * K, num_players);
     TORCH_CHECK((size_t)workspace.numel() >= need, "workspace too small: need ", need, " bytes");
     check_hip(ana::launch_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
@@ -225,7 +225,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
           double tau2, double unknown_sigma, bool record_first_prior, int64_t blocks,
           int64_t epoch, bool host_fp64, Tensor tele_evoff, Tensor tele_events, Tensor tele_stats,
           int64_t progress, int64_t progress_value, int64_t progress_at, int64_t epoch_ptr,
-          int64_t chunk_len, bool ctrl_ready, Tensor ovf) {
+          int64_t chunk_len, bool ctrl_ready) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
@@ -288,13 +288,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
     check(ctrl, "ctrl", torch::kInt32, dev);
     TORCH_CHECK(link.numel() == M * S * ana::kLinkWords, "link must be [M, 2K]");
     TORCH_CHECK(deps.numel() == M, "deps must have M entries");
-    TORCH_CHECK(ctrl.numel() >= 64, "ctrl must have 64 entries");
-    // push mode: the schedule of this window wrote need << 16 (same rule, kernels.hip)
-    if (ana::push_mode(M * S)) {
-      check(ovf, "ovf", torch::kInt32, dev);
-      TORCH_CHECK(ovf.numel() >= M, "push mode needs an M-entry zeroed overflow ring");
-      prm.ovf = ovf.data_ptr<int32_t>();
-    }
+    TORCH_CHECK(ctrl.numel() >= 48, "ctrl must have 48 entries");
     TORCH_CHECK(blocks >= 1 && blocks <= 65535, "blocks must be 1..65535");
     // the executor writes packed rows; other layouts go through a packed buffer
     const bool packed = out.s_sig == out.s_mu + S && out.delta == out.s_mu + 2 * S &&
@@ -634,8 +628,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("acquire", &reader_acquire,
            "next filled window as (slot, base, tensor view of pinned memory) or None at EOF")
       .def("release", &ana::RecordReader::release, "return the oldest acquired slot");
-  m.def("push_mode", [](int64_t nslots) { return ana::push_mode(nslots); },
-        "ANA_RATE_PUSH=1 and a window past the micro-batch schedule");
   m.def("cu_masked_stream", &cu_masked_stream, "HIP stream limited to N CUs (spread over XCDs)");
   m.def("progress_signal", &progress_signal, "8-B signal-memory word for the executor's tail signal");
   m.def("stream_wait_value64", &stream_wait_value64, "hipStreamWaitValue64(stream, ptr, >= value)");

@@ -92,10 +92,6 @@ struct RateParams {
   // 1: ctrl[1..15] were zeroed by the schedule launched just before on this stream
   // (launch_schedule zero_ctrl), so the launch skips its own zeroing dispatch
   int32_t ctrl_ready;
-  // push mode (ANA_RATE_PUSH, dataflow.hip): a match is rated by the wave whose
-  // publish completes its last dependency.  ovf: M zeroed int32, the overflow
-  // ring of completed matches a wave's LDS queue had no room for (match + 1)
-  int32_t* ovf;
 };
 
 // Per-match outputs.  The participant record of the reference

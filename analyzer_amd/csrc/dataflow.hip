@@ -126,7 +126,6 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
 // participant's slot facts and granules (section 4 of the executor loop).
 struct Batch {
   int32_t m = 0;
-  uint32_t m0 = 0u, m1 = 0u;  // meta words (push mode re-queues stale matches from them)
   int my_h = -1, my_bit = 0, mode = 0, n0 = 0, n1 = 0, rank0 = 1, rank1 = 1, first = 0, prevdup = -1;
   int32_t id = -1;
   bool inr = false, islast = false, own = false, any_dup = false;
@@ -138,7 +137,7 @@ struct Batch {
 // which frees the registers its code pins).  DIAG: the timing build
 // (ANA_RATE_DIAG=1) -- every wave clocks its iterations and its wait with
 // s_memrealtime and adds them to ctrl[20..27] at exit (launch_rate).
-template <int K, int G, bool TELE, bool DIAG, bool PUSH>
+template <int K, int G, bool TELE, bool DIAG>
 __global__ void __launch_bounds__(256)
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
@@ -160,11 +159,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // {match index, slot << 8 | lane in chunk, meta0, meta1, player ids...}
   constexpr int SP = (4 + S + 3) / 4 * 4;
   __shared__ int32_t lpick[kWavesPerBlock][NG][SP];
-  // PUSH: the wave's queue of matches whose last dependency its own publishes
-  // completed, entries in the pick-slot format (records fetched at publish time)
-  constexpr int QCAP = PUSH ? 128 : 1;
-  constexpr int kQueueH = 15;  // "chunk" index of a queued pick (no pend bit behind it)
-  __shared__ int32_t lq[kWavesPerBlock][QCAP][SP];
   __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -215,34 +209,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     dval[h] = kNone;
     need[h] = 0u;
   }
-  // PUSH: queue ring (wave-uniform), and what the last publishes returned: the
-  // successor, its counter before the increment, and its record (fetched with the
-  // increment, used if the increment completed it)
-  uint32_t qhead = 0u, qtail = 0u, n_proc = 0u;
-  uint32_t pc_old = 0u, pc_succ = kNoMatch;
-  [[maybe_unused]] int32_t pc_rec[PUSH ? R : 1];
-#pragma unroll
-  for (int k = 0; k < (PUSH ? R : 1); ++k) pc_rec[k] = -1;
-  // the entry for a record: {match, queue tag, meta0, meta1 | dup flag, ids}
-  auto queue_entry = [&](int32_t* dst, int32_t mq, const int32_t* rr) {
-    const uint32_t m0q = (uint32_t)rr[S];
-    bool dup = false;
-#pragma unroll
-    for (int a = 0; a < S; ++a)
-#pragma unroll
-      for (int b = 0; b < a; ++b) dup |= rr[a] >= 0 && rr[a] == rr[b];
-    (void)m0q;
-    int32_t w[SP];
-    w[0] = mq;
-    w[1] = kQueueH << 8;
-    w[2] = rr[S];
-    w[3] = dup ? (rr[S + 1] | 8) : (rr[S + 1] & ~8);
-#pragma unroll
-    for (int k = 0; k < SP - 4; ++k) w[4 + k] = k < S ? rr[k] : -1;
-    v4i* d4 = reinterpret_cast<v4i*>(dst);
-#pragma unroll
-    for (int q = 0; q < SP / 4; ++q) d4[q] = v4i{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
-  };
   bool exhausted = false, tk_pending = false;
   unsigned tk = 0;                 // ticket returned to lane 0
   uint32_t spins = 0, iter = 0;
@@ -265,34 +231,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // one unconditional LDS read: a free slot's stale count is masked by pend = 0,
     // and without local hand-off the counts stay 0
     uint64_t ready[kH];
-    if constexpr (PUSH) {
-      // the matches the last publishes completed join the queue (the ring's free
-      // room first, the global overflow ring past it); chunk matches still pending
-      // are sources (no in-window predecessor) and always ready
-      const bool done = pc_succ != kNoMatch && ((pc_old & 0xffffu) + 1u == (pc_old >> 16));
-      const uint64_t cb = __ballot(done);
-      if (cb) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(cb >> 32),
-                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)cb, 0u));
-        const uint32_t room = (uint32_t)QCAP - (qtail - qhead);
-        const uint32_t nc = (uint32_t)__popcll(cb);
-        if (done && rank < room) queue_entry(&lq[wv][(qtail + rank) & (QCAP - 1)][0], (int32_t)pc_succ, pc_rec);
-        if (nc > room) {
-          unsigned base = 0;
-          if (lane == 0)
-            base = __hip_atomic_fetch_add((gu32*)&ctrl[49], nc - room, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          base = __builtin_amdgcn_readfirstlane(base);
-          if (done && rank >= room)
-            __hip_atomic_store((gu32*)(prm.ovf + base + (rank - room)), pc_succ + 1u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
-        qtail += nc < room ? nc : room;
-        n_local += nc;
-      }
-      pc_succ = kNoMatch;
-#pragma unroll
-      for (int h = 0; h < kH; ++h) ready[h] = pend[h];
-    } else {
+    {
       const hvec lv = lloc[wv][lane];
 #pragma unroll
       for (int h = 0; h < kH; ++h)
@@ -309,12 +248,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // oldest chunk first) sat on every hop.  Chunks go in slot order: a wave
     // rarely has more ready matches than groups (2-3.4 per iteration on the
     // bench), so age order buys nothing measurable.
-    int my_h = -1, my_bit = 0, nassigned = 0, nq = 0;
-    if constexpr (PUSH) {  // queued matches first, then chunk sources
-      const uint32_t ql = qtail - qhead;
-      nq = ql < (uint32_t)NG ? (int)ql : NG;
-      nassigned = nq;
-    }
+    int my_h = -1, my_bit = 0, nassigned = 0;
 #pragma unroll
     for (int h = 0; h < kH; ++h) {
       const uint64_t rdy = ready[h];
@@ -342,16 +276,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     int32_t my_m = 0, my_id = -1;
     uint32_t my_m0 = 0u, my_m1 = 0u;
     if (g < nassigned) {  // two LDS reads, one wait
-      const int32_t* slot = (PUSH && g < nq) ? &lq[wv][(qhead + (uint32_t)g) & (QCAP - 1)][0] : &lpick[wv][g][0];
-      const v4i pk = *reinterpret_cast<const v4i*>(slot);
-      if (j < S) my_id = slot[4 + j];
+      const v4i pk = *reinterpret_cast<const v4i*>(&lpick[wv][g][0]);
+      if (j < S) my_id = lpick[wv][g][4 + j];
       my_m = pk.x;
       my_h = pk.y >> 8;
       my_bit = pk.y & 255;
       my_m0 = (uint32_t)pk.z;
       my_m1 = (uint32_t)pk.w;
     }
-    if constexpr (PUSH) qhead += (uint32_t)nq;
     const bool worked = nassigned > 0;
     if constexpr (DIAG) {
       d_worked += worked ? 1u : 0u;
@@ -372,8 +304,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       nb.my_h = my_h;
       nb.my_bit = my_bit;
       nb.m = m;
-      nb.m0 = m0;
-      nb.m1 = m1;
       nb.mode = mode;
       nb.n0 = meta_n0(m0);
       nb.n1 = meta_n1(m0);
@@ -508,35 +438,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         __hip_atomic_fetch_add((gu32*)&ctrl[14], (unsigned)__popcll(stale_lanes), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
       const bool gstale = (stale_lanes & gmask) != 0ull;
-      if constexpr (PUSH) {
-        // queued matches go back to the queue (chunk sources have no predecessor,
-        // so they are never stale): the group's lanes rebuild the entry
-        const bool back = gstale && my_h == kQueueH;
-        const uint64_t lb = __ballot(back && j == 0);
-        if (lb) {
-          const int leader_rank = (int)__popcll(lb & ((1ull << gbase) - 1ull));
-          const uint32_t room = (uint32_t)QCAP - (qtail - qhead);
-          const int nb_ = (int)__popcll(lb);
-          if (back && leader_rank < (int)room) {
-            int32_t* e = &lq[wv][(qtail + (uint32_t)leader_rank) & (QCAP - 1)][0];
-            if (j == 0) {
-              e[0] = bt.m; e[1] = kQueueH << 8; e[2] = (int32_t)bt.m0; e[3] = (int32_t)bt.m1;
-            }
-            if (j < SP - 4) e[4 + j] = j < S ? (inr ? id : -1) : -1;
-          }
-          if (nb_ > (int)room) {
-            unsigned base = 0;
-            if (lane == 0)
-              base = __hip_atomic_fetch_add((gu32*)&ctrl[49], (unsigned)(nb_ - (int)room), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-            base = __builtin_amdgcn_readfirstlane(base);
-            if (back && j == 0 && leader_rank >= (int)room)
-              __hip_atomic_store((gu32*)(prm.ovf + base + (leader_rank - (int)room)), (uint32_t)bt.m + 1u,
-                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          qtail += (uint32_t)nb_ < room ? (uint32_t)nb_ : room;
-        }
-      }
 #pragma unroll
       for (int h = 0; h < kH; ++h) {
         uint64_t back = 0ull;
@@ -548,7 +449,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       if (gstale) my_h = -1;
     }
-    if constexpr (PUSH) n_proc += (uint32_t)__popcll(__ballot(my_h >= 0 && j == 0));
     if (my_h >= 0) {
       const float smu = __int_as_float(gs.x), ssg = __int_as_float(gs.z);
       const float mmu = __int_as_float(gm.x), msg = __int_as_float(gm.z);
@@ -653,24 +553,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         __builtin_amdgcn_raw_buffer_store_b128(
             ok ? granule(nsm, stag, nss, succ) : granule(rsmu, stag, rssg, succ),
             rs, off, 0, 16);
-        if (PUSH && succ != kNoMatch) {
-          // the increment's old value says whether this publish completes the
-          // successor; its record comes along, for the queue at the next top
-          pc_old = __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          pc_succ = succ;
-          const int32_t* src = rec + (int64_t)succ * R;
-          if constexpr (R % 4 == 0) {
-#pragma unroll
-            for (int k = 0; k < R / 4; ++k) {
-              const v4i v = reinterpret_cast<const v4i*>(src)[k];
-              pc_rec[4 * k] = v.x; pc_rec[4 * k + 1] = v.y; pc_rec[4 * k + 2] = v.z; pc_rec[4 * k + 3] = v.w;
-            }
-          } else {
-#pragma unroll
-            for (int k = 0; k < R; ++k) pc_rec[k] = src[k];
-          }
-          n_global += (uint32_t)__popcll(__ballot(true));
-        } else if (succ != kNoMatch) {  // the successor verifies the tags, so no store wait
+        if (succ != kNoMatch) {  // the successor verifies the tags, so no store wait
           int lh = -1;
           int32_t lcb = 0;
           if (local_ok) {
@@ -778,8 +661,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         orows[mm * orow + 5 * S] = (est == kAfk || est == kInvalidRosters) ? 0.f : NAN;
         reinterpret_cast<uint8_t*>(orows + mm * orow + 5 * S + 1)[0] = est;
       }
-      const uint64_t pm = __ballot(mm < M && est == kRated && (!PUSH || nd == 0u));
-      if constexpr (PUSH) n_proc += (uint32_t)__popcll(__ballot(mm < M && est != kRated));
+      const uint64_t pm = __ballot(mm < M && est == kRated);
 #pragma unroll
       for (int h = 0; h < kH; ++h)
         if (h == staging) {
@@ -823,13 +705,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // the readiness at the top waits for them, so what it sees is one rating
     // phase fresher than a poll issued before the wait
     ++iter;
-    if constexpr (!PUSH) {
 #pragma unroll
-      for (int h = 0; h < kH; ++h)
-        if ((pend[h] >> lane) & 1ull)
-          dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-    }
+    for (int h = 0; h < kH; ++h)
+      if ((pend[h] >> lane) & 1ull)
+        dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
 
     // ---------------------------------------------- (11) retire finished chunks
     {
@@ -848,23 +728,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     bool held = false;
 #pragma unroll
     for (int h = 0; h < kH; ++h) held |= cbase[h] >= 0;
-    bool finished = exhausted && !held && !tk_pending;
-    if constexpr (PUSH) {
-      // processed matches are counted GPU-wide (ctrl[48]); a wave with nothing of
-      // its own left -- no chunk, no queue, no publish whose completion it has not
-      // seen -- leaves once every match of the window is processed
-      if (n_proc >= 1024u || (finished && n_proc)) {
-        if (lane == 0) __hip_atomic_fetch_add((gu32*)&ctrl[48], n_proc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        n_proc = 0u;
-      }
-      if (finished) finished = qtail == qhead && __ballot(pc_succ != kNoMatch) == 0ull;
-      if (finished) {
-        uint32_t total = 0;
-        if (lane == 0) total = __hip_atomic_load((gu32*)&ctrl[48], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        finished = (int64_t)__builtin_amdgcn_readfirstlane(total) >= M;
-      }
-    }
-    if (finished) {
+    if (exhausted && !held && !tk_pending) {
       if (lane == 0) {  // diagnostics: wave iterations (ctrl[15]), hand-offs (ctrl[26..27])
         __hip_atomic_fetch_add((gu32*)&ctrl[15], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add((gu32*)&ctrl[26], n_local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -901,47 +765,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     if (worked || staging >= 0) {
       spins = 0;
     } else {
-      if constexpr (PUSH) {
-        // an idle wave with an empty queue takes matches from the overflow ring
-        uint32_t ot = 0u, oh = 0u, got = 0u, start = 0u;
-        if (lane == 0) {
-          ot = __hip_atomic_load((gu32*)&ctrl[49], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          oh = __hip_atomic_load((gu32*)&ctrl[50], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          while (oh < ot) {  // claim up to NG entries below the tail
-            const uint32_t n = ot - oh < (uint32_t)NG ? ot - oh : (uint32_t)NG;
-            const uint32_t old = atomicCAS(&ctrl[50], oh, oh + n);
-            if (old == oh) {
-              got = n;
-              start = oh;
-              break;
-            }
-            oh = old;
-          }
-        }
-        got = __builtin_amdgcn_readfirstlane(got);
-        start = __builtin_amdgcn_readfirstlane(start);
-        if (got) {
-          if (lane < (int)got) {
-            uint32_t v = 0u;
-            gu32* cell = (gu32*)(prm.ovf + start + lane);
-            // the producer reserved the cell before storing into it
-            while ((v = __hip_atomic_load(cell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u)
-              __builtin_amdgcn_s_sleep(1);
-            __hip_atomic_store(cell, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-            int32_t rr[R];
-            const int32_t* src = rec + (int64_t)(v - 1u) * R;
-#pragma unroll
-            for (int k = 0; k < R; ++k) rr[k] = src[k];
-            queue_entry(&lq[wv][(qtail + (uint32_t)lane) & (QCAP - 1)][0], (int32_t)(v - 1u), rr);
-          }
-          qtail += got;
-          spins = 0;
-          continue;
-        }
-      }
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       if (now - t0 > kProgressTicks) {
-        const uint32_t p = __hip_atomic_load((gu32*)&ctrl[PUSH ? 48 : 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t p = __hip_atomic_load((gu32*)&ctrl[3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (p != seen_progress) {
           seen_progress = p;
           t0 = now;
@@ -993,7 +819,7 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
   if (!prm.ctrl_ready) hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, 15);
   // the diagnostic words are zeroed by every launch (not by the schedule's zeroing)
-  hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 44);
+  hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 28);
   if (M <= 0) return 0;
   if (prm.chunk_len < 1 || prm.chunk_len > kChunk) return (int)hipErrorInvalidValue;
   if ((int64_t)prm.num_players * kRowFloats * 4 > kOutOfRange) return (int)hipErrorInvalidValue;
@@ -1011,19 +837,14 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // with the scalar-bookkeeping executor: 3v3 8 lanes, 5v5 16 lanes (20.0 vs
   // 21.2 ms for 12.5M matches with 10) -> auto = off.
   const bool tight = prm.tight_groups > 0;
-  // push mode: the prepass wrote need << 16 into deps (kernels.hip push_mode); the
-  // fused-telemetry build keeps the polling executor
-  const bool push = prm.ovf != nullptr && !tp.evoff;
-#define ANA_RATE_LAUNCH_D(k, g, tele, diag, pu)                                                        \
-  hipLaunchKernelGGL((rate_dataflow_kernel<k, g, tele, diag, pu>), dim3((unsigned)blocks), dim3(256), 0, s, \
+#define ANA_RATE_LAUNCH_D(k, g, tele, diag)                                                        \
+  hipLaunchKernelGGL((rate_dataflow_kernel<k, g, tele, diag>), dim3((unsigned)blocks), dim3(256), 0, s, \
                      rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, tp)
 #define ANA_RATE_LAUNCH(k, g)                                      \
   do {                                                             \
-    if (tp.evoff) ANA_RATE_LAUNCH_D(k, g, true, false, false);     \
-    else if (push && prm.diag) ANA_RATE_LAUNCH_D(k, g, false, true, true); \
-    else if (push) ANA_RATE_LAUNCH_D(k, g, false, false, true);    \
-    else if (prm.diag) ANA_RATE_LAUNCH_D(k, g, false, true, false); \
-    else ANA_RATE_LAUNCH_D(k, g, false, false, false);             \
+    if (tp.evoff) ANA_RATE_LAUNCH_D(k, g, true, false);            \
+    else if (prm.diag) ANA_RATE_LAUNCH_D(k, g, false, true);       \
+    else ANA_RATE_LAUNCH_D(k, g, false, false);                    \
   } while (0)
   switch (K) {
     case 1: ANA_RATE_LAUNCH(1, 2); break;

@@ -20,9 +20,6 @@ int launch_reset_tags(float* state, int64_t P, hipStream_t s);
 int launch_epoch_bump(int32_t* e, hipStream_t s);
 
 size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
-// ANA_RATE_PUSH=1 and a window past the micro-batch schedule: the prepass writes
-// deps[m] = need << 16 and the rate launch runs the push-mode executor
-bool push_mode(int64_t nslots);
 
 // Stable LSD radix sort of (key, value) pairs on the low ``bits`` key bits
 // (radix_sort.hip).  Ping-pongs between the two buffer pairs; *result_in_alt

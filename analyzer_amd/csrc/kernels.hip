@@ -291,47 +291,6 @@ sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uin
   }
 }
 
-// Push-mode executor (dataflow.hip, ANA_RATE_PUSH): the match's dependency count
-// goes into the high half of its counter, deps[m] = need << 16, so the producer
-// whose increment completes it sees that in the value its atomic returns.
-// need = the distinct players of a rating match with an earlier occurrence
-// (kLinkHasPred on their first slot) -- what the executor's install counts.
-template <int K>
-__global__ void __launch_bounds__(256)
-sched_need_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link, int64_t M,
-                  int64_t P, int32_t* __restrict__ deps) {
-  constexpr int S = 2 * K, R = S + 2;
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  int32_t r[R];
-#pragma unroll
-  for (int k = 0; k < R; ++k) r[k] = rec[m * R + k];
-  uint32_t nd = 0;
-  if (early_status<K>(r, P) == kRated) {
-    const uint32_t m0 = (uint32_t)r[S];
-#pragma unroll
-    for (int a = 0; a < S; ++a) {
-      const bool ina = (a < K ? a : a - K) < (int)(a < K ? meta_n0(m0) : meta_n1(m0));
-      bool firsto = ina;
-#pragma unroll
-      for (int b = 0; b < a; ++b) {
-        const bool inb = (b < K ? b : b - K) < (int)(b < K ? meta_n0(m0) : meta_n1(m0));
-        if (inb && r[b] == r[a]) firsto = false;
-      }
-      if (firsto && (link[m * S + a] & kLinkHasPred)) ++nd;
-    }
-  }
-  deps[m] = (int32_t)(nd << 16);
-}
-
-bool push_mode(int64_t n) {
-  static const bool on = [] {
-    const char* v = getenv("ANA_RATE_PUSH");
-    return v && atoi(v) != 0;
-  }();
-  return on && n > kSmallSched;
-}
-
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s,
                     bool zero_ctrl, int32_t* epoch_bump) {
@@ -373,23 +332,13 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
   if (n <= 0) return 0;
   if (n > kMaxSlots || P >= 0x7fffffffLL || K < 1 || K > 5) return (int)hipErrorInvalidValue;
   if (ws_bytes < schedule_workspace_bytes(n, P)) return (int)hipErrorInvalidValue;
-  if (!push_mode(n)) ANA_HIP_CHECK(hipMemsetAsync(deps, 0, (size_t)M * 4, s));  // push: sched_need writes them
+  ANA_HIP_CHECK(hipMemsetAsync(deps, 0, (size_t)M * 4, s));
   char* p = static_cast<char*>(ws);
   uint32_t* keys_a = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* vals_a = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* keys_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* vals_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
-  const int e = launch_sched_sort(K, rec, M, (uint32_t)P, keys_a, vals_a, keys_b, vals_b, p, link, s);
-  if (e != 0 || !push_mode(n)) return e;
-  const unsigned grid = (unsigned)((M + 255) / 256);
-  switch (K) {
-    case 1: hipLaunchKernelGGL(sched_need_kernel<1>, dim3(grid), dim3(256), 0, s, rec, link, M, P, deps); break;
-    case 2: hipLaunchKernelGGL(sched_need_kernel<2>, dim3(grid), dim3(256), 0, s, rec, link, M, P, deps); break;
-    case 3: hipLaunchKernelGGL(sched_need_kernel<3>, dim3(grid), dim3(256), 0, s, rec, link, M, P, deps); break;
-    case 4: hipLaunchKernelGGL(sched_need_kernel<4>, dim3(grid), dim3(256), 0, s, rec, link, M, P, deps); break;
-    case 5: hipLaunchKernelGGL(sched_need_kernel<5>, dim3(grid), dim3(256), 0, s, rec, link, M, P, deps); break;
-  }
-  return (int)hipGetLastError();
+  return launch_sched_sort(K, rec, M, (uint32_t)P, keys_a, vals_a, keys_b, vals_b, p, link, s);
 }
 
 }  // namespace ana

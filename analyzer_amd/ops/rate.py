@@ -30,7 +30,7 @@ from .native import native
 RATED, AFK, INVALID_ROSTERS, UNSUPPORTED_MODE = 0, 1, 2, 3
 ERR_SEED, ERR_SIGMA, ERR_EMPTY_ROSTER, ERR_NUMERIC, ERR_BAD_RECORD = 4, 5, 6, 7, 8
 NOT_PROCESSED = 255
-CTRL_WORDS = 64  # executor control words (csrc/dataflow.hip launch_rate)
+CTRL_WORDS = 48  # executor control words (csrc/dataflow.hip launch_rate)
 STATUS_NAMES = {RATED: "rated", AFK: "afk", INVALID_ROSTERS: "invalid_rosters",
                 UNSUPPORTED_MODE: "unsupported_mode", ERR_SEED: "error_seed",
                 ERR_SIGMA: "error_sigma", ERR_EMPTY_ROSTER: "error_empty_roster",
@@ -316,22 +316,10 @@ class BatchRater:
                       self.host_fp64, *telemetry,
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
                       epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
-                      self.chunk_len(M, tele), ctrl_ready, self._overflow_ring(dev, M, K))
+                      self.chunk_len(M, tele), ctrl_ready)
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out
-
-    def _overflow_ring(self, device, M: int, K: int) -> torch.Tensor:
-        """Push-mode executor (ANA_RATE_PUSH): M zeroed int32 cells for completed
-        matches a wave's queue had no room for (consumers re-zero them)."""
-        if device.type != "cuda" or not native().push_mode(M * 2 * K):
-            return torch.empty(0, dtype=torch.int32, device=device)
-        key = (str(device), "ovf")
-        buf = self._ws.get(key)
-        if buf is None or buf.numel() < M:
-            buf = torch.zeros(max(M, 1), dtype=torch.int32, device=device)
-            self._ws[key] = buf
-        return buf
 
     def stale_retries(self, device) -> int:
         """Granule reads of the last launch that found their predecessor's write not

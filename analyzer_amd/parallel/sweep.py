@@ -257,7 +257,7 @@ def rate_window_dp(rater, merger: SweepMerger, roster, rec, K=None, out=None, ch
             break
         merger.resweep(roster)
         if schedule is not None:
-            schedule.deps.bitwise_and_(-65536)  # counts back to 0 (push mode keeps need << 16); links are reusable
+            schedule.deps.zero_()  # the executor counted them up; links are reusable
         out = res
     merger.merge(roster)
     return res

@@ -151,7 +151,7 @@ class WindowPipeline:
                 with trace_range("resweep", window=self.windows_rated):
                     self.merger.resweep(self.roster)
                     if prep.schedule is not None:
-                        prep.schedule.deps.bitwise_and_(-65536)  # counts back to 0; push-mode need stays
+                        prep.schedule.deps.zero_()
                     res = self.rater.rate(self.roster, prep.rec, self.K, out=res, check=check,
                                           schedule=prep.schedule)
                 self.merger.rated()

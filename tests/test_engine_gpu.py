@@ -483,58 +483,3 @@ def _rccl_entry(rank, port, outdir, args):
         torch.save(res, os.path.join(outdir, "r0.pt"))
     finally:
         dist.destroy_process_group()
-
-
-PUSH_CASES = [  # (name, players, matches, K, blocks, pattern)
-    ("uniform", 20000, 200000, 3, 512, "random"),
-    ("dense_one_block", 1000, 100000, 3, 1, "random"),   # 4 waves: queues overflow
-    ("serial", 1000, 20000, 3, 8, "serial"),
-    ("5v5_ties_dups", 5000, 60000, 5, 512, "random"),
-]
-
-
-def _push_case(name, P, M, K, blocks, pattern, dev):
-    spec = StreamSpec(team_size=K, seed=41, p_afk=0.05, p_tie=0.1, p_hot=0.2, p_uneven=0.05,
-                      p_unsupported=0.02)
-    rec = make_stream(spec, M, P, K=K, device=dev)
-    if pattern == "serial":
-        rec[:, :2 * K] = torch.arange(2 * K, dtype=torch.int32, device=dev)
-    roster = make_roster(RosterSpec(num_players=P, seed=40), device=dev)
-    br = R.BatchRater(blocks=blocks)
-    res = br.rate(roster, rec, K)
-    ctrl = br._ctrl(dev).cpu()
-    out = {k: getattr(res, k).cpu().clone() for k in ("s_mu", "s_sig", "delta", "m_mu", "m_sig", "quality")}
-    out.update(status=res.status.cpu().clone(), state=roster.state.cpu(), overflow=int(ctrl[49]),
-               stale=int(ctrl[14]))
-    return out
-
-
-def _push_entry(rank, outdir):
-    import os
-
-    os.environ["ANA_RATE_PUSH"] = "1"
-    from analyzer_amd.ops.native import native
-
-    assert native().push_mode(1 << 20)
-    dev = torch.device("cuda:0")
-    out = {c[0]: _push_case(*c, dev) for c in PUSH_CASES}
-    torch.save(out, os.path.join(outdir, "push.pt"))
-
-
-def test_push_executor_bit_identical_to_polling(gpu_device, tmp_path):
-    """ANA_RATE_PUSH=1 (the wave whose publish completes a match's last
-    dependency rates it; csrc/dataflow.hip PUSH) gives the same bits as the
-    polling executor: roster and every output row, on uniform, serial, 5v5 and
-    one-workgroup windows (the last one overflows the LDS queues into the ring)."""
-    import torch.multiprocessing as mp
-
-    mp.spawn(_push_entry, args=(str(tmp_path),), nprocs=1, join=True)
-    got = torch.load(str(tmp_path / "push.pt"), weights_only=True)
-    for c in PUSH_CASES:
-        ref = _push_case(*c, gpu_device)
-        g = got[c[0]]
-        assert torch.equal(g["state"].view(torch.int32), ref["state"].view(torch.int32)), c[0]
-        assert torch.equal(g["status"], ref["status"]), c[0]
-        for k in ("s_mu", "s_sig", "delta", "m_mu", "m_sig", "quality"):
-            assert torch.equal(g[k].nan_to_num(-7).view(torch.int32), ref[k].nan_to_num(-7).view(torch.int32)), (c[0], k)
-    assert got["dense_one_block"]["overflow"] > 0  # the overflow ring was exercised
