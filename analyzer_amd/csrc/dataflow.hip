@@ -158,7 +158,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // this iteration's pick per group, written by the lane holding the match:
   // {match index, slot << 8 | lane in chunk, meta0, meta1, player ids...}
   constexpr int SP = (4 + S + 3) / 4 * 4;
-  __shared__ int32_t lpick[kWavesPerBlock][NG][SP];
+  __shared__ __attribute__((aligned(16))) int32_t lpick[kWavesPerBlock][NG][SP];  // v4i slots
   __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;

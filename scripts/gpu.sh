@@ -14,7 +14,6 @@
 #   skew       bench.py --skew 2 and 3
 #   dp         bench.py --gpus 2 and 4 on this one GPU (gloo rehearsal of the spawn path)
 #   accuracy   sweep-DP accuracy, 8 ranks x 10M matches over 1M players, sweeps 1,2,4,8
-#   push       push-mode executor (ANA_RATE_PUSH): bit identity + serial/window A/B
 #   hop        quick executor A/B (serial chain + 10M window, local hand-off, timing build)
 #   merge      sweep-merge message/decode kernels at P = 1M, 10M on one GPU
 #   exactdp    exact DP (C2) rehearsal, 2/4 gloo ranks on one GPU, rounds + time per window
@@ -72,15 +71,6 @@ for task in "$@"; do
           --players 1e6 --matches-per-rank 1e7 --windows 1 --warm-windows 1 --sweeps 1,2,4,8
       run accuracy/dp4_skew 900 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 4 \
           --players 2e4 --matches-per-rank 2e5 --windows 8 --warm-windows 1 --sweeps 1,2,3,4
-      ;;
-    push)  # push-mode executor vs polling: bit identity test, then serial chain / 10M window / configs
-      run push/test 300 $PY -u -m pytest tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread -k push
-      for mode in 0 1; do
-        ANA_RATE_PUSH=$mode run push/serial_$mode 300 $PY scripts/tune_rate.py --pattern serial --players 1000 \
-            --matches 20000 --rounds 2 --blocks 8
-        ANA_RATE_PUSH=$mode run push/random_$mode 300 $PY scripts/tune_rate.py --pattern random --rounds 2
-      done
-      grep -h "^round 1" gpurun_out/push/*.log | cut -c1-150
       ;;
     idle)  # idle back-off and grid size sweep of the executor (10M window + serial chain)
       run idle/random 400 $PY scripts/tune_rate.py --pattern random --rounds 2 --idle=-1,2,8,16 --blocks 512,1024
