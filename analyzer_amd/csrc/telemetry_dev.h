@@ -103,7 +103,10 @@ namespace ana {
 constexpr int kTeleChunk = 32;
 constexpr int kTeleRowBytes = kTeleChunk * 2 + 16;
 constexpr int kTeleARows = 32;
-constexpr int kTeleMfmaLoads = 4;
+#ifndef ANA_TELE_LOADS
+#define ANA_TELE_LOADS 8  // 1.87 vs 1.95 ms (4) and 2.08 ms (2) for 400M events, profiles/r2/tele_loads_ab.log
+#endif
+constexpr int kTeleMfmaLoads = ANA_TELE_LOADS;  // 64-event loads per lane in flight
 constexpr int kTeleBOffset = kTeleARows * kTeleRowBytes;           // within a set
 // A^T window + B^T, + 64 B so set 1 starts 16 banks over (both sets take stores together)
 constexpr int kTeleSetBytes = kTeleBOffset + 16 * kTeleRowBytes + 64;
