@@ -132,6 +132,7 @@ class EngineConfig:
     ANA_DIST_BACKEND        nccl      process group backend (gloo: N ranks on one GPU)
     CHECKPOINT_DIR / _EVERY -- / 1    re-rate checkpoints (runtime/rerate.py)
     ANA_TRACE               0         roctx ranges + Chrome trace (utils/trace.py)
+    ANA_CHECK_ROUNDS        0         exact DP race detector: rounds share no player (parallel/exact_dp.py)
     ======================  ========  =============================================
     """
 
@@ -146,6 +147,7 @@ class EngineConfig:
     checkpoint_every: int = 1
     checkpoint_dir: Optional[str] = None
     trace: bool = False
+    check_rounds: bool = False
 
     # read by the native extension itself (csrc/bindings.cpp, kernels), per launch
     NATIVE_KNOBS = {
@@ -173,4 +175,5 @@ class EngineConfig:
             checkpoint_every=int(_env(env, "CHECKPOINT_EVERY") or 1),
             checkpoint_dir=_env(env, "CHECKPOINT_DIR"),
             trace=(env.get("ANA_TRACE") or "0") not in ("", "0"),
+            check_rounds=(env.get("ANA_CHECK_ROUNDS") or "0") not in ("", "0"),
         )

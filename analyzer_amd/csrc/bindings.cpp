@@ -484,6 +484,48 @@ void pack_rows(Tensor rec, int64_t K, Tensor status, Tensor state, Tensor out) {
   }
 }
 
+// C2 race detector: rec [M, 2K+2] (the window), idx int64 [m] (one round's matches),
+// owner int64 [P] (zeroed once per window), flag int32 [1]
+void check_round(Tensor rec, int64_t K, Tensor idx, int64_t round, Tensor owner, Tensor flag) {
+  const auto dev = rec.device();
+  check(rec, "rec", torch::kInt32, dev);
+  check(idx, "idx", torch::kInt64, dev);
+  check(owner, "owner", torch::kInt64, dev);
+  check(flag, "flag", torch::kInt32, dev);
+  TORCH_CHECK(K >= 1 && K <= 5 && rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  TORCH_CHECK(round >= 0 && round < 0xffffffffLL, "round out of range");
+  const int64_t m = idx.numel(), P = owner.numel();
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_check_round(rec.data_ptr<int32_t>(), (int)K, idx.data_ptr<int64_t>(), m, P,
+                                      (uint32_t)round,
+                                      reinterpret_cast<unsigned long long*>(owner.data_ptr<int64_t>()),
+                                      reinterpret_cast<uint32_t*>(flag.data_ptr<int32_t>()), stream_of(rec)),
+              "check_round");
+    return;
+  }
+  const int S = 2 * (int)K;
+  const int32_t* rp = rec.data_ptr<int32_t>();
+  const int64_t* ip = idx.data_ptr<int64_t>();
+  uint64_t* own = reinterpret_cast<uint64_t*>(owner.data_ptr<int64_t>());
+  int32_t* fl = flag.data_ptr<int32_t>();
+  for (int64_t i = 0; i < m; ++i) {
+    const int32_t* r = rp + ip[i] * (S + 2);
+    if (ana::early_status_k(r, S, P) != ana::kRated) continue;
+    const uint32_t m0 = (uint32_t)r[S];
+    const uint64_t mine = ((uint64_t)(round + 1) << 32) | (uint64_t)(ip[i] + 1);
+    for (int j = 0; j < S; ++j) {
+      const int n = j < K ? (int)ana::meta_n0(m0) : (int)ana::meta_n1(m0);
+      const int32_t p = r[j];
+      if ((j < K ? j : j - K) >= n || p < 0 || p >= P) continue;
+      if ((uint32_t)(own[p] >> 32) == (uint32_t)(round + 1)) {
+        if (own[p] != mine) fl[0] |= 1;
+      } else {
+        own[p] = mine;
+      }
+    }
+  }
+}
+
 void unpack_rows(Tensor buf, Tensor state) {
   const auto dev = state.device();
   check(buf, "buf", torch::kFloat32, dev);
@@ -615,6 +657,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
   m.def("sweep_apply", &sweep_apply, "K9: decode summed messages against the common start (-> s, s2)");
   m.def("pack_rows", &pack_rows, "C2: changed rows of a round slice -> fixed-capacity [cap, 33] entries");
+  m.def("check_round", &check_round, "C2 race detector: one round's matches share no player (flag |= 1)");
   m.def("unpack_rows", &unpack_rows, "C2: write gathered entries (id >= 0) into the roster, tags zeroed");
   m.def("write_record_file", &write_record_file, "P3: write a match-record file (ANAREC01)");
   py::class_<ana::RecordReader>(m, "RecordReader")

@@ -150,6 +150,18 @@ ANA_HD uint8_t early_status(const int32_t* r, int64_t P) {
   return kRated;
 }
 
+// early_status for a runtime team size (S = 2K slots)
+ANA_HD uint8_t early_status_k(const int32_t* r, int S, int64_t P) {
+  switch (S / 2) {
+    case 1: return early_status<1>(r, P);
+    case 2: return early_status<2>(r, P);
+    case 3: return early_status<3>(r, P);
+    case 4: return early_status<4>(r, P);
+    case 5: return early_status<5>(r, P);
+    default: return kErrBadRecord;
+  }
+}
+
 // ---------------------------------------------------------------- RNG (K7)
 // Counter-based: every random number is a pure function of (seed, index,
 // field), so device and host generators produce bit-identical streams and any

@@ -76,4 +76,8 @@ int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, fl
 int launch_pack_rows(const int32_t* rec, int K, int64_t m, const uint8_t* status, int64_t sstride,
                      const float* state, float* out, int64_t cap, hipStream_t st);
 int launch_unpack_rows(const float* buf, int64_t n, float* state, hipStream_t st);
+// exact-DP race detector: matches idx[0..m) of round ``round`` share no player
+// (owner: P 64-bit claims, zeroed once; *flag |= 1 on a conflict)
+int launch_check_round(const int32_t* rec, int K, const int64_t* idx, int64_t m, int64_t P, uint32_t round,
+                       unsigned long long* owner, uint32_t* flag, hipStream_t st);
 }  // namespace ana

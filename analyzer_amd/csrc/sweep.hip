@@ -156,6 +156,46 @@ __global__ void unpack_rows_kernel(const float* __restrict__ buf, int64_t n, flo
   for (int k = 0; k < kRowFloats; ++k) state[(int64_t)id * kRowFloats + k] = (k & 1) ? 0.f : b[k];
 }
 
+// Race detector for exact DP: the matches of one round must share no
+// player.  owner[p] holds (round + 1) << 32 | (match + 1) of the last claim; a
+// slot whose player was claimed in the SAME round by ANOTHER match sets *flag.
+// Rounds only grow, so the table never needs clearing between rounds.
+__global__ void check_round_kernel(const int32_t* __restrict__ rec, int S, const int64_t* __restrict__ idx,
+                                   int64_t m, int64_t P, uint32_t round,
+                                   unsigned long long* __restrict__ owner, uint32_t* __restrict__ flag) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m * S) return;
+  const int K = S / 2;
+  const int64_t i = e / S;
+  const int j = (int)(e % S);
+  const int64_t mi = idx[i];
+  const int32_t* r = rec + mi * (S + 2);
+  const uint32_t m0 = (uint32_t)r[S];
+  const int n = j < K ? (int)meta_n0(m0) : (int)meta_n1(m0);
+  const int32_t p = r[j];
+  if (early_status_k(r, S, P) != kRated || (j < K ? j : j - K) >= n || p < 0 || p >= P) return;
+  const unsigned long long mine = ((unsigned long long)(round + 1u) << 32) | (unsigned long long)(mi + 1);
+  unsigned long long cur = owner[p];
+  for (;;) {
+    if ((uint32_t)(cur >> 32) == round + 1u) {  // claimed this round
+      if (cur != mine) atomicOr(flag, 1u);
+      return;
+    }
+    const unsigned long long prev = atomicCAS(owner + p, cur, mine);
+    if (prev == cur) return;
+    cur = prev;
+  }
+}
+
+int launch_check_round(const int32_t* rec, int K, const int64_t* idx, int64_t m, int64_t P, uint32_t round,
+                       unsigned long long* owner, uint32_t* flag, hipStream_t st) {
+  if (m <= 0) return 0;
+  const int64_t n = m * 2 * K;
+  hipLaunchKernelGGL(check_round_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rec, 2 * K, idx,
+                     m, P, round, owner, flag);
+  return (int)hipGetLastError();
+}
+
 int launch_pack_rows(const int32_t* rec, int K, int64_t m, const uint8_t* status, int64_t sstride,
                      const float* state, float* out, int64_t cap, hipStream_t st) {
   if (cap <= 0) return 0;

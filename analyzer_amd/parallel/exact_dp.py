@@ -36,6 +36,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from ..config import EngineConfig
 from ..ops.native import native
 from ..ops.rate import BatchRater, RateResult, Roster
 from .comm import world
@@ -67,6 +68,25 @@ class RoundPlan:
         self.round_max = sizes.max(1).astype(np.int64) if M else np.zeros(0, np.int64)
 
 
+def check_rounds(rec: torch.Tensor, K: int, plan: "RoundPlan", num_players: int) -> int:
+    """Race detector: the first round whose matches share a player, or
+    -1.  One kernel per round claims every rated slot's player for its match in a
+    64-bit owner table (csrc/sweep.hip check_round_kernel); a second claim by
+    another match of the same round raises the flag."""
+    dev = rec.device
+    owner = torch.zeros(max(num_players, 1), dtype=torch.int64, device=dev)
+    flag = torch.zeros(1, dtype=torch.int32, device=dev)
+    order = torch.from_numpy(plan.order).to(dev)
+    for r in range(plan.n_rounds):
+        lo, hi = int(plan.bounds[r, 0]), int(plan.bounds[r, -1])
+        native().check_round(rec, K, order[lo:hi], r, owner, flag)
+        if rec.device.type == "cpu" and int(flag[0]):
+            return r
+    if int(flag[0]):  # device: one sync at the end; find the round on the host
+        return check_rounds(rec.cpu(), K, plan, num_players)
+    return -1
+
+
 def rate_exact_dp(rater: BatchRater, roster: Roster, rec: torch.Tensor, K: int,
                   group=None, level: Optional[torch.Tensor] = None) -> RateResult:
     """Rate ``rec`` exactly across the ranks of ``group`` (replicated roster).
@@ -84,6 +104,10 @@ def rate_exact_dp(rater: BatchRater, roster: Roster, rec: torch.Tensor, K: int,
     if level is None:
         level, _ = rounds(rec, K, roster.num_players)
     plan = RoundPlan(level, size)
+    if EngineConfig.from_env().check_rounds:
+        bad = check_rounds(rec, K, plan, roster.num_players)
+        if bad >= 0:
+            raise RuntimeError("exact DP: round %d has two matches sharing a player" % bad)
     S = 2 * K
     # this rank's matches, in round order, gathered once
     mine = np.concatenate([np.arange(plan.bounds[r, rank], plan.bounds[r, rank + 1])

@@ -301,3 +301,31 @@ def test_resweep_error_falls_per_sweep():
     for e in errs:
         assert e["null_mismatch"] == 0
     assert t["sweeps"]["4"]["records_shared_mu"]["dmu_max"] < 5e-3
+
+
+def test_round_check_flags_shared_players():
+    """C2 race detector (ANA_CHECK_ROUNDS): the levelizer's rounds pass; a plan
+    that puts a player's two consecutive matches in one round is caught."""
+    import numpy as np
+
+    from analyzer_amd.parallel.exact_dp import RoundPlan, check_rounds, rounds
+
+    P, M, K = 60, 400, 3
+    rec = make_stream(StreamSpec(team_size=K, seed=3, p_afk=0.05, p_unsupported=0.05), M, P, K=K)
+    level, _ = rounds(rec, K, P)
+    assert check_rounds(rec, K, RoundPlan(level, 2), P) == -1
+    bad = level.clone()
+    bad[:] = 1  # everything in one round: players repeat
+    assert check_rounds(rec, K, RoundPlan(bad, 2), P) == 0
+
+
+def _exact_checked(rank, size, P, M, K, seed):
+    import os
+
+    os.environ["ANA_CHECK_ROUNDS"] = "1"
+    return _exact(rank, size, P, M, K, seed)
+
+
+def test_exact_dp_with_round_check(tmp_path):
+    res = run_ranks(_exact_checked, 2, tmp_path, 40, 300, 3, 9)
+    assert len(res) == 2

@@ -483,3 +483,19 @@ def _rccl_entry(rank, port, outdir, args):
         torch.save(res, os.path.join(outdir, "r0.pt"))
     finally:
         dist.destroy_process_group()
+
+
+def test_exact_dp_round_check_on_device(gpu_device):
+    """The C2 race detector's kernel (csrc/sweep.hip check_round_kernel) on the
+    device: the levelizer's rounds pass, a one-round plan of a window with
+    repeated players is flagged -- at the same round as the host path."""
+    from analyzer_amd.parallel.exact_dp import RoundPlan, check_rounds, rounds
+
+    P, M, K = 2000, 20000, 3
+    rec = make_stream(StreamSpec(team_size=K, seed=5, p_afk=0.05), M, P, K=K, device=gpu_device)
+    level, _ = rounds(rec, K, P)
+    assert check_rounds(rec, K, RoundPlan(level, 4), P) == -1
+    bad = level.clone()
+    bad[M // 2:] = bad[M // 2]  # the second half collapses into one round
+    plan = RoundPlan(bad, 4)
+    assert check_rounds(rec, K, plan, P) == check_rounds(rec.cpu(), K, plan, P) >= 0
