@@ -81,11 +81,13 @@ class ResidentRoster:
         new = rows < 0
         if new.any():
             nk = keys[new]
+            # fetch and upload first: a failing fetch must not leave keys mapped to
+            # rows that were never written (the next batch would reuse the rows)
+            ratings, attrs = fetch(nk)
             nr = self.n + np.arange(nk.size)
+            self._upload_arrays(np.asarray(ratings, dtype=np.float64), np.asarray(attrs, dtype=np.float64))
             self.by_key[nk] = nr
             rows[new] = nr
-            ratings, attrs = fetch(nk)
-            self._upload_arrays(np.asarray(ratings, dtype=np.float64), np.asarray(attrs, dtype=np.float64))
         return rows
 
     def _upload_arrays(self, vals: np.ndarray, attrs: np.ndarray) -> None:
@@ -110,17 +112,20 @@ class ResidentRoster:
 
     def rows_for(self, players: Sequence) -> List[int]:
         """Row of every player object (uploading the ones not seen before)."""
-        rows, new = [], []
+        rows, new, fresh = [], [], {}
         get = self.rows.get
         for pl in players:
             r = get(pl.api_id)
             if r is None:
-                r = self.n + len(new)
-                self.rows[pl.api_id] = r
-                new.append(pl)
+                r = fresh.get(pl.api_id)
+                if r is None:
+                    r = self.n + len(new)
+                    fresh[pl.api_id] = r
+                    new.append(pl)
             rows.append(r)
         if new:
-            self._upload(new)
+            self._upload(new)  # the map only learns rows that were written
+            self.rows.update(fresh)
         return rows
 
     def _grow(self, need: int) -> None:

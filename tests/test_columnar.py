@@ -130,3 +130,20 @@ def test_columnar_telemetry_into_participant_stats():
             assert st is not None and st["events"] >= 0
             total += st["events"]
     assert 5 * 10 <= total <= 9 * 10
+
+
+def test_resident_roster_failed_fetch_leaves_no_rows():
+    """A fetch that raises (store error) must not map keys to unwritten rows."""
+    from analyzer_amd.runtime.resident import ResidentRoster
+
+    rr = ResidentRoster("cpu", capacity=4)
+
+    def boom(keys):
+        raise IOError("store down")
+
+    with pytest.raises(IOError):
+        rr.rows_for_keys(np.array([3, 7]), boom)
+    assert rr.n == 0 and (rr.by_key < 0).all()
+    ok = lambda keys: (np.full((len(keys), 14), np.nan), np.zeros((len(keys), 3)))
+    assert rr.rows_for_keys(np.array([7, 3]), ok).tolist() == [0, 1]
+    assert rr.rows_for_keys(np.array([3, 9]), ok).tolist() == [1, 2]
