@@ -208,7 +208,7 @@ static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& 
   check(events, "events", torch::kInt32, dev);
   check(stats, "stats", torch::kFloat32, dev);
   TORCH_CHECK(evoff.numel() == M + 1, "evoff must have M + 1 entries");
-  TORCH_CHECK(events.dim() == 2 && events.size(1) == 4, "events must be [E, 4]");
+  TORCH_CHECK(events.dim() == 2 && events.size(1) == 2, "events must be [E, 2] (8-B events, telemetry_core.h)");
   TORCH_CHECK(stats.numel() == M * 2 * K * ana::kStatFeatures, "stats must be [M, 2K, 8]");
   tp.evoff = evoff.data_ptr<int64_t>();
   tp.events = events.data_ptr<int32_t>();
@@ -353,7 +353,7 @@ void gen_events(Tensor rec, int64_t K, Tensor evoff, int64_t seed, int64_t min_e
   TORCH_CHECK(K >= 1 && K <= 5 && rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
   const int64_t M = rec.size(0);
   TORCH_CHECK(evoff.numel() == M + 1, "evoff must have M + 1 entries");
-  TORCH_CHECK(events.dim() == 2 && events.size(1) == 4, "events must be [E, 4]");
+  TORCH_CHECK(events.dim() == 2 && events.size(1) == 2, "events must be [E, 2] (8-B events, telemetry_core.h)");
   ana::GenEventParams g{(uint64_t)seed, (int32_t)min_events, (int32_t)max_events};
   if (dev.is_cuda())
     check_hip(ana::launch_gen_events((int)K, g, base, rec.data_ptr<int32_t>(),

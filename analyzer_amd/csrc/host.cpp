@@ -74,10 +74,10 @@ int host_gen_events(int K, const GenEventParams& g, int64_t base, const int32_t*
     const uint32_t m0 = (uint32_t)rec[m * (S + 2) + S];
     const int n0 = meta_n0(m0) < K ? meta_n0(m0) : K, n1 = meta_n1(m0) < K ? meta_n1(m0) : K;
     for (int64_t e = evoff[m]; e < evoff[m + 1]; ++e) {
-      int32_t* ev = events + e * 4;
+      int32_t* ev = events + e * 2;
       gen_event(g, (uint64_t)(base + m), e - evoff[m], (int32_t)m, n0 + n1, ev);
-      const int r = event_slot(ev[1]);
-      ev[1] = (ev[1] & ~0xff) | (r < n0 ? r : K + (r - n0));
+      const int r = event_slot(ev[0]);
+      ev[0] = (ev[0] & ~0xff) | (r < n0 ? r : K + (r - n0));
     }
   }
   return 0;
@@ -90,16 +90,16 @@ int64_t host_telemetry(int K, const TelemetryParams& tp) {
   for (int64_t i = 0; i < M * S * kStatFeatures; ++i) tp.stats[i] = 0.f;
   for (int64_t m = 0; m < M; ++m)
     for (int64_t e = tp.evoff[m]; e < tp.evoff[m + 1]; ++e) {
-      const int32_t* ev = tp.events + e * 4;
-      const int slot = event_slot(ev[1]);
-      if (ev[0] != m || slot >= S) {  // strict: the event must name the match whose CSR range holds it
+      const int32_t* ev = tp.events + e * 2;
+      const int slot = event_slot(ev[0]);
+      if (event_tag(ev[0]) != (uint32_t)(m & 0xffff) || slot >= S) {  // strict attribution
         ++bad;
         continue;
       }
       float value, add;
-      memcpy(&value, ev + 2, 4);
-      const int f = event_feature(event_type(ev[1]), value, add);
-      float* row = tp.stats + ((int64_t)ev[0] * S + slot) * kStatFeatures;
+      memcpy(&value, ev + 1, 4);
+      const int f = event_feature(event_type(ev[0]), value, add);
+      float* row = tp.stats + ((int64_t)m * S + slot) * kStatFeatures;
       if (f >= 0) row[f] += add;
       row[kStatEvents] += 1.f;
     }

@@ -19,7 +19,7 @@ __global__ void gen_event_counts_kernel(GenEventParams g, int64_t base, int64_t 
   if (m < M) counts[m] = gen_event_count(g, (uint64_t)(base + m));
 }
 
-// one wave per match: lanes write the match's events with coalesced 16-B stores
+// one wave per match: lanes write the match's events with coalesced 8-B stores
 template <int K>
 __global__ void __launch_bounds__(256)
 gen_events_kernel(GenEventParams g, int64_t base, const int32_t* __restrict__ rec,
@@ -32,11 +32,11 @@ gen_events_kernel(GenEventParams g, int64_t base, const int32_t* __restrict__ re
     const int n0 = meta_n0(m0) < K ? meta_n0(m0) : K, n1 = meta_n1(m0) < K ? meta_n1(m0) : K;
     const int64_t e0 = evoff[m], e1 = evoff[m + 1];
     for (int64_t e = e0 + lane; e < e1; e += 64) {
-      int32_t ev[4];
+      int32_t ev[2];
       gen_event(g, (uint64_t)(base + m), e - e0, (int32_t)m, n0 + n1, ev);
-      const int r = event_slot(ev[1]);  // participant index -> record slot
-      ev[1] = (ev[1] & ~0xff) | (r < n0 ? r : K + (r - n0));
-      reinterpret_cast<int4*>(events)[e] = make_int4(ev[0], ev[1], ev[2], ev[3]);
+      const int r = event_slot(ev[0]);  // participant index -> record slot
+      ev[0] = (ev[0] & ~0xff) | (r < n0 ? r : K + (r - n0));
+      reinterpret_cast<int2*>(events)[e] = make_int2(ev[0], ev[1]);
     }
   }
 }

@@ -4,12 +4,14 @@
 // to the "telesuck" queue, worker.py:148-161).  Shared by the gfx950 kernels
 // (standalone and fused into the dataflow executor) and the host mirror.
 //
-// Event (16 B, int4): x = window-local match index, y = slot | type << 8,
-// z = value (float bits), w = game time in seconds (float bits).  Events of a
-// window are grouped by match (one telemetry file per match) and indexed by a
-// CSR offset array evoff[M + 1].  An event is attributed to the match it
-// names iff it sits in that match's CSR range and its slot is < 2K; other
-// events are counted as malformed.
+// Event (8 B, int2): x = slot | type << 8 | (window-local match index & 0xffff) << 16,
+// y = value (float bits).  Events of a window are grouped by match (one
+// telemetry file per match) and indexed by a CSR offset array evoff[M + 1], so
+// the match is implied by the position: the 16-bit match tag only checks it.
+// An event is attributed to the match whose CSR range holds it iff its tag
+// names that match (mod 2^16) and its slot is < 2K; other events are counted as
+// malformed.  (Round 1 used 16-B events with the full match index and the game
+// time; the aggregation reads neither, and the stream is bandwidth-bound.)
 #pragma once
 
 #include <math.h>
@@ -45,6 +47,10 @@ enum EventType : int {
 
 ANA_HD int event_slot(int32_t meta) { return meta & 0xff; }
 ANA_HD int event_type(int32_t meta) { return (meta >> 8) & 0xff; }
+ANA_HD uint32_t event_tag(int32_t meta) { return (uint32_t)meta >> 16; }  // match & 0xffff
+ANA_HD int32_t event_meta(int slot, int type, int64_t match) {
+  return (int32_t)((uint32_t)slot | ((uint32_t)type << 8) | ((uint32_t)(match & 0xffff) << 16));
+}
 
 // feature touched by an event type and the amount it adds (-1: none)
 ANA_HD int event_feature(int type, float value, float& add) {
@@ -62,7 +68,7 @@ ANA_HD int event_feature(int type, float value, float& add) {
 
 struct TelemetryParams {
   const int64_t* evoff;   // [M + 1] CSR offsets into events (nullptr: no telemetry)
-  const int32_t* events;  // [E, 4]
+  const int32_t* events;  // [E, 2]
   float* stats;           // [M, 2K, kStatFeatures]
   int64_t num_matches;
   int32_t impl = 1;       // device tile routine: 1 one-hot MFMA, 0 LDS float atomics
@@ -94,14 +100,10 @@ ANA_HD void gen_event(const GenEventParams& g, uint64_t gm, int64_t e, int32_t m
   // explicit fmaf: host and device round identically (no contraction differences)
   const float value = type == kEvDamage ? fmaf(950.f, u, 50.f) : type == kEvGold ? fmaf(290.f, u, 10.f)
                     : type == kEvFarm ? fmaf(9.f, u, 1.f) : type == kEvHeal ? fmaf(480.f, u, 20.f) : 1.f;
-  const float t = (float)((h >> 48) & 0xffff) * (1800.f / 65536.f);  // 225 * 2^-13: exact scale
-  out[0] = m_local;
-  out[1] = slot | (type << 8);
-  union { float f; int32_t i; } v, w;
+  out[0] = event_meta(slot, type, m_local);
+  union { float f; int32_t i; } v;
   v.f = value;
-  w.f = t;
-  out[2] = v.i;
-  out[3] = w.i;
+  out[1] = v.i;
 }
 
 }  // namespace ana

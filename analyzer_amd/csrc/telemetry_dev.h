@@ -3,7 +3,7 @@
 //
 // The tile's stat block [T][2K][kStatFeatures] lives in the wave's LDS
 // scratch; events of the tile (contiguous: evoff is a CSR index) are streamed
-// with 16-B loads (8 per lane in flight), folded in with LDS float atomics
+// with 8-B loads (8 per lane in flight), folded in with LDS float atomics
 // (ds_add_f32: contention only among a match's participants); the block then
 // leaves LDS as one contiguous, coalesced store -- the per-match stat rows of
 // consecutive matches are adjacent in the [M][2K][F] output.
@@ -33,24 +33,25 @@ __device__ __forceinline__ void telemetry_tile(const TelemetryParams& tp, int64_
   // 8 events per lane in flight: the loads of a batch retire in one round trip
   constexpr int kBatch = 8;
   for (int64_t base = e0; base < e1; base += 64 * kBatch) {
-    int4 ev[kBatch];
+    int2 ev[kBatch];
 #pragma unroll
     for (int q = 0; q < kBatch; ++q) {
       const int64_t e = base + q * 64 + lane;
-      ev[q] = e < e1 ? reinterpret_cast<const int4*>(tp.events)[e] : make_int4(-1, 0, 0, 0);
+      ev[q] = e < e1 ? reinterpret_cast<const int2*>(tp.events)[e] : make_int2(-1, 0);
     }
 #pragma unroll
     for (int q = 0; q < kBatch; ++q) {
       if (base + q * 64 + lane >= e1) continue;
-      const int64_t ml = (int64_t)ev[q].x - m0;
-      const int slot = event_slot(ev[q].y);
+      // the tile-relative match its tag names (tiles are far shorter than 2^16 matches)
+      const int64_t ml = (int64_t)((event_tag(ev[q].x) - (uint32_t)(m0 & 0xffff)) & 0xffffu);
+      const int slot = event_slot(ev[q].x);
       const int64_t e = base + q * 64 + lane;
       if (ml < 0 || ml >= m1 - m0 || slot >= S || e < tp.evoff[m0 + ml] || e >= tp.evoff[m0 + ml + 1]) {
         ++bad;
         continue;
       }
       float add;
-      const int f = event_feature(event_type(ev[q].y), __int_as_float(ev[q].z), add);
+      const int f = event_feature(event_type(ev[q].x), __int_as_float(ev[q].y), add);
       float* row = lds + (ml * S + slot) * kPad;
       if constexpr (D == 1) {  // diagnostic: no LDS adds (timing only)
         bad += f == 99;
@@ -171,7 +172,7 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   const int t = lane & 31, half = lane >> 5;
   const int fr = lane & 15, fg = lane >> 4;  // fragment row/column and k-group
   uint8_t* mine_set = lds + half * kTeleSetBytes;
-  const int4* __restrict__ evs = reinterpret_cast<const int4*>(tp.events) + e0;
+  const int2* __restrict__ evs = reinterpret_cast<const int2*>(tp.events) + e0;
   // two live 16-row accumulators: row tiles c and c + 1
   tele_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
   int c = 0;
@@ -215,18 +216,17 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   // vmcnt waits); other waves on the SIMD cover the gap between groups.  Loads
   // are unconditional (positions past the span re-read its last event; the
   // decode masks them): conditional loads make the compiler wait for all.
-  // (forcing full 16-B buffer loads instead of the 12-B loads the compiler emits for
-  // the 3 used words measured slower: 2.51 vs 1.95 ms)
+  // (events are 8 B since round 2: half the bytes of the round-1 16-B records)
   const int elast = ne > 0 ? ne - 1 : 0;
   for (int pr = 0; pr < ne; pr += 64 * NB) {
-    int4 ev[NB];
+    int2 ev[NB];
 #pragma unroll
     for (int q = 0; q < NB; ++q) ev[q] = evs[min(pr + 64 * q + lane, elast)];
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     const int pb = pr + 64 * q;
     if (pb >= ne) break;
-    const int4 cur = ev[q];
+    const int2 cur = ev[q];
     // the two chunks: first/last positions and the row tiles they can touch
     const int n1 = ne - pb - kTeleChunk;  // events of chunk 1 (<= 0: none)
     const int ms0 = match_at(pb);
@@ -238,17 +238,18 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
     // decode this lane's event (branch-free); it must sit in the CSR range of the
     // match it names, and its slot must be < 2K
     const int e = pb + lane;
-    const int64_t xw = (int64_t)cur.x - m0;
-    const int seg = xw < 0 ? 0 : xw >= nm ? nm - 1 : (int)xw;
-    const int slot = event_slot(cur.y);
+    // the span-relative match the event's 16-bit tag names (spans are <= 63 matches)
+    const int xw = (int)((event_tag(cur.x) - (uint32_t)(m0 & 0xffff)) & 0xffffu);
+    const int seg = xw >= nm ? nm - 1 : xw;
+    const int slot = event_slot(cur.x);
     const int r0 = rel[seg], r1e = rel[seg + 1];
     const bool ok = e < ne && xw == seg && slot < S && e >= r0 && e < r1e;
     bad += (e < ne && !ok) ? 1u : 0u;
     const int row = seg * S + slot;
     // type -> B columns (event_feature): 0..2 kills/deaths/assists at column 1 + type,
     // 3..6 damage/gold/farm/heal as (hi, mid, lo) at columns 3 type - 5 .. 3 type - 3
-    const int type = event_type(cur.y);
-    const float value = __int_as_float(cur.z);
+    const int type = event_type(cur.x);
+    const float value = __int_as_float(cur.y);
     const bool counted = ok && type < 3;
     const bool summed = ok && type >= 3 && type <= 6;
     const bool finite = __builtin_isfinite(value);
@@ -337,12 +338,12 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
     // rare slow path: add the tile's Inf/NaN values on top of the stored sums
     __threadfence();
     for (int e = lane; e < ne; e += 64) {
-      const int4 x = evs[e];
-      const int xm = (int)((int64_t)x.x - m0);
-      const int slot = event_slot(x.y);
-      if (xm < 0 || xm >= nm || slot >= S || e < rel[xm] || e >= rel[xm + 1]) continue;
+      const int2 x = evs[e];
+      const int xm = (int)((event_tag(x.x) - (uint32_t)(m0 & 0xffff)) & 0xffffu);
+      const int slot = event_slot(x.x);
+      if (xm >= nm || slot >= S || e < rel[xm] || e >= rel[xm + 1]) continue;
       float add;
-      const int f = event_feature(event_type(x.y), __int_as_float(x.z), add);
+      const int f = event_feature(event_type(x.x), __int_as_float(x.y), add);
       if (f >= 3 && !__builtin_isfinite(add)) atomicAdd(dst + (xm * S + slot) * kStatFeatures + f, add);
     }
   }

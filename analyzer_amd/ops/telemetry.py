@@ -7,15 +7,16 @@ aggregated on the device into one stat vector per participant slot,
 ``stats[M, 2K, 8]`` = (kills, deaths, assists, damage, gold, farm, healing,
 events) -- aligned with the rating outputs ``[M, 2K]``:
 
-* ``aggregate`` runs the standalone kernel (one wave per 16-match tile, LDS
-  float atomics, coalesced tile stores; csrc/telemetry.hip);
+* ``aggregate`` runs the standalone kernel (one wave per span of matches, a
+  one-hot GEMM on the matrix cores -- or LDS float atomics, ANA_TELE_IMPL=0 --
+  and coalesced stat stores; csrc/telemetry.hip, telemetry_dev.h);
 * ``BatchRater.rate(..., telemetry=(evoff, events, stats))`` runs it INSIDE the
   dataflow launch: waves with no ready match aggregate telemetry tiles instead
   of sleeping, so a latency-bound rating absorbs the bandwidth-bound
   aggregation (the fused streaming mode).
 
-Events are 16-B records grouped by match with CSR offsets ``evoff[M+1]``
-(layout: csrc/telemetry_core.h).  ``make_telemetry`` generates them with the
+Events are 8-B records (slot | type << 8 | 16-bit match tag << 16, value bits)
+grouped by match with CSR offsets ``evoff[M+1]`` (layout: csrc/telemetry_core.h).  ``make_telemetry`` generates them with the
 counter RNG (deterministic per global match index, device or host).
 """
 from __future__ import annotations
@@ -41,7 +42,7 @@ class TelemetrySpec:
 
 class Telemetry(NamedTuple):
     evoff: torch.Tensor   # [M + 1] int64
-    events: torch.Tensor  # [E, 4] int32
+    events: torch.Tensor  # [E, 2] int32: slot | type << 8 | match tag << 16, value bits
 
     @property
     def num_events(self) -> int:
@@ -55,7 +56,7 @@ def make_telemetry(spec: TelemetrySpec, rec: torch.Tensor, K: int, base: int = 0
     evoff = torch.zeros(M + 1, dtype=torch.int64, device=rec.device)
     torch.cumsum(counts, 0, out=evoff[1:])
     E = int(evoff[-1].item())
-    events = torch.empty((E, 4), dtype=torch.int32, device=rec.device)
+    events = torch.empty((E, 2), dtype=torch.int32, device=rec.device)
     native().gen_events(rec, K, evoff, spec.seed, spec.min_events, spec.max_events, base, events)
     return Telemetry(evoff, events)
 
@@ -84,10 +85,10 @@ def aggregate_reference(tel: Telemetry, K: int) -> np.ndarray:
     out = np.zeros((M, 2 * K, len(STAT_NAMES)), dtype=np.float64)
     if ev.shape[0] == 0:
         return out
-    m = ev[:, 0].astype(np.int64)
-    slot = ev[:, 1] & 0xFF
-    typ = (ev[:, 1] >> 8) & 0xFF
-    val = ev[:, 2].view(np.float32).astype(np.float64)
+    m = np.repeat(np.arange(M, dtype=np.int64), np.diff(tel.evoff.cpu().numpy()))  # CSR position
+    slot = ev[:, 0] & 0xFF
+    typ = (ev[:, 0] >> 8) & 0xFF
+    val = ev[:, 1].view(np.float32).astype(np.float64)
     add = np.where(typ <= 2, 1.0, val)
     feat = np.where(typ <= 6, typ, -1)
     ok = feat >= 0

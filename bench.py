@@ -189,7 +189,17 @@ def main(argv=None) -> int:
     torch.cuda.synchronize()
     prepared = {0: pipe.prepare(windows[0])}
 
-    tstream = torch.cuda.Stream(dev) if tele is not None and args.telemetry_mode == "overlap" else None
+    tstream = None
+    if tele is not None and args.telemetry_mode == "overlap":
+        # ANA_TELE_CUS=n: the co-running aggregation confined to n CUs (HIP CU mask),
+        # so it takes bandwidth without slowing every executor wave
+        n_cus = int(os.environ.get("ANA_TELE_CUS") or 0)
+        if n_cus > 0:
+            from analyzer_amd.ops.native import native
+
+            tstream = torch.cuda.ExternalStream(native().cu_masked_stream(dev.index or 0, n_cus), device=dev)
+        else:
+            tstream = torch.cuda.Stream(dev)
 
     def step(i):
         # rate window i, then the prepass of window i+1 on the side stream behind

@@ -17,6 +17,7 @@
 #   hop        quick executor A/B (serial chain + 10M window, local hand-off, timing build)
 #   merge      sweep-merge message/decode kernels at P = 1M, 10M on one GPU
 #   exactdp    exact DP (C2) rehearsal, 2/4 gloo ranks on one GPU, rounds + time per window
+#   tele       config 4 telemetry placement (separate / fused / CU-masked overlap)
 #   tail       prepass start point sweep for config 2 (ANA_PREPASS_AT, serial)
 #   ab         in-call A/B of executor builds (AB_LIBS, scripts/ab_build.sh), interleaved rounds
 #   micro      executor hop latency A/B (scripts/tune_rate.py: serial / uniform / skewed, timing build)
@@ -105,6 +106,14 @@ for task in "$@"; do
     exactdp)  # exact DP rehearsal: 2 and 4 gloo ranks on this one GPU, 1M-match window
       run exactdp/r2 600 $PY scripts/exact_dp_rehearsal.py --ranks 2
       run exactdp/r4 600 $PY scripts/exact_dp_rehearsal.py --ranks 4
+      ;;
+    tele)  # config 4 telemetry placement: separate, fused, overlap on all / 16 / 32 / 64 CUs
+      run tele/separate 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode separate
+      run tele/fused 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode fused
+      for n in ${TELE_CUS:-0 16 32 64}; do
+        ANA_TELE_CUS=$n run tele/overlap_cus$n 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode overlap
+      done
+      for f in gpurun_out/tele/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
       ;;
     tail)  # where the next window's prepass starts (ANA_PREPASS_AT sweep, config 2; 0 = with the launch)
       for r in 1 2; do

@@ -255,16 +255,17 @@ def test_telemetry_impls_vs_oracle_edges(gpu_device, monkeypatch, K, impl):
     tel = make_telemetry(TelemetrySpec(seed=5, min_events=0, max_events=90), rec, K)
     ev = tel.events.clone()
     idx = torch.randperm(ev.shape[0], generator=torch.Generator().manual_seed(K))[:60]
-    ev[idx[:20], 1] = (ev[idx[:20], 1] & ~0xFF) | (2 * K)            # slot out of range
-    ev[idx[20:40], 0] = (ev[idx[20:40], 0] + 1) % M                  # names the next match
-    ev[idx[40:50], 1] = (ev[idx[40:50], 1] & 0xFF) | (3 << 8)        # damage events ...
-    ev[:, 2].view(torch.float32)[idx[40:50]] = float("inf")          # ... of infinite value
+    ev[idx[:20], 0] = (ev[idx[:20], 0] & ~0xFF) | (2 * K)            # slot out of range
+    ev[idx[20:40], 0] = ev[idx[20:40], 0] + (1 << 16)                # tag names the next match
+    ev[idx[40:50], 0] = (ev[idx[40:50], 0] & ~0xFF00) | (3 << 8)     # damage events ...
+    ev[:, 1].view(torch.float32)[idx[40:50]] = float("inf")          # ... of infinite value
     evn = ev.numpy()
-    m = evn[:, 0].astype(np.int64)
     seg = np.repeat(np.arange(M), np.diff(tel.evoff.numpy()))
-    slot, typ = evn[:, 1] & 0xFF, (evn[:, 1] >> 8) & 0xFF
-    ok = (m == seg) & (slot < 2 * K)
-    val = evn[:, 2].view(np.float32).astype(np.float64)
+    m = seg
+    tag = (evn[:, 0] >> 16) & 0xFFFF
+    slot, typ = evn[:, 0] & 0xFF, (evn[:, 0] >> 8) & 0xFF
+    ok = (tag == seg & 0xFFFF) & (slot < 2 * K)
+    val = evn[:, 1].view(np.float32).astype(np.float64)
     add, feat = np.where(typ <= 2, 1.0, val), np.where(typ <= 6, typ, -1)
     ref = np.zeros((M, 2 * K, 8))
     sel = ok & (feat >= 0)

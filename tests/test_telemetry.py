@@ -21,8 +21,8 @@ def test_generator_layout_and_determinism():
     assert counts.min() >= 10 and counts.max() <= 40 and tel.num_events == counts.sum()
     ev = tel.events.numpy()
     m = np.repeat(np.arange(rec.shape[0]), counts)
-    assert (ev[:, 0] == m).all()
-    slot = ev[:, 1] & 0xFF
+    assert ((ev[:, 0] >> 16) & 0xFFFF == m & 0xFFFF).all()  # 16-bit match tag
+    slot = ev[:, 0] & 0xFF
     n0 = ((rec[:, 6] >> 8) & 0xFF).numpy()[m]
     n1 = ((rec[:, 6] >> 16) & 0xFF).numpy()[m]
     assert (((slot < n0)) | ((slot >= K) & (slot < K + n1))).all()  # real participants only
@@ -30,7 +30,9 @@ def test_generator_layout_and_determinism():
     assert torch.equal(tel.events, again.events)
     # the events of a match depend on its global index only
     tail = make_telemetry(TelemetrySpec(seed=5, min_events=10, max_events=40), rec[100:], K, base=100)
-    assert torch.equal(tail.events[:, 1:], tel.events[int(tel.evoff[100]):, 1:])
+    o = int(tel.evoff[100])
+    assert torch.equal(tail.events[:, 1], tel.events[o:, 1])                   # values
+    assert torch.equal(tail.events[:, 0] & 0xFFFF, tel.events[o:, 0] & 0xFFFF)  # slot, type
 
 
 def test_host_aggregation_matches_oracle():
@@ -62,8 +64,8 @@ def test_malformed_events_are_dropped_and_counted():
     rec = _stream(M=20, K=K, P=10, seed=6)
     tel = make_telemetry(TelemetrySpec(seed=2, min_events=3, max_events=3), rec, K)
     ev = tel.events.clone()
-    ev[0, 1] = (ev[0, 1] & ~0xFF) | 7   # slot 7 >= 2K
-    ev[5, 0] = 19                        # names a match in another tile
+    ev[0, 0] = (ev[0, 0] & ~0xFF) | 7                     # slot 7 >= 2K
+    ev[5, 0] = (ev[5, 0] & 0xFFFF) | (19 << 16)            # names a match in another tile
     from analyzer_amd.ops.native import native
     stats = allocate_stats(20, K, "cpu")
     bad = native().telemetry(tel.evoff, ev, K, stats, torch.zeros(1, dtype=torch.int32))
@@ -78,7 +80,7 @@ def test_strict_attribution_same_tile_other_match():
     rec = _stream(M=20, K=K, P=10, seed=7)
     tel = make_telemetry(TelemetrySpec(seed=3, min_events=2, max_events=2), rec, K)
     ev = tel.events.clone()
-    ev[4, 0] = 3                         # event of match 2 names match 3 (same tile)
+    ev[4, 0] = (ev[4, 0] & 0xFFFF) | (3 << 16)  # event of match 2 names match 3 (same tile)
     from analyzer_amd.ops.native import native
     stats = allocate_stats(20, K, "cpu")
     bad = native().telemetry(tel.evoff, ev, K, stats, torch.zeros(1, dtype=torch.int32))
