@@ -14,6 +14,7 @@
 #   skew       bench.py --skew 2 and 3
 #   dp         bench.py --gpus 2 and 4 on this one GPU (gloo rehearsal of the spawn path)
 #   accuracy   sweep-DP accuracy, 8 ranks x 10M matches over 1M players, sweeps 1,2,4,8
+#   graph      micro-batches (eager vs HIP graph, scripts/bench_graph.py) + prepass alone
 #   hop        quick executor A/B (serial chain + 10M window, local hand-off, timing build)
 #   merge      sweep-merge message/decode kernels at P = 1M, 10M on one GPU
 #   exactdp    exact DP (C2) rehearsal, 2/4 gloo ranks on one GPU, rounds + time per window
@@ -78,6 +79,10 @@ for task in "$@"; do
       run idle/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 --rounds 2 \
           --blocks 8 --idle=-1,2,8
       grep -h "^round 1" gpurun_out/idle/*.log | cut -c1-120
+      ;;
+    graph)  # worker-sized micro-batches: eager vs HIP-graph replay; schedule prepass alone
+      run graph/microbatch 300 $PY scripts/bench_graph.py
+      run graph/sched 300 $PY scripts/sched_time.py
       ;;
     hop)  # quick executor A/B: serial chain + 10M window, production + timing build
       run hop/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 \
