@@ -37,6 +37,13 @@ def _env(env: Mapping[str, str], key: str) -> Optional[str]:
     return v if v else None
 
 
+def _tristate(v: Optional[str]) -> Optional[bool]:
+    """'1'/'0' -> True/False; unset, empty or 'auto' -> None."""
+    if v is None or v == "" or v.lower() == "auto":
+        return None
+    return v != "0"
+
+
 @dataclass(frozen=True)
 class RaterConfig:
     unknown_player_sigma: int = 500
@@ -123,9 +130,10 @@ class EngineConfig:
     variable                default   consumer
     ======================  ========  =============================================
     ANA_RATE_BLOCKS         512       persistent grid of a window launch (ops/rate.py)
-    ANA_PREPASS_AT          0.8       tail overlap point of the next prepass (runtime/engine.py)
+    ANA_PREPASS_AT          0.7       tail overlap point of the next prepass (runtime/engine.py)
     ANA_PREPASS_CUS         0         CU-masked prepass stream, 0 = off (runtime/engine.py)
-    ANA_PREPASS_SERIAL      1         prepass on the main stream; 0 = tail overlap (runtime/engine.py)
+    ANA_PREPASS_SERIAL      auto      1 prepass on the main stream, 0 tail overlap; auto: serial
+                                      for K <= 4, overlap for 5v5 (runtime/engine.py)
     ANA_MERGE_BUCKET_MB     16        sweep-merge bucket size (parallel/sweep.py)
     COMM_DTYPE              fp32      sweep-merge message precision (bench.py, rerate)
     SWEEPS                  1         causal sweeps per window (bench.py, rerate)
@@ -137,9 +145,9 @@ class EngineConfig:
     """
 
     rate_blocks: int = 512
-    prepass_at: float = 0.8
+    prepass_at: float = 0.7
     prepass_cus: int = 0
-    prepass_serial: bool = True
+    prepass_serial: Optional[bool] = None  # None = auto (WindowPipeline.serial_prepass)
     merge_bucket_mb: float = 16.0
     comm_dtype: str = "fp32"
     sweeps: int = 1
@@ -165,9 +173,9 @@ class EngineConfig:
     def from_env(env: Mapping[str, str] = os.environ) -> "EngineConfig":
         return EngineConfig(
             rate_blocks=int(_env(env, "ANA_RATE_BLOCKS") or 512),
-            prepass_at=float(_env(env, "ANA_PREPASS_AT") or 0.8) if env.get("ANA_PREPASS_AT") != "0" else 0.0,
+            prepass_at=float(_env(env, "ANA_PREPASS_AT") or 0.7) if env.get("ANA_PREPASS_AT") != "0" else 0.0,
             prepass_cus=int(_env(env, "ANA_PREPASS_CUS") or 0),
-            prepass_serial=(env.get("ANA_PREPASS_SERIAL") or "1") not in ("", "0"),
+            prepass_serial=_tristate(env.get("ANA_PREPASS_SERIAL")),
             merge_bucket_mb=float(_env(env, "ANA_MERGE_BUCKET_MB") or 16),
             comm_dtype=_env(env, "COMM_DTYPE") or "fp32",
             sweeps=int(_env(env, "SWEEPS") or 1),

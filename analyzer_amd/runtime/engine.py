@@ -13,13 +13,15 @@ Two schedule buffer sets alternate; events order "schedule(i+1) may reuse the
 set that rate(i-1) consumed" and "rate(i) needs schedule(i)".  On the CPU the
 same API runs the host mirror sequentially.
 
-Default since round 2 (``ANA_PREPASS_SERIAL=1``): the prepass runs on the main
-stream between launches.  Measured on MI355X for config 2, the co-running
-prepass slows the latency-bound executor by more than it hides (step 7.79 ms
-serial vs 7.94-8.17 ms with tail overlap at 0.9-0.8, profiles/r2/tail_sweep.log),
-so the overlap below is opt-in (``ANA_PREPASS_SERIAL=0``).
+Placement (``ANA_PREPASS_SERIAL``, default auto): for 1v1..4v4 the prepass runs
+on the main stream between launches; for 5v5 it overlaps the executor's tail.
+Measured on MI355X (profiles/r2/prepass_placement.log), the co-running prepass
+slows the 3v3 executor by more than it hides (config 2: 8.07 ms serial vs
+8.34-8.47 ms overlapped at 0.7-0.3), while the 5v5 executor -- 3000+ levels,
+~75% of its wave iterations idle, a 5.4 ms prepass over 125M slots -- absorbs
+it (config 3: 22.12 ms overlapped at 0.7 vs 22.9-23.2 ms serial).
 
-Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.8): the
+Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.7): the
 prepass of window i+1 does not start with rate(i) -- co-running the two for the
 whole launch costs the latency-bound executor about as much as the prepass
 itself -- but when rate(i) reaches its tail: the executor stores its launch
@@ -63,16 +65,17 @@ class WindowPipeline:
         self.merger = merger
         self.device = roster.device
         self.cuda = self.device.type == "cuda"
-        self.side = self._side_stream() if self.cuda else None
         self._set = 0
         self._free: List[Optional[torch.cuda.Event]] = [None, None]
         self.windows_rated = 0
         # tail overlap: signal word + number of the last enqueued rate launch
         self.ecfg = EngineConfig.from_env()
-        # serial prepass (the default): nothing to overlap, no tail signal
-        self.tail = 0.0 if self.ecfg.prepass_serial else self.ecfg.prepass_at
+        self.serial = self.serial_prepass(self.K, self.ecfg)
+        # serial prepass: nothing to overlap, no tail signal
+        self.tail = 0.0 if self.serial else self.ecfg.prepass_at
         self._signal = 0
         self._seq = 0
+        self.side = self._side_stream() if self.cuda else None
         if self.cuda and self.tail > 0:
             from ..ops.native import native
 
@@ -80,15 +83,20 @@ class WindowPipeline:
             if native().can_wait_value(dev):
                 self._signal = native().progress_signal(dev)
 
+    @staticmethod
+    def serial_prepass(K: int, ecfg: EngineConfig) -> bool:
+        """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial
+        below 5v5 (see the module docstring for the measurements)."""
+        if ecfg.prepass_serial is not None:
+            return ecfg.prepass_serial
+        return K < 5
+
     def _side_stream(self):
         """Side stream of the prepass; ``ANA_PREPASS_CUS=n`` confines it to n CUs
         (HIP CU mask) so it trickles alongside the executor instead of bursting."""
-        import os
-
-        ecfg = EngineConfig.from_env()
-        if ecfg.prepass_serial:
-            return torch.cuda.current_stream(self.device)  # no overlap (the default)
-        n = ecfg.prepass_cus
+        if self.serial:
+            return torch.cuda.current_stream(self.device)  # no overlap
+        n = self.ecfg.prepass_cus
         if n > 0:
             from ..ops.native import native
 

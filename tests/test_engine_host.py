@@ -147,3 +147,16 @@ def test_skewed_activity_draw(skew):
     for x in (100, 10_000):
         frac = float((ids < x).double().mean())
         assert abs(frac - (x / P) ** (1.0 / skew)) < 0.01, (x, frac)
+
+
+def test_prepass_placement_knob():
+    """ANA_PREPASS_SERIAL: 1/0 force the placement; unset or auto -> serial below 5v5."""
+    from analyzer_amd.config import EngineConfig
+    from analyzer_amd.runtime.engine import WindowPipeline
+
+    auto = EngineConfig.from_env({})
+    assert auto.prepass_serial is None and EngineConfig.from_env({"ANA_PREPASS_SERIAL": "auto"}).prepass_serial is None
+    assert WindowPipeline.serial_prepass(3, auto) and not WindowPipeline.serial_prepass(5, auto)
+    on, off = (EngineConfig.from_env({"ANA_PREPASS_SERIAL": v}) for v in ("1", "0"))
+    assert WindowPipeline.serial_prepass(5, on) and not WindowPipeline.serial_prepass(3, off)
+    assert auto.prepass_at == 0.7 and EngineConfig.from_env({"ANA_PREPASS_AT": "0"}).prepass_at == 0.0
