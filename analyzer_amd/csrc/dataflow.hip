@@ -834,9 +834,11 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   if (blocks < kHeads) blocks = kHeads;
   // lanes per match: the next power of two (DPP butterfly sums) or exactly 2K
   // (more matches per wave iteration, bpermute-tree sums).  Measured on MI355X
-  // with the scalar-bookkeeping executor: 3v3 8 lanes, 5v5 16 lanes (20.0 vs
-  // 21.2 ms for 12.5M matches with 10) -> auto = off.
-  const bool tight = prm.tight_groups > 0;
+  // with this executor: 3v3 6.23-6.26 ms with 8 lanes vs 6.27-6.30 with 6 (10M
+  // window), 5v5 18.23-18.42 ms with 10 lanes vs 18.42-18.61 with 16 (12.5M;
+  // config 3 step 21.5 vs 21.9 ms, profiles/r2/tight_groups.log) -> auto = tight
+  // for 5v5 only.
+  const bool tight = prm.tight_groups > 0 || (prm.tight_groups < 0 && K == 5);
 #define ANA_RATE_LAUNCH_D(k, g, tele, diag)                                                        \
   hipLaunchKernelGGL((rate_dataflow_kernel<k, g, tele, diag>), dim3((unsigned)blocks), dim3(256), 0, s, \
                      rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, tp)
