@@ -47,7 +47,7 @@ replicas racing on MySQL rows (/root/reference/worker.py:91,174-194).
 from __future__ import annotations
 
 import os
-from typing import Dict, List, Optional
+from typing import Callable, Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -197,11 +197,35 @@ class SweepMerger:
             e.record()
             self._events.append((name, e))
 
-    def merge(self, roster) -> None:
+    def merge(self, roster, overlap: Optional[Callable[[], None]] = None) -> None:
         """Combine every rank's window into the replicated roster (in place):
         messages -> all-reduce -> decode, pipelined over row buckets; the decode
-        also writes the next window's common start."""
+        also writes the next window's common start.
+
+        ``overlap``: independent main-stream work (the next window's schedule
+        prepass, runtime/engine.py) enqueued once every bucket's all-reduce is in
+        flight and before the first decode waits for one, so the collectives run
+        under it instead of in front of it."""
         if self.world <= 1:
+            self.windows += 1
+            if overlap is not None:
+                overlap()
+            return
+        if overlap is not None:
+            self._ev("begin")
+            launched = []
+            for lo, hi in self.buckets():
+                self.messages(roster, lo, hi)
+                launched.append((lo, hi, self._launch_reduce(lo, hi)))
+            self._ev("messages")
+            overlap()
+            self._ev("overlap")
+            for lo, hi, fin in launched:
+                fin()
+                self._ev("allreduce")
+                self.decode(roster, lo, hi, into=self.start)
+                self._ev("apply")
+            self._synced = True
             self.windows += 1
             return
         pending = None  # (lo, hi, finisher) of the bucket whose reduce is in flight

@@ -133,9 +133,10 @@ class WindowPipeline:
         return Prepared(rec, sched, ready, used)
 
     def rate(self, prep: Prepared, out: Optional[RateResult] = None, check: bool = False,
-             telemetry=None) -> RateResult:
+             telemetry=None, overlap: Optional[Callable[[], None]] = None) -> RateResult:
         """Rate a prepared window on the main stream (+ DP merge if configured);
-        ``telemetry`` = (evoff, events, stats) aggregates K8 stats in the same launch."""
+        ``telemetry`` = (evoff, events, stats) aggregates K8 stats in the same launch.
+        ``overlap``: work the merge enqueues while its all-reduces are in flight."""
         main = torch.cuda.current_stream(self.device) if self.cuda else None
         if prep.ready is not None:
             main.wait_event(prep.ready)
@@ -170,7 +171,9 @@ class WindowPipeline:
             self._free[prep.buffer_set] = done
         if self.merger is not None:
             with trace_range("merge", window=self.windows_rated):
-                self.merger.merge(self.roster)
+                self.merger.merge(self.roster, overlap=overlap)
+        elif overlap is not None:
+            overlap()
         self.windows_rated += 1
         return res
 
@@ -182,6 +185,13 @@ class WindowPipeline:
         if self.cuda and next_rec is not None:
             produced = torch.cuda.Event()
             produced.record(torch.cuda.current_stream(self.device))
+        if self.serial and self.merger is not None and self.cuda and next_rec is not None:
+            # serial prepass + DP merge: the prepass needs no roster, so it goes onto
+            # the main stream while the merge's all-reduces are on the wire
+            held: List[Prepared] = []
+            res = self.rate(prep, overlap=lambda: held.append(self.prepare(next_rec, produced=produced)),
+                            **rate_kwargs)
+            return res, held[0]
         res = self.rate(prep, **rate_kwargs)
         nxt = self.prepare(next_rec, produced=produced) if next_rec is not None else None
         return res, nxt

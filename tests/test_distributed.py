@@ -173,15 +173,18 @@ def _sweep_buckets(rank, size, P, M, K, seed, comm_dtype, bucket_rows):
     roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.5))
     rec = make_stream(StreamSpec(team_size=K, seed=seed + 1 + rank, p_afk=0.0), M, P, K=K)
     out = {}
-    for rows in (None, bucket_rows):
+    for rows, tag in ((None, "whole"), (bucket_rows, "bucketed"), (bucket_rows, "overlap")):
         merger = SweepMerger(P, "cpu", comm_dtype=comm_dtype,
                              bucket_rows=P if rows is None else rows)
         local = roster.clone()
         merger.begin(local)
         BatchRater().rate(local, rec, K)
-        merger.merge(local)
-        out["whole" if rows is None else "bucketed"] = local.state
-        out["n_buckets_%s" % ("whole" if rows is None else "bucketed")] = len(merger.buckets())
+        calls = []
+        # "overlap": all buckets' all-reduces launched, the overlapped work, then the decodes
+        merger.merge(local, overlap=(lambda: calls.append(1)) if tag == "overlap" else None)
+        out[tag] = local.state
+        out["n_buckets_%s" % tag] = len(merger.buckets())
+        out["calls_%s" % tag] = len(calls)
     return out
 
 
@@ -195,6 +198,8 @@ def test_sweep_merge_bucketed_pipeline_matches_single_bucket(tmp_path, comm_dtyp
     for r in res:
         assert r["n_buckets_whole"] == 1 and r["n_buckets_bucketed"] == 7
         assert torch.equal(r["whole"].nan_to_num(-7), r["bucketed"].nan_to_num(-7))
+        assert r["calls_overlap"] == 1 and r["calls_bucketed"] == 0
+        assert torch.equal(r["whole"].nan_to_num(-7), r["overlap"].nan_to_num(-7))
     assert torch.equal(res[0]["bucketed"].nan_to_num(-7), res[1]["bucketed"].nan_to_num(-7))
 
 
