@@ -164,6 +164,36 @@ std::tuple<Tensor, int64_t> levels(Tensor rec, int64_t K, int64_t num_players) {
   return {level, depth};
 }
 
+// K5 device levelizer over a fresh schedule (its deps are consumed): (level [M], depth).
+std::tuple<Tensor, int64_t> levels_device(Tensor rec, int64_t K, int64_t num_players, Tensor link,
+                                          Tensor deps) {
+  const auto dev = rec.device();
+  TORCH_CHECK(dev.is_cuda(), "levels_device runs on the device (host: levels)");
+  check(rec, "rec", torch::kInt32, dev);
+  check(link, "link", torch::kInt32, dev);
+  check(deps, "deps", torch::kInt32, dev);
+  TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
+  TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  const int64_t M = rec.size(0);
+  TORCH_CHECK(link.dim() == 2 && link.size(0) == M && link.size(1) == 2 * K, "link must be [M, 2K]");
+  TORCH_CHECK(deps.numel() == M, "deps must have M entries");
+  TORCH_CHECK(M * 2 * K <= ana::kMaxSlots, "more than 2^28 slots in one window (split the stream)");
+  TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
+  auto level = torch::empty({M}, rec.options());
+  auto pushed = torch::zeros({M}, rec.options());
+  auto ctrl = torch::zeros({4}, rec.options());
+  check_hip(ana::launch_levels((int)K, rec.data_ptr<int32_t>(),
+                               reinterpret_cast<const uint32_t*>(link.data_ptr<int32_t>()),
+                               deps.data_ptr<int32_t>(), pushed.data_ptr<int32_t>(),
+                               level.data_ptr<int32_t>(), M, num_players,
+                               reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), stream_of(rec)),
+            "levels");
+  const auto c = ctrl.cpu();
+  TORCH_CHECK(c[3].item<int32_t>() == 0,
+              "device levelizer made no progress for 5 s (schedule and stream disagree)");
+  return {level, (int64_t)c[2].item<int32_t>()};
+}
+
 void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
               Tensor workspace, Tensor ctrl, bool zero_ctrl, int64_t epoch_bump_ptr) {
   const auto dev = rec.device();
@@ -646,6 +676,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gen_roster", &gen_roster, "K7: synthetic roster (state [P,16], attrs [P,4])");
   m.def("gen_stream", &gen_stream, "K7: synthetic match stream rec [M, 2K+2]");
   m.def("schedule_workspace_bytes", &schedule_workspace_bytes);
+  m.def("levels_device", &levels_device);
   m.def("sort_pairs", &sort_pairs, "stable LSD radix sort of int32 (key, value) pairs (device)");
   m.def("levels", &levels, "K5 host levelizer: per-match conflict-free round (0 = stateless)");
   m.def("schedule", &schedule, "K5: per-slot occurrence index (chronological order per player)");

@@ -34,6 +34,12 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
                       uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
                       hipStream_t s);
+// Device levelizer (levels.hip): level[m] = 0 for a match without state, else
+// 1 + the largest level of its players' previous matches -- the exact-DP rounds --
+// as a dataflow over a fresh schedule (link, deps zeroed; deps are consumed).
+// pushed: int32 [M] zeroed scratch; ctrl: uint32 [4] zeroed ([2] depth, [3] error).
+int launch_levels(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, int32_t* pushed,
+                  int32_t* level, int64_t M, int64_t P, uint32_t* ctrl, hipStream_t s);
 // link: uint32 [M][2K] = next match of the player (kNoMatch: none) | kLinkHasPred
 //       if the player has an earlier occurrence in the window
 // deps: int32 [M] zeroed: the completion counters the executor counts up (a

@@ -273,7 +273,7 @@ class BatchRater:
              telemetry=None, progress=None, epoch_dev: Optional[torch.Tensor] = None) -> RateResult:
         """Rate every match of ``rec`` in order, updating ``roster`` in place.
 
-        ``telemetry`` = (evoff [M+1] int64, events [E,4] int32, stats [M,2K,8] f32):
+        ``telemetry`` = (evoff [M+1] int64, events [E,2] int32, stats [M,2K,8] f32):
         per-participant telemetry is aggregated into ``stats`` in the same launch
         (K8 fused streaming mode: idle dataflow waves take telemetry tiles).
         ``progress`` = (signal address, launch number, chunk index): the tail

@@ -1,9 +1,10 @@
 """Exact data-parallel rating by conflict-free rounds.
 
 Exact chronological semantics (/root/reference/worker.py:176,191-192) allow
-parallelism only between matches that share no player.  The levelizer (K5,
-``native().levels``, C++) gives every match its round: 1 + the latest round of
-any of its players, 0 for matches that touch no state (they go with round 1).
+parallelism only between matches that share no player.  The levelizer (K5: on
+the device a dataflow over the rating's own schedule, csrc/levels.hip; on the
+host a C++ walk) gives every match its round: 1 + the latest round of any of its
+players, 0 for matches that touch no state (they go with round 1).
 Matches of one round are disjoint, so ranks split each round into contiguous
 slices, rate their slice against their replica, and exchange ONLY the rows
 they changed.  The result is bit-identical to one process rating the window in
@@ -42,8 +43,17 @@ from ..ops.rate import BatchRater, RateResult, Roster
 from .comm import world
 
 
-def rounds(rec: torch.Tensor, K: int, num_players: int):
-    """(level per match [M] int32 on the host, number of rounds)."""
+def rounds(rec: torch.Tensor, K: int, num_players: int, rater: Optional[BatchRater] = None):
+    """(level per match [M] int32 on the host, number of rounds).
+
+    A device stream is levelized on the device (csrc/levels.hip: a dataflow over
+    the same radix schedule the rating uses, milliseconds per 10M-match window);
+    a host stream by the sequential C++ walk (host.cpp levels_k).  Both give the
+    same levels (tests/test_engine_gpu.py)."""
+    if rec.is_cuda:
+        sched = (rater or BatchRater()).schedule(rec, K, num_players, tag="_levels")
+        level, depth = native().levels_device(rec.contiguous(), K, num_players, sched.link, sched.deps)
+        return level.cpu(), int(depth)
     level, depth = native().levels(rec.detach().cpu().contiguous(), K, num_players)
     return level, int(depth)
 
@@ -102,7 +112,7 @@ def rate_exact_dp(rater: BatchRater, roster: Roster, rec: torch.Tensor, K: int,
     if M == 0:
         return out
     if level is None:
-        level, _ = rounds(rec, K, roster.num_players)
+        level, _ = rounds(rec.to(dev) if dev.type == "cuda" else rec, K, roster.num_players, rater)
     plan = RoundPlan(level, size)
     if EngineConfig.from_env().check_rounds:
         bad = check_rounds(rec, K, plan, roster.num_players)

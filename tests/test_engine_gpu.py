@@ -486,6 +486,24 @@ def _rccl_entry(rank, port, outdir, args):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("P,M,K,skew", [(20, 3000, 3, 1), (5000, 100000, 3, 1), (300, 20000, 5, 1),
+                                          (100_000, 400_000, 3, 2), (50, 400, 2, 1), (40, 700, 1, 1),
+                                          (1_000_000, 1_000_000, 4, 1)])
+def test_device_levels_match_host(gpu_device, P, M, K, skew):
+    """K5 device levelizer (csrc/levels.hip, a dataflow over the radix or the
+    micro-batch schedule) == the sequential host walk, level for level."""
+    from analyzer_amd.ops.native import native
+    from analyzer_amd.parallel.exact_dp import rounds
+
+    ss = StreamSpec(team_size=K, seed=P + 3, p_afk=0.05, p_unsupported=0.05, p_uneven=0.05, p_hot=0.2,
+                    skew=skew)
+    rec = make_stream(ss, M, P, K=K)
+    lh, dh = native().levels(rec, K, P)
+    ld, dd = rounds(rec.to(gpu_device), K, P)
+    assert dd == int(dh) and int(lh.max()) == dd
+    assert torch.equal(ld, lh)
+
+
 def test_exact_dp_round_check_on_device(gpu_device):
     """The C2 race detector's kernel (csrc/sweep.hip check_round_kernel) on the
     device: the levelizer's rounds pass, a one-round plan of a window with
