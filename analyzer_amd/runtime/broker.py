@@ -22,8 +22,12 @@ nowhere -- the reference never declares ``SEW_QUEUE``, worker.py:87-90), and
 topic-exchange bindings with ``*`` / ``#`` patterns.  Time comes from an
 injectable clock so batching tests are deterministic.
 
-No pika in this image: ``connect(uri)`` returns a MemoryBroker for
-``memory://`` URIs and raises a clear error for ``amqp://`` ones.
+``connect(uri)`` returns a MemoryBroker for ``memory://`` URIs and, for
+``amqp://`` ones, a ``PikaBroker``: the same surface over a real
+``pika.BlockingConnection`` (pika 0.10, the reference's pin, or 1.x).  This
+image has no pika, so the adapter is tested against a fake pika
+module of both API generations (tests/test_worker.py); against a live
+RabbitMQ its parity is unpinned.
 """
 from __future__ import annotations
 
@@ -337,17 +341,114 @@ class MemoryBroker:
         self._stop = True
 
 
-def connect(uri: str, clock: Optional[Callable[[], float]] = None) -> MemoryBroker:
+class PikaChannel:
+    """The worker's channel surface over a pika ``BlockingChannel``."""
+
+    def __init__(self, pika, ch):
+        self._pika = pika
+        self._ch = ch
+        # pika >= 1.0: basic_consume(queue, on_message_callback); 0.10: (callback, queue=)
+        self._v1 = int(str(getattr(pika, "__version__", "0")).split(".")[0] or 0) >= 1
+
+    def queue_declare(self, queue: str, durable: bool = False, **kw) -> None:
+        self._ch.queue_declare(queue=queue, durable=durable, **kw)
+
+    def basic_qos(self, prefetch_count: int = 0, **kw) -> None:
+        self._ch.basic_qos(prefetch_count=int(prefetch_count), **kw)
+
+    def basic_consume(self, *args, **kwargs) -> str:
+        queue = kwargs.get("queue")
+        callback = kwargs.get("on_message_callback") or kwargs.get("consumer_callback")
+        for a in args:
+            if callable(a):
+                callback = a
+            elif isinstance(a, str) and queue is None:
+                queue = a
+        if queue is None or callback is None:
+            raise TypeError("basic_consume needs a queue and a callback")
+        # pika hands (channel, method, properties, body) with the attribute names the
+        # worker reads (method.delivery_tag, properties.headers); the worker acks
+        # through this adapter, so give it the adapter as the channel
+        cb = lambda _ch, method, props, body: callback(self, method, props, body)  # noqa: E731
+        if self._v1:
+            return self._ch.basic_consume(queue=queue, on_message_callback=cb)
+        return self._ch.basic_consume(cb, queue=queue)
+
+    def basic_ack(self, delivery_tag: int = 0, multiple: bool = False) -> None:
+        self._ch.basic_ack(delivery_tag=delivery_tag, multiple=multiple)
+
+    def basic_nack(self, delivery_tag: int = 0, multiple: bool = False, requeue: bool = True) -> None:
+        self._ch.basic_nack(delivery_tag=delivery_tag, multiple=multiple, requeue=requeue)
+
+    def basic_publish(self, exchange: str = "", routing_key: str = "", body=b"",
+                      properties=None, **_) -> None:
+        if isinstance(properties, BasicProperties):
+            properties = self._pika.BasicProperties(headers=properties.headers,
+                                                    delivery_mode=properties.delivery_mode,
+                                                    content_type=properties.content_type)
+        self._ch.basic_publish(exchange=exchange, routing_key=routing_key, body=body,
+                               properties=properties)
+
+    def close(self) -> None:
+        self._ch.close()
+
+
+class PikaBroker:
+    """The worker's connection surface (``channel``, ``add_timeout`` /
+    ``remove_timeout``, ``run``) over ``pika.BlockingConnection`` -- the
+    reference's transport (/root/reference/worker.py:85-92,98-99,221)."""
+
+    def __init__(self, uri: str, pika=None):
+        if pika is None:
+            import pika  # noqa: F811 -- optional dependency
+        self._pika = pika
+        self.conn = pika.BlockingConnection(pika.URLParameters(uri))
+        self.channels: List[PikaChannel] = []
+        self._stop = False
+
+    def channel(self) -> PikaChannel:
+        ch = PikaChannel(self._pika, self.conn.channel())
+        self.channels.append(ch)
+        return ch
+
+    def add_timeout(self, delay: float, callback: Callable[[], None]):
+        if hasattr(self.conn, "call_later"):   # pika >= 1.0
+            return self.conn.call_later(delay, callback)
+        return self.conn.add_timeout(delay, callback)  # pika 0.10
+
+    def call_later(self, delay: float, callback: Callable[[], None]):
+        return self.add_timeout(delay, callback)
+
+    def remove_timeout(self, timeout_id) -> None:
+        self.conn.remove_timeout(timeout_id)
+
+    def process_data_events(self, time_limit: float = 0.0) -> None:
+        self.conn.process_data_events(time_limit=time_limit)
+
+    def run(self, until: Optional[Callable[[], bool]] = None, idle_exit: bool = False) -> None:
+        """``start_consuming`` that also honours ``until`` / ``stop()``: the
+        blocking loop in 0.1-s slices (deliveries and timers fire inside)."""
+        self._stop = False
+        while not self._stop and not (until and until()):
+            self.conn.process_data_events(time_limit=0.1)
+
+    def stop(self) -> None:
+        self._stop = True
+
+    def close(self) -> None:
+        self.conn.close()
+
+
+def connect(uri: str, clock: Optional[Callable[[], float]] = None):
     """Broker for a ``RABBITMQ_URI``.  ``memory://`` (or empty) -> in-process
-    broker.  ``amqp://`` needs pika, which this image does not ship."""
+    broker; ``amqp://`` / ``amqps://`` -> ``PikaBroker`` (needs pika)."""
     if not uri or uri.startswith("memory:"):
         return MemoryBroker(clock)
     if uri.startswith("amqp"):
         try:
-            import pika  # noqa: F401
+            import pika
         except ImportError as e:
             raise RuntimeError("RABBITMQ_URI=%s needs the pika package, which is not installed; "
                                "use RABBITMQ_URI=memory:// for the in-process broker" % uri) from e
-        raise RuntimeError("the AMQP adapter is not built into this release; "
-                           "use RABBITMQ_URI=memory://")
+        return PikaBroker(uri, pika)
     raise ValueError("unsupported broker URI %r" % uri)

@@ -384,3 +384,123 @@ def test_sqlalchemy_store_rollback_and_quarantine(tmp_path):
     s = store.session()
     assert all(m.trueskill_quality is None for m in s.load_matches([m.api_id for m in ms]))  # rolled back
     s.close()
+
+
+# ------------------------------------------------- real-AMQP adapter (PikaBroker)
+def _fake_pika(version):
+    """A pika module stand-in with the API shape of pika 0.10 (the reference's
+    pin) or 1.x, delivering through a MemoryBroker underneath.  pika itself is
+    not installed here, so against a live RabbitMQ this path is parity-unpinned."""
+    import types
+
+    mod = types.ModuleType("pika")
+    mod.__version__ = version
+    v1 = version.startswith("1")
+    calls = []
+
+    class BasicProperties:
+        def __init__(self, headers=None, delivery_mode=None, content_type=None):
+            self.headers, self.delivery_mode, self.content_type = headers, delivery_mode, content_type
+
+    class URLParameters:
+        def __init__(self, url):
+            self.url = url
+
+    class Channel:
+        def __init__(self, ch):
+            self._ch = ch
+
+        def queue_declare(self, queue, durable=False, **kw):
+            calls.append(("queue_declare", queue, durable))
+            self._ch.queue_declare(queue, durable=durable)
+
+        def basic_qos(self, prefetch_count=0, **kw):
+            calls.append(("basic_qos", prefetch_count))
+            self._ch.basic_qos(prefetch_count=prefetch_count)
+
+        if v1:
+            def basic_consume(self, queue, on_message_callback, auto_ack=False):
+                calls.append(("basic_consume_v1", queue))
+                return self._ch.basic_consume(on_message_callback, queue=queue)
+        else:
+            def basic_consume(self, consumer_callback, queue="", no_ack=False):
+                calls.append(("basic_consume_v0", queue))
+                return self._ch.basic_consume(consumer_callback, queue=queue)
+
+        def basic_ack(self, delivery_tag=0, multiple=False):
+            self._ch.basic_ack(delivery_tag, multiple)
+
+        def basic_nack(self, delivery_tag=None, multiple=False, requeue=True):
+            self._ch.basic_nack(delivery_tag, multiple, requeue)
+
+        def basic_publish(self, exchange, routing_key, body, properties=None, mandatory=False):
+            assert properties is None or isinstance(properties, BasicProperties)
+            hdr = B.BasicProperties(headers=properties.headers) if properties is not None else None
+            self._ch.basic_publish(exchange=exchange, routing_key=routing_key, body=body, properties=hdr)
+
+    class BlockingConnection:
+        def __init__(self, params):
+            assert isinstance(params, URLParameters)
+            self.clock = B.ManualClock()
+            self.mem = B.MemoryBroker(self.clock)
+            mod.last = self
+
+        def channel(self):
+            return Channel(self.mem.channel())
+
+        if v1:
+            def call_later(self, delay, callback):
+                return self.mem.add_timeout(delay, callback)
+        else:
+            def add_timeout(self, deadline, callback_method):
+                return self.mem.add_timeout(deadline, callback_method)
+
+        def remove_timeout(self, timeout_id):
+            self.mem.remove_timeout(timeout_id)
+
+        def process_data_events(self, time_limit=0):
+            if not self.mem.process_data_events():  # idle: let time pass to the next timer
+                dl = self.mem.next_deadline()
+                if dl is not None:
+                    self.clock.t = max(self.clock.t, dl)
+
+        def close(self):
+            self.mem.close()
+
+    mod.BasicProperties, mod.URLParameters, mod.BlockingConnection = BasicProperties, URLParameters, BlockingConnection
+    mod.calls = calls
+    return mod
+
+
+@pytest.mark.parametrize("version", ["0.10.0", "1.3.2"])
+def test_pika_adapter_worker_matches_memory_broker(monkeypatch, version):
+    """RABBITMQ_URI=amqp://... goes through PikaBroker: declares, qos, the consume
+    signature of the installed pika generation, timers, ack / nack / fan-out --
+    and rates exactly what the in-process broker rates."""
+    fake = _fake_pika(version)
+    monkeypatch.setitem(sys.modules, "pika", fake)
+    n, players, batch = 11, 20, 4
+    ref, ref_matches, _ = make_worker(n=n, players=players, batch=batch, docrunchmatch=True)
+    publish(ref.channel, "analyze", [m.api_id for m in ref_matches])
+    ref.start_consuming()
+
+    store = MemoryStore()
+    matches = populate(store, n, players, team_size=3, seed=3)
+    cfg = WorkerConfig(batchsize=batch, chunksize=3, idle_timeout=1.0, engine="python",
+                       rabbitmq_uri="amqp://guest:guest@rabbit:5672/%2F", docrunchmatch=True)
+    w = Worker(cfg, store=store, rater_cfg=RaterConfig()).connect()
+    assert isinstance(w.rabbit, B.PikaBroker)
+    assert ("basic_qos", batch) in fake.calls
+    assert ("basic_consume_v1" if version.startswith("1") else "basic_consume_v0", "analyze") in fake.calls
+    mem = fake.last.mem
+    publish(mem.channels[0], "analyze", [m.api_id for m in matches])
+    w.start_consuming(until=lambda: w.stats.acked == n)
+    assert w.stats.batches == 3 and w.stats.acked == n  # 4 + 4 by size, 3 by the max-latency timer
+    assert mem.depth("crunch_global") == n
+    assert ratings(matches) == ratings(ref_matches)
+
+
+def test_amqp_uri_without_pika_is_a_clear_error(monkeypatch):
+    monkeypatch.setitem(sys.modules, "pika", None)  # import pika -> ImportError
+    with pytest.raises(RuntimeError, match="needs the pika package"):
+        B.connect("amqp://localhost")
