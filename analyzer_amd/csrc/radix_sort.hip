@@ -212,7 +212,8 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
                 const int32_t* __restrict__ rec, uint32_t kend,
                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
-                int64_t tiles, int slots_per_match, uint32_t* __restrict__ link) {
+                int64_t tiles, int slots_per_match, uint32_t* __restrict__ link,
+                uint32_t vlo = 0u, uint32_t vhi = 0xffffffffu, int bounds = 1) {
   constexpr int kR = 1 << RB;
   constexpr int DPT = kR / kThreads;  // digits per thread in the scans
   static_assert(DPT >= 1 && DPT * kThreads == kR, "radix must be a multiple of the block");
@@ -310,11 +311,11 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
         const bool first = i == (int)tstart[d];
         const bool last = i + 1 == hi || i + 1 >= nvalid;
         const uint32_t v = sval[i];
-        if (first || last) {  // sched_fixup reads the boundary pairs of every run
+        if (bounds && (first || last)) {  // sched_fixup reads the boundary pairs of every run
           st32<NT>(kout + o, kk);
           st32<NT>(vout + o, v);
         }
-        if (kk < kend) {
+        if (kk < kend && v >= vlo && v < vhi) {  // this part's slot range (link_parts)
           uint32_t w = (!last && skey[i + 1] == kk) ? sval[i + 1] / (uint32_t)slots_per_match
                                                      : kNoMatch;
           if (!first && skey[i - 1] == kk) w |= kLinkHasPred;
@@ -323,6 +324,25 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
       }
     }
   }
+}
+
+// The LINK pass in parts by slot range.  Its link stores are random 4-B writes,
+// each its own fabric request (PMC: one TCC_EA0_WRREQ per store), and they stay
+// cheap only while the link array they land in fits the 256-MB Infinity Cache:
+// 60M 3v3 slots (240 MB) take 0.85 ms, 96M (config 5, 384 MB) 2.61 ms and 125M
+// 5v5 slots (500 MB) 3.35 ms.  A larger array is written in ceil(bytes / 256 MB)
+// passes over the sorted pairs, each storing only the links of its slot range
+// (the LDS sort is repeated; the boundary pairs go out once): config 5 in two
+// parts 2 x 0.91 ms, its step 13.40 -> 12.56 ms.  Splitting config 2's 240 MB
+// as well costs more than it saves (8.13 -> 8.46 ms).  ANA_LINK_PARTS overrides
+// the count (1 = one pass).
+static int link_parts(int64_t n) {
+  if (const char* e = getenv("ANA_LINK_PARTS")) {
+    const int v = atoi(e);
+    if (v >= 1) return v > 16 ? 16 : v;
+  }
+  const int64_t bytes = n * 4, part = 256ll << 20;
+  return (int)((bytes + part - 1) / part);
 }
 
 // Completes the links of the run-boundary slots of the LINK pass: one thread per
@@ -421,15 +441,20 @@ static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits,
     else
       hipLaunchKernelGGL((radix_upsweep<0, RB, NT>), grid, block, 0, s, ki, nullptr, kend, n, shift, counts, tiles);
     hipLaunchKernelGGL(radix_rowscan, dim3(kR), block, 0, s, counts, tiles, totals);
+    const int parts = last ? link_parts(n) : 1;
     if (first && last)
-      hipLaunchKernelGGL((radix_downsweep<K, true, RB, NT>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko, vo,
-                         n, shift, counts, totals, tiles, S, link);
+      for (int q = 0; q < parts; ++q)
+        hipLaunchKernelGGL((radix_downsweep<K, true, RB, NT>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
+                           vo, n, shift, counts, totals, tiles, S, link, (uint32_t)(n * q / parts),
+                           (uint32_t)(n * (q + 1) / parts), q == 0 ? 1 : 0);
     else if (first)
       hipLaunchKernelGGL((radix_downsweep<K, false, RB, NT>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
                          vo, n, shift, counts, totals, tiles, S, nullptr);
     else if (last)
-      hipLaunchKernelGGL((radix_downsweep<0, true, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
-                         shift, counts, totals, tiles, S, link);
+      for (int q = 0; q < parts; ++q)
+        hipLaunchKernelGGL((radix_downsweep<0, true, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo,
+                           n, shift, counts, totals, tiles, S, link, (uint32_t)(n * q / parts),
+                           (uint32_t)(n * (q + 1) / parts), q == 0 ? 1 : 0);
     else
       hipLaunchKernelGGL((radix_downsweep<0, false, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
                          shift, counts, totals, tiles, S, nullptr);

@@ -90,6 +90,23 @@ def test_schedule_matches_host(gpu_device, P, M, K):
     np.testing.assert_array_equal(need[rated], deps_h.numpy()[rated])
 
 
+@pytest.mark.parametrize("P,M,K", [(20, 3000, 3), (70_000, 400_000, 3), (17_000_000, 300_000, 5)])
+def test_schedule_link_parts_match_host(gpu_device, P, M, K, monkeypatch):
+    """The link pass split into slot-range parts (ANA_LINK_PARTS; automatic above
+    256 MB of links) writes the same links and boundary pairs as one pass."""
+    monkeypatch.setenv("ANA_LINK_PARTS", "3")
+    rec = make_stream(StreamSpec(team_size=K, seed=P + 5, p_afk=0.05, p_hot=0.2, p_uneven=0.05), M, P, K=K)
+    br = R.BatchRater()
+    link_h, deps_h = (t.clone() for t in br.schedule(rec, K, P))
+    link_d, deps_d = br.schedule(rec.to(gpu_device), K, P)
+    slots, first = _stateful_slots(rec.numpy(), K, P)
+    link_d = link_d.cpu().numpy()
+    np.testing.assert_array_equal(link_d[slots], link_h.numpy()[slots])
+    need = (first & ((link_d & R.Schedule.HAS_PRED) != 0)).sum(1)
+    rated = slots.any(1)
+    np.testing.assert_array_equal(need[rated], deps_h.numpy()[rated])
+
+
 @pytest.mark.parametrize("name", sorted(SPECS))
 def test_device_matches_object_rater(gpu_device, name):
     rspec, sspec, K = SPECS[name]
