@@ -36,8 +36,11 @@ def _ext_suffix() -> str:
     return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 
-def target_path() -> Path:
-    return PKG / ("_C" + _ext_suffix())
+def target_path(diag: bool = False) -> Path:
+    """The in-tree library: ``_C`` (production) or ``_C_diag`` (``--diag``: also
+    the telemetry kernel's diagnostic / tuning variants, ANA_TELE_DEBUG and
+    ANA_TELE_SPAN; load it with ANA_NATIVE_LIB)."""
+    return PKG / (("_C_diag" if diag else "_C") + _ext_suffix())
 
 
 def _torch_paths():
@@ -61,8 +64,10 @@ def _compile(cmd, src: Path, obj: Path, force: bool) -> str:
     return "built %s" % src.name
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
-    out = target_path()
+def build(force: bool = False, jobs: int = 4, verbose: bool = False, diag: bool = False) -> Path:
+    out = target_path(diag)
+    objdir = BUILD / "diag" if diag else BUILD
+    dflags = ["-DANA_DIAG_BUILD=1"] if diag else []
     sources = [CSRC / n for n in HIP_SOURCES + CPP_SOURCES if (CSRC / n).exists()]
     if not force and out.exists() and out.stat().st_mtime >= max(_deps_mtime(s) for s in sources):
         # the in-tree library is newer than every source: nothing to do (a GPU box
@@ -78,14 +83,14 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
         src = CSRC / name
         if not src.exists():
             continue
-        obj = BUILD / (name + ".o")
+        obj = objdir / (name + ".o")
         cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
-               "-I" + str(CSRC)] + HIP_FLAGS.get(name, []) + ["-c", str(src), "-o", str(obj)]
+               "-I" + str(CSRC)] + HIP_FLAGS.get(name, []) + dflags + ["-c", str(src), "-o", str(obj)]
         tasks.append((cmd, src, obj))
         objs.append(obj)
     for name in CPP_SOURCES:
         src = CSRC / name
-        obj = BUILD / (name + ".o")
+        obj = objdir / (name + ".o")
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-pthread", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                "-D_GLIBCXX_USE_CXX11_ABI=1", "-I" + str(CSRC), "-I" + ROCM + "/include",
@@ -96,7 +101,6 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> Path:
         for msg in ex.map(lambda t: _compile(t[0], t[1], t[2], force), tasks):
             if verbose:
                 print(msg, flush=True)
-    out = target_path()
     newest = max(o.stat().st_mtime for o in objs)
     if force or not out.exists() or out.stat().st_mtime < newest:
         cmd = ["g++", "-shared", "-o", str(out)] + [str(o) for o in objs]
@@ -122,8 +126,10 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=4)
+    ap.add_argument("--diag", action="store_true",
+                    help="build _C_diag with the diagnostic kernel variants (scripts/tune_tele.py)")
     args = ap.parse_args(argv)
-    path = build(force=args.force, jobs=args.jobs, verbose=True)
+    path = build(force=args.force, jobs=args.jobs, verbose=True, diag=args.diag)
     print(path)
     return 0
 

@@ -406,8 +406,13 @@ int64_t telemetry(Tensor evoff, Tensor events, int64_t K, Tensor stats, Tensor b
   if (dev.is_cuda()) {
     check(bad, "bad", torch::kInt32, dev);
     TORCH_CHECK(bad.numel() >= 1, "bad must have an entry");
-    check_hip(ana::launch_telemetry((int)K, tp, reinterpret_cast<uint32_t*>(bad.data_ptr<int32_t>()),
-                                    stream_of(events)), "telemetry");
+    const int rc = ana::launch_telemetry((int)K, tp, reinterpret_cast<uint32_t*>(bad.data_ptr<int32_t>()),
+                                         stream_of(events));
+    TORCH_CHECK(rc != (int)hipErrorNotSupported,
+                "ANA_TELE_DEBUG / ANA_TELE_SPAN select diagnostic telemetry variants, which only the "
+                "diagnostic library has: python -m analyzer_amd.build_ext --diag, then "
+                "ANA_NATIVE_LIB=<path of analyzer_amd/_C_diag*.so>");
+    check_hip(rc, "telemetry");
     return -1;
   }
   return ana::host_telemetry((int)K, tp);

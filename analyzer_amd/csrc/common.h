@@ -19,6 +19,12 @@
 
 #include <stdint.h>
 
+// 1 in the diagnostic library (python -m analyzer_amd.build_ext --diag): kernel
+// variants that exist only to take a kernel apart (telemetry.hip)
+#ifndef ANA_DIAG_BUILD
+#define ANA_DIAG_BUILD 0
+#endif
+
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #define ANA_HD __host__ __device__ __forceinline__

@@ -92,12 +92,18 @@ static void launch_tele(const TelemetryParams& tp, uint32_t* bad, hipStream_t s)
                      tp, bad);
 }
 
+// The production library instantiates the two implementations only; the
+// diagnostic variants (no adds / no MFMA / decode only) and the tuning spans
+// are in the diagnostic build (python -m analyzer_amd.build_ext --diag).
 template <int K>
 static void launch_tele_k(const TelemetryParams& tp, uint32_t* bad, hipStream_t s, int impl, int dbg,
                           int span) {
+#if ANA_DIAG_BUILD
   if (dbg == 1) return launch_tele<K, 1, kTeleTile>(tp, bad, s);
   if (dbg == 2) return launch_tele<K, 2, kTeleTile>(tp, bad, s);
+#endif
   if (impl == 0) return launch_tele<K, 0, kTeleTile>(tp, bad, s);
+#if ANA_DIAG_BUILD
   const int d = dbg == 6 ? 6 : dbg == 7 ? 7 : 3;
 #define ANA_TELE_SPAN(sp)                                                                     \
   if (span == sp) {                                                                           \
@@ -109,6 +115,10 @@ static void launch_tele_k(const TelemetryParams& tp, uint32_t* bad, hipStream_t 
 #undef ANA_TELE_SPAN
   if (d == 6) return launch_tele<K, 6, kTeleMaxSpan>(tp, bad, s);
   if (d == 7) return launch_tele<K, 7, kTeleMaxSpan>(tp, bad, s);
+#else
+  (void)dbg;
+  (void)span;
+#endif
   return launch_tele<K, 3, kTeleMaxSpan>(tp, bad, s);
 }
 
@@ -122,6 +132,11 @@ int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_
   const int dbg = dbg_env ? atoi(dbg_env) : 0;
   const int span = span_env ? atoi(span_env) : kTeleMaxSpan;
   const int impl = tele_impl();
+#if !ANA_DIAG_BUILD
+  // diagnostic / tuning variants are not in this library: refuse instead of
+  // silently timing the production kernel under their name
+  if (dbg != 0 || span != kTeleMaxSpan) return (int)hipErrorNotSupported;
+#endif
   switch (K) {
     case 1: launch_tele_k<1>(tp, bad, s, impl, dbg, span); break;
     case 2: launch_tele_k<2>(tp, bad, s, impl, dbg, span); break;

@@ -25,6 +25,18 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
     args = ap.parse_args()
+    # dbg<D> and non-default spans live in the diagnostic library only
+    # (python -m analyzer_amd.build_ext --diag -> analyzer_amd/_C_diag*.so)
+    diag = any(v.startswith("dbg") or (v.partition("s")[2] not in ("", "63")) for v in args.variants.split(","))
+    if diag and not os.environ.get("ANA_NATIVE_LIB"):
+        import glob
+
+        libs = glob.glob(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                      "analyzer_amd", "_C_diag*.so"))
+        if not libs:
+            sys.exit("variants %s need the diagnostic library: python -m analyzer_amd.build_ext --diag"
+                     % args.variants)
+        os.environ["ANA_NATIVE_LIB"] = libs[0]
     dev = torch.device("cuda:0")
     M, K = args.matches, args.team_size
     rec = make_stream(StreamSpec(team_size=K, seed=5), M, args.players, device=dev)

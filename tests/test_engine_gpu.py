@@ -1,4 +1,6 @@
 """MI355X kernels vs the C++ host mirror / object rater (numerics tests, ``-m gpu``)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -325,6 +327,25 @@ def test_graph_rater_matches_eager(gpu_device):
         for f in ("quality", "s_mu", "s_sig", "delta", "m_mu", "m_sig"):
             assert torch.equal(getattr(got, f).nan_to_num(-7), getattr(exp, f).nan_to_num(-7)), f
         assert torch.equal(roster.state[:, 0::2].nan_to_num(-7), ref.state[:, 0::2].nan_to_num(-7))
+
+
+def test_telemetry_diagnostic_variants_need_the_diag_library(gpu_device, monkeypatch):
+    """ANA_TELE_DEBUG / non-default ANA_TELE_SPAN name kernel variants that only the
+    diagnostic build (build_ext --diag) contains: the production library refuses them
+    instead of timing its default kernel under their name."""
+    from analyzer_amd.ops.telemetry import TelemetrySpec, aggregate, make_telemetry
+
+    if os.environ.get("ANA_NATIVE_LIB"):
+        pytest.skip("another library is loaded")
+    rec = make_stream(StreamSpec(team_size=3, seed=3), 200, 100, K=3, device=gpu_device)
+    tel = make_telemetry(TelemetrySpec(seed=1, min_events=5, max_events=9), rec, 3)
+    ref = aggregate(tel, 3)
+    for var, val in (("ANA_TELE_DEBUG", "7"), ("ANA_TELE_SPAN", "32")):
+        monkeypatch.setenv(var, val)
+        with pytest.raises(RuntimeError, match="diagnostic library"):
+            aggregate(tel, 3)
+        monkeypatch.delenv(var)
+    assert torch.equal(aggregate(tel, 3), ref)
 
 
 def test_fused_rate_telemetry_on_device(gpu_device):
