@@ -147,6 +147,7 @@ class EngineConfig:
     rate_blocks: int = 512
     prepass_at: float = 0.7
     prepass_cus: int = 0
+    prepass_exclusive: bool = False  # with prepass_cus: the executor gets the other CUs
     prepass_serial: Optional[bool] = None  # None = auto (WindowPipeline.serial_prepass)
     merge_bucket_mb: float = 16.0
     comm_dtype: str = "fp32"
@@ -165,6 +166,7 @@ class EngineConfig:
         "ANA_RATE_DIAG": "timing build of the executor: per-phase clocks in ctrl[20..39] (default 0)",
         "ANA_TELE_IMPL": "telemetry aggregation: 1 one-hot MFMA GEMM (default), 0 LDS atomics",
         "ANA_TELE_FUSED_TAIL": "fused telemetry only after the executor's chunks are drained",
+        "ANA_TELE_ROLE": "fused telemetry: one wave in N aggregates from the start (default 2; 0 = idle waves take tiles)",
         "ANA_SCHED_SMALL": "micro-batch schedule: hash lists (default) or bitonic sort",
         "ANA_SORT_RB / ANA_SORT_NT": "radix-sort tile rows / non-temporal loads (tuning)",
     }
@@ -175,6 +177,7 @@ class EngineConfig:
             rate_blocks=int(_env(env, "ANA_RATE_BLOCKS") or 512),
             prepass_at=float(_env(env, "ANA_PREPASS_AT") or 0.7) if env.get("ANA_PREPASS_AT") != "0" else 0.0,
             prepass_cus=int(_env(env, "ANA_PREPASS_CUS") or 0),
+            prepass_exclusive=env.get("ANA_PREPASS_EXCLUSIVE", "0") not in ("", "0", "false"),
             prepass_serial=_tristate(env.get("ANA_PREPASS_SERIAL")),
             merge_bucket_mb=float(_env(env, "ANA_MERGE_BUCKET_MB") or 16),
             comm_dtype=_env(env, "COMM_DTYPE") or "fp32",

@@ -245,6 +245,9 @@ static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& 
   tp.stats = stats.data_ptr<float>();
   if (dev.is_cuda()) tp.impl = ana::tele_impl();
   if (const char* e = std::getenv("ANA_TELE_FUSED_TAIL")) tp.fused_tail = std::atoi(e);  // A/B knob
+  // fused: every 2nd wave aggregates first (14.4 -> 11.4 ms per config 4 step, profiles/r2/tele_role_split.log)
+  tp.role_stride = 2;
+  if (const char* e = std::getenv("ANA_TELE_ROLE")) tp.role_stride = std::atoi(e);
   return tp;
 }
 
@@ -587,7 +590,7 @@ void unpack_rows(Tensor buf, Tensor state) {
 // bandwidth-bound kernels trickle alongside the latency-bound executor instead
 // of bursting.  Returns the raw handle for torch.cuda.ExternalStream; the
 // stream lives until process exit (one per pipeline).
-int64_t cu_masked_stream(int64_t device, int64_t num_cus) {
+int64_t cu_masked_stream(int64_t device, int64_t num_cus, bool invert) {
   hipDeviceProp_t prop;
   check_hip((int)hipGetDeviceProperties(&prop, (int)device), "hipGetDeviceProperties");
   const int total = prop.multiProcessorCount;
@@ -596,6 +599,10 @@ int64_t cu_masked_stream(int64_t device, int64_t num_cus) {
   for (int64_t i = 0; i < num_cus; ++i) {
     const int cu = (int)(i * total / num_cus);
     mask[cu / 32] |= 1u << (cu % 32);
+  }
+  if (invert) {  // every CU but those N (the complement of the same call without invert)
+    for (int c = 0; c < total; ++c) mask[c / 32] ^= 1u << (c % 32);
+    TORCH_CHECK(num_cus < total, "an inverted mask needs num_cus < ", total);
   }
   int prev = 0;
   check_hip((int)hipGetDevice(&prev), "hipGetDevice");
@@ -707,7 +714,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("acquire", &reader_acquire,
            "next filled window as (slot, base, tensor view of pinned memory) or None at EOF")
       .def("release", &ana::RecordReader::release, "return the oldest acquired slot");
-  m.def("cu_masked_stream", &cu_masked_stream, "HIP stream limited to N CUs (spread over XCDs)");
+  m.def("cu_masked_stream", &cu_masked_stream, "HIP stream limited to N CUs (spread over XCDs), or to the others",
+        py::arg("device"), py::arg("num_cus"), py::arg("invert") = false);
   m.def("progress_signal", &progress_signal, "8-B signal-memory word for the executor's tail signal");
   m.def("stream_wait_value64", &stream_wait_value64, "hipStreamWaitValue64(stream, ptr, >= value)");
   m.def("can_wait_value", &can_wait_value, "hipDeviceAttributeCanUseStreamWaitValue");

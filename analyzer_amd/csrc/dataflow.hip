@@ -212,8 +212,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   bool exhausted = false, tk_pending = false;
   unsigned tk = 0;                 // ticket returned to lane 0
   uint32_t spins = 0, iter = 0;
-  // K8 fused mode: telemetry tiles fill the time a wave would spend waiting
-  const int64_t tele_tiles = TELE && tp.evoff ? (tp.num_matches + kTeleTile - 1) / kTeleTile : 0;
+  // K8 fused mode.  Default: telemetry tiles fill the time a wave would spend
+  // waiting.  Role split (tp.role_stride): aggregation waves stream 63-match
+  // spans from the start -- spread one per (block group, SIMD) so no SIMD and no
+  // XCD gets them all -- while the rating waves keep their dependency chains
+  // moving; an aggregation wave joins the rating when the events run out.
+  const bool tele_role = TELE && tp.role_stride > 0 && tp.impl != 0;
+  const int tele_span = tele_role ? kTeleMaxSpan : kTeleTile;
+  const int64_t tele_tiles = TELE && tp.evoff ? (tp.num_matches + tele_span - 1) / tele_span : 0;
   bool tele_done = tele_tiles == 0;
   auto tele_claim = [&]() -> int64_t {
     unsigned t = 0;
@@ -222,6 +228,26 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     t = __builtin_amdgcn_readfirstlane(t);
     return (int64_t)t < tele_tiles ? (int64_t)t : -1;
   };
+  auto tele_run = [&](int64_t t) {
+    if constexpr (TELE) {
+      if (tele_role) telemetry_tile_mfma<K, 0, kTeleMaxSpan>(tp, t, lane, tele[wv], &ctrl[13]);
+      else if (tp.impl) telemetry_tile_mfma<K>(tp, t, lane, tele[wv], &ctrl[13]);
+      else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+    }
+  };
+  if constexpr (TELE) {
+    if (tele_role) {
+      const int b = blockIdx.x, per = tp.role_stride >= 4 ? tp.role_stride / 4 : 1;
+      const bool agg = tp.role_stride >= 4   ? (wv == ((b >> 3) & 3) && ((b >> 5) % per) == 0)
+                       : tp.role_stride == 2 ? ((wv & 1) == ((b >> 3) & 1))
+                                             : true;  // 1: every wave aggregates first
+      while (agg && !tele_done) {
+        const int64_t t = tele_claim();
+        if (t < 0) tele_done = true;
+        else tele_run(t);
+      }
+    }
+  }
   const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : prm.idle_spins < 0 ? 0u : 8u;
   const int cl = prm.chunk_len;  // matches per ticket (<= kChunk lanes)
 
@@ -754,8 +780,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         while (!tele_done) {  // leftover telemetry tiles
           const int64_t t = tele_claim();
           if (t < 0) tele_done = true;
-          else if (tp.impl) telemetry_tile_mfma<K>(tp, t, lane, tele[wv], &ctrl[13]);
-          else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+          else tele_run(t);
         }
       }
       break;
@@ -786,11 +811,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       if constexpr (TELE) {
         // nothing ready for a while: aggregate a telemetry tile instead of sleeping
-        if (!tele_done && (!tp.fused_tail || !held)) {
+        if (!tele_done && ((!tp.fused_tail && !tele_role) || !held)) {
           const int64_t t = tele_claim();
           if (t >= 0) {
-            if (tp.impl) telemetry_tile_mfma<K>(tp, t, lane, tele[wv], &ctrl[13]);
-            else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
+            tele_run(t);
             spins = 0;
             continue;
           }

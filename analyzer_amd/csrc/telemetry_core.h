@@ -74,6 +74,10 @@ struct TelemetryParams {
   int32_t impl = 1;       // device tile routine: 1 one-hot MFMA, 0 LDS float atomics
   int32_t fused_tail = 0; // fused executor: 0 = any idle wave aggregates, 1 = only waves
                           // holding no chunks (the window's tail; measured slower: 15.9 vs 14.6 ms)
+  int32_t role_stride = 2; // fused executor, MFMA impl: > 0 = one wave in role_stride is an
+                           // aggregation wave (63-match spans) until the events are done, then
+                           // joins the rating; the rating waves never hold a tile while they
+                           // hold matches.  0 = idle rating waves take 16-match tiles.
 };
 
 struct GenEventParams {

@@ -76,6 +76,14 @@ class WindowPipeline:
         self._signal = 0
         self._seq = 0
         self.side = self._side_stream() if self.cuda else None
+        # ANA_PREPASS_EXCLUSIVE (with ANA_PREPASS_CUS=n): the rating launches go to a
+        # stream masked to the other CUs, so the two never share a CU
+        self.exec_stream = None
+        if self.cuda and not self.serial and self.ecfg.prepass_cus > 0 and self.ecfg.prepass_exclusive:
+            from ..ops.native import native
+
+            handle = native().cu_masked_stream(self.device.index or 0, self.ecfg.prepass_cus, True)
+            self.exec_stream = torch.cuda.ExternalStream(handle, device=self.device)
         if self.cuda and self.tail > 0:
             from ..ops.native import native
 
@@ -150,8 +158,15 @@ class WindowPipeline:
             at = int(self.tail * ((M + cl - 1) // cl))
             progress = (self._signal, self._seq, at)
         with trace_range("rate", window=self.windows_rated, matches=int(prep.rec.shape[0])):
-            res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
-                                  schedule=prep.schedule, telemetry=telemetry, progress=progress)
+            if self.exec_stream is not None:
+                self.exec_stream.wait_stream(main)
+                with torch.cuda.stream(self.exec_stream):
+                    res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
+                                          schedule=prep.schedule, telemetry=telemetry, progress=progress)
+                main.wait_stream(self.exec_stream)
+            else:
+                res = self.rater.rate(self.roster, prep.rec, self.K, out=out, check=check,
+                                      schedule=prep.schedule, telemetry=telemetry, progress=progress)
         if self.merger is not None:
             # causal re-sweeps (parallel/sweep.py): re-rate from the prefix of the
             # earlier ranks' messages, reusing the links (only the counters reset)

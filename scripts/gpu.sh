@@ -18,6 +18,8 @@
 #   hop        quick executor A/B (serial chain + 10M window, local hand-off, timing build)
 #   merge      sweep-merge message/decode kernels at P = 1M, 10M on one GPU
 #   exactdp    exact DP (C2) rehearsal, 2/4 gloo ranks on one GPU, rounds + time per window
+#   role       config 4 fused executor with dedicated aggregation waves (ANA_TELE_ROLE sweep)
+#   excl       prepass on its own CUs beside the executor on the rest (ANA_PREPASS_EXCLUSIVE sweep)
 #   tele       config 4 telemetry placement (separate / fused / CU-masked overlap)
 #   tail       prepass start point sweep for config 2 (ANA_PREPASS_AT, serial)
 #   ab         in-call A/B of executor builds (AB_LIBS, scripts/ab_build.sh), interleaved rounds
@@ -111,6 +113,26 @@ for task in "$@"; do
     exactdp)  # exact DP rehearsal: 2 and 4 gloo ranks on this one GPU, 1M-match window
       run exactdp/r2 600 $PY scripts/exact_dp_rehearsal.py --ranks 2
       run exactdp/r4 600 $PY scripts/exact_dp_rehearsal.py --ranks 4
+      ;;
+    role)  # config 4 fused executor: dedicated aggregation waves (ANA_TELE_ROLE) vs idle-wave tiles vs separate
+      run role/test 300 $PY -u -m pytest tests/test_engine_gpu.py -k fused_rate_telemetry -x -v --timeout 120 --timeout-method thread
+      run role/separate 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode separate
+      for n in ${ROLES:-0 2 4 8 16}; do
+        ANA_TELE_ROLE=$n run role/fused_role$n 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode fused
+      done
+      ;;
+    excl)  # prepass of window i+1 on n CUs of its own while the executor rates window i on the others
+      run excl/serial 400 $PY bench.py --steps 20 --warmup 3
+      for n in ${EXCL_CUS:-32 48 64}; do
+        ANA_PREPASS_SERIAL=0 ANA_PREPASS_AT=0 ANA_PREPASS_CUS=$n ANA_PREPASS_EXCLUSIVE=1 ANA_RATE_BLOCKS=$((2 * (256 - n))) \
+          run excl/cus$n 400 $PY bench.py --steps 20 --warmup 3 --check
+      done
+      run excl/c3_default 400 $PY bench.py --config 3 --steps 10 --warmup 2
+      for n in ${EXCL_CUS3:-48 64}; do
+        ANA_PREPASS_AT=0 ANA_PREPASS_CUS=$n ANA_PREPASS_EXCLUSIVE=1 ANA_RATE_BLOCKS=$((2 * (256 - n))) \
+          run excl/c3_cus$n 400 $PY bench.py --config 3 --steps 10 --warmup 2 --check
+      done
+      grep -h -o '"ms_per_step": [0-9.]*' gpurun_out/excl/*.log
       ;;
     tele)  # config 4 telemetry placement: separate, fused, overlap on all / 16 / 32 / 64 CUs
       run tele/separate 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode separate

@@ -348,9 +348,14 @@ def test_telemetry_diagnostic_variants_need_the_diag_library(gpu_device, monkeyp
     assert torch.equal(aggregate(tel, 3), ref)
 
 
-def test_fused_rate_telemetry_on_device(gpu_device):
+@pytest.mark.parametrize("role", [0, 2, 4, 8])
+def test_fused_rate_telemetry_on_device(gpu_device, monkeypatch, role):
+    """Fused aggregation, idle-wave tiles (role 0) and dedicated aggregation
+    waves (ANA_TELE_ROLE): same stats as the oracle, same ratings as without."""
     from analyzer_amd.ops.telemetry import (TelemetrySpec, aggregate_reference, allocate_stats,
                                             make_telemetry)
+
+    monkeypatch.setenv("ANA_TELE_ROLE", str(role))
 
     K, P, M = 3, 20000, 400000
     roster = make_roster(RosterSpec(num_players=P, seed=5), device=gpu_device)
