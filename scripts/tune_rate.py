@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--tight", default="-1", help="ANA_RATE_TIGHT values (2K lanes per match; -1 auto)")
     ap.add_argument("--local", default="1", help="ANA_RATE_LOCAL values (LDS local hand-off)")
     ap.add_argument("--diag", default="0", help="ANA_RATE_DIAG values (timing build)")
+    ap.add_argument("--split", default="0", help="ANA_RATE_SPLIT values (0 default executor, 1/2 split-role 16/8 chunks)")
     ap.add_argument("--skew", type=int, default=1)
     ap.add_argument("--rated", type=float, default=1.0,
                     help="fraction of players with stored ratings (1.0 = steady state, no seeding)")
@@ -51,16 +52,17 @@ def main():
                           + torch.arange(2 * K, dtype=torch.int32, device=dev)[None, :])
     out = RateResult.allocate(M, K, dev)
     results = {}
-    combos = [(int(b), int(i), int(t), int(lo), int(d)) for b in args.blocks.split(",")
+    combos = [(int(b), int(i), int(t), int(lo), int(d), int(sp)) for b in args.blocks.split(",")
               for i in args.idle.split(",") for t in args.tight.split(",")
-              for lo in args.local.split(",") for d in args.diag.split(",")]
+              for lo in args.local.split(",") for d in args.diag.split(",") for sp in args.split.split(",")]
     for rnd in range(args.rounds):
-        for b, idle, tg, loc, dg in combos:
+        for b, idle, tg, loc, dg, sp in combos:
+            os.environ["ANA_RATE_SPLIT"] = str(sp)
             os.environ["ANA_RATE_TIGHT"] = str(tg)
             os.environ["ANA_RATE_IDLE"] = str(idle)
             os.environ["ANA_RATE_LOCAL"] = str(loc)
             os.environ["ANA_RATE_DIAG"] = str(dg)
-            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg)
+            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg) + ("/split%d" % sp if sp else "")
             roster = make_roster(RosterSpec(num_players=P, seed=1, p_rated=args.rated,
                                             p_mode_rated=args.rated), device=dev)
             br = BatchRater(blocks=b)
@@ -81,6 +83,9 @@ def main():
                     " hand-offs local %d global %d" % (rnd, key, (t1 - t0) * 1e3, (t2 - t1) * 1e3, stale,
                                                        d["wave_iterations"], M / max(d["wave_iterations"], 1),
                                                        d["local_handoffs"], d["global_handoffs"]))
+            if sp:
+                line += " | rater iterations %d (%.2f matches each)" % (
+                    d["worked_iterations"], d["groups_assigned"] / max(d["worked_iterations"], 1))
             if dg:
                 line += " | worked iterations %d (%.2f matches each): issue %.3f + wait %.3f + after %.3f us" % (
                     d["worked_iterations"], d["matches_per_worked_iteration"], d["issue_us"], d["wait_us"],

@@ -561,3 +561,24 @@ def test_exact_dp_round_check_on_device(gpu_device):
     bad[M // 2:] = bad[M // 2]  # the second half collapses into one round
     plan = RoundPlan(bad, 4)
     assert check_rounds(rec, K, plan, P) == check_rounds(rec.cpu(), K, plan, P) >= 0
+
+
+@pytest.mark.parametrize("K,skew", [(3, 1), (3, 3), (5, 1)])
+def test_split_executor_bit_identical(gpu_device, monkeypatch, K, skew):
+    """ANA_RATE_SPLIT=1 (scheduler wave + rater waves per workgroup) rates a
+    contended window exactly like the default executor: same statuses, outputs
+    and roster, bit for bit."""
+    P, M = 20000, 400000
+    rec = make_stream(StreamSpec(team_size=K, seed=41, skew=skew), M, P, K=K, device=gpu_device)
+    base = make_roster(RosterSpec(num_players=P, seed=42), device=gpu_device)
+    outs = []
+    for split in ("0", "1"):
+        monkeypatch.setenv("ANA_RATE_SPLIT", split)
+        roster = base.clone()
+        br = R.BatchRater()
+        res = br.rate(roster, rec, K)
+        torch.cuda.synchronize()
+        outs.append((roster.state[:, ::2].clone(), res.status.clone(), res.s_mu.clone(), res.m_sig.clone(),
+                     res.delta.clone(), res.quality.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a.nan_to_num(-7), b.nan_to_num(-7))
