@@ -338,12 +338,17 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
       out = ana::RateOut{b + 5 * S, reinterpret_cast<uint8_t*>(b + 5 * S + 1), b, b + S, b + 2 * S,
                          b + 3 * S, b + 4 * S, W, W, W * 4};
     }
-    check_hip(ana::launch_rate((int)K, rec.data_ptr<int32_t>(),
-                               reinterpret_cast<const uint32_t*>(link.data_ptr<int32_t>()),
-                               deps.data_ptr<int32_t>(), state.data_ptr<float>(),
-                               attrs.data_ptr<float>(), fp, out,
-                               reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm, tp,
-                               (int)blocks, stream_of(rec)), "rate");
+    const int rc = ana::launch_rate((int)K, rec.data_ptr<int32_t>(),
+                                    reinterpret_cast<const uint32_t*>(link.data_ptr<int32_t>()),
+                                    deps.data_ptr<int32_t>(), state.data_ptr<float>(),
+                                    attrs.data_ptr<float>(), fp, out,
+                                    reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm, tp,
+                                    (int)blocks, stream_of(rec));
+    TORCH_CHECK(rc != (int)hipErrorNotSupported,
+                "ANA_RATE_SPLIT selects the split-role executor, which only the diagnostic library "
+                "has: python -m analyzer_amd.build_ext --diag, then ANA_NATIVE_LIB=<path of "
+                "analyzer_amd/_C_diag*.so>");
+    check_hip(rc, "rate");
     if (!packed) {
       using torch::indexing::Slice;
       s_mu.copy_(staged.index({Slice(), Slice(0, S)}));

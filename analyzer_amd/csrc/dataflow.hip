@@ -837,8 +837,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   }
 }
 
+#if ANA_DIAG_BUILD
 // ---------------------------------------------------------------------------
-// Split-role executor (ANA_RATE_SPLIT=1, windows only).  Each workgroup has one
+// Split-role executor (ANA_RATE_SPLIT=1/2, windows only; diagnostic library).
+// Bit-identical to rate_dataflow_kernel and not faster: 10M 3v3 window 6.43 ms
+// (8 held chunks) vs 6.52, 7.56 ms with 16; serial hop 3.1 / 5.5 us vs 2.3 --
+// the scheduler's poll round trip replaces the rater's, and a local hand-off
+// now goes rater -> LDS -> scheduler -> queue -> rater
+// (profiles/r2/split_executor_experiment.log).  Each workgroup has one
 // SCHEDULER wave and three RATER waves.  The scheduler holds kSplitHeld chunks
 // (records in LDS), polls their completion counters in a loop of its own and
 // pushes every ready match into an LDS ready queue; the raters pop up to NG
@@ -1369,6 +1375,8 @@ rate_split_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ 
   }
 }
 
+#endif  // ANA_DIAG_BUILD
+
 __global__ void __launch_bounds__(64) zero_ctrl_kernel(uint32_t* __restrict__ p, int n) {
   if ((int)threadIdx.x < n) p[threadIdx.x] = 0u;
 }
@@ -1405,6 +1413,9 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // config 3 step 21.5 vs 21.9 ms, profiles/r2/tight_groups.log) -> auto = tight
   // for 5v5 only.
   const bool tight = prm.tight_groups > 0 || (prm.tight_groups < 0 && K == 5);
+#if !ANA_DIAG_BUILD
+  if (prm.split > 0) return (int)hipErrorNotSupported;  // diagnostic library only
+#else
   if (prm.split > 0 && !tp.evoff && !prm.diag && prm.chunk_len == kChunk) {
     // split-role executor: one scheduler wave + three rater waves per workgroup
 #define ANA_SPLIT_LAUNCH(k, g)                                                                          \
@@ -1427,6 +1438,7 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
 #undef ANA_SPLIT_LAUNCH
     return (int)hipGetLastError();
   }
+#endif
 #define ANA_RATE_LAUNCH_D(k, g, tele, diag)                                                        \
   hipLaunchKernelGGL((rate_dataflow_kernel<k, g, tele, diag>), dim3((unsigned)blocks), dim3(256), 0, s, \
                      rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, tp)

@@ -123,6 +123,7 @@ for task in "$@"; do
       done
       ;;
     split)  # split-role executor (ANA_RATE_SPLIT=1) vs the default: bit-identity tests, then configs 2 / 3 / skew 2
+      export ANA_NATIVE_LIB=$(ls "$ROOT"/analyzer_amd/_C_diag*.so)  # the split executor is diagnostic-only
       run split/test 300 $PY -u -m pytest tests/test_engine_gpu.py -k split_executor -x -v --timeout 120 --timeout-method thread
       for v in ${SPLITS:-0 1}; do
         ANA_RATE_SPLIT=$v run split/c2_split$v 300 $PY bench.py --steps 20 --warmup 3 --check
@@ -132,13 +133,16 @@ for task in "$@"; do
         ANA_RATE_SPLIT=$v run split/skew2_split$v 400 $PY bench.py --skew 2 --steps 3 --warmup 1 --check
       done
       grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/split/*.log
+      unset ANA_NATIVE_LIB
       ;;
     splithop)  # split-role executor: hop latency and 10M window, 16 / 8 held chunks per scheduler
+      export ANA_NATIVE_LIB=$(ls "$ROOT"/analyzer_amd/_C_diag*.so)
       run splithop/test 300 $PY -u -m pytest tests/test_engine_gpu.py -k split_executor -x -v --timeout 120 --timeout-method thread
       run splithop/random 300 $PY scripts/tune_rate.py --pattern random --rounds 2 --split 0,1,2
       run splithop/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 --rounds 2 \
           --blocks 8 --split 0,1,2
       grep -h "^round 1" gpurun_out/splithop/*.log | cut -c1-260
+      unset ANA_NATIVE_LIB
       ;;
     excl)  # prepass of window i+1 on n CUs of its own while the executor rates window i on the others
       run excl/serial 400 $PY bench.py --steps 20 --warmup 3

@@ -563,17 +563,35 @@ def test_exact_dp_round_check_on_device(gpu_device):
     assert check_rounds(rec, K, plan, P) == check_rounds(rec.cpu(), K, plan, P) >= 0
 
 
+def _diag_library_loaded() -> bool:
+    return "_C_diag" in os.path.basename(os.environ.get("ANA_NATIVE_LIB", ""))
+
+
+def test_split_executor_needs_the_diag_library(gpu_device, monkeypatch):
+    if os.environ.get("ANA_NATIVE_LIB"):
+        pytest.skip("another library is loaded")
+    rec = make_stream(StreamSpec(team_size=3, seed=3), 4000, 500, K=3, device=gpu_device)
+    roster = make_roster(RosterSpec(num_players=500, seed=4), device=gpu_device)
+    monkeypatch.setenv("ANA_RATE_SPLIT", "1")
+    with pytest.raises(RuntimeError, match="diagnostic library"):
+        R.BatchRater().rate(roster, rec, 3)
+
+
+@pytest.mark.parametrize("split", ["1", "2"])
 @pytest.mark.parametrize("K,skew", [(3, 1), (3, 3), (5, 1)])
-def test_split_executor_bit_identical(gpu_device, monkeypatch, K, skew):
-    """ANA_RATE_SPLIT=1 (scheduler wave + rater waves per workgroup) rates a
-    contended window exactly like the default executor: same statuses, outputs
-    and roster, bit for bit."""
+def test_split_executor_bit_identical(gpu_device, monkeypatch, K, skew, split):
+    """ANA_RATE_SPLIT=1/2 (diagnostic library: scheduler wave + rater waves per
+    workgroup, 16 / 8 held chunks) rates a contended window exactly like the
+    default executor: same statuses, outputs and roster, bit for bit.
+    Run with ANA_NATIVE_LIB=analyzer_amd/_C_diag*.so (scripts/gpu.sh split)."""
+    if not _diag_library_loaded():
+        pytest.skip("needs ANA_NATIVE_LIB=<analyzer_amd/_C_diag*.so>")
     P, M = 20000, 400000
     rec = make_stream(StreamSpec(team_size=K, seed=41, skew=skew), M, P, K=K, device=gpu_device)
     base = make_roster(RosterSpec(num_players=P, seed=42), device=gpu_device)
     outs = []
-    for split in ("0", "1"):
-        monkeypatch.setenv("ANA_RATE_SPLIT", split)
+    for sp in ("0", split):
+        monkeypatch.setenv("ANA_RATE_SPLIT", sp)
         roster = base.clone()
         br = R.BatchRater()
         res = br.rate(roster, rec, K)
