@@ -72,8 +72,10 @@ def parse(argv=None):
                     help="config 4: overlap = the MFMA aggregation kernel co-runs with the rating "
                          "launch on its own stream; fused = executor waves aggregate in their idle "
                          "time; separate = aggregation after the rating on the same stream")
-    ap.add_argument("--comm-dtype", default=EngineConfig.from_env().comm_dtype,
-                    choices=["fp32", "fp16", "bf16"], help="sweep-merge message precision (N > 1)")
+    ap.add_argument("--comm-dtype", default=None, choices=["fp32", "fp16", "bf16"],
+                    help="sweep-merge message precision (N > 1; default COMM_DTYPE, else fp16 for one "
+                         "sweep -- at 8 x 10M the compressed messages leave the sweep error unchanged, "
+                         "profiles/r2/slice_size_accuracy.log -- and fp32 for causal re-sweeps)")
     ap.add_argument("--sweeps", type=int, default=EngineConfig.from_env().sweeps,
                     help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
                          "N = exact sequential semantics (parallel/sweep.py)")
@@ -89,9 +91,9 @@ def parse(argv=None):
             args.players = 10_000_000
         if args.matches_per_gpu == 10_000_000:
             args.matches_per_gpu = 16_000_000
-        if "COMM_DTYPE" not in os.environ and "--comm-dtype" not in (argv or sys.argv):
-            args.comm_dtype = "fp16"
         args.ring = min(args.ring, 2)
+    if args.comm_dtype is None:
+        args.comm_dtype = os.environ.get("COMM_DTYPE") or ("fp16" if args.sweeps <= 1 else "fp32")
     return args
 
 

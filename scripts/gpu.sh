@@ -19,6 +19,7 @@
 #   merge      sweep-merge message/decode kernels at P = 1M, 10M on one GPU
 #   exactdp    exact DP (C2) rehearsal, 2/4 gloo ranks on one GPU, rounds + time per window
 #   role       config 4 fused executor with dedicated aggregation waves (ANA_TELE_ROLE sweep)
+#   slices     sweep-DP accuracy and 1-GPU step time vs slice size (fixed 80M-match history)
 #   split      split-role executor (scheduler + rater waves) vs the default, tests + configs 2/3/skew
 #   excl       prepass on its own CUs beside the executor on the rest (ANA_PREPASS_EXCLUSIVE sweep)
 #   tele       config 4 telemetry placement (separate / fused / CU-masked overlap)
@@ -121,6 +122,18 @@ for task in "$@"; do
       for n in ${ROLES:-0 2 4 8 16}; do
         ANA_TELE_ROLE=$n run role/fused_role$n 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode fused
       done
+      ;;
+    slices)  # sweep-DP accuracy vs slice size at a fixed 80M-match history (8 ranks, 1M players) + 1-GPU window time
+      for w in 1 2 4 8; do
+        mpr=$((10000000 / w))
+        run slices/acc_w$w 600 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 8 --players 1e6 \
+            --matches-per-rank $mpr --windows $w --warm-windows 1 --sweeps 1,2
+        run slices/bench_w$w 300 $PY bench.py --matches-per-gpu $mpr --steps $((20 * w)) --warmup 3
+      done
+      run slices/acc_fp16 600 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 8 --players 1e6 \
+          --matches-per-rank 10000000 --windows 1 --warm-windows 1 --sweeps 1 --comm-dtype fp16
+      run slices/acc_bf16 600 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 8 --players 1e6 \
+          --matches-per-rank 10000000 --windows 1 --warm-windows 1 --sweeps 1 --comm-dtype bf16
       ;;
     split)  # split-role executor (ANA_RATE_SPLIT=1) vs the default: bit-identity tests, then configs 2 / 3 / skew 2
       export ANA_NATIVE_LIB=$(ls "$ROOT"/analyzer_amd/_C_diag*.so)  # the split executor is diagnostic-only
