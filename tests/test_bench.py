@@ -1,0 +1,44 @@
+"""bench.py argument contract (CPU): BASELINE config defaults, the merge precision
+default and the rank-count check that runs before any GPU call."""
+import os
+import sys
+
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import bench  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _clean_env(monkeypatch):
+    for var in ("COMM_DTYPE", "SWEEPS", "WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(var, raising=False)
+
+
+def test_config_defaults():
+    a = bench.parse([])
+    assert (a.config, a.team_size, a.matches_per_gpu, a.players) == (2, 3, 10_000_000, 1_000_000)
+    a = bench.parse(["--config", "3"])
+    assert (a.team_size, a.matches_per_gpu) == (5, 12_500_000)
+    a = bench.parse(["--config", "5"])
+    assert (a.players, a.matches_per_gpu, a.ring) == (10_000_000, 16_000_000, 2)
+    a = bench.parse(["--config", "2", "--matches-per-gpu", "1250000"])
+    assert a.matches_per_gpu == 1_250_000
+
+
+def test_merge_precision_default(monkeypatch):
+    # one sweep: fp16 messages (accuracy identical to fp32, profiles/r2/slice_size_accuracy.log)
+    assert bench.parse([]).comm_dtype == "fp16"
+    # causal re-sweeps aim at the exact result: fp32 unless asked otherwise
+    assert bench.parse(["--sweeps", "4"]).comm_dtype == "fp32"
+    assert bench.parse(["--sweeps", "4", "--comm-dtype", "bf16"]).comm_dtype == "bf16"
+    monkeypatch.setenv("COMM_DTYPE", "fp32")
+    assert bench.parse([]).comm_dtype == "fp32"
+
+
+def test_world_size_must_match_gpus(monkeypatch):
+    # under torchrun, --gpus must equal WORLD_SIZE; checked before the GPU is touched
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    with pytest.raises(SystemExit, match="--gpus 3 but WORLD_SIZE=2"):
+        bench.main(["--gpus", "3"])
