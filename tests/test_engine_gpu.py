@@ -486,10 +486,20 @@ def _rccl_single_rank(rank, size, P, M, K, seed):
     merger.begin(roster)
     R.BatchRater().rate(roster, rec, K)
     posterior = roster.state.clone()
+    # the bench's N > 1 default: fp16 messages (+ int32 touch counts, two collectives per
+    # bucket), with the next window's work enqueued while the all-reduces are in flight
+    r16 = roster.clone()
+    m16 = SweepMerger(P, dev, world_size=2, bucket_rows=P // 3 + 1, comm_dtype="fp16")
+    m16.start.copy_(merger.start)  # the same window start (the pre-rating roster)
+    m16._synced = True
+    m16.begin(r16)
     merger.merge(roster)
+    ran = []
+    m16.merge(r16, overlap=lambda: ran.append(torch.ones(4, device=dev).sum()))
     torch.cuda.synchronize()
+    assert len(ran) == 1
     return {"x": x.cpu(), "z": z.float().cpu(), "y": y.float().cpu(), "g": g[:1000].cpu(),
-            "posterior": posterior.cpu(), "merged": roster.state.cpu()}
+            "posterior": posterior.cpu(), "merged": roster.state.cpu(), "merged16": r16.state.cpu()}
 
 
 def test_rccl_single_rank_collectives_and_merge(gpu_device, tmp_path, monkeypatch):
@@ -511,6 +521,9 @@ def test_rccl_single_rank_collectives_and_merge(gpu_device, tmp_path, monkeypatc
     got = r["merged"].view(P, 8, 4)[..., 0::2]
     np.testing.assert_allclose(got[..., 0].numpy(), post[..., 0].numpy(), rtol=0, atol=2e-3, equal_nan=True)
     np.testing.assert_allclose(got[..., 1].numpy(), post[..., 1].numpy(), rtol=1e-4, atol=0, equal_nan=True)
+    g16 = r["merged16"].view(P, 8, 4)[..., 0::2]
+    np.testing.assert_allclose(g16[..., 0].numpy(), post[..., 0].numpy(), rtol=0, atol=1.0, equal_nan=True)
+    np.testing.assert_allclose(g16[..., 1].numpy(), post[..., 1].numpy(), rtol=2e-3, atol=0, equal_nan=True)
 
 
 def _rccl_entry(rank, port, outdir, args):
