@@ -73,9 +73,11 @@ def parse(argv=None):
                          "launch on its own stream; fused = executor waves aggregate in their idle "
                          "time; separate = aggregation after the rating on the same stream")
     ap.add_argument("--comm-dtype", default=None, choices=["fp32", "fp16", "bf16"],
-                    help="sweep-merge message precision (N > 1; default COMM_DTYPE, else fp16 for one "
+                    help="sweep-merge message precision (N > 1; default COMM_DTYPE, else bf16 for one "
                          "sweep -- at 8 x 10M the compressed messages leave the sweep error unchanged, "
-                         "profiles/r2/slice_size_accuracy.log -- and fp32 for causal re-sweeps)")
+                         "profiles/r2/slice_size_accuracy.log, and RCCL's bf16 sums keep fp32's range "
+                         "where fp16 sums of 8 ranks' mean shifts could overflow -- fp16 for config 5 "
+                         "(BASELINE: fp16 moments) and fp32 for causal re-sweeps)")
     ap.add_argument("--sweeps", type=int, default=EngineConfig.from_env().sweeps,
                     help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
                          "N = exact sequential semantics (parallel/sweep.py)")
@@ -93,7 +95,8 @@ def parse(argv=None):
             args.matches_per_gpu = 16_000_000
         args.ring = min(args.ring, 2)
     if args.comm_dtype is None:
-        args.comm_dtype = os.environ.get("COMM_DTYPE") or ("fp16" if args.sweeps <= 1 else "fp32")
+        one_sweep = "fp16" if args.config == 5 else "bf16"
+        args.comm_dtype = os.environ.get("COMM_DTYPE") or (one_sweep if args.sweeps <= 1 else "fp32")
     return args
 
 

@@ -28,8 +28,10 @@ def test_config_defaults():
 
 
 def test_merge_precision_default(monkeypatch):
-    # one sweep: fp16 messages (accuracy identical to fp32, profiles/r2/slice_size_accuracy.log)
-    assert bench.parse([]).comm_dtype == "fp16"
+    # one sweep: bf16 messages (accuracy identical to fp32, profiles/r2/slice_size_accuracy.log;
+    # fp32 range in RCCL's sums); config 5 keeps BASELINE's fp16 moments
+    assert bench.parse([]).comm_dtype == "bf16"
+    assert bench.parse(["--config", "5"]).comm_dtype == "fp16"
     # causal re-sweeps aim at the exact result: fp32 unless asked otherwise
     assert bench.parse(["--sweeps", "4"]).comm_dtype == "fp32"
     assert bench.parse(["--sweeps", "4", "--comm-dtype", "bf16"]).comm_dtype == "bf16"

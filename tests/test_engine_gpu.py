@@ -486,20 +486,25 @@ def _rccl_single_rank(rank, size, P, M, K, seed):
     merger.begin(roster)
     R.BatchRater().rate(roster, rec, K)
     posterior = roster.state.clone()
-    # the bench's N > 1 default: fp16 messages (+ int32 touch counts, two collectives per
-    # bucket), with the next window's work enqueued while the all-reduces are in flight
-    r16 = roster.clone()
-    m16 = SweepMerger(P, dev, world_size=2, bucket_rows=P // 3 + 1, comm_dtype="fp16")
-    m16.start.copy_(merger.start)  # the same window start (the pre-rating roster)
-    m16._synced = True
-    m16.begin(r16)
+    # the bench's N > 1 defaults: bf16 (fp16 for config 5) messages + int32 touch counts, two
+    # collectives per bucket, with the next window's work enqueued while they are in flight
+    half = {}
+    for cd in ("bf16", "fp16"):
+        rh = roster.clone()
+        mh = SweepMerger(P, dev, world_size=2, bucket_rows=P // 3 + 1, comm_dtype=cd)
+        mh.start.copy_(merger.start)  # the same window start (the pre-rating roster)
+        mh._synced = True
+        mh.begin(rh)
+        half[cd] = (rh, mh)
     merger.merge(roster)
     ran = []
-    m16.merge(r16, overlap=lambda: ran.append(torch.ones(4, device=dev).sum()))
+    for cd, (rh, mh) in half.items():
+        mh.merge(rh, overlap=lambda: ran.append(torch.ones(4, device=dev).sum()))
     torch.cuda.synchronize()
-    assert len(ran) == 1
+    assert len(ran) == 2
     return {"x": x.cpu(), "z": z.float().cpu(), "y": y.float().cpu(), "g": g[:1000].cpu(),
-            "posterior": posterior.cpu(), "merged": roster.state.cpu(), "merged16": r16.state.cpu()}
+            "posterior": posterior.cpu(), "merged": roster.state.cpu(),
+            "merged_bf16": half["bf16"][0].state.cpu(), "merged_fp16": half["fp16"][0].state.cpu()}
 
 
 def test_rccl_single_rank_collectives_and_merge(gpu_device, tmp_path, monkeypatch):
@@ -521,9 +526,10 @@ def test_rccl_single_rank_collectives_and_merge(gpu_device, tmp_path, monkeypatc
     got = r["merged"].view(P, 8, 4)[..., 0::2]
     np.testing.assert_allclose(got[..., 0].numpy(), post[..., 0].numpy(), rtol=0, atol=2e-3, equal_nan=True)
     np.testing.assert_allclose(got[..., 1].numpy(), post[..., 1].numpy(), rtol=1e-4, atol=0, equal_nan=True)
-    g16 = r["merged16"].view(P, 8, 4)[..., 0::2]
-    np.testing.assert_allclose(g16[..., 0].numpy(), post[..., 0].numpy(), rtol=0, atol=1.0, equal_nan=True)
-    np.testing.assert_allclose(g16[..., 1].numpy(), post[..., 1].numpy(), rtol=2e-3, atol=0, equal_nan=True)
+    for cd, tol_mu, tol_sig in (("fp16", 1.0, 2e-3), ("bf16", 8.0, 1e-2)):  # as test_distributed
+        gh = r["merged_" + cd].view(P, 8, 4)[..., 0::2]
+        np.testing.assert_allclose(gh[..., 0].numpy(), post[..., 0].numpy(), rtol=0, atol=tol_mu, equal_nan=True)
+        np.testing.assert_allclose(gh[..., 1].numpy(), post[..., 1].numpy(), rtol=tol_sig, atol=0, equal_nan=True)
 
 
 def _rccl_entry(rank, port, outdir, args):
