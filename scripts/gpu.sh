@@ -30,6 +30,7 @@
 #   pmc        rocprofv3 --pmc passes over the executor (10M-match window, tune_rate.py: one
 #              process, no side-stream waits -- counter collection serialises dispatches, and a
 #              stream wait on the executor's tail signal then never returns)
+#   telepmc    rocprofv3 counters of the standalone telemetry aggregation
 #   rerate     config 5 end to end: 1B matches / 10M players, checkpoint + kill + resume
 #   worker     streaming worker on the device (ENGINE=native), memory + sqlite stores
 set -o pipefail
@@ -215,6 +216,16 @@ for task in "$@"; do
         $PY scripts/pmc_kernel.py "gpurun_out/pmc/$tag/$name" rate_dataflow >> gpurun_out/pmc/$tag/executor.txt
       done
       cat gpurun_out/pmc/$tag/executor.txt
+      ;;
+    telepmc)  # counters of the standalone K8 aggregation (10M 3v3 window, ~400M events)
+      for set in "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" \
+                 "FETCH_SIZE" "WRITE_SIZE"; do
+        name=$(echo $set | cut -d' ' -f1)
+        (cd /tmp && run telepmc/$name 120 rocprofv3 --pmc $set --kernel-trace --stats \
+            -d "$ROOT/gpurun_out/telepmc/$name" -o run --output-format csv -- $PY "$ROOT/scripts/tele_once.py") || exit $?
+        $PY scripts/pmc_kernel.py "gpurun_out/telepmc/$name" telemetry_kernel >> gpurun_out/telepmc/tele.txt
+      done
+      cat gpurun_out/telepmc/tele.txt
       ;;
     rerate)
       rm -rf /tmp/ck5
