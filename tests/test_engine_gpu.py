@@ -604,7 +604,7 @@ def test_split_executor_bit_identical(gpu_device, monkeypatch, K, skew, split):
     default executor: same statuses, outputs and roster, bit for bit.
     Run with ANA_NATIVE_LIB=analyzer_amd/_C_diag*.so (scripts/gpu.sh split)."""
     if not _diag_library_loaded():
-        pytest.skip("needs ANA_NATIVE_LIB=<analyzer_amd/_C_diag*.so>")
+        pytest.skip("runs in test_split_executor_in_diag_library_process (needs ANA_NATIVE_LIB=_C_diag)")
     P, M = 20000, 400000
     rec = make_stream(StreamSpec(team_size=K, seed=41, skew=skew), M, P, K=K, device=gpu_device)
     base = make_roster(RosterSpec(num_players=P, seed=42), device=gpu_device)
@@ -619,3 +619,27 @@ def test_split_executor_bit_identical(gpu_device, monkeypatch, K, skew, split):
                      res.delta.clone(), res.quality.clone()))
     for a, b in zip(*outs):
         assert torch.equal(a.nan_to_num(-7), b.nan_to_num(-7))
+
+
+def test_split_executor_in_diag_library_process(gpu_device):
+    """The split-role executor lives in the diagnostic library only; one process
+    can load one native library, so the bit-identity tests above run in a child
+    process that loads the in-tree _C_diag (skipped when it was not built:
+    python -m analyzer_amd.build_ext --diag)."""
+    import glob
+    import subprocess
+    import sys
+
+    if _diag_library_loaded() or os.environ.get("ANA_NATIVE_LIB"):
+        pytest.skip("already running against another library")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    libs = glob.glob(os.path.join(root, "analyzer_amd", "_C_diag*.so"))
+    if not libs:
+        pytest.skip("diagnostic library not built")
+    env = dict(os.environ, ANA_NATIVE_LIB=libs[0])
+    res = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                          os.path.abspath(__file__), "-k", "split_executor_bit_identical",
+                          "--timeout", "120", "--timeout-method", "thread"],
+                         cwd=root, env=env, capture_output=True, text=True, timeout=600)
+    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-2000:]
+    assert "6 passed" in res.stdout, res.stdout[-2000:]
