@@ -78,6 +78,10 @@ def parse(argv=None):
                          "profiles/r2/slice_size_accuracy.log, and RCCL's bf16 sums keep fp32's range "
                          "where fp16 sums of 8 ranks' mean shifts could overflow -- fp16 for config 5 "
                          "(BASELINE: fp16 moments) and fp32 for causal re-sweeps)")
+    ap.add_argument("--merges-per-step", type=int, default=1,
+                    help="N > 1: split each GPU's step into this many windows with a sweep merge after "
+                         "each (same matches per step; shorter slices cut the sweep-DP error ~linearly, "
+                         "profiles/r2/slice_size_accuracy.log)")
     ap.add_argument("--sweeps", type=int, default=EngineConfig.from_env().sweeps,
                     help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
                          "N = exact sequential semantics (parallel/sweep.py)")
@@ -94,6 +98,10 @@ def parse(argv=None):
         if args.matches_per_gpu == 10_000_000:
             args.matches_per_gpu = 16_000_000
         args.ring = min(args.ring, 2)
+    if args.merges_per_step < 1 or args.matches_per_gpu % args.merges_per_step:
+        ap.error("--merges-per-step must divide --matches-per-gpu")
+    if args.merges_per_step > 1 and args.config == 4:
+        ap.error("--merges-per-step is for the rating configs (2, 3, 5)")
     if args.comm_dtype is None:
         one_sweep = "fp16" if args.config == 5 else "bf16"
         args.comm_dtype = os.environ.get("COMM_DTYPE") or (one_sweep if args.sweeps <= 1 else "fp32")
@@ -172,14 +180,16 @@ def main(argv=None) -> int:
     from analyzer_amd.runtime.engine import WindowPipeline
 
     P, M, K = args.players, args.matches_per_gpu, args.team_size
+    sub = args.merges_per_step           # windows per step (a merge after each when N > 1)
+    Mw = M // sub                        # matches per window and GPU
     roster = make_roster(RosterSpec(num_players=P, seed=args.seed), device=dev)
     spec = StreamSpec(team_size=K, seed=args.seed + 1, skew=args.skew)
-    n_windows = max(1, min(args.ring, args.steps + args.warmup))
-    total_windows = args.steps + args.warmup
-    windows = [make_stream(spec, M, P, K=K, base=(w * world + rank) * M, device=dev)
+    n_windows = max(1, min(args.ring, (args.steps + args.warmup) * sub))
+    total_windows = (args.steps + args.warmup) * sub
+    windows = [make_stream(spec, Mw, P, K=K, base=(w * world + rank) * Mw, device=dev)
                for w in range(n_windows)]
     rater = BatchRater()
-    out = RateResult.allocate(M, K, dev)
+    out = RateResult.allocate(Mw, K, dev)
     tele = stats = None
     if args.config == 4:
         from analyzer_amd.ops.telemetry import TelemetrySpec, aggregate, allocate_stats, make_telemetry
@@ -227,7 +237,7 @@ def main(argv=None) -> int:
             _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out,
                                            telemetry=(t.evoff, t.events, stats))
 
-    for i in range(args.warmup):
+    for i in range(args.warmup * sub):
         step(i)
     torch.cuda.synchronize()
     if world > 1:
@@ -236,7 +246,7 @@ def main(argv=None) -> int:
     if merger is not None:
         merger.timing = True  # stage events on the main stream (no syncs)
     t0 = time.perf_counter()
-    for i in range(args.warmup, total_windows):
+    for i in range(args.warmup * sub, total_windows):
         step(i)
     torch.cuda.synchronize()
     if world > 1:
@@ -318,6 +328,7 @@ def main(argv=None) -> int:
                 "seq_len": 2 * K,
                 "players": P,
                 "matches_per_gpu": M,
+                "merges_per_step": sub,
                 "team_size": K,
                 "parallelism": "dp%d" % world,
                 "mode": ("exact" if world == 1 else

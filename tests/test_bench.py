@@ -44,3 +44,12 @@ def test_world_size_must_match_gpus(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "2")
     with pytest.raises(SystemExit, match="--gpus 3 but WORLD_SIZE=2"):
         bench.main(["--gpus", "3"])
+
+
+def test_merges_per_step():
+    a = bench.parse(["--merges-per-step", "8"])
+    assert a.merges_per_step == 8 and a.matches_per_gpu == 10_000_000  # same matches per step
+    with pytest.raises(SystemExit):
+        bench.parse(["--merges-per-step", "3"])   # must divide the step
+    with pytest.raises(SystemExit):
+        bench.parse(["--config", "4", "--merges-per-step", "2"])
