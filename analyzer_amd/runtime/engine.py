@@ -20,6 +20,9 @@ slows the 3v3 executor by more than it hides (config 2: 8.07 ms serial vs
 8.34-8.47 ms overlapped at 0.7-0.3), while the 5v5 executor -- 3000+ levels,
 ~75% of its wave iterations idle, a 5.4 ms prepass over 125M slots -- absorbs
 it (config 3: 22.12 ms overlapped at 0.7 vs 22.9-23.2 ms serial).
+``ANA_PREPASS_CUS=n`` confines an overlapped prepass to n CUs, and with
+``ANA_PREPASS_EXCLUSIVE=1`` the rating launches get the other CUs; both measured
+slower than the defaults (profiles/r2/prepass_cu_mask.log, prepass_exclusive_cus.log).
 
 Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.7): the
 prepass of window i+1 does not start with rate(i) -- co-running the two for the
