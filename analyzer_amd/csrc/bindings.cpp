@@ -306,8 +306,8 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   if (const char* e = std::getenv("ANA_RATE_LOCAL")) prm.local_handoff = std::atoi(e);  // A/B knob
   prm.diag = 0;
   if (const char* e = std::getenv("ANA_RATE_DIAG")) prm.diag = std::atoi(e);  // timing build
-  prm.split = 0;
-  if (const char* e = std::getenv("ANA_RATE_SPLIT")) prm.split = std::atoi(e);  // A/B knob
+  prm.impl = 1;
+  if (const char* e = std::getenv("ANA_RATE_IMPL")) prm.impl = std::atoi(e);  // A/B knob
   prm.tight_groups = -1;
   if (const char* e = std::getenv("ANA_RATE_TIGHT")) prm.tight_groups = std::atoi(e);
   prm.progress = reinterpret_cast<uint64_t*>((intptr_t)progress);
@@ -344,10 +344,6 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
                                     attrs.data_ptr<float>(), fp, out,
                                     reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()), prm, tp,
                                     (int)blocks, stream_of(rec));
-    TORCH_CHECK(rc != (int)hipErrorNotSupported,
-                "ANA_RATE_SPLIT selects the split-role executor, which only the diagnostic library "
-                "has: python -m analyzer_amd.build_ext --diag, then ANA_NATIVE_LIB=<path of "
-                "analyzer_amd/_C_diag*.so>");
     check_hip(rc, "rate");
     if (!packed) {
       using torch::indexing::Slice;

@@ -1,5 +1,5 @@
-// Device helpers shared by the dataflow executor (dataflow.hip) and the
-// diagnostic split-role executor (split_exec.hip): control-word constants,
+// Device helpers shared by the dataflow executors (dataflow.hip: lane groups,
+// lane_exec.hip: one lane per match): control-word constants,
 // DPP group sums, tagged granules and wave-uniform reductions.
 #pragma once
 

@@ -20,7 +20,6 @@
 #   exactdp    exact DP (C2) rehearsal, 2/4 gloo ranks on one GPU, rounds + time per window
 #   role       config 4 fused executor with dedicated aggregation waves (ANA_TELE_ROLE sweep)
 #   slices     sweep-DP accuracy and 1-GPU step time vs slice size (fixed 80M-match history)
-#   split      split-role executor (scheduler + rater waves) vs the default, tests + configs 2/3/skew
 #   excl       prepass on its own CUs beside the executor on the rest (ANA_PREPASS_EXCLUSIVE sweep)
 #   tele       config 4 telemetry placement (separate / fused / CU-masked overlap)
 #   tail       prepass start point sweep for config 2 (ANA_PREPASS_AT, serial)
@@ -135,28 +134,6 @@ for task in "$@"; do
           --matches-per-rank 10000000 --windows 1 --warm-windows 1 --sweeps 1 --comm-dtype fp16
       run slices/acc_bf16 600 $PY -m analyzer_amd.parallel.accuracy --device cuda --ranks 8 --players 1e6 \
           --matches-per-rank 10000000 --windows 1 --warm-windows 1 --sweeps 1 --comm-dtype bf16
-      ;;
-    split)  # split-role executor (ANA_RATE_SPLIT=1) vs the default: bit-identity tests, then configs 2 / 3 / skew 2
-      export ANA_NATIVE_LIB=$(ls "$ROOT"/analyzer_amd/_C_diag*.so)  # the split executor is diagnostic-only
-      run split/test 300 $PY -u -m pytest tests/test_engine_gpu.py -k split_executor -x -v --timeout 120 --timeout-method thread
-      for v in ${SPLITS:-0 1}; do
-        ANA_RATE_SPLIT=$v run split/c2_split$v 300 $PY bench.py --steps 20 --warmup 3 --check
-      done
-      for v in ${SPLITS:-0 1}; do
-        ANA_RATE_SPLIT=$v run split/c3_split$v 300 $PY bench.py --config 3 --steps 10 --warmup 2 --check
-        ANA_RATE_SPLIT=$v run split/skew2_split$v 400 $PY bench.py --skew 2 --steps 3 --warmup 1 --check
-      done
-      grep -H -o '"ms_per_step": [0-9.]*' gpurun_out/split/*.log
-      unset ANA_NATIVE_LIB
-      ;;
-    splithop)  # split-role executor: hop latency and 10M window, 16 / 8 held chunks per scheduler
-      export ANA_NATIVE_LIB=$(ls "$ROOT"/analyzer_amd/_C_diag*.so)
-      run splithop/test 300 $PY -u -m pytest tests/test_engine_gpu.py -k split_executor -x -v --timeout 120 --timeout-method thread
-      run splithop/random 300 $PY scripts/tune_rate.py --pattern random --rounds 2 --split 0,1,2
-      run splithop/serial 300 $PY scripts/tune_rate.py --pattern serial --players 1000 --matches 20000 --rounds 2 \
-          --blocks 8 --split 0,1,2
-      grep -h "^round 1" gpurun_out/splithop/*.log | cut -c1-260
-      unset ANA_NATIVE_LIB
       ;;
     excl)  # prepass of window i+1 on n CUs of its own while the executor rates window i on the others
       run excl/serial 400 $PY bench.py --steps 20 --warmup 3

@@ -188,6 +188,37 @@ def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K
         assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32))
 
 
+@pytest.mark.parametrize("K,P,M,skew,pattern", [(3, 16, 4000, 1, "random"), (3, 100000, 1000000, 1, "random"),
+                                                (5, 2000, 200000, 1, "random"), (3, 100000, 300000, 3, "random"),
+                                                (1, 500, 50000, 1, "random"), (2, 300, 30000, 2, "random"),
+                                                (4, 5000, 100000, 1, "random"), (3, 1000, 3000, 1, "serial")])
+def test_lane_executor_matches_group_executor_and_host(gpu_device, monkeypatch, K, P, M, skew, pattern):
+    """The per-lane executor (ANA_RATE_IMPL=1, csrc/lane_exec.hip: one lane rates
+    a whole match) against the lane-group executor (0) and the fp64 host mirror:
+    identical statuses and sequential results within the fp32 tolerance (team sums
+    are added in a different order, so not bit for bit)."""
+    rs = RosterSpec(num_players=P, seed=P + 5, p_tier_null=0.02, p_tier_bad=0.02)
+    ss = StreamSpec(team_size=K, seed=M + 7, skew=skew, p_afk=0.05, p_tie=0.05, p_uneven=0.1,
+                    p_unsupported=0.02, p_hot=0.1)
+    rec = make_stream(ss, M, P, K=K)
+    if pattern == "serial":  # every match has the same 2K players: a chain M deep
+        rec[:, :2 * K] = torch.arange(2 * K, dtype=torch.int32)
+    host = make_roster(rs)
+    rh = R.BatchRater(host_fp64=True).rate(host, rec, K)
+    outs = {}
+    for impl in ("0", "1"):
+        monkeypatch.setenv("ANA_RATE_IMPL", impl)
+        ro = make_roster(rs, device=gpu_device)
+        rater = R.BatchRater()
+        res = rater.rate(ro, rec.to(gpu_device), K)
+        assert int(rater.error_flags(gpu_device).sum()) == 0
+        np.testing.assert_array_equal(res.status.cpu().numpy(), rh.status.numpy())
+        assert_close_to_fp64(res, ro, rh, host)
+        outs[impl] = (res, ro)
+    a, b = outs["0"][0], outs["1"][0]
+    np.testing.assert_allclose(a.s_mu.cpu().numpy(), b.s_mu.cpu().numpy(), rtol=0, atol=6e-3, equal_nan=True)
+
+
 @pytest.mark.parametrize("n,bits", [(1, 8), (4095, 20), (4097, 12), (1_000_003, 20), (300_000, 32)])
 def test_radix_sort_pairs_stable(gpu_device, n, bits):
     from analyzer_amd.ops.native import native
@@ -580,66 +611,3 @@ def test_exact_dp_round_check_on_device(gpu_device):
     bad[M // 2:] = bad[M // 2]  # the second half collapses into one round
     plan = RoundPlan(bad, 4)
     assert check_rounds(rec, K, plan, P) == check_rounds(rec.cpu(), K, plan, P) >= 0
-
-
-def _diag_library_loaded() -> bool:
-    return "_C_diag" in os.path.basename(os.environ.get("ANA_NATIVE_LIB", ""))
-
-
-def test_split_executor_needs_the_diag_library(gpu_device, monkeypatch):
-    if os.environ.get("ANA_NATIVE_LIB"):
-        pytest.skip("another library is loaded")
-    rec = make_stream(StreamSpec(team_size=3, seed=3), 4000, 500, K=3, device=gpu_device)
-    roster = make_roster(RosterSpec(num_players=500, seed=4), device=gpu_device)
-    monkeypatch.setenv("ANA_RATE_SPLIT", "1")
-    with pytest.raises(RuntimeError, match="diagnostic library"):
-        R.BatchRater().rate(roster, rec, 3)
-
-
-@pytest.mark.parametrize("split", ["1", "2"])
-@pytest.mark.parametrize("K,skew", [(3, 1), (3, 3), (5, 1)])
-def test_split_executor_bit_identical(gpu_device, monkeypatch, K, skew, split):
-    """ANA_RATE_SPLIT=1/2 (diagnostic library: scheduler wave + rater waves per
-    workgroup, 16 / 8 held chunks) rates a contended window exactly like the
-    default executor: same statuses, outputs and roster, bit for bit.
-    Run with ANA_NATIVE_LIB=analyzer_amd/_C_diag*.so (scripts/gpu.sh split)."""
-    if not _diag_library_loaded():
-        pytest.skip("runs in test_split_executor_in_diag_library_process (needs ANA_NATIVE_LIB=_C_diag)")
-    P, M = 20000, 400000
-    rec = make_stream(StreamSpec(team_size=K, seed=41, skew=skew), M, P, K=K, device=gpu_device)
-    base = make_roster(RosterSpec(num_players=P, seed=42), device=gpu_device)
-    outs = []
-    for sp in ("0", split):
-        monkeypatch.setenv("ANA_RATE_SPLIT", sp)
-        roster = base.clone()
-        br = R.BatchRater()
-        res = br.rate(roster, rec, K)
-        torch.cuda.synchronize()
-        outs.append((roster.state[:, ::2].clone(), res.status.clone(), res.s_mu.clone(), res.m_sig.clone(),
-                     res.delta.clone(), res.quality.clone()))
-    for a, b in zip(*outs):
-        assert torch.equal(a.nan_to_num(-7), b.nan_to_num(-7))
-
-
-def test_split_executor_in_diag_library_process(gpu_device):
-    """The split-role executor lives in the diagnostic library only; one process
-    can load one native library, so the bit-identity tests above run in a child
-    process that loads the in-tree _C_diag (skipped when it was not built:
-    python -m analyzer_amd.build_ext --diag)."""
-    import glob
-    import subprocess
-    import sys
-
-    if _diag_library_loaded() or os.environ.get("ANA_NATIVE_LIB"):
-        pytest.skip("already running against another library")
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    libs = glob.glob(os.path.join(root, "analyzer_amd", "_C_diag*.so"))
-    if not libs:
-        pytest.skip("diagnostic library not built")
-    env = dict(os.environ, ANA_NATIVE_LIB=libs[0])
-    res = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
-                          os.path.abspath(__file__), "-k", "split_executor_bit_identical",
-                          "--timeout", "120", "--timeout-method", "thread"],
-                         cwd=root, env=env, capture_output=True, text=True, timeout=600)
-    assert res.returncode == 0, res.stdout[-3000:] + res.stderr[-2000:]
-    assert "6 passed" in res.stdout, res.stdout[-2000:]
