@@ -208,7 +208,7 @@ rate_lane_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ l
     // slot facts as bit masks (bit j): in roster; owns the gather (first occurrence
     // of its player); publishes (last occurrence).  Repeated players only (rare):
     // nibble j of fsel = first slot of the same player, of psel = latest earlier
-    // one (15: none)
+    // one (15: none); 64 bits for the 10 slots of 5v5
     int32_t id[S];
     uint32_t inr = 0u;
 #pragma unroll
@@ -218,9 +218,10 @@ rate_lane_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ l
       inr |= in ? 1u << j : 0u;
     }
     inr = opaque(inr);
-    uint32_t own = inr, last = inr, fsel = 0u, psel = 0xffffffffu;
+    uint32_t own = inr, last = inr;
+    uint64_t fsel = 0u, psel = ~0ull;  // 4 bits per slot: up to 16 slots
 #pragma unroll
-    for (int j = 0; j < S; ++j) fsel |= (uint32_t)j << (4 * j);
+    for (int j = 0; j < S; ++j) fsel |= (uint64_t)j << (4 * j);
     if (dup) {
 #pragma unroll
       for (int j = 1; j < S; ++j) {
@@ -234,8 +235,8 @@ rate_lane_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ l
           }
         }
         if (f != (uint32_t)j) own &= ~(1u << j);
-        fsel = (fsel & ~(15u << (4 * j))) | (f << (4 * j));
-        psel = (psel & ~(15u << (4 * j))) | (pv << (4 * j));
+        fsel = (fsel & ~(15ull << (4 * j))) | ((uint64_t)f << (4 * j));
+        psel = (psel & ~(15ull << (4 * j))) | ((uint64_t)pv << (4 * j));
       }
     }
     own = opaque(own);
@@ -495,7 +496,7 @@ rate_lane_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ l
       if (dup) {  // duplicates see the pre-match values of their first occurrence
 #pragma unroll
         for (int j = 1; j < S; ++j) {
-          const uint32_t f = (fsel >> (4 * j)) & 15u;
+          const uint32_t f = (uint32_t)(fsel >> (4 * j)) & 15u;
 #pragma unroll
           for (int i = 0; i < j; ++i)
             if (f == (uint32_t)i) {
@@ -539,7 +540,7 @@ rate_lane_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ l
       if (dup) {  // a repeated player's delta is against its previous slot's write
 #pragma unroll
         for (int j = 1; j < S; ++j) {
-          const uint32_t pv = (psel >> (4 * j)) & 15u;
+          const uint32_t pv = (uint32_t)(psel >> (4 * j)) & 15u;
 #pragma unroll
           for (int i = 0; i < j; ++i)
             if (pv == (uint32_t)i) dl[j] = (nsm[j] - nss[j]) - (nsm[i] - nss[i]);
