@@ -23,14 +23,13 @@ BUILD = PKG.parent / "build" / "analyzer_amd"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-HIP_SOURCES = ["kernels.hip", "radix_sort.hip", "dataflow.hip", "lane_exec.hip", "sweep.hip", "telemetry.hip",
-               "levels.hip"]
+HIP_SOURCES = ["kernels.hip", "radix_sort.hip", "dataflow.hip", "sweep.hip", "telemetry.hip", "levels.hip"]
 # per-file device flags.  The executor's divisions/sqrt take the 1-ulp hardware
 # paths (v_rcp_f32 instead of the ~10-instruction IEEE division expansion: -9%
 # static instructions); NaN/Inf semantics are untouched (no -ffinite-math-only),
 # which the NULL = NaN convention relies on.
 HIP_FLAGS = {n: ["-fapprox-func", "-freciprocal-math", "-fno-signed-zeros"]
-             for n in ("dataflow.hip", "lane_exec.hip")}
+             for n in ("dataflow.hip",)}
 CPP_SOURCES = ["host.cpp", "ingest.cpp", "bindings.cpp"]
 
 

@@ -164,7 +164,6 @@ class EngineConfig:
         "ANA_RATE_TIGHT": "2K lanes per match instead of the next power of two (-1 auto)",
         "ANA_RATE_LOCAL": "LDS local hand-off of successors held by the producing wave (default 1)",
         "ANA_RATE_DIAG": "timing build of the executor: per-phase clocks in ctrl[20..39] (default 0)",
-        "ANA_RATE_IMPL": "executor: 1 one lane per match (default, csrc/lane_exec.hip), 0 lane groups (dataflow.hip)",
         "ANA_TELE_IMPL": "telemetry aggregation: 1 one-hot MFMA GEMM (default), 0 LDS atomics",
         "ANA_TELE_FUSED_TAIL": "fused telemetry only after the executor's chunks are drained",
         "ANA_TELE_ROLE": "fused telemetry: one wave in N aggregates from the start (default 2; 0 = idle waves take tiles)",

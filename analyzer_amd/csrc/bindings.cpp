@@ -306,8 +306,6 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   if (const char* e = std::getenv("ANA_RATE_LOCAL")) prm.local_handoff = std::atoi(e);  // A/B knob
   prm.diag = 0;
   if (const char* e = std::getenv("ANA_RATE_DIAG")) prm.diag = std::atoi(e);  // timing build
-  prm.impl = 1;
-  if (const char* e = std::getenv("ANA_RATE_IMPL")) prm.impl = std::atoi(e);  // A/B knob
   prm.tight_groups = -1;
   if (const char* e = std::getenv("ANA_RATE_TIGHT")) prm.tight_groups = std::atoi(e);
   prm.progress = reinterpret_cast<uint64_t*>((intptr_t)progress);

@@ -98,8 +98,6 @@ struct RateParams {
   // 1: ctrl[1..15] were zeroed by the schedule launched just before on this stream
   // (launch_schedule zero_ctrl), so the launch skips its own zeroing dispatch
   int32_t ctrl_ready;
-  // executor: 1 = per-lane matches (lane_exec.hip, default), 0 = lane groups (dataflow.hip)
-  int32_t impl;
 };
 
 // Per-match outputs.  The participant record of the reference

@@ -797,8 +797,6 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // window), 5v5 18.23-18.42 ms with 10 lanes vs 18.42-18.61 with 16 (12.5M;
   // config 3 step 21.5 vs 21.9 ms, profiles/r2/tight_groups.log) -> auto = tight
   // for 5v5 only.
-  if (prm.impl == 1)
-    return launch_rate_lane(K, rec, link, deps, state, attrs, first_prior, out, ctrl, prm, tp, blocks, s);
   const bool tight = prm.tight_groups > 0 || (prm.tight_groups < 0 && K == 5);
 #define ANA_RATE_LAUNCH_D(k, g, tele, diag)                                                        \
   hipLaunchKernelGGL((rate_dataflow_kernel<k, g, tele, diag>), dim3((unsigned)blocks), dim3(256), 0, s, \

@@ -1,5 +1,4 @@
-// Device helpers shared by the dataflow executors (dataflow.hip: lane groups,
-// lane_exec.hip: one lane per match): control-word constants,
+// Device helpers of the dataflow executor (dataflow.hip): control-word constants,
 // DPP group sums, tagged granules and wave-uniform reductions.
 #pragma once
 

@@ -59,12 +59,6 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
                 const float* attrs, float* first_prior, const RateOut& out, uint32_t* ctrl,
                 const RateParams& prm, const TelemetryParams& tp, int blocks, hipStream_t s);
 
-// the per-lane executor (lane_exec.hip): one lane rates one whole match;
-// launch_rate dispatches to it for RateParams::impl == 1
-int launch_rate_lane(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, float* state,
-                     const float* attrs, float* first_prior, const RateOut& out, uint32_t* ctrl,
-                     const RateParams& prm, const TelemetryParams& tp, int blocks, hipStream_t s);
-
 
 // K8 (telemetry.hip)
 int launch_gen_event_counts(const GenEventParams& g, int64_t base, int64_t M, int64_t* counts,

@@ -35,7 +35,6 @@ def main():
     ap.add_argument("--tight", default="-1", help="ANA_RATE_TIGHT values (2K lanes per match; -1 auto)")
     ap.add_argument("--local", default="1", help="ANA_RATE_LOCAL values (LDS local hand-off)")
     ap.add_argument("--diag", default="0", help="ANA_RATE_DIAG values (timing build)")
-    ap.add_argument("--impl", default="1", help="ANA_RATE_IMPL values (1 per-lane executor, 0 lane groups)")
     ap.add_argument("--skew", type=int, default=1)
     ap.add_argument("--rated", type=float, default=1.0,
                     help="fraction of players with stored ratings (1.0 = steady state, no seeding)")
@@ -54,15 +53,14 @@ def main():
     results = {}
     combos = [(int(b), int(i), int(t), int(lo), int(d), int(sp)) for b in args.blocks.split(",")
               for i in args.idle.split(",") for t in args.tight.split(",")
-              for lo in args.local.split(",") for d in args.diag.split(",") for sp in args.impl.split(",")]
+              for lo in args.local.split(",") for d in args.diag.split(",") for sp in ("0",)]
     for rnd in range(args.rounds):
         for b, idle, tg, loc, dg, sp in combos:
-            os.environ["ANA_RATE_IMPL"] = str(sp)
             os.environ["ANA_RATE_TIGHT"] = str(tg)
             os.environ["ANA_RATE_IDLE"] = str(idle)
             os.environ["ANA_RATE_LOCAL"] = str(loc)
             os.environ["ANA_RATE_DIAG"] = str(dg)
-            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg) + ("/impl%d" % sp)
+            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg)
             roster = make_roster(RosterSpec(num_players=P, seed=1, p_rated=args.rated,
                                             p_mode_rated=args.rated), device=dev)
             br = BatchRater(blocks=b)

@@ -188,37 +188,6 @@ def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K
         assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32))
 
 
-@pytest.mark.parametrize("K,P,M,skew,pattern", [(3, 16, 4000, 1, "random"), (3, 100000, 1000000, 1, "random"),
-                                                (5, 2000, 200000, 1, "random"), (3, 100000, 300000, 3, "random"),
-                                                (1, 500, 50000, 1, "random"), (2, 300, 30000, 2, "random"),
-                                                (4, 5000, 100000, 1, "random"), (3, 1000, 3000, 1, "serial")])
-def test_lane_executor_matches_group_executor_and_host(gpu_device, monkeypatch, K, P, M, skew, pattern):
-    """The per-lane executor (ANA_RATE_IMPL=1, csrc/lane_exec.hip: one lane rates
-    a whole match) against the lane-group executor (0) and the fp64 host mirror:
-    identical statuses and sequential results within the fp32 tolerance (team sums
-    are added in a different order, so not bit for bit)."""
-    rs = RosterSpec(num_players=P, seed=P + 5, p_tier_null=0.02, p_tier_bad=0.02)
-    ss = StreamSpec(team_size=K, seed=M + 7, skew=skew, p_afk=0.05, p_tie=0.05, p_uneven=0.1,
-                    p_unsupported=0.02, p_hot=0.1)
-    rec = make_stream(ss, M, P, K=K)
-    if pattern == "serial":  # every match has the same 2K players: a chain M deep
-        rec[:, :2 * K] = torch.arange(2 * K, dtype=torch.int32)
-    host = make_roster(rs)
-    rh = R.BatchRater(host_fp64=True).rate(host, rec, K)
-    outs = {}
-    for impl in ("0", "1"):
-        monkeypatch.setenv("ANA_RATE_IMPL", impl)
-        ro = make_roster(rs, device=gpu_device)
-        rater = R.BatchRater()
-        res = rater.rate(ro, rec.to(gpu_device), K)
-        assert int(rater.error_flags(gpu_device).sum()) == 0
-        np.testing.assert_array_equal(res.status.cpu().numpy(), rh.status.numpy())
-        assert_close_to_fp64(res, ro, rh, host)
-        outs[impl] = (res, ro)
-    a, b = outs["0"][0], outs["1"][0]
-    np.testing.assert_allclose(a.s_mu.cpu().numpy(), b.s_mu.cpu().numpy(), rtol=0, atol=6e-3, equal_nan=True)
-
-
 @pytest.mark.parametrize("n,bits", [(1, 8), (4095, 20), (4097, 12), (1_000_003, 20), (300_000, 32)])
 def test_radix_sort_pairs_stable(gpu_device, n, bits):
     from analyzer_amd.ops.native import native
