@@ -44,6 +44,14 @@ def _tristate(v: Optional[str]) -> Optional[bool]:
     return v != "0"
 
 
+def _resident_default(env: Mapping[str, str]) -> bool:
+    v = env.get("RESIDENT")
+    if v:
+        return v == "true"
+    uri = env.get("DATABASE_URI") or ""
+    return uri == "" or uri.startswith(("memory:", "columnar:"))
+
+
 @dataclass(frozen=True)
 class RaterConfig:
     unknown_player_sigma: int = 500
@@ -81,7 +89,10 @@ class WorkerConfig:
     # new: aggregate per-participant telemetry (participant_stats) in the rating launch
     dotelemetry: bool = False
     telemetry_events: str = "100,300"
-    # new: ENGINE=native keeps the player table resident on the device across batches
+    # new: ENGINE=native keeps the player table resident on the device across batches.
+    # Default (RESIDENT unset): on for the in-process stores only -- a resident roster
+    # never re-reads the store, so with a shared SQL database another worker replica's
+    # writes would be overwritten with stale ratings.  RESIDENT=true opts in anyway.
     resident: bool = True
     # new: the run is a benchmark -- synthetic telemetry may be persisted (worker.connect)
     synthetic_telemetry: bool = False
@@ -110,7 +121,7 @@ class WorkerConfig:
             dotelemetry=env.get("DOTELEMETRY") == "true",
             telemetry_events=_env(env, "TELEMETRY_EVENTS") or "100,300",
             synthetic_telemetry=env.get("SYNTHETIC_TELEMETRY") == "true",
-            resident=(env.get("RESIDENT") or "true") == "true",
+            resident=_resident_default(env),
             skip_rated=env.get("SKIP_RATED") == "true",
         )
 

@@ -111,6 +111,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       __builtin_amdgcn_make_buffer_rsrc(state, 0, (int)(P * kRowFloats * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rl = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint32_t*>(link), 0, (int)(M * S * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(deps, 0, (int)(M * 4), 0x00020000);
   const int head = blockIdx.x % kHeads;
   // watchdog: give up only after kTimeoutTicks without ANY chunk retiring GPU-wide
   // (ctrl[3] counts retired chunks), so long dependency chains never trip it
@@ -123,7 +124,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   uint64_t d_issue = 0, d_wait = 0, d_after = 0, d_it0 = 0;
   uint64_t d_t[4] = {0, 0, 0, 0}, d_p[5] = {0, 0, 0, 0, 0};  // after-phase split (timing build)
   uint64_t d_s[4] = {0, 0, 0, 0}, d_i[3] = {0, 0, 0};         // issue-phase split (timing build)
-  uint32_t d_worked = 0, d_groups = 0;
+  uint32_t d_worked = 0, d_groups = 0, d_near = 0, d_pend = 0;
 
   // per lane: the record of match cbase[h] + lane (ids, meta0, meta1), kept in
   // registers so the lane that picks a match hands the whole record to its group
@@ -184,6 +185,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   }
   const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : prm.idle_spins < 0 ? 0u : 8u;
   const int cl = prm.chunk_len;  // matches per ticket (<= kChunk lanes)
+  // chunks in the window (hoisted: a 64-bit division is ~130 scalar instructions)
+  const int64_t nchunks = (M + cl - 1) / cl;
 
   for (;;) {
     if constexpr (DIAG) d_it0 = __builtin_amdgcn_s_memrealtime();
@@ -196,6 +199,21 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
       for (int h = 0; h < kH; ++h)
         ready[h] = __ballot(dval[h] != kNone && dval[h] + lv[h] == need[h]) & pend[h];
+      if constexpr (DIAG) {
+        uint32_t nn = 0, np = 0;
+#pragma unroll
+        for (int h = 0; h < kH; ++h) {
+          nn += (uint32_t)__popcll(__ballot(dval[h] != kNone && dval[h] + lv[h] + 1u == need[h]) & pend[h]);
+          np += (uint32_t)__popcll(pend[h]);
+        }
+        bool any = false;
+#pragma unroll
+        for (int h = 0; h < kH; ++h) any |= ready[h] != 0ull;
+        if (any) {
+          d_near += nn;
+          d_pend += np;
+        }
+      }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // state loads stay below the poll
     if constexpr (DIAG) d_i[0] = __builtin_amdgcn_s_memrealtime();
@@ -318,7 +336,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       const int64_t c = (int64_t)t * kHeads + head;
       // tail signal: the first ticket of each shard at or past progress_at, and its
       // first ticket past the end (so a threshold beyond the window still fires)
-      const int64_t nchunks = (M + cl - 1) / cl;
       if (prm.progress && lane == 0 &&
           ((c >= prm.progress_at && c < prm.progress_at + kHeads) ||
            (c >= nchunks && c < nchunks + kHeads)))
@@ -665,11 +682,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // the readiness at the top waits for them, so what it sees is one rating
     // phase fresher than a poll issued before the wait
     ++iter;
+    // straight-line sc1 buffer loads (served past the non-coherent L1); a lane
+    // whose match is not pending loads out of range and gets 0, which readiness
+    // masks with pend -- no exec branch per chunk
 #pragma unroll
     for (int h = 0; h < kH; ++h)
-      if ((pend[h] >> lane) & 1ull)
-        dval[h] = __hip_atomic_load((gu32*)(deps + cbase[h] + lane), __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
+      dval[h] = __builtin_amdgcn_raw_buffer_load_b32(rd, ((pend[h] >> lane) & 1ull) ? (cbase[h] + lane) * 4 : kOutOfRange,
+                                                     0, 16);
+
 
     // ---------------------------------------------- (11) retire finished chunks
     {
@@ -680,6 +700,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           cbase[h] = -1;
           ++retired;
         }
+      retired = __builtin_amdgcn_readfirstlane(retired);  // uniform: no waterfall loop
       if (retired && lane == 0)
         __hip_atomic_fetch_add((gu32*)&ctrl[3], retired, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -699,6 +720,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           // [24..25] the wait, [28..29] after it (rating, publish, bookkeeping)
           __hip_atomic_fetch_add((gu32*)&ctrl[20], d_worked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_fetch_add((gu32*)&ctrl[21], d_groups, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          // [30] matches one dependency short of ready, [31] pending, summed over worked iterations
+          __hip_atomic_fetch_add((gu32*)&ctrl[30], d_near, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add((gu32*)&ctrl[31], d_pend, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[22]), (unsigned long long)d_issue);
           atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[24]), (unsigned long long)d_wait);
           atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[28]), (unsigned long long)d_after);

@@ -356,7 +356,10 @@ class BatchRater:
                 # list), this batch's loads, next polls + ticket
                 "issue_ready_us": per(u64(40)), "issue_assign_us": per(u64(42)),
                 "issue_loads_us": per(u64(44)), "issue_polls_us": per(u64(46)),
-                "local_handoffs": c[26], "global_handoffs": c[27]}
+                "local_handoffs": c[26], "global_handoffs": c[27],
+                # held matches one dependency short of ready / pending, per worked iteration
+                "near_ready_per_worked_iteration": c[30] / worked if worked else 0.0,
+                "pending_per_worked_iteration": c[31] / worked if worked else 0.0}
 
     def telemetry_errors(self, device) -> int:
         """Malformed telemetry events seen by the last fused launch (syncs)."""

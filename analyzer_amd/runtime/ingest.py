@@ -103,7 +103,7 @@ class OutputSink:
         self.ring = int(slots) > 0
         self._slots = [None] * max(1, int(slots))
         self._next = 0
-        self._pending: Deque[Tuple[int, dict, Optional[torch.cuda.Event], int]] = collections.deque()
+        self._pending: Deque[Tuple[int, dict, Optional[torch.cuda.Event], int, int]] = collections.deque()
         self._copied = {}
         self.bytes = 0
 
@@ -134,6 +134,10 @@ class OutputSink:
             if res.packed is not None:  # one DMA of the packed rows, host views rebuilt
                 buf = self._slot(i, res.packed.shape, torch.float32)
                 buf.copy_(res.packed, non_blocking=True)
+                # the caching allocator must not hand these blocks to later main-stream
+                # work while this copy may still be reading them: a caller that drops
+                # ``res`` right away (rate_file: a fresh result every window) is safe
+                res.packed.record_stream(self.copy_stream)
                 S = res.s_mu.shape[1]
                 host = {"quality": buf[:, 5 * S], "status": buf.view(torch.uint8)[:, 4 * (5 * S + 1)]}
                 for k, f in enumerate(("s_mu", "s_sig", "delta", "m_mu", "m_sig")):
@@ -145,12 +149,14 @@ class OutputSink:
                     src = getattr(res, f)
                     dst = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
                     dst.copy_(src, non_blocking=True)
+                    src.record_stream(self.copy_stream)
                     host[f] = dst
                     self.bytes += src.numel() * src.element_size()
             ev = torch.cuda.Event()
             ev.record(self.copy_stream)
-        self._copied[id(res.packed if res.packed is not None else res.s_mu)] = ev
-        self._pending.append((base, host, ev, i))
+        key = id(res.packed if res.packed is not None else res.s_mu)
+        self._copied[key] = ev
+        self._pending.append((base, host, ev, i, key))
         self.poll()
 
     def copied(self, res: RateResult) -> Optional[torch.cuda.Event]:
@@ -160,13 +166,15 @@ class OutputSink:
     def poll(self, block: bool = False, limit: Optional[int] = None) -> None:
         n = 0
         while self._pending and (limit is None or n < limit):
-            base, host, ev, _ = self._pending[0]
+            base, host, ev, _, key = self._pending[0]
             if not block and ev is not None and not ev.query():
                 return
             if ev is not None:
                 ev.synchronize()
             self.on_ready(base, host)
             self._pending.popleft()
+            if self._copied.get(key) is ev:  # delivered: no stale event under a recycled id
+                del self._copied[key]
             n += 1
 
     def flush(self) -> None:

@@ -128,6 +128,16 @@ class ResidentRoster:
             self.rows.update(fresh)
         return rows
 
+    def forget(self, api_ids) -> int:
+        """Drop cached rows of these players (rated elsewhere, e.g. by the Python
+        engine): their next batch re-reads them from the store.  The rows
+        themselves stay allocated (orphaned) until the roster is rebuilt."""
+        n = 0
+        for a in api_ids:
+            if self.rows.pop(a, None) is not None:
+                n += 1
+        return n
+
     def _grow(self, need: int) -> None:
         cap = self.capacity
         while cap < need:
@@ -352,6 +362,11 @@ class ResidentBatchRater:
         """Undo the last batch on the device roster (the store rolled back)."""
         if self._undo is not None:
             idx, saved = self._undo
+            # the snapshot may predate an EpochClock reset (before_launch renumbers
+            # epochs after 255 launches): restore values with zeroed tag words, which
+            # no launch's epoch ever matches, as unpack_rows does
+            saved = saved.clone()
+            saved[:, 1::2] = 0.0
             self.resident.roster.state.index_copy_(0, idx, saved)
             self._undo = None
 

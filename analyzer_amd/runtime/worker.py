@@ -207,10 +207,10 @@ class Worker:
                     and hasattr(session, "load_batch")):
                 # columnar path: no per-object work (runtime/columnar.py)
                 with trace_range("load", ids=len(ids)):
-                    batch = session.load_batch(ids, self.cfg.chunksize)
-                with trace_range("rate", matches=len(batch), engine="native"):
-                    quarantined = self._rate_batch(batch, session, counts)
-                matches = batch.ids
+                    mb = session.load_batch(ids, self.cfg.chunksize)
+                with trace_range("rate", matches=len(mb), engine="native"):
+                    quarantined = self._rate_batch(mb, session, counts)
+                matches = mb.ids
             else:
                 with trace_range("load", ids=len(ids)):
                     matches = list(session.load_matches(ids, self.cfg.chunksize))
@@ -224,6 +224,7 @@ class Worker:
                         quarantined = self._rate_native(session, matches, counts)
                     else:
                         quarantined = self._rate_python(session, matches, counts)
+                        self._forget_resident(matches)
             with trace_range("commit"):
                 session.commit()
             if self._object_rater is not None and hasattr(self._object_rater, "commit"):
@@ -258,6 +259,15 @@ class Worker:
                 logger.error("quarantined match %s: %r", match.api_id, e)
                 bad.append(match.api_id)
         return bad
+
+    def _forget_resident(self, matches) -> None:
+        """Players the Python engine just rated: the device-resident copies are
+        stale, so their next native batch re-reads them from the store."""
+        res = getattr(self._object_rater, "resident", None)
+        if res is None or not hasattr(res, "forget"):
+            return
+        res.forget({p.player[0].api_id for m in matches for r in m.rosters for p in r.participants
+                    if p.player})
 
     def _batched(self):
         if self._object_rater is None:

@@ -78,10 +78,16 @@ def parse(argv=None):
                          "profiles/r2/slice_size_accuracy.log, and RCCL's bf16 sums keep fp32's range "
                          "where fp16 sums of 8 ranks' mean shifts could overflow -- fp16 for config 5 "
                          "(BASELINE: fp16 moments) and fp32 for causal re-sweeps)")
-    ap.add_argument("--merges-per-step", type=int, default=1,
+    ap.add_argument("--merges-per-step", type=int, default=None,
                     help="N > 1: split each GPU's step into this many windows with a sweep merge after "
                          "each (same matches per step; shorter slices cut the sweep-DP error ~linearly, "
-                         "profiles/r2/slice_size_accuracy.log)")
+                         "profiles/r2/slice_size_accuracy.log).  Default: 1 on one GPU (nothing to "
+                         "merge), 8 for N > 1 (one sweep then keeps Spearman(mu - sigma) >= 0.99 against "
+                         "the exact sequential result at 8 x 10M 3v3 over 1M players)")
+    ap.add_argument("--accuracy", type=int, default=1,
+                    help="N > 1: after timing, rank 0 measures the sweep-DP error of this run's "
+                         "configuration against the exact sequential rating (parallel/accuracy.py, "
+                         "N ranks simulated on its GPU) and reports it in the JSON line (0 = skip)")
     ap.add_argument("--sweeps", type=int, default=EngineConfig.from_env().sweeps,
                     help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
                          "N = exact sequential semantics (parallel/sweep.py)")
@@ -98,6 +104,9 @@ def parse(argv=None):
         if args.matches_per_gpu == 10_000_000:
             args.matches_per_gpu = 16_000_000
         args.ring = min(args.ring, 2)
+    if args.merges_per_step is None:
+        n = args.gpus if args.gpus is not None else int(os.environ.get("WORLD_SIZE") or 1)
+        args.merges_per_step = 8 if n > 1 and args.config != 4 and args.sweeps <= 1 else 1
     if args.merges_per_step < 1 or args.matches_per_gpu % args.merges_per_step:
         ap.error("--merges-per-step must divide --matches-per-gpu")
     if args.merges_per_step > 1 and args.config == 4:
@@ -289,6 +298,27 @@ def main(argv=None) -> int:
                                windows[0], K)
         if tele is not None:
             verify["note"] = "rating only (telemetry is checked by tests/test_telemetry.py)"
+    accuracy = None
+    if world > 1 and args.accuracy and rank == 0 and args.config != 4:
+        # untimed: the error this run's settings leave against the exact sequential
+        # result -- the same N, roster, slice length, merges, sweeps and message dtype,
+        # the N ranks simulated with the same kernels on this GPU (parallel/accuracy.py)
+        from analyzer_amd.parallel.accuracy import run as accuracy_run
+
+        t_acc = time.perf_counter()
+        tab = accuracy_run(world, P, Mw, sub, [args.sweeps], device=dev, team_size=K, seed=args.seed,
+                           comm_dtype=args.comm_dtype, p_rated=RosterSpec().p_rated, warm_windows=1)
+        st = tab["sweeps"][str(args.sweeps)]
+        sh = st["tracks"].get("shared", {})
+        accuracy = {"vs": "exact sequential rating of the same %d x %d matches (one step)" % (world, M),
+                    "shared_dmu_median": sh.get("dmu_median"), "shared_dmu_p99": sh.get("dmu_p99"),
+                    "shared_dmu_max": sh.get("dmu_max"),
+                    "spearman_mu_minus_sigma": sh.get("spearman_mu_minus_sigma"),
+                    "sigma_ratio_p01_p99": [sh.get("sigma_ratio_p01"), sh.get("sigma_ratio_p99")],
+                    "records_dmu_median": st.get("records_shared_mu", {}).get("dmu_median"),
+                    "seconds": round(time.perf_counter() - t_acc, 2)}
+    if world > 1:
+        dist.barrier()  # the other ranks wait for rank 0's untimed accuracy pass
     value = world * M / (ms / 1000.0)
     metric = "matches/sec rated (whole node), 3v3 TrueSkill, 1M-player roster"
     extra = {}
@@ -319,6 +349,7 @@ def main(argv=None) -> int:
             "data": "synthetic (on-device counter RNG stream, random-init %d-player roster)" % P,
             "merge_ms": merge_ms,
             "verify": verify,
+            "accuracy": accuracy,
             "rccl_world": dist.get_world_size() if world > 1 else None,
             "dist_backend": backend if world > 1 else None,
             "config": {

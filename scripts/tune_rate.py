@@ -81,9 +81,6 @@ def main():
                     " hand-offs local %d global %d" % (rnd, key, (t1 - t0) * 1e3, (t2 - t1) * 1e3, stale,
                                                        d["wave_iterations"], M / max(d["wave_iterations"], 1),
                                                        d["local_handoffs"], d["global_handoffs"]))
-            if sp:
-                line += " | rater iterations %d (%.2f matches each)" % (
-                    d["worked_iterations"], d["groups_assigned"] / max(d["worked_iterations"], 1))
             if dg:
                 line += " | worked iterations %d (%.2f matches each): issue %.3f + wait %.3f + after %.3f us" % (
                     d["worked_iterations"], d["matches_per_worked_iteration"], d["issue_us"], d["wait_us"],
@@ -92,6 +89,8 @@ def main():
                     d["after_prior_us"], d["after_update_us"], d["after_publish_us"], d["after_rest_us"])
                 line += " issue [ready %.3f assign %.3f loads %.3f polls %.3f]" % (
                     d["issue_ready_us"], d["issue_assign_us"], d["issue_loads_us"], d["issue_polls_us"])
+                line += " near-ready %.2f of %.1f pending" % (d["near_ready_per_worked_iteration"],
+                                                               d["pending_per_worked_iteration"])
             if args.pattern == "serial":
                 line += " | %.3f us per hop" % ((t2 - t1) * 1e6 / M)
             print(line, flush=True)

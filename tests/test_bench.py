@@ -53,3 +53,19 @@ def test_merges_per_step():
         bench.parse(["--merges-per-step", "3"])   # must divide the step
     with pytest.raises(SystemExit):
         bench.parse(["--config", "4", "--merges-per-step", "2"])
+
+
+def test_merges_per_step_default_is_accuracy_bounded(monkeypatch):
+    """One GPU has nothing to merge (one window per step); N > 1 merges 8 times per
+    step so that one sweep keeps Spearman(mu - sigma) >= 0.99 against the exact
+    sequential result (profiles/r2/slice_size_accuracy.log); causal re-sweeps are
+    exact already and keep one window."""
+    assert bench.parse([]).merges_per_step == 1
+    assert bench.parse(["--gpus", "8"]).merges_per_step == 8
+    assert bench.parse(["--gpus", "2", "--config", "3"]).merges_per_step == 8
+    assert bench.parse(["--gpus", "8", "--sweeps", "8"]).merges_per_step == 1
+    assert bench.parse(["--gpus", "8", "--config", "4"]).merges_per_step == 1
+    assert bench.parse(["--gpus", "8", "--merges-per-step", "2"]).merges_per_step == 2
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    assert bench.parse([]).merges_per_step == 8
+    assert bench.parse([]).accuracy == 1

@@ -504,3 +504,56 @@ def test_amqp_uri_without_pika_is_a_clear_error(monkeypatch):
     monkeypatch.setitem(sys.modules, "pika", None)  # import pika -> ImportError
     with pytest.raises(RuntimeError, match="needs the pika package"):
         B.connect("amqp://localhost")
+
+
+def test_resident_default_only_for_in_process_stores():
+    """A resident roster never re-reads the store: with a SQL database
+    that other worker replicas write it is off unless RESIDENT=true opts in."""
+    assert WorkerConfig.from_env({}).resident
+    assert WorkerConfig.from_env({"DATABASE_URI": "memory://"}).resident
+    assert WorkerConfig.from_env({"DATABASE_URI": "columnar://"}).resident
+    assert not WorkerConfig.from_env({"DATABASE_URI": "sqlite:////tmp/x.db"}).resident
+    assert not WorkerConfig.from_env({"DATABASE_URI": "mysql+cymysql://u@h/db"}).resident
+    assert WorkerConfig.from_env({"DATABASE_URI": "sqlite:////tmp/x.db", "RESIDENT": "true"}).resident
+    assert not WorkerConfig.from_env({"RESIDENT": "false"}).resident
+
+
+def test_resident_rollback_zeroes_tags_and_restores_values():
+    """rollback() restores the pre-batch values with zeroed tag words: the saved
+    tags may belong to an epoch numbering that EpochClock has since reset."""
+    import torch
+
+    from analyzer_amd.runtime.resident import ResidentBatchRater
+
+    store = MemoryStore()
+    matches = populate(store, 6, 10, team_size=3, seed=5)
+    rr = ResidentBatchRater(device="cpu", capacity=16, roster_capacity=64)
+    rr.rate(matches[:3])
+    before = rr.resident.roster.state.clone()
+    before[:, 1::2] = 7.0  # pretend tags of a live epoch
+    rr.resident.roster.state.copy_(before)
+    rr.rate(matches[3:])
+    assert not torch.equal(rr.resident.roster.state[:, 0::2], before[:, 0::2])
+    rr.rollback()
+    st = rr.resident.roster.state
+    n = rr.resident.n
+    assert torch.equal(st[:n, 0::2].nan_to_num(-1.0), before[:n, 0::2].nan_to_num(-1.0))
+    touched = st[:n, 1::2] == 0.0
+    assert bool(touched.any())  # the restored rows carry zero tags
+    assert bool(((st[:n, 1::2] == 0.0) | (st[:n, 1::2] == 7.0)).all())
+
+
+def test_python_fallback_forgets_resident_rows():
+    """Matches the native engine cannot take (teams > 5) are rated by the Python
+    engine; the device-resident copies of their players are dropped so the next
+    native batch re-reads the store instead of writing back stale ratings."""
+    from analyzer_amd.runtime.resident import ResidentRoster
+
+    res = ResidentRoster("cpu", capacity=8)
+    pls = [Player(api_id="p%d" % i) for i in range(3)]
+    res.rows_for(pls)
+    assert set(res.rows) == {"p0", "p1", "p2"}
+    assert res.forget(["p1", "nope"]) == 1
+    assert set(res.rows) == {"p0", "p2"}
+    again = res.rows_for([pls[1]])
+    assert again[0] == 3  # re-uploaded into a fresh row
