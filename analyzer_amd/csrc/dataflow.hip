@@ -94,6 +94,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   constexpr int SP = (4 + S + 3) / 4 * 4;
   __shared__ __attribute__((aligned(16))) int32_t lpick[kWavesPerBlock][NG][SP];  // v4i slots
   __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
+  // each group's output row, assembled here so it leaves as whole 16-B quads
+  // (one store instruction writes the rows of every group: full lines, where
+  // per-field stores sent 6-7 partial-line writes per match to the fabric)
+  constexpr int OQ = (5 * S + 2 + 3) / 4;
+  __shared__ __attribute__((aligned(16))) float lrow[kWavesPerBlock][NG][4 * OQ];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int j = lane % G;
@@ -562,16 +567,29 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       // match's packed 128-B row (ops/rate.py RateResult) keep them from competing
       // with the roster for cache (-6%) and make each match one line (-3%)
       float* const orm = orows + (int64_t)m * orow;  // [s_mu | s_sig | delta | m_mu | m_sig][S], quality, status
+      float* const lr = lrow[wv][g];
       if (j < S) {
-        __builtin_nontemporal_store(ok ? nsm : NAN, orm + j);
-        __builtin_nontemporal_store(ok ? nss : NAN, orm + S + j);
-        __builtin_nontemporal_store(ok ? dl : NAN, orm + 2 * S + j);
-        __builtin_nontemporal_store(ok ? nmm : NAN, orm + 3 * S + j);
-        __builtin_nontemporal_store(ok ? nms : NAN, orm + 4 * S + j);
+        lr[j] = ok ? nsm : NAN;
+        lr[S + j] = ok ? nss : NAN;
+        lr[2 * S + j] = ok ? dl : NAN;
+        lr[3 * S + j] = ok ? nmm : NAN;
+        lr[4 * S + j] = ok ? nms : NAN;
       }
       if (j == 0) {
-        __builtin_nontemporal_store(gst == kRated ? q : NAN, orm + 5 * S);
-        reinterpret_cast<uint8_t*>(orm + 5 * S + 1)[0] = gst;
+        lr[5 * S] = gst == kRated ? q : NAN;
+        lr[5 * S + 1] = __uint_as_float((uint32_t)gst);  // the status byte, upper bytes 0
+      }
+      if (j == (G > 1 ? 1 : 0)) {
+#pragma unroll
+        for (int k = 5 * S + 2; k < 4 * OQ; ++k) lr[k] = 0.f;  // row padding
+      }
+      // (the group's LDS writes and reads are the same wave's, in order)
+#pragma unroll
+      for (int t = 0; t < (OQ + G - 1) / G; ++t) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const int qd = j + t * G;
+        if (qd < OQ)
+          __builtin_nontemporal_store(reinterpret_cast<const v4f*>(lr)[qd], reinterpret_cast<v4f*>(orm) + qd);
       }
     }
     };
