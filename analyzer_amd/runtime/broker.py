@@ -107,6 +107,7 @@ class Channel:
         self.number = number
         self.prefetch_count = 0  # 0 = unlimited (AMQP default)
         self.consumers: List[Tuple[str, Callable]] = []
+        self.bulk: Dict[int, Callable] = {}  # consumer index -> bulk callback (in-process extension)
         self.unacked: Dict[int, Tuple[str, Message]] = {}
         self._tags = itertools.count(1)
         self.is_open = True
@@ -138,6 +139,12 @@ class Channel:
         if queue not in self.broker.queues:
             raise KeyError("NOT_FOUND - no queue '%s'" % queue)
         tag = "ctag%d.%d" % (self.number, len(self.consumers) + 1)
+        if kwargs.get("bulk_callback") is not None:
+            # in-process extension: deliver every deliverable message of the queue (up to
+            # the prefetch window) in ONE call of bulk_callback(channel, [(method, props,
+            # body), ...]) -- the same deliveries, tags and order as one call per message,
+            # without the per-message Python dispatch
+            self.bulk[len(self.consumers)] = kwargs["bulk_callback"]
         self.consumers.append((queue, callback))
         return tag
 
@@ -191,6 +198,28 @@ class Channel:
                 cb(self, method, msg.properties, msg.body)
                 return True
         return False
+
+    def _deliver_bulk(self) -> int:
+        """Deliveries to a bulk consumer (see basic_consume); 0 if none is ready."""
+        if not self.is_open or not self.bulk:
+            return 0
+        room = self.prefetch_count - len(self.unacked) if self.prefetch_count else 1 << 30
+        if room <= 0:
+            return 0
+        for i, (qname, cb) in enumerate(self.consumers):
+            q = self.broker.queues[qname]
+            bulk = self.bulk.get(i)
+            if bulk is None or not q.ready:
+                continue
+            out = []
+            for _ in range(min(room, len(q.ready))):
+                msg = q.ready.popleft()
+                tag = next(self._tags)
+                self.unacked[tag] = (qname, msg)
+                out.append((Method(tag, msg.routing_key, msg.exchange, msg.redelivered), msg.properties, msg.body))
+            bulk(self, out)
+            return len(out)
+        return 0
 
     def start_consuming(self, until: Optional[Callable[[], bool]] = None) -> None:
         self.broker.run(until=until)
@@ -309,8 +338,13 @@ class MemoryBroker:
         while True:
             progressed = self._fire_due_timers()
             for ch in self.channels:
-                while ch._deliver_one():
-                    n += 1
+                while True:
+                    k = ch._deliver_bulk()
+                    if not k:
+                        if not ch._deliver_one():
+                            break
+                        k = 1
+                    n += k
                     progressed = True
                     self._fire_due_timers()
             if not progressed:

@@ -39,6 +39,7 @@ import torch
 
 from ..config import MODES, TRACK_COLUMNS
 from ..ops import rate as R
+from ..utils.trace import trace_range
 from .objects import STAT_COLUMNS, Match, ParticipantStats
 
 RATING_COLS = tuple(c + s for c in TRACK_COLUMNS for s in ("_mu", "_sigma"))
@@ -289,18 +290,20 @@ class ResidentBatchRater:
             raise ValueError("teams of %d players exceed the batched engine (max %d)" % (K, MAX_TEAM))
         keys = batch.player
         valid = keys >= 0
-        uniq, inv = np.unique(keys[valid], return_inverse=True)
-        rows_u = self.resident.rows_for_keys(uniq, fetch)
+        with trace_range("rate.rows"):
+            uniq, inv = np.unique(keys[valid], return_inverse=True)
+            rows_u = self.resident.rows_for_keys(uniq, fetch)
         slot = np.full(keys.shape, -1, dtype=np.int64)
         slot[valid] = rows_u[inv]
         S = 2 * K
-        rec = np.empty((M, S + 2), dtype=np.int64)
-        rec[:, :S] = slot.reshape(M, S)
-        rec[:, S], rec[:, S + 1] = batch.record_meta()
-        rec_t = torch.from_numpy(rec.astype(np.uint32).view(np.int32)).to(self.device, non_blocking=True)
-        roster = self.resident.roster
-        idx = torch.from_numpy(rows_u).to(self.device, non_blocking=True)
-        self._undo = (idx, roster.state.index_select(0, idx)) if rows_u.size else None
+        with trace_range("rate.encode_h2d"):
+            rec = np.empty((M, S + 2), dtype=np.int64)
+            rec[:, :S] = slot.reshape(M, S)
+            rec[:, S], rec[:, S + 1] = batch.record_meta()
+            rec_t = torch.from_numpy(rec.astype(np.uint32).view(np.int32)).to(self.device, non_blocking=True)
+            roster = self.resident.roster
+            idx = torch.from_numpy(rows_u).to(self.device, non_blocking=True)
+            self._undo = (idx, roster.state.index_select(0, idx)) if rows_u.size else None
         stats = None
         if telemetry is not None:
             from ..ops.telemetry import allocate_stats, make_telemetry
@@ -308,12 +311,14 @@ class ResidentBatchRater:
             stats = allocate_stats(M, K, self.device)
             res = self._eager(rec_t, K, (tel.evoff, tel.events, stats))
         else:
-            g = self._graph(K, M) if self.use_graphs else None
-            res = g.rate(rec_t) if g is not None else self._eager(rec_t, K, None)
-        packed = res.packed.cpu().numpy()
-        final = roster.state.index_select(0, idx).cpu().numpy() if rows_u.size else None
-        if self.device.type == "cuda":
-            self.rater.check_errors(self.device)
+            with trace_range("rate.launch"):
+                g = self._graph(K, M) if self.use_graphs else None
+                res = g.rate(rec_t) if g is not None else self._eager(rec_t, K, None)
+        with trace_range("rate.d2h"):
+            packed = res.packed.cpu().numpy()
+            final = roster.state.index_select(0, idx).cpu().numpy() if rows_u.size else None
+            if self.device.type == "cuda":
+                self.rater.check_errors(self.device)
         status = packed.view(np.uint8)[:, 4 * (5 * S + 1)].copy()
         batch.status = status
         batch.quality = packed[:, 5 * S].astype(np.float64)
