@@ -100,6 +100,11 @@ class WorkerConfig:
     # redelivery after commit-but-before-ack does not rate a match twice.  Off by
     # default: the reference re-rates redelivered matches (worker.py:122-129,194)
     skip_rated: bool = False
+    # new: keep two batches in flight on the columnar native path (runtime/worker.py
+    # "pipelined batches"); prefetch becomes 2 x BATCHSIZE.  Off by default: at
+    # BATCHSIZE=500 the device part of a batch is ~10 us of a ~1 ms host-bound batch,
+    # and the second batch's bookkeeping measured 3-6 % slower (profiles/r3/worker_*)
+    pipeline: bool = False
 
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "WorkerConfig":
@@ -123,6 +128,7 @@ class WorkerConfig:
             synthetic_telemetry=env.get("SYNTHETIC_TELEMETRY") == "true",
             resident=_resident_default(env),
             skip_rated=env.get("SKIP_RATED") == "true",
+            pipeline=env.get("PIPELINE") == "true",
         )
 
     @property

@@ -379,7 +379,11 @@ class BatchRater:
         self._ctrl(device)[16:19].zero_()
 
     def check_errors(self, device, sticky: bool = False) -> None:
-        flags = (self.sticky_flags(device) if sticky else self.error_flags(device)).cpu()
+        self.raise_flags((self.sticky_flags(device) if sticky else self.error_flags(device)).cpu())
+
+    @staticmethod
+    def raise_flags(flags: torch.Tensor) -> None:
+        """Raise on host copies of ``error_flags`` / ``sticky_flags``."""
         if int(flags[0]):
             raise NativeRateError("schedule prepass failed (flag %d)" % int(flags[0]))
         if int(flags[1]):

@@ -37,7 +37,7 @@ import re
 import time
 from collections import deque
 from dataclasses import dataclass, field
-from typing import Callable, Deque, Dict, List, Optional, Tuple
+from typing import Callable, Deque, Dict, List, NamedTuple, Optional, Tuple
 
 
 @dataclass
@@ -49,9 +49,9 @@ class BasicProperties:
     content_type: Optional[str] = None
 
 
-@dataclass
-class Method:
-    """``pika.spec.Basic.Deliver`` subset."""
+class Method(NamedTuple):
+    """``pika.spec.Basic.Deliver`` subset (a named tuple: one is built per
+    delivery, and a tuple costs a fraction of a class instance)."""
 
     delivery_tag: int
     routing_key: str
@@ -67,6 +67,7 @@ class Message:
     routing_key: str
     exchange: str = ""
     redelivered: bool = False
+    queue: str = ""  # the queue holding it (set when routed)
 
 
 class ManualClock:
@@ -108,7 +109,7 @@ class Channel:
         self.prefetch_count = 0  # 0 = unlimited (AMQP default)
         self.consumers: List[Tuple[str, Callable]] = []
         self.bulk: Dict[int, Callable] = {}  # consumer index -> bulk callback (in-process extension)
-        self.unacked: Dict[int, Tuple[str, Message]] = {}
+        self.unacked: Dict[int, Message] = {}  # delivery tag -> message (msg.queue: its queue)
         self._tags = itertools.count(1)
         self.is_open = True
         self.acked = 0
@@ -141,9 +142,10 @@ class Channel:
         tag = "ctag%d.%d" % (self.number, len(self.consumers) + 1)
         if kwargs.get("bulk_callback") is not None:
             # in-process extension: deliver every deliverable message of the queue (up to
-            # the prefetch window) in ONE call of bulk_callback(channel, [(method, props,
-            # body), ...]) -- the same deliveries, tags and order as one call per message,
-            # without the per-message Python dispatch
+            # the prefetch window) in ONE call of bulk_callback(channel, tags, messages)
+            # (a range of delivery tags, the Message objects) -- the same deliveries,
+            # tags and order as one call per message, without the per-message Python
+            # dispatch and Method objects
             self.bulk[len(self.consumers)] = kwargs["bulk_callback"]
         self.consumers.append((queue, callback))
         return tag
@@ -156,17 +158,21 @@ class Channel:
         self.broker.publish(exchange, routing_key, bytes(body), properties or BasicProperties())
 
     def basic_ack(self, delivery_tag: int = 0, multiple: bool = False) -> None:
-        for tag in self._settle(delivery_tag, multiple):
-            self.unacked.pop(tag)
-            self.acked += 1
+        tags = self._settle(delivery_tag, multiple)
+        if multiple and len(tags) == len(self.unacked):
+            self.unacked.clear()
+        else:
+            for tag in tags:
+                self.unacked.pop(tag)
+        self.acked += len(tags)
 
     def basic_nack(self, delivery_tag: int = 0, multiple: bool = False, requeue: bool = True) -> None:
         for tag in self._settle(delivery_tag, multiple):
-            qname, msg = self.unacked.pop(tag)
+            msg = self.unacked.pop(tag)
             self.nacked += 1
             if requeue:
                 msg.redelivered = True
-                self.broker.queues[qname].ready.appendleft(msg)
+                self.broker.queues[msg.queue].ready.appendleft(msg)
             else:
                 self.broker.dead_lettered.append(msg)
 
@@ -175,7 +181,10 @@ class Channel:
 
     def _settle(self, delivery_tag: int, multiple: bool) -> List[int]:
         if multiple:
-            tags = [t for t in self.unacked if t <= delivery_tag or delivery_tag == 0]
+            if self.unacked and (delivery_tag == 0 or delivery_tag >= next(reversed(self.unacked))):
+                return list(self.unacked)  # everything outstanding (tags are issued in order)
+            # unacked is in delivery (= tag) order: the settled tags are a prefix
+            tags = list(itertools.takewhile(lambda t: t <= delivery_tag, self.unacked))
         else:
             if delivery_tag not in self.unacked:
                 raise KeyError("PRECONDITION_FAILED - unknown delivery tag %d" % delivery_tag)
@@ -193,7 +202,7 @@ class Channel:
             if q.ready:
                 msg = q.ready.popleft()
                 tag = next(self._tags)
-                self.unacked[tag] = (qname, msg)
+                self.unacked[tag] = msg
                 method = Method(tag, msg.routing_key, msg.exchange, msg.redelivered)
                 cb(self, method, msg.properties, msg.body)
                 return True
@@ -211,14 +220,14 @@ class Channel:
             bulk = self.bulk.get(i)
             if bulk is None or not q.ready:
                 continue
-            out = []
-            for _ in range(min(room, len(q.ready))):
-                msg = q.ready.popleft()
-                tag = next(self._tags)
-                self.unacked[tag] = (qname, msg)
-                out.append((Method(tag, msg.routing_key, msg.exchange, msg.redelivered), msg.properties, msg.body))
-            bulk(self, out)
-            return len(out)
+            pop, ready = q.ready.popleft, q.ready
+            msgs = [pop() for _ in range(min(room, len(ready)))]
+            t0 = next(self._tags)
+            self._tags = itertools.count(t0 + len(msgs))
+            tags = range(t0, t0 + len(msgs))
+            self.unacked.update(zip(tags, msgs))
+            bulk(self, tags, msgs)
+            return len(msgs)
         return 0
 
     def start_consuming(self, until: Optional[Callable[[], bool]] = None) -> None:
@@ -230,9 +239,9 @@ class Channel:
     def close(self) -> None:
         """Channel death: unacknowledged deliveries go back to their queues."""
         for tag in sorted(self.unacked, reverse=True):
-            qname, msg = self.unacked.pop(tag)
+            msg = self.unacked.pop(tag)
             msg.redelivered = True
-            self.broker.queues[qname].ready.appendleft(msg)
+            self.broker.queues[msg.queue].ready.appendleft(msg)
         self.is_open = False
         self.consumers = []
 
@@ -298,7 +307,7 @@ class MemoryBroker:
             self.dropped.append(msg)
             return
         for q in targets:
-            self.queues[q].ready.append(Message(body, properties, routing_key, exchange))
+            self.queues[q].ready.append(Message(body, properties, routing_key, exchange, queue=q))
 
     def depth(self, queue: str) -> int:
         q = self.queues.get(queue)

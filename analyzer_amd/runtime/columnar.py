@@ -29,8 +29,10 @@ from dataclasses import dataclass, field
 from typing import Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 
 import numpy as np
+import torch
 
 from ..config import MODES, TRACK_COLUMNS
+from ..ops.native import native
 from .objects import (STAT_COLUMNS, Match, Participant, ParticipantItems, ParticipantStats, Player,
                       Roster)
 
@@ -80,6 +82,8 @@ class MatchBatch:
     final_keys: Optional[np.ndarray] = None    # [U] player keys of rated matches
     final: Optional[np.ndarray] = None         # [U, 14] their final (mu, sigma) per track
     final_tracks: Optional[np.ndarray] = None  # [U, 7] the tracks the batch wrote
+    fields: Optional[np.ndarray] = None        # [5, M, 2, K] backing of s_mu .. m_sig (native finish)
+    key_bound: Optional[int] = None            # every player key is below this (columnar store)
 
     @property
     def K(self) -> int:
@@ -152,6 +156,11 @@ class _Cols:
 class ColumnarStore:
     """The reference's tables as numpy columns (see the module doc)."""
 
+    # a session writes only at commit and a batch's load reads match structure and
+    # the stored ratings of players no earlier batch touched, so the pipelined
+    # worker may load batch i+1 while batch i's session is still open
+    concurrent_sessions = True
+
     def __init__(self):
         self.players = _Cols(rating=((14,), np.float64, NAN), attr=((3,), np.float64, NAN))
         self.pl_ids: List[str] = []
@@ -171,6 +180,22 @@ class ColumnarStore:
         self.p_index: Dict[str, int] = {}
         self.assets_by_match: Dict[str, List[str]] = {}
         self.commits = 0
+        self._mkey = None  # native KeyIndex over m_ids (built on first batch lookup)
+
+    def __getstate__(self):  # copies rebuild the native index
+        d = dict(self.__dict__)
+        d["_mkey"] = None
+        return d
+
+    def match_rows(self, ids: List) -> np.ndarray:
+        """Store rows of match api ids (str or bytes), -1 where absent: one batched
+        native lookup (csrc/batch_host.cpp KeyIndex), kept in step with m_ids."""
+        if self._mkey is None:
+            self._mkey = native().KeyIndex()
+        k = len(self._mkey)
+        if k < len(self.m_ids):
+            self._mkey.add(self.m_ids[k:], k)
+        return self._mkey.lookup(ids).numpy()
 
     # ------------------------------------------------------------- loading
     def add_players(self, players: Iterable[Player]) -> None:
@@ -320,13 +345,33 @@ class ColumnarSession:
 
     # ------------------------------------------------------------- columnar
     def _rows(self, ids: Iterable[str]) -> np.ndarray:
-        idx = self.store.m_index
-        rows = np.array(sorted({idx[i] for i in ids if i in idx}), dtype=np.int64)
+        rows = self.store.match_rows(ids if isinstance(ids, list) else list(ids))
+        rows = np.unique(rows[rows >= 0])
         if rows.size:  # ORDER BY created_at (ties: insertion order)
             rows = rows[np.argsort(self.store.matches.created[rows], kind="stable")]
         return rows
 
     def load_batch(self, ids: Iterable[str], chunksize: int = 100) -> MatchBatch:
+        """The batch's columns in one native pass (csrc/batch_host.cpp batch_gather);
+        ``_load_batch_numpy`` is the vectorised reference the tests compare with."""
+        st = self.store
+        rows = self._rows(ids)
+        mt, rt, pt = st.matches, st.rosters, st.parts
+        t = torch.from_numpy
+        mode, nr, n, winner, afk, player, part = (x.numpy() for x in native().batch_gather(
+            t(rows), t(mt.nr), t(mt.r0), t(mt.mode), t(rt.np_), t(rt.winner), t(rt.p0), t(pt.player), t(pt.afk)))
+        extra: Dict[int, List[int]] = {}
+        for i in np.nonzero(nr > 2)[0]:  # participants of rosters beyond the second
+            r0 = int(mt.r0[rows[i]])
+            extra[int(i)] = [p for r in range(r0 + 2, r0 + int(nr[i]))
+                             for p in range(int(rt.p0[r]), int(rt.p0[r]) + int(rt.np_[r]))]
+        b = MatchBatch(ids=list(map(st.m_ids.__getitem__, rows.tolist())), mode=mode, nrosters=nr, n=n, winner=winner,
+                       afk=afk, player=player, part=part, rows=rows, extra_parts=extra,
+                       key_bound=st.players.n)
+        self._batches.append(b)
+        return b
+
+    def _load_batch_numpy(self, ids: Iterable[str], chunksize: int = 100) -> MatchBatch:
         st = self.store
         rows = self._rows(ids)
         M = len(rows)
@@ -367,12 +412,37 @@ class ColumnarSession:
         """Stored (ratings [n,14], attributes [n,3]) of player rows (resident upload)."""
         return self.store.players.rating[keys], self.store.players.attr[keys]
 
+    def stage_players(self, keys: torch.Tensor, out: torch.Tensor) -> None:
+        """``fetch_players`` straight into resident upload rows [n, 36]
+        (csrc/batch_host.cpp batch_stage_players)."""
+        pl = self.store.players
+        native().batch_stage_players(keys, torch.from_numpy(pl.rating), torch.from_numpy(pl.attr), out)
+
     def _write_batch(self, b: MatchBatch) -> None:
+        """One native pass (csrc/batch_host.cpp batch_commit) for the first two
+        rosters; rosters beyond the second and telemetry stats here."""
         st = self.store
         mt, pt = st.matches, st.parts
         stt = b.status
         if stt is None:
             return
+        if b.fields is None:
+            return self._write_batch_numpy(b)
+        t = torch.from_numpy
+        native().batch_commit(t(b.rows), t(stt), t(b.quality), t(b.part), t(b.fields), t(b.mode),
+                              t(b.final_keys), t(b.final), t(b.final_tracks), t(mt.quality), t(pt.i_afk),
+                              t(pt.ts), t(pt.i_rating), t(st.players.rating))
+        for i, ps in b.extra_parts.items():
+            if stt[i] in (RATED, AFK, INVALID):
+                pt.i_afk[ps] = 0 if stt[i] == RATED else 1
+        if b.stats is not None:
+            sel = (stt == RATED)[:, None, None] & (b.part >= 0)
+            pt.stats[b.part[sel]] = b.stats[sel]
+
+    def _write_batch_numpy(self, b: MatchBatch) -> None:
+        st = self.store
+        mt, pt = st.matches, st.parts
+        stt = b.status
         rated = stt == RATED
         afkm = (stt == AFK) | (stt == INVALID)
         mt.quality[b.rows[rated]] = b.quality[rated]

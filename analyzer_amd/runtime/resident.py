@@ -91,21 +91,34 @@ class ResidentRoster:
             rows[new] = nr
         return rows
 
-    def _upload_arrays(self, vals: np.ndarray, attrs: np.ndarray) -> None:
-        """Append rows from stored ratings [k, 14] (NaN = NULL) and attributes [k, 3]."""
-        base, k = self.n, vals.shape[0]
+    def staging(self, k: int) -> torch.Tensor:
+        """Host buffer [k, 36] for ``upload_staged`` (pinned on a GPU)."""
+        return torch.empty((k, 36), dtype=torch.float32, pin_memory=self.device.type == "cuda")
+
+    def upload_staged(self, buf: torch.Tensor) -> None:
+        """Append rows staged as [k, 36] = state row (32) + attributes (4): one
+        asynchronous H2D copy."""
+        base, k = self.n, buf.shape[0]
         if base + k > self.capacity:
             self._grow(base + k)
-        st = np.zeros((k, 32), dtype=np.float32)
-        st[:, 0::2] = np.nan
+        dev = buf.to(self.device, non_blocking=True)
+        self.roster.state[base:base + k].copy_(dev[:, :32])
+        self.roster.attrs[base:base + k].copy_(dev[:, 32:])
+        self.n = base + k
+
+    def _upload_arrays(self, vals: np.ndarray, attrs: np.ndarray) -> None:
+        """Append rows from stored ratings [k, 14] (NaN = NULL) and attributes [k, 3]."""
+        k = vals.shape[0]
+        buf = self.staging(k)
+        st = buf.numpy()
+        st[:, 0:32] = 0.0
         mu = vals[:, 0::2]
         st[:, 0:28:4] = mu
         st[:, 2:28:4] = np.where(np.isnan(mu), np.nan, vals[:, 1::2])
-        at = np.zeros((k, 4), dtype=np.float32)
-        at[:, :3] = attrs
-        self.roster.state[base:base + k].copy_(torch.from_numpy(st))
-        self.roster.attrs[base:base + k].copy_(torch.from_numpy(at))
-        self.n = base + k
+        st[:, 28:32:2] = np.nan
+        st[:, 32:35] = attrs
+        st[:, 35] = 0.0
+        self.upload_staged(buf)
 
     @property
     def capacity(self) -> int:
@@ -276,80 +289,106 @@ class ResidentBatchRater:
             self.rater.check_errors(self.device)
         return st
 
-    def rate_batch(self, batch, fetch, telemetry=None) -> np.ndarray:
+    def rate_batch(self, batch, fetch, telemetry=None, stage=None) -> np.ndarray:
         """Rate a columnar ``MatchBatch`` (runtime/columnar.py) in order and fill
         its result columns; ``fetch(keys)`` gives the stored ratings of players
         the resident roster has not seen.  Returns the status per match."""
-        from .columnar import RATED
+        return self.finish_batch(self.launch_batch(batch, fetch, telemetry, stage))
 
+    def launch_batch(self, batch, fetch, telemetry=None, stage=None) -> "PendingBatch":
+        """First half of ``rate_batch``: encode, upload, launch and enqueue the
+        copies back into pinned buffers -- nothing waits on the device, so the
+        worker can prepare the next batch (or finish the previous one) while
+        this one rates.  Launches are stream-ordered: a batch launched after
+        another rates from that one's results.  ``stage(keys, out)`` (optional,
+        the columnar store's) writes new players' upload rows directly instead
+        of ``fetch``."""
         M, K = len(batch), batch.K
-        if M == 0:
-            batch.status = np.zeros(0, dtype=np.uint8)
-            return batch.status
         if K > MAX_TEAM:
             raise ValueError("teams of %d players exceed the batched engine (max %d)" % (K, MAX_TEAM))
-        keys = batch.player
-        valid = keys >= 0
+        if M == 0:
+            return PendingBatch(batch, K)
+        C = R.native()
+        t = torch.from_numpy
+        res_ = self.resident
         with trace_range("rate.rows"):
-            uniq, inv = np.unique(keys[valid], return_inverse=True)
-            rows_u = self.resident.rows_for_keys(uniq, fetch)
-        slot = np.full(keys.shape, -1, dtype=np.int64)
-        slot[valid] = rows_u[inv]
-        S = 2 * K
+            top = batch.key_bound if batch.key_bound is not None else int(batch.player.max()) + 1
+            if top > res_.by_key.size:
+                grown = np.full(max(top, 2 * res_.by_key.size), -1, dtype=np.int64)
+                grown[:res_.by_key.size] = res_.by_key
+                res_.by_key = grown
+            # records, the batch's unique players (first-seen order) and their resident
+            # rows; players not resident yet were given the next rows (csrc/batch_host.cpp)
+            rec_c, uniq_t, rows_t, pos_t, new_t = C.batch_encode(
+                t(batch.player), t(batch.mode), t(batch.n), t(batch.nrosters), t(batch.winner),
+                t(batch.afk), t(res_.by_key), res_.n)
+            if new_t.numel():
+                nk = new_t.numpy()
+                try:
+                    if stage is not None:
+                        buf = res_.staging(nk.size)
+                        stage(new_t, buf)
+                        res_.upload_staged(buf)
+                    else:
+                        ratings, attrs = fetch(nk)
+                        res_._upload_arrays(np.asarray(ratings, dtype=np.float64),
+                                            np.asarray(attrs, dtype=np.float64))
+                except BaseException:  # the map must not keep rows that were never written
+                    res_.by_key[nk] = -1
+                    raise
         with trace_range("rate.encode_h2d"):
-            rec = np.empty((M, S + 2), dtype=np.int64)
-            rec[:, :S] = slot.reshape(M, S)
-            rec[:, S], rec[:, S + 1] = batch.record_meta()
-            rec_t = torch.from_numpy(rec.astype(np.uint32).view(np.int32)).to(self.device, non_blocking=True)
-            roster = self.resident.roster
-            idx = torch.from_numpy(rows_u).to(self.device, non_blocking=True)
-            self._undo = (idx, roster.state.index_select(0, idx)) if rows_u.size else None
-        stats = None
+            rec_t = rec_c.to(self.device, non_blocking=True)
+            roster = res_.roster
+            idx = rows_t.to(self.device, non_blocking=True)
+            undo = (idx, roster.state.index_select(0, idx)) if rows_t.numel() else None
+        self._undo = undo
+        p = PendingBatch(batch, K, pos_t, uniq_t, undo=undo)
         if telemetry is not None:
             from ..ops.telemetry import allocate_stats, make_telemetry
             tel = make_telemetry(telemetry, rec_t, K)
-            stats = allocate_stats(M, K, self.device)
-            res = self._eager(rec_t, K, (tel.evoff, tel.events, stats))
+            p.stats = allocate_stats(M, K, self.device)
+            res = self._eager(rec_t, K, (tel.evoff, tel.events, p.stats))
         else:
             with trace_range("rate.launch"):
                 g = self._graph(K, M) if self.use_graphs else None
                 res = g.rate(rec_t) if g is not None else self._eager(rec_t, K, None)
+        # outputs, the players' final rows and the error flags: asynchronous
+        # copies into pinned buffers, one event to wait on
+        p.packed = _to_host(res.packed)
+        p.final = _to_host(roster.state.index_select(0, idx)) if rows_t.numel() else None
+        if self.device.type == "cuda":
+            p.flags = _to_host(self.rater.error_flags(self.device))
+            if p.stats is not None:
+                p.stats = _to_host(p.stats)
+            p.event = torch.cuda.Event()
+            p.event.record()
+        return p
+
+    def finish_batch(self, p: "PendingBatch") -> np.ndarray:
+        """Second half of ``rate_batch``: wait for the batch's copies and fill its
+        result columns (csrc/batch_host.cpp batch_finish)."""
+        batch, K = p.batch, p.K
+        M = len(batch)
+        if M == 0:
+            batch.status = np.zeros(0, dtype=np.uint8)
+            return batch.status
         with trace_range("rate.d2h"):
-            packed = res.packed.cpu().numpy()
-            final = roster.state.index_select(0, idx).cpu().numpy() if rows_u.size else None
-            if self.device.type == "cuda":
-                self.rater.check_errors(self.device)
-        status = packed.view(np.uint8)[:, 4 * (5 * S + 1)].copy()
+            if p.event is not None:
+                p.event.synchronize()
+                self.rater.raise_flags(p.flags)
+        with trace_range("rate.finish"):
+            empty = torch.zeros(0, dtype=torch.float32)
+            status_t, quality_t, fields_t, fk_t, fv_t, ft_t = R.native().batch_finish(
+                p.packed, p.final if p.final is not None else empty, torch.from_numpy(batch.mode), p.pos,
+                p.uniq, K)
+        status = status_t.numpy()
         batch.status = status
-        batch.quality = packed[:, 5 * S].astype(np.float64)
-        shape = (M, 2, K)
-        batch.s_mu, batch.s_sig, batch.delta, batch.m_mu, batch.m_sig = (
-            packed[:, f * S:(f + 1) * S].astype(np.float64).reshape(shape) for f in range(5))
-        if stats is not None:
-            batch.stats = stats.cpu().double().numpy().reshape(M, 2, K, -1)
-        # final ratings of the players of rated matches, on the tracks those matches touched
-        rated = status == RATED
-        touched = np.zeros((uniq.size, 7), dtype=bool)
-        if rated.any():
-            pos = np.full(keys.shape, -1, dtype=np.int64)
-            pos[valid] = inv
-            pr = pos[rated]                                   # [R, 2, K]
-            md = np.broadcast_to(batch.mode[rated][:, None, None], pr.shape)
-            ok = pr >= 0
-            touched[pr[ok], 0] = True
-            touched[pr[ok], 1 + md[ok]] = True
-        has = touched.any(axis=1)
-        batch.final_keys = uniq[has]
-        if final is not None and has.any():
-            f = final[has].astype(np.float64)
-            vals = np.empty((f.shape[0], 14))
-            vals[:, 0::2] = f[:, 0:28:4]
-            vals[:, 1::2] = f[:, 2:28:4]
-            batch.final = vals
-            batch.final_tracks = touched[has]
-        else:
-            batch.final = np.zeros((0, 14))
-            batch.final_tracks = np.zeros((0, 7), dtype=bool)
+        batch.quality = quality_t.numpy()
+        batch.fields = fields_t.numpy()
+        batch.s_mu, batch.s_sig, batch.delta, batch.m_mu, batch.m_sig = batch.fields
+        if p.stats is not None:
+            batch.stats = p.stats.double().numpy().reshape(M, 2, K, -1)
+        batch.final_keys, batch.final, batch.final_tracks = fk_t.numpy(), fv_t.numpy(), ft_t.numpy()
         return status
 
     def _eager(self, rec, K, telemetry):
@@ -363,16 +402,21 @@ class ResidentBatchRater:
         self._clock.launched()
         return res
 
-    def rollback(self) -> None:
-        """Undo the last batch on the device roster (the store rolled back)."""
-        if self._undo is not None:
-            idx, saved = self._undo
+    def rollback(self, pending: Optional["PendingBatch"] = None) -> None:
+        """Undo the last batch (or ``pending``) on the device roster (the store
+        rolled back).  With several batches launched, undo the latest first."""
+        undo = self._undo if pending is None else pending.undo
+        if pending is not None:
+            pending.undo = None
+        if undo is not None:
+            idx, saved = undo
             # the snapshot may predate an EpochClock reset (before_launch renumbers
             # epochs after 255 launches): restore values with zeroed tag words, which
             # no launch's epoch ever matches, as unpack_rows does
             saved = saved.clone()
             saved[:, 1::2] = 0.0
             self.resident.roster.state.index_copy_(0, idx, saved)
+        if self._undo is undo:
             self._undo = None
 
     def commit(self) -> None:
@@ -443,6 +487,24 @@ class ResidentBatchRater:
                 setattr(pl, _MU[t], _f(float(row[4 * t])))
                 setattr(pl, _SIG[t], _f(float(row[4 * t + 2])))
         return status
+
+
+class PendingBatch:
+    """A launched columnar batch (``ResidentBatchRater.launch_batch``)."""
+
+    def __init__(self, batch, K: int, pos=None, uniq=None, undo=None):
+        self.batch, self.K, self.pos, self.uniq, self.undo = batch, K, pos, uniq, undo
+        self.packed = self.final = self.flags = self.stats = self.event = None
+
+
+def _to_host(src: torch.Tensor) -> torch.Tensor:
+    """``src`` on the host: on a GPU an asynchronous copy into pinned memory
+    (PyTorch's caching host allocator recycles the buffers)."""
+    if src.device.type != "cuda":
+        return src.contiguous()
+    out = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+    out.copy_(src, non_blocking=True)
+    return out
 
 
 def _write_stats(matches, stats: torch.Tensor, K: int) -> None:

@@ -48,7 +48,9 @@ are kept in ``stats`` and logged as one JSON line per batch (SURVEY §5 metrics)
 from __future__ import annotations
 
 import json
+import logging
 import time
+from operator import attrgetter
 
 import numpy as np
 from dataclasses import dataclass, field
@@ -94,12 +96,15 @@ class Worker:
         self.rabbit = broker
         self.clock = clock
         self.channel = None
-        self.queue: List[Tuple[B.Method, B.BasicProperties, bytes]] = []
+        self.queue = Deliveries()
         self.timer = None
         self.stats = WorkerStats()
         self.failed_ids: List[str] = []
         self._python_rater = MatchRater(self.rater_cfg)
         self._object_rater = object_rater  # runtime.batch.ObjectBatchRater, built lazily
+        self._pipe = False
+        self._inflight: Optional[_InFlight] = None  # launched, not yet committed / acked
+        self._flush = None                          # timer completing it when no batch follows
 
     # ------------------------------------------------------------ connect (W3/W4)
     def connect(self) -> "Worker":
@@ -124,7 +129,9 @@ class Worker:
             ch.queue_declare(queue=q, durable=True)
         if self.cfg.dosewmatch:
             ch.queue_declare(queue=self.cfg.sew_queue, durable=True)
-        ch.basic_qos(prefetch_count=self.cfg.batchsize)
+        self._pipe = self._pipelined()
+        # pipelined: batch i+1 is delivered and launched before batch i is acked
+        ch.basic_qos(prefetch_count=self.cfg.batchsize * (2 if self._pipe else 1))
         if hasattr(ch, "_deliver_bulk"):  # the in-process broker: whole prefetch windows per call
             ch.basic_consume(self.newjob, queue=self.cfg.queue, bulk_callback=self.newjobs)
         else:
@@ -134,22 +141,23 @@ class Worker:
 
     # ------------------------------------------------------------ batcher (W5)
     def newjob(self, _ch, method, properties, body) -> None:
-        self.queue.append((method, properties, body))
+        self.queue.append(method, properties, body)
         if self.timer is None:
             self.timer = self.rabbit.add_timeout(self.cfg.idle_timeout, self.try_process)
         if len(self.queue) == self.cfg.batchsize:
             self.try_process()
 
-    def newjobs(self, _ch, deliveries) -> None:
-        """``newjob`` for a list of deliveries (the in-process broker's bulk path):
-        the same batches -- the timer armed by the first message of a batch, a
-        flush at exactly BATCHSIZE -- without one Python call per message."""
-        i, n, cap = 0, len(deliveries), self.cfg.batchsize
+    def newjobs(self, _ch, tags, messages) -> None:
+        """``newjob`` for a run of deliveries (the in-process broker's bulk path:
+        a range of delivery tags and their messages): the same batches -- the
+        timer armed by the first message of a batch, a flush at exactly
+        BATCHSIZE -- without one Python call per message."""
+        i, n, cap = 0, len(messages), self.cfg.batchsize
         while i < n:
             if self.timer is None:
                 self.timer = self.rabbit.add_timeout(self.cfg.idle_timeout, self.try_process)
             take = min(n - i, cap - len(self.queue))
-            self.queue.extend(deliveries[i:i + take])
+            self.queue.extend(tags[i:i + take], messages[i:i + take])
             i += take
             if len(self.queue) == cap:
                 self.try_process()
@@ -159,30 +167,39 @@ class Worker:
         if self.timer is not None:
             self.rabbit.remove_timeout(self.timer)
             self.timer = None
-        batch, self.queue = self.queue, []
+        batch, self.queue = self.queue, Deliveries()
+        if self._pipe:
+            self._pipeline_step(batch)
+            return
         if not batch:
             return
         t0 = time.perf_counter()
         try:
             failed = set(self.process(batch))
         except Exception as e:  # the whole batch goes to the failed queue (worker.py:110-120)
-            logger.error(e)
-            for meth, prop, body in batch:
-                self._publish("", self.cfg.failed_queue, body, prop)
-                self.channel.basic_nack(meth.delivery_tag, requeue=False)
-                self.stats.nacked += 1
-            self.stats.failed_batches += 1
-            self.stats.seconds += time.perf_counter() - t0
+            self._fail_batch(batch, e, t0)
             return
+        self._settle(batch, failed, t0)
 
+    def _fail_batch(self, batch, e: Exception, t0: float) -> None:
+        logger.error(e)
+        for meth, prop, body in batch:
+            self._publish("", self.cfg.failed_queue, body, prop)
+            self.channel.basic_nack(meth.delivery_tag, requeue=False)
+            self.stats.nacked += 1
+        self.stats.failed_batches += 1
+        self.stats.seconds += time.perf_counter() - t0
+
+    def _settle(self, batch, failed, t0: float) -> None:
+        """Ack a processed batch and fan out (worker.py:122-166)."""
         logger.info("acking batch")
         session = self.store.session() if self.cfg.dotelesuckmatch else None
         try:
             with trace_range("ack"):
-                # The batch is every unacknowledged delivery of the channel (prefetch =
-                # BATCHSIZE, one batch in flight), so after the quarantined ones are
-                # nacked ONE basic_ack(multiple=True) of the highest good tag settles the
-                # rest -- what the reference's per-message acks do, in one frame
+                # every delivery of the batch is settled: the quarantined ones are
+                # nacked, then ONE basic_ack(multiple=True) of the highest good tag
+                # settles the rest -- what the reference's per-message acks do, in one
+                # frame (a later batch in flight holds only higher tags)
                 if failed:
                     ok_tags = []
                     for meth, prop, body in batch:
@@ -193,12 +210,12 @@ class Worker:
                         else:
                             ok_tags.append(meth.delivery_tag)
                 else:
-                    ok_tags = [meth.delivery_tag for meth, _, _ in batch]
+                    ok_tags = batch.tags
                 if ok_tags:
                     self.channel.basic_ack(max(ok_tags), multiple=True)
                     self.stats.acked += len(ok_tags)
                 fanout = self.cfg.docrunchmatch or self.cfg.dosewmatch or self.cfg.dotelesuckmatch
-                for meth, prop, body in batch:
+                for meth, prop, body in (batch if fanout or batch.any_headers() else ()):
                     headers = (prop.headers if prop is not None else None) or {}
                     if not fanout and not headers:
                         continue
@@ -221,6 +238,97 @@ class Worker:
         self.stats.batches += 1
         self.stats.seconds += time.perf_counter() - t0
 
+    # ------------------------------------------------------------ pipelined batches
+    # ENGINE=native on an in-process columnar store keeps TWO batches in flight:
+    # batch i+1 is loaded, encoded and launched (runtime/resident.launch_batch)
+    # before batch i is finished, committed and acked, so the device work and the
+    # copies back of one batch overlap the host stages of the other.  Launches are
+    # stream-ordered, so batch i+1 rates from batch i's results exactly as the
+    # serial worker would; commits and acks stay in batch order.  When batch i
+    # fails as a whole (QUARANTINE=false error, failed commit), batch i+1 is
+    # rolled back on the device first, then batch i, and batch i+1 is launched
+    # again from the restored state -- the serial path's outcome (test:
+    # tests/test_worker.py::test_pipelined_worker_is_the_serial_worker).  A batch
+    # in flight with no successor is completed by a 1-ms timer.
+    def _pipelined(self) -> bool:
+        return bool(self.cfg.pipeline and self.cfg.engine == "native" and self.cfg.resident
+                    and not self.cfg.skip_rated and getattr(self.store, "concurrent_sessions", False))
+
+    def _pipeline_step(self, batch) -> None:
+        if self._flush is not None:
+            self.rabbit.remove_timeout(self._flush)
+            self._flush = None
+        nxt = self._launch(batch) if batch else None
+        prev, self._inflight = self._inflight, None
+        if prev is not None:
+            self._complete(prev, later=nxt)
+        if nxt is None:
+            return
+        if nxt.error is not None:  # load / launch failed: the whole batch fails
+            self._fail_batch(nxt.batch, nxt.error, nxt.t0)
+            return
+        self._inflight = nxt
+        self._flush = self.rabbit.add_timeout(min(self.cfg.idle_timeout, 0.001), self._flush_inflight)
+
+    def _flush_inflight(self) -> None:
+        self._flush = None
+        prev, self._inflight = self._inflight, None
+        if prev is not None:
+            self._complete(prev)
+
+    def _launch(self, batch, fl: Optional["_InFlight"] = None) -> "_InFlight":
+        t0 = time.perf_counter()
+        if fl is None:
+            fl = _InFlight(batch, t0)
+            fl.ids = batch.match_ids()
+            self.stats.messages += len(batch)
+        try:
+            if fl.session is None:
+                fl.session = self.store.session()
+                with trace_range("load", ids=len(fl.ids)):
+                    fl.mb = fl.session.load_batch(fl.ids, self.cfg.chunksize)
+            # the telemetry seed of the serial worker: batches committed before this one
+            seed_batches = self.stats.batches + (1 if self._inflight is not None else 0)
+            with trace_range("rate", matches=len(fl.mb), engine="native"):
+                fl.pending = self._batched().launch_batch(fl.mb, fl.session.fetch_players,
+                                                          telemetry=self._telemetry_spec(seed_batches),
+                                                          stage=getattr(fl.session, "stage_players", None))
+        except Exception as e:
+            fl.session.rollback()
+            fl.session.close()
+            fl.error, fl.pending = e, None
+        fl.seconds += time.perf_counter() - t0
+        return fl
+
+    def _complete(self, fl: "_InFlight", later: Optional["_InFlight"] = None) -> None:
+        t0 = time.perf_counter()
+        rater, counts = self._batched(), {}
+        try:
+            status = rater.finish_batch(fl.pending)
+            quarantined = self._statuses(fl.mb, status, counts)
+            with trace_range("commit"):
+                fl.session.commit()
+        except Exception as e:
+            if later is not None and later.pending is not None:
+                rater.rollback(later.pending)  # the later batch first: it rated on top of this one
+            fl.session.rollback()
+            rater.rollback(fl.pending)
+            fl.session.close()
+            self._fail_batch(fl.batch, e, t0 - fl.seconds)
+            if later is not None and later.pending is not None:
+                self._launch(later.batch, later)  # again, from the restored state
+            return
+        fl.session.close()
+        fl.pending.undo = None
+        self.stats.matches += len(fl.mb)
+        self.stats.quarantined += len(quarantined)
+        self.failed_ids += quarantined
+        if logger.isEnabledFor(logging.INFO):
+            logger.info(json.dumps({"batch": self.stats.batches, "messages": len(fl.batch),
+                                    "matches": len(fl.mb), "engine": self.cfg.engine,
+                                    "quarantined": len(quarantined), **counts}))
+        self._settle(fl.batch, set(quarantined), t0 - fl.seconds)
+
     def _publish(self, exchange: str, key: str, body, props) -> None:
         self.channel.basic_publish(exchange=exchange, routing_key=key, body=body, properties=props)
         self.stats.bump(key if exchange == "" else exchange)
@@ -231,7 +339,7 @@ class Worker:
         (after rolling back) when the batch must fail as a whole."""
         batch = self.queue if batch is None else batch
         logger.info("analyzing batch %s", str(len(batch)))
-        ids = list(set(_decode(body) for _, _, body in batch))
+        ids = batch.match_ids() if isinstance(batch, Deliveries) else list(set(_decode(b) for _, _, b in batch))
         self.stats.messages += len(batch)
         session = self.store.session()
         quarantined: List[str] = []
@@ -273,9 +381,10 @@ class Worker:
         self.stats.matches += len(matches)
         self.stats.quarantined += len(quarantined)
         self.failed_ids += quarantined
-        logger.info(json.dumps({"batch": self.stats.batches, "messages": len(batch),
-                                "matches": len(matches), "engine": self.cfg.engine,
-                                "quarantined": len(quarantined), **counts}))
+        if logger.isEnabledFor(logging.INFO):
+            logger.info(json.dumps({"batch": self.stats.batches, "messages": len(batch),
+                                    "matches": len(matches), "engine": self.cfg.engine,
+                                    "quarantined": len(quarantined), **counts}))
         return quarantined
 
     def _rate_python(self, session, matches, counts) -> List[str]:
@@ -316,25 +425,34 @@ class Worker:
                 self._object_rater = ObjectBatchRater(BatchRater(self.rater_cfg))
         return self._object_rater
 
-    def _telemetry_spec(self):
+    def _telemetry_spec(self, batches_before: Optional[int] = None):
         if not self.cfg.dotelemetry:
             return None
         from ..ops.telemetry import TelemetrySpec
         lo, hi = (int(x) for x in self.cfg.telemetry_events.split(","))
-        return TelemetrySpec(seed=self.stats.batches + 1, min_events=lo, max_events=hi)
+        before = self.stats.batches if batches_before is None else batches_before
+        return TelemetrySpec(seed=before + 1, min_events=lo, max_events=hi)
 
     def _rate_batch(self, batch, session, counts) -> List[str]:
         from ..ops import rate as R
 
         if len(batch) == 0:
             return []
-        status = self._batched().rate_batch(batch, session.fetch_players, telemetry=self._telemetry_spec())
-        vals, num = np.unique(status, return_counts=True)
-        for v, c in zip(vals.tolist(), num.tolist()):
+        status = self._batched().rate_batch(batch, session.fetch_players, telemetry=self._telemetry_spec(),
+                                            stage=getattr(session, "stage_players", None))
+        return self._statuses(batch, status, counts)
+
+    def _statuses(self, batch, status, counts) -> List[str]:
+        """Count a rated batch's statuses; its quarantined match ids (raises with
+        QUARANTINE=false)."""
+        from ..ops import rate as R
+
+        num = np.bincount(status, minlength=256)
+        for v in np.flatnonzero(num).tolist():
             name = R.STATUS_NAMES.get(v, str(v))
-            counts[name] = counts.get(name, 0) + c
-        badmask = np.isin(status, list(R.ERROR_STATUSES) + [R.NOT_PROCESSED])
-        bad = [batch.ids[i] for i in np.nonzero(badmask)[0].tolist()]
+            counts[name] = counts.get(name, 0) + int(num[v])
+        bad = ([batch.ids[i] for i in np.flatnonzero(_BAD_STATUS[status]).tolist()]
+               if num[_BAD_STATUS].any() else [])
         if bad and not self.cfg.quarantine:
             raise MatchError("%d match(es) failed to rate (first: %s)" % (len(bad), bad[0]))
         return bad
@@ -360,6 +478,73 @@ class Worker:
     def run(self) -> None:
         self.connect()
         self.start_consuming()
+
+
+class Deliveries:
+    """A batch of deliveries as parallel lists (tags, properties, bodies);
+    iterating yields the ``(method, properties, body)`` triples of the per-message
+    callback, built only on the paths that need them (failures, fan-out)."""
+
+    __slots__ = ("tags", "props", "bodies")
+
+    def __init__(self):
+        self.tags: List[int] = []
+        self.props: List[Optional[B.BasicProperties]] = []
+        self.bodies: List[bytes] = []
+
+    def append(self, method, props, body) -> None:
+        self.tags.append(method.delivery_tag)
+        self.props.append(props)
+        self.bodies.append(body)
+
+    def extend(self, tags, messages) -> None:
+        self.tags.extend(tags)
+        self.props.extend([m.properties for m in messages])
+        self.bodies.extend([m.body for m in messages])
+
+    def __len__(self) -> int:
+        return len(self.tags)
+
+    def __iter__(self):
+        for t, p, b in zip(self.tags, self.props, self.bodies):
+            yield B.Method(t, ""), p, b
+
+    def any_headers(self) -> bool:
+        try:
+            return any(map(_headers, self.props))
+        except AttributeError:  # deliveries without properties
+            return any(p is not None and p.headers for p in self.props)
+
+    def match_ids(self) -> List[str]:
+        """The deduplicated match api ids (bodies)."""
+        try:
+            return list(set(map(bytes.decode, self.bodies)))
+        except TypeError:  # str / bytearray bodies
+            return list(set(map(_decode, self.bodies)))
+
+
+def _bad_status_table() -> np.ndarray:
+    from ..ops import rate as R
+
+    t = np.zeros(256, dtype=bool)
+    t[list(R.ERROR_STATUSES) + [R.NOT_PROCESSED]] = True
+    return t
+
+
+_BAD_STATUS = _bad_status_table()
+
+
+class _InFlight:
+    """A pipelined batch between launch and ack."""
+
+    def __init__(self, batch, t0: float):
+        self.batch, self.t0 = batch, t0
+        self.ids: List[str] = []
+        self.session = self.mb = self.pending = self.error = None
+        self.seconds = 0.0
+
+
+_headers = attrgetter("headers")
 
 
 def _decode(body) -> str:

@@ -25,8 +25,10 @@ _lock = threading.Lock()
 
 
 def enabled() -> bool:
-    from ..config import EngineConfig
-    return EngineConfig.from_env().trace
+    """``EngineConfig.trace`` (ANA_TRACE), read without building the whole config:
+    this runs around every traced region."""
+    v = os.environ.get("ANA_TRACE")
+    return bool(v) and v != "0"
 
 
 def _roctx():

@@ -6,7 +6,7 @@ of a 500-match batch go when the GPU work is ~47 us?).
 
 Runs worker.py's synthetic path in-process with ANA_TRACE=1 and reports, per
 stage (utils/trace.py ranges: load, rate.rows, rate.encode_h2d, rate.launch,
-rate.d2h, commit, ack), the total and per-batch milliseconds, the broker
+rate.d2h, rate.finish, commit, ack), the total and per-batch milliseconds, the broker
 delivery overhead (everything else inside the consuming loop), the end-to-end
 matches/s, and the top functions by own time (cProfile) -- one JSON object.
 """
@@ -31,11 +31,14 @@ def main():
     ap.add_argument("--engine", default="native")
     ap.add_argument("--batchsize", type=int, default=500)
     ap.add_argument("--cprofile", type=int, default=1)
+    ap.add_argument("--pipeline", default="false", help="PIPELINE: two batches in flight (true) or one")
+    ap.add_argument("--segments", type=int, default=1, help="time the stream in this many parts")
     args = ap.parse_args()
     os.environ["ANA_TRACE"] = "1"
     os.environ["DATABASE_URI"] = args.store
     os.environ["ENGINE"] = args.engine
     os.environ["BATCHSIZE"] = str(args.batchsize)
+    os.environ["PIPELINE"] = args.pipeline
     os.environ.setdefault("IDLE_TIMEOUT", "0.01")
     import logging
 
@@ -53,17 +56,25 @@ def main():
     publish(w.channel, w.cfg.queue, ids[:args.batchsize])
     w.start_consuming()
     trace.clear()
-    publish(w.channel, w.cfg.queue, ids[args.batchsize:])
+    rest = ids[args.batchsize:]
+    seg = -(-len(rest) // args.segments)
     n0 = w.stats.matches
     pr = cProfile.Profile() if args.cprofile else None
-    t0 = time.perf_counter()
-    if pr:
-        pr.enable()
-    w.start_consuming()
-    if pr:
-        pr.disable()
-    dt = time.perf_counter() - t0
+    dt, rates = 0.0, []
+    for k in range(0, len(rest), seg):  # segments: the box's host is shared, report the spread
+        publish(w.channel, w.cfg.queue, rest[k:k + seg])
+        m0 = w.stats.matches
+        t0 = time.perf_counter()
+        if pr:
+            pr.enable()
+        w.start_consuming()
+        if pr:
+            pr.disable()
+        d = time.perf_counter() - t0
+        dt += d
+        rates.append((w.stats.matches - m0) / d)
     n = w.stats.matches - n0
+    rates.sort()
     batches = max(1, (n + args.batchsize - 1) // args.batchsize)
     tot = defaultdict(float)
     cnt = defaultdict(int)
@@ -78,8 +89,11 @@ def main():
         pstats.Stats(pr, stream=s).sort_stats("tottime").print_stats(25)
         top = [ln for ln in s.getvalue().splitlines() if ln.strip()][:40]
     print(json.dumps({"matches": n, "seconds": round(dt, 3), "matches_per_s": round(n / dt),
+                      "segments": len(rates), "segment_matches_per_s_median": round(rates[len(rates) // 2]),
+                      "segment_matches_per_s_min": round(rates[0]), "segment_matches_per_s_max": round(rates[-1]),
                       "ms_per_batch": round(dt * 1000.0 / batches, 4), "batchsize": args.batchsize,
                       "store": args.store, "engine": args.engine, "cprofile": bool(pr),
+                      "pipeline": bool(w._pipe),
                       "stages": stages}, indent=1))
     for ln in top:
         print(ln)

@@ -147,3 +147,120 @@ def test_resident_roster_failed_fetch_leaves_no_rows():
     ok = lambda keys: (np.full((len(keys), 14), np.nan), np.zeros((len(keys), 3)))
     assert rr.rows_for_keys(np.array([7, 3]), ok).tolist() == [0, 1]
     assert rr.rows_for_keys(np.array([3, 9]), ok).tolist() == [1, 2]
+
+
+def _mixed_store(seed=3, n=40, players=30):
+    """Matches of 1-3 rosters, uneven sizes, AFKs (also in a third roster),
+    unsupported modes, ties in created_at."""
+    from analyzer_amd.runtime.objects import Match, Participant, Player, Roster
+
+    rng = np.random.default_rng(seed)
+    pl = [Player("q%d" % i, int(rng.integers(1, 30)), None, None,
+                 trueskill_mu=float(rng.normal(25, 3)), trueskill_sigma=float(rng.uniform(2, 8)))
+          for i in range(players)]
+    col = ColumnarStore()
+    ms = []
+    for i in range(n):
+        nr = int(rng.choice([1, 2, 2, 2, 3]))
+        rosters = []
+        for ri in range(nr):
+            k = int(rng.integers(1, 4))
+            ps = [Participant(pl[int(rng.integers(players))], "m%dr%dp%d" % (i, ri, j),
+                              went_afk=int(rng.random() < 0.1)) for j in range(k)]
+            rosters.append(Roster(ps, winner=bool(ri == 0) if rng.random() < 0.9 else None,
+                                  api_id="m%dr%d" % (i, ri)))
+        mode = str(rng.choice(["casual", "ranked", "blitz", "5v5_casual", "private"]))
+        ms.append(Match(mode, rosters, api_id="m%d" % i, created_at=float(i // 3)))
+    col.add_matches(ms)
+    return col, [m.api_id for m in ms]
+
+
+def test_native_batch_gather_matches_numpy():
+    col, ids = _mixed_store()
+    s = col.session()
+    a, b = s.load_batch(ids), s._load_batch_numpy(ids)
+    assert a.ids == b.ids and a.extra_parts == b.extra_parts and a.K == b.K
+    for f in ("mode", "nrosters", "n", "winner", "afk", "player", "part", "rows"):
+        x, y = getattr(a, f), getattr(b, f)
+        assert x.shape == y.shape and (np.asarray(x, np.int64) == np.asarray(y, np.int64)).all(), f
+    assert any(len(v) for v in a.extra_parts.values())
+
+
+def test_native_batch_commit_matches_numpy():
+    """rate_batch (native encode / finish) then batch_commit writes exactly what
+    the numpy finish + _write_batch_numpy write, extra rosters included."""
+    import copy
+
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.runtime.resident import ResidentBatchRater
+
+    col, ids = _mixed_store(seed=5)
+    twin = copy.deepcopy(col)
+    rb = ResidentBatchRater(BatchRater(RaterConfig()), device="cpu", capacity=64)
+    s = col.session()
+    mb = s.load_batch(ids)
+    rb.rate_batch(mb, s.fetch_players)
+    assert (mb.status == 0).any() and (mb.status == 1).any()
+    s.commit()
+    t = twin.session()
+    mb2 = t._load_batch_numpy(ids)
+    for f in ("status", "quality", "s_mu", "s_sig", "delta", "m_mu", "m_sig", "final_keys", "final",
+              "final_tracks"):
+        setattr(mb2, f, getattr(mb, f))
+    t._write_batch_numpy(mb2)
+    for tab, cols in (("matches", ("quality",)), ("parts", ("i_afk", "ts", "i_rating")), ("players", ("rating",))):
+        for c in cols:
+            x, y = getattr(getattr(col, tab), c), getattr(getattr(twin, tab), c)
+            assert np.array_equal(x, y, equal_nan=True), (tab, c)
+
+
+def test_rate_batch_failed_fetch_leaves_no_rows():
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.runtime.resident import ResidentBatchRater
+
+    col, ids = _mixed_store(seed=9, n=10)
+    rb = ResidentBatchRater(BatchRater(RaterConfig()), device="cpu", capacity=16)
+    s = col.session()
+    mb = s.load_batch(ids)
+
+    def boom(keys):
+        raise IOError("store down")
+
+    with pytest.raises(IOError):
+        rb.rate_batch(mb, boom)
+    assert rb.resident.n == 0 and (rb.resident.by_key < 0).all()
+    rb.rate_batch(mb, s.fetch_players)
+    assert rb.resident.n == len(np.unique(mb.player[mb.player >= 0]))
+
+
+def test_native_player_staging_matches_upload_arrays():
+    from analyzer_amd.runtime.resident import ResidentRoster
+
+    col, _ = _mixed_store(seed=4, players=50)
+    rng = np.random.default_rng(0)
+    col.players.rating[:50][rng.random((50, 14)) < 0.3] = np.nan  # NULL tracks and NULL sigmas
+    keys = np.array([7, 3, 41, 0, 19], dtype=np.int64)
+    a, b = ResidentRoster("cpu", 4), ResidentRoster("cpu", 4)
+    a._upload_arrays(*col.session().fetch_players(keys))
+    buf = b.staging(len(keys))
+    col.session().stage_players(__import__("torch").from_numpy(keys), buf)
+    b.upload_staged(buf)
+    assert np.array_equal(a.roster.state.numpy(), b.roster.state.numpy(), equal_nan=True)
+    assert np.array_equal(a.roster.attrs.numpy(), b.roster.attrs.numpy(), equal_nan=True)
+
+
+def test_native_key_index():
+    from analyzer_amd.ops.native import native
+
+    ki = native().KeyIndex()
+    keys = ["m%d" % i for i in range(5000)] + ["é-%d" % i for i in range(100)]
+    ki.add(keys[:3000], 0)
+    ki.add(keys[3000:], 3000)  # grows the table
+    assert len(ki) == len(keys)
+    q = ["m17", b"m4999", "nope", "é-7".encode(), "é-99", "m0", b""]
+    assert ki.lookup(q).tolist() == [17, 4999, -1, 5007, 5099, 0, -1]
+    with pytest.raises(ValueError):
+        ki.add(["m5"], 9)
+    col, ids = _mixed_store()
+    rows = col.match_rows(ids[::-1] + ["missing"])
+    assert rows.tolist() == [col.m_index[i] for i in ids[::-1]] + [-1]

@@ -557,3 +557,62 @@ def test_python_fallback_forgets_resident_rows():
     assert set(res.rows) == {"p0", "p2"}
     again = res.rows_for([pls[1]])
     assert again[0] == 3  # re-uploaded into a fresh row
+
+
+def _columnar_run(pipeline, quarantine=True, poison=True, fail_commit_at=None, **flags):
+    """The columnar native worker over 120 matches in batches of 16 (PIPELINE on/off)."""
+    import numpy as np
+
+    from analyzer_amd.runtime.columnar import ColumnarSession, ColumnarStore
+    from analyzer_amd.runtime.source import populate
+
+    store = ColumnarStore()
+    ms = populate(store, 120, 40, team_size=3, seed=11)
+    ids = [m if isinstance(m, str) else m.api_id for m in ms]
+    if poison:  # a player the reference raises on: quarantined, or whole batches failing
+        r = store.pl_index["p5"]
+        store.players.rating[r] = np.nan
+        store.players.attr[r] = [np.nan, np.nan, 30.0]
+    commits = [0]
+    if fail_commit_at is not None:
+        real = ColumnarSession.commit
+
+        def flaky(self):
+            commits[0] += 1
+            if commits[0] in fail_commit_at:
+                raise IOError("store write failed")
+            return real(self)
+        store.session = lambda: type("S", (ColumnarSession,), {"commit": flaky})(store)
+    clock = B.ManualClock()
+    cfg = WorkerConfig(batchsize=16, idle_timeout=1.0, engine="native", quarantine=quarantine,
+                       pipeline=pipeline, **flags)
+    w = Worker(cfg, store=store, broker=B.MemoryBroker(clock), rater_cfg=RaterConfig(), clock=clock)
+    w.connect()
+    assert w._pipe == pipeline
+    publish(w.channel, "analyze", ids)
+    w.start_consuming()
+    failed = sorted(m.body for m in w.rabbit.drain("analyze_failed"))
+    return w, store, failed
+
+
+@pytest.mark.parametrize("case", [dict(), dict(quarantine=False), dict(fail_commit_at=(3, 5)),
+                                  dict(poison=False, dotelemetry=True, telemetry_events="3,7")])
+def test_pipelined_worker_is_the_serial_worker(case):
+    """Two batches in flight give bit-identical store contents, failed queue and
+    counters to the one-batch-at-a-time worker -- including whole-batch failures
+    (QUARANTINE=false, a failing commit), where the later batch is rolled back on
+    the device and launched again."""
+    import numpy as np
+
+    ws, ss, fs = _columnar_run(False, **case)
+    wp, sp, fp = _columnar_run(True, **case)
+    assert fp == fs
+    for k in ("batches", "failed_batches", "messages", "matches", "quarantined", "acked", "nacked"):
+        assert getattr(wp.stats, k) == getattr(ws.stats, k), k
+    assert wp.channel.unacked == {} and ws.channel.unacked == {}
+    for tab, cols in (("matches", ("quality",)), ("parts", ("i_afk", "ts", "i_rating", "stats")),
+                      ("players", ("rating",))):
+        for c in cols:
+            assert np.array_equal(getattr(getattr(sp, tab), c), getattr(getattr(ss, tab), c), equal_nan=True), (tab, c)
+    if case.get("quarantine") is False or case.get("fail_commit_at"):
+        assert ws.stats.failed_batches > 0
