@@ -423,8 +423,9 @@ int64_t telemetry(Tensor evoff, Tensor events, int64_t K, Tensor stats, Tensor b
 }
 
 // ------------------------------------------------------------- K9 / C1
-void check_rows(const Tensor& t, const char* name, int64_t P, int64_t cols, const torch::Device& dev) {
-  check(t, name, torch::kFloat32, dev);
+void check_rows(const Tensor& t, const char* name, int64_t P, int64_t cols, const torch::Device& dev,
+                torch::ScalarType ty = torch::kFloat32) {
+  check(t, name, ty, dev);
   TORCH_CHECK(t.dim() == 2 && t.size(0) == P && t.size(1) == cols, name, " must be [P, ", cols, "]");
 }
 
@@ -479,6 +480,71 @@ void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor s2, Tenso
                           s.data_ptr<float>(), p2, scaled, vst.data_ptr<float>(),
                           (float)unknown_sigma, P);
   }
+}
+
+// compressed merge operands: msg [P, 14] bf16/fp16, cnt [P, 2] int32 (sweep.hip);
+// the CPU path goes through the fp32 host mirror and torch's conversions
+void sweep_delta_packed(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma,
+                        Tensor msg, Tensor cnt) {
+  const auto dev = s.device();
+  const int64_t P = s.size(0);
+  check_rows(s0, "s0", P, ana::kRowFloats, dev);
+  check_rows(prior, "prior", P, ana::kRowFloats, dev);
+  check_rows(s, "state", P, ana::kRowFloats, dev);
+  check_rows(attrs, "attrs", P, 4, dev);
+  TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
+                  msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
+              "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
+  check_rows(cnt, "cnt", P, 2, dev, torch::kInt32);
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_sweep_delta_packed(s0.data_ptr<float>(), prior.data_ptr<float>(), s.data_ptr<float>(),
+                                             attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma,
+                                             msg.scalar_type() == torch::kBFloat16 ? 1 : 0, msg.data_ptr(),
+                                             cnt.data_ptr<int32_t>(), P, stream_of(s)),
+              "sweep_delta_packed");
+    return;
+  }
+  Tensor buf = torch::empty({P, 16}, s.options());
+  ana::host_sweep_delta(s0.data_ptr<float>(), prior.data_ptr<float>(), s.data_ptr<float>(),
+                        attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, true,
+                        buf.data_ptr<float>(), P);
+  msg.copy_(buf.slice(1, 0, 14));
+  cnt.copy_(buf.slice(1, 14, 16));
+}
+
+void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor s, Tensor s2, Tensor vst,
+                        double unknown_sigma) {
+  const auto dev = s.device();
+  const int64_t P = s.size(0);
+  check_rows(s0, "s0", P, ana::kRowFloats, dev);
+  TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
+                  msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
+              "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
+  check_rows(cnt, "cnt", P, 2, dev, torch::kInt32);
+  check_rows(attrs, "attrs", P, 4, dev);
+  check_rows(s, "state", P, ana::kRowFloats, dev);
+  float* p2 = nullptr;
+  if (s2.numel()) {
+    check_rows(s2, "s2", P, ana::kRowFloats, dev);
+    p2 = s2.data_ptr<float>();
+  }
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_sweep_apply_packed(s0.data_ptr<float>(), msg.data_ptr(), cnt.data_ptr<int32_t>(),
+                                             msg.scalar_type() == torch::kBFloat16 ? 1 : 0,
+                                             attrs.data_ptr<float>(), s.data_ptr<float>(), p2,
+                                             vst.data_ptr<float>(), (float)unknown_sigma, P, stream_of(s)),
+              "sweep_apply_packed");
+    return;
+  }
+  Tensor buf = torch::empty({P, 16}, s.options());
+  buf.slice(1, 0, 14).copy_(msg);
+  buf.slice(1, 14, 16).copy_(cnt);
+  ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
+                        s.data_ptr<float>(), p2, true, vst.data_ptr<float>(), (float)unknown_sigma, P);
 }
 
 // ------------------------------------------------------------- C2 exchange
@@ -703,6 +769,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("STAT_FEATURES") = ana::kStatFeatures;
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
   m.def("sweep_apply", &sweep_apply, "K9: decode summed messages against the common start (-> s, s2)");
+  m.def("sweep_delta_packed", &sweep_delta_packed, "K9: messages straight into bf16/fp16 + int32 all-reduce operands");
+  m.def("sweep_apply_packed", &sweep_apply_packed, "K9: decode bf16/fp16 + int32 summed messages (-> s, s2)");
   m.def("pack_rows", &pack_rows, "C2: changed rows of a round slice -> fixed-capacity [cap, 33] entries");
   m.def("check_round", &check_round, "C2 race detector: one round's matches share no player (flag |= 1)");
   m.def("unpack_rows", &unpack_rows, "C2: write gathered entries (id >= 0) into the roster, tags zeroed");

@@ -79,6 +79,13 @@ int launch_sweep_delta(const float* s0, const float* a, const float* s, const fl
 // decoded rows to s and (s2 != nullptr) s2
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                        const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st);
+// compressed merges: msg [P][14] bf16 (bf16 != 0) or fp16 + cnt [P][2] int32
+int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, const float* attrs,
+                              const float* vst, float unknown_sigma, int bf16, void* msg, int32_t* cnt,
+                              int64_t P, hipStream_t st);
+int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
+                              const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
+                              int64_t P, hipStream_t st);
 // C2 exact-DP exchange (sweep.hip): fixed-capacity [cap][33] entries of changed rows
 int launch_pack_rows(const int32_t* rec, int K, int64_t m, const uint8_t* status, int64_t sstride,
                      const float* state, float* out, int64_t cap, hipStream_t st);

@@ -89,6 +89,117 @@ __global__ void sweep_apply_kernel(const float4* __restrict__ s0, const float4* 
   }
 }
 
+// ------------------------------------------------- compressed (fp16 / bf16) messages
+// COMM_DTYPE=bf16/fp16 merges used to write the fp32 [P][16] buffer, convert it
+// into the 16-bit message block + int32 touch counts for the all-reduce, and
+// convert back before decoding: four extra passes over the buffer per bucket.
+// These variants write / read the all-reduce operands directly: msg [P][14] in
+// the 16-bit type (round to nearest even, as torch's .to()), cnt [P][2] int32
+// (the base-16 touch fields, exact integers).
+// The empty asm pins x as the rounded fp32 message: without it the compiler folds
+// the message's last fma into the conversion (v_fma_mixlo_f16, one rounding
+// instead of two), which is not what the fp32 path + .to() produce on ties.
+template <typename H>
+__device__ __forceinline__ uint16_t to_half_bits(float x);
+template <>
+__device__ __forceinline__ uint16_t to_half_bits<__bf16>(float x) {
+  asm("" : "+v"(x));
+  return __builtin_bit_cast(uint16_t, (__bf16)x);
+}
+template <>
+__device__ __forceinline__ uint16_t to_half_bits<_Float16>(float x) {
+  asm("" : "+v"(x));
+  return __builtin_bit_cast(uint16_t, (_Float16)x);
+}
+template <typename H>
+__device__ __forceinline__ float from_half_bits(uint32_t b) {
+  return (float)__builtin_bit_cast(H, (uint16_t)b);
+}
+
+template <typename H>
+__global__ void sweep_delta_packed_kernel(const float4* __restrict__ s0, const float4* a0,
+                                          const float4* __restrict__ s, const float4* __restrict__ attrs,
+                                          const float* __restrict__ vst, float unknown_sigma,
+                                          uint32_t* __restrict__ msg, int2* __restrict__ cnt, int64_t P) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  float c[kRowFloats], a[kRowFloats], b[kRowFloats], o[16];
+  load_row(s0, p, c);
+  if (a0 != s0) load_row(a0, p, a);
+  else
+#pragma unroll
+    for (int k = 0; k < kRowFloats; ++k) a[k] = c[k];
+  load_row(s, p, b);
+  const float4 at = attrs[p];
+  const float attr[4] = {at.x, at.y, at.z, at.w};
+  sweep_delta_player(c, a, b, attr, vst, unknown_sigma, true, o);
+#pragma unroll
+  for (int k = 0; k < 7; ++k)  // 14 halves = 7 words (28 B per player)
+    msg[p * 7 + k] = (uint32_t)to_half_bits<H>(o[2 * k]) | ((uint32_t)to_half_bits<H>(o[2 * k + 1]) << 16);
+  cnt[p] = make_int2((int)o[14], (int)o[15]);
+}
+
+template <typename H>
+__global__ void sweep_apply_packed_kernel(const float4* __restrict__ s0, const uint32_t* __restrict__ msg,
+                                          const int2* __restrict__ cnt, const float4* __restrict__ attrs,
+                                          float4* s, float4* s2, const float* __restrict__ vst,
+                                          float unknown_sigma, int64_t P) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  float a[kRowFloats], d[16], o[kRowFloats];
+  load_row(s0, p, a);
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const uint32_t w = msg[p * 7 + k];
+    d[2 * k] = from_half_bits<H>(w & 0xffffu);
+    d[2 * k + 1] = from_half_bits<H>(w >> 16);
+  }
+  const int2 c = cnt[p];
+  d[14] = (float)c.x;
+  d[15] = (float)c.y;
+  const float4 at = attrs[p];
+  const float attr[4] = {at.x, at.y, at.z, at.w};
+  sweep_apply_player(a, d, attr, vst, unknown_sigma, true, o);
+#pragma unroll
+  for (int k = 0; k < kRowVec; ++k) {
+    const float4 v = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    s[p * kRowVec + k] = v;
+    if (s2) s2[p * kRowVec + k] = v;
+  }
+}
+
+int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, const float* attrs,
+                              const float* vst, float unknown_sigma, int bf16, void* msg, int32_t* cnt,
+                              int64_t P, hipStream_t st) {
+  if (P <= 0) return 0;
+  const dim3 grid((unsigned)((P + 255) / 256)), block(256);
+  auto args = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, block, 0, st, reinterpret_cast<const float4*>(s0),
+                       reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(s),
+                       reinterpret_cast<const float4*>(attrs), vst, unknown_sigma,
+                       reinterpret_cast<uint32_t*>(msg), reinterpret_cast<int2*>(cnt), P);
+  };
+  if (bf16) args(sweep_delta_packed_kernel<__bf16>);
+  else args(sweep_delta_packed_kernel<_Float16>);
+  return (int)hipGetLastError();
+}
+
+int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
+                              const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
+                              int64_t P, hipStream_t st) {
+  if (P <= 0) return 0;
+  const dim3 grid((unsigned)((P + 255) / 256)), block(256);
+  auto args = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, block, 0, st, reinterpret_cast<const float4*>(s0),
+                       reinterpret_cast<const uint32_t*>(msg), reinterpret_cast<const int2*>(cnt),
+                       reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
+                       reinterpret_cast<float4*>(s2), vst, unknown_sigma, P);
+  };
+  if (bf16) args(sweep_apply_packed_kernel<__bf16>);
+  else args(sweep_apply_packed_kernel<_Float16>);
+  return (int)hipGetLastError();
+}
+
 int launch_sweep_delta(const float* s0, const float* a, const float* s, const float* attrs,
                        const float* vst, float unknown_sigma, int scaled, float* buf, int64_t P,
                        hipStream_t st) {

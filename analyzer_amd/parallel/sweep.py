@@ -64,7 +64,7 @@ COMM_DTYPES = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloa
 class SweepMerger:
     def __init__(self, num_players: int, device, cfg: Optional[RaterConfig] = None,
                  group=None, comm_dtype: str = "fp32", bucket_rows: Optional[int] = None,
-                 sweeps: int = 1, world_size: Optional[int] = None):
+                 sweeps: int = 1, world_size: Optional[int] = None, force: bool = False):
         self.P = int(num_players)
         self.device = torch.device(device)
         self.cfg = cfg or RaterConfig.from_env()
@@ -75,6 +75,9 @@ class SweepMerger:
         if comm_dtype not in COMM_DTYPES:
             raise ValueError("comm_dtype must be one of %s" % sorted(COMM_DTYPES))
         self.sweeps = max(1, int(sweeps))
+        # force: run the merge kernels even on one rank (the all-reduce of one rank
+        # is the identity) -- bench.py --force-merge prices the merge without comm
+        self.force = bool(force)
         # fp16/bf16: messages use the base-relative encoding (sweep_core.h) and
         # travel compressed; the touch counters travel separately as int32
         self.comm_dtype = comm_dtype
@@ -83,13 +86,20 @@ class SweepMerger:
         self.start = torch.empty((self.P, 32), **f)   # common window start
         self.prior = None                            # this rank's prior (re-sweeps only)
         self.buf = torch.empty((self.P, 16), **f)
+        # fp16/bf16: merge() writes and reads the all-reduce operands directly
+        # (messages [P, 14] in the comm dtype + touch counts [P, 2] int32)
+        self.msg = torch.empty((self.P, 14), dtype=COMM_DTYPES[comm_dtype], device=self.device) \
+            if comm_dtype != "fp32" else None
+        self.cnt = torch.empty((self.P, 2), dtype=torch.int32, device=self.device) \
+            if comm_dtype != "fp32" else None
         self.vst = torch.tensor(vst_table(), **f)
         self._none = torch.empty(0, **f)
         self.comm_bytes = self.P * (16 * 4 if not self.scaled else
                                     14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4)
-        if bucket_rows is None:
+        if bucket_rows is None:  # ANA_MERGE_BUCKET_MB of all-reduce operands per bucket
             mb = EngineConfig.from_env().merge_bucket_mb
-            bucket_rows = int(mb * (1 << 20)) // (16 * 4) if mb > 0 else self.P
+            row_bytes = 16 * 4 if not self.scaled else 14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4
+            bucket_rows = int(mb * (1 << 20)) // row_bytes if mb > 0 else self.P
         self.bucket_rows = max(1, min(int(bucket_rows), max(self.P, 1)))
         self.windows = 0
         self._synced = False   # start == the roster as the last merge left it
@@ -132,6 +142,24 @@ class SweepMerger:
                              self.scaled)
         roster.epoch = roster.epoch if roster.epoch is not None else 0  # decode wrote tag 0
 
+    def messages_packed(self, roster, lo: int = 0, hi: Optional[int] = None) -> None:
+        """``messages`` straight into the compressed all-reduce operands (first sweep)."""
+        hi = self.P if hi is None else hi
+        native().sweep_delta_packed(self.start[lo:hi], self.start[lo:hi], roster.state[lo:hi],
+                                    roster.attrs[lo:hi], self.vst, float(self.cfg.unknown_player_sigma),
+                                    self.msg[lo:hi], self.cnt[lo:hi])
+
+    def decode_packed(self, roster, lo: int = 0, hi: Optional[int] = None, into=None) -> None:
+        """``decode`` of the compressed summed messages."""
+        hi = self.P if hi is None else hi
+        s2 = into[lo:hi] if into is not None else self._none
+        native().sweep_apply_packed(self.start[lo:hi], self.msg[lo:hi], self.cnt[lo:hi], roster.attrs[lo:hi],
+                                    roster.state[lo:hi], s2, self.vst, float(self.cfg.unknown_player_sigma))
+        roster.epoch = roster.epoch if roster.epoch is not None else 0
+
+    def _packed(self) -> bool:
+        return self.msg is not None and (self._sweep <= 1 or self.prior is None)
+
     # legacy name: decode the all-reduced messages into the roster only
     def apply(self, roster, lo: int = 0, hi: Optional[int] = None) -> None:
         self.decode(roster, lo, hi)
@@ -151,18 +179,20 @@ class SweepMerger:
             buf[:, :14].copy_(parts[0])
             buf[:, 14:].copy_(parts[1])
 
-    def _launch_reduce(self, lo: int, hi: int):
+    def _launch_reduce(self, lo: int, hi: int, packed: bool = False):
         """Start the all-reduce of rows [lo, hi); returns a finisher that waits
         for it (stream-ordered, the host does not block on RCCL) and unpacks."""
         buf = self.buf[lo:hi]
-        parts = self._split(buf)
-        works = [all_reduce_sum(t, group=self.group, async_op=True) for t in parts]
+        parts = [self.msg[lo:hi], self.cnt[lo:hi]] if packed else self._split(buf)
+        # one rank (force): the sum over ranks is the message itself
+        works = [all_reduce_sum(t, group=self.group, async_op=True) for t in parts] if self.world > 1 else []
 
         def finish():
             for w in works:
                 if w is not None:
                     w.wait()
-            self._join(buf, parts)
+            if not packed:
+                self._join(buf, parts)
         return finish
 
     def reduce(self, lo: int = 0, hi: Optional[int] = None) -> None:
@@ -206,24 +236,27 @@ class SweepMerger:
         prepass, runtime/engine.py) enqueued once every bucket's all-reduce is in
         flight and before the first decode waits for one, so the collectives run
         under it instead of in front of it."""
-        if self.world <= 1:
+        if self.world <= 1 and not self.force:
             self.windows += 1
             if overlap is not None:
                 overlap()
             return
+        packed = self._packed()
+        msg = self.messages_packed if packed else self.messages
+        dec = self.decode_packed if packed else self.decode
         if overlap is not None:
             self._ev("begin")
             launched = []
             for lo, hi in self.buckets():
-                self.messages(roster, lo, hi)
-                launched.append((lo, hi, self._launch_reduce(lo, hi)))
+                msg(roster, lo, hi)
+                launched.append((lo, hi, self._launch_reduce(lo, hi, packed)))
             self._ev("messages")
             overlap()
             self._ev("overlap")
             for lo, hi, fin in launched:
                 fin()
                 self._ev("allreduce")
-                self.decode(roster, lo, hi, into=self.start)
+                dec(roster, lo, hi, into=self.start)
                 self._ev("apply")
             self._synced = True
             self.windows += 1
@@ -231,21 +264,21 @@ class SweepMerger:
         pending = None  # (lo, hi, finisher) of the bucket whose reduce is in flight
         self._ev("begin")
         for lo, hi in self.buckets():
-            self.messages(roster, lo, hi)
+            msg(roster, lo, hi)
             self._ev("messages")
-            fin = self._launch_reduce(lo, hi)
+            fin = self._launch_reduce(lo, hi, packed)
             if pending is not None:
                 plo, phi, pfin = pending
                 pfin()
                 self._ev("allreduce")
-                self.decode(roster, plo, phi, into=self.start)
+                dec(roster, plo, phi, into=self.start)
                 self._ev("apply")
             pending = (lo, hi, fin)
         if pending is not None:
             plo, phi, pfin = pending
             pfin()
             self._ev("allreduce")
-            self.decode(roster, plo, phi, into=self.start)
+            dec(roster, plo, phi, into=self.start)
             self._ev("apply")
         self._synced = True
         self.windows += 1

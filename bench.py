@@ -88,6 +88,9 @@ def parse(argv=None):
                     help="N > 1: after timing, rank 0 measures the sweep-DP error of this run's "
                          "configuration against the exact sequential rating (parallel/accuracy.py, "
                          "N ranks simulated on its GPU) and reports it in the JSON line (0 = skip)")
+    ap.add_argument("--force-merge", action="store_true",
+                    help="N = 1: run the merge kernels after every window anyway (messages + decode, "
+                         "no collective) -- prices the DP merge's device work against --merges-per-step")
     ap.add_argument("--sweeps", type=int, default=EngineConfig.from_env().sweeps,
                     help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
                          "N = exact sequential semantics (parallel/sweep.py)")
@@ -207,7 +210,8 @@ def main(argv=None) -> int:
         tele = [make_telemetry(tspec, windows[w], K, base=(w * world + rank) * M) for w in range(n_windows)]
         stats = allocate_stats(M, K, dev)
         n_events = sum(t.num_events for t in tele) / n_windows
-    merger = SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps) if world > 1 else None
+    merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge)
+              if world > 1 or args.force_merge else None)
     pipe = WindowPipeline(rater, roster, K, merger=merger)
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     torch.cuda.synchronize()
@@ -367,7 +371,8 @@ def main(argv=None) -> int:
                          % (args.sweeps, "s" if args.sweeps > 1 else "")),
                 "bench_config": args.config,
                 "skew": args.skew,
-                "comm_dtype": args.comm_dtype if world > 1 else None,
+                "comm_dtype": args.comm_dtype if world > 1 or args.force_merge else None,
+                "force_merge": bool(args.force_merge),
                 "sweeps": args.sweeps if world > 1 else None,
                 **extra,
             },

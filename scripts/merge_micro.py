@@ -47,7 +47,17 @@ def main():
             msg = time_ms(lambda: m.messages(roster), a.reps)
             dec = time_ms(lambda: m.decode(roster, into=m.start), a.reps)
             state_mb = P * 128 / 1e6
-            out.append({"players": P, "comm_dtype": dtype, "messages_ms": msg, "decode_ms": dec,
+            extra = {}
+            if dtype != "fp32":
+                # what merge() runs for a compressed dtype: the fp32 path needs a split
+                # into the comm operands and a join back; the packed kernels neither
+                split = time_ms(lambda: m._join(m.buf, m._split(m.buf)), a.reps)
+                extra = {"fp32_path_split_join_ms": split,
+                         "packed_messages_ms": time_ms(lambda: m.messages_packed(roster), a.reps),
+                         "packed_decode_ms": time_ms(lambda: m.decode_packed(roster, into=m.start), a.reps)}
+                extra["packed_total_ms"] = extra["packed_messages_ms"] + extra["packed_decode_ms"]
+                extra["fp32_path_total_ms"] = msg + dec + split
+            out.append({"players": P, "comm_dtype": dtype, "messages_ms": msg, "decode_ms": dec, **extra,
                         "message_bytes_per_rank": m.comm_bytes,
                         # messages: read start + prior(=start) + roster + attrs, write buf
                         "messages_GBps": (3 * state_mb + P * 16 / 1e6 + P * 64 / 1e6) / msg,

@@ -188,7 +188,7 @@ def _sweep_buckets(rank, size, P, M, K, seed, comm_dtype, bucket_rows):
     return out
 
 
-@pytest.mark.parametrize("comm_dtype", ["fp32", "fp16"])
+@pytest.mark.parametrize("comm_dtype", ["fp32", "fp16", "bf16"])
 def test_sweep_merge_bucketed_pipeline_matches_single_bucket(tmp_path, comm_dtype):
     """The pipelined merge (messages / async all-reduce / apply per row bucket,
     ragged last bucket) gives the one-bucket result bit for bit: every stage is

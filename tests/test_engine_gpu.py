@@ -245,6 +245,36 @@ def test_sweep_kernels_match_host(gpu_device, scaled, resweep):
     assert torch.equal(sh.nan_to_num(-7), sh2.nan_to_num(-7))
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_packed_sweep_kernels_match_fp32_path(gpu_device, dtype):
+    """The compressed-operand merge kernels (messages straight into bf16/fp16 +
+    int32, decode straight from them) == the fp32 kernels followed by torch's
+    conversions, bit for bit."""
+    from analyzer_amd.ops.native import native
+    from analyzer_amd.models.tiers import vst_table
+
+    P = 6000
+    start = make_roster(RosterSpec(num_players=P, seed=5, p_rated=0.5), device=gpu_device)
+    after = start.clone()
+    R.BatchRater().rate(after, make_stream(StreamSpec(team_size=3, seed=6), 20000, P, device=gpu_device), 3)
+    vst = torch.tensor(vst_table(), dtype=torch.float32, device=gpu_device)
+    buf = torch.empty((P, 16), device=gpu_device)
+    native().sweep_delta(start.state, start.state, after.state, start.attrs, vst, 500.0, True, buf)
+    msg = torch.empty((P, 14), dtype=dtype, device=gpu_device)
+    cnt = torch.empty((P, 2), dtype=torch.int32, device=gpu_device)
+    native().sweep_delta_packed(start.state, start.state, after.state, start.attrs, vst, 500.0, msg, cnt)
+    assert torch.equal(msg.view(torch.int16), buf[:, :14].to(dtype).view(torch.int16))
+    assert torch.equal(cnt, buf[:, 14:].to(torch.int32))
+    msg2, cnt2 = msg * 2, cnt * 2  # a "sum" of two ranks
+    joined = torch.cat([msg2.float(), cnt2.float()], dim=1)
+    s_ref, s2_ref = start.state.clone(), torch.zeros_like(start.state)
+    native().sweep_apply(start.state, joined, start.attrs, s_ref, s2_ref, vst, 500.0, True)
+    s_p, s2_p = start.state.clone(), torch.zeros_like(start.state)
+    native().sweep_apply_packed(start.state, msg2, cnt2, start.attrs, s_p, s2_p, vst, 500.0)
+    assert torch.equal(s_p.nan_to_num(-7), s_ref.nan_to_num(-7))
+    assert torch.equal(s2_p.nan_to_num(-7), s_ref.nan_to_num(-7))
+
+
 def test_telemetry_device_generator_and_aggregation(gpu_device):
     from analyzer_amd.ops.telemetry import TelemetrySpec, aggregate, aggregate_reference, make_telemetry
 
