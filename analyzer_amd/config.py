@@ -158,7 +158,16 @@ class EngineConfig:
     CHECKPOINT_DIR / _EVERY -- / 1    re-rate checkpoints (runtime/rerate.py)
     ANA_TRACE               0         roctx ranges + Chrome trace (utils/trace.py)
     ANA_CHECK_ROUNDS        0         exact DP race detector: rounds share no player (parallel/exact_dp.py)
+    ANA_RATE_IDLE           0         executor: max s_sleep rounds of an idle wave (0 = 8, < 0 none)
+    ANA_RATE_LOCAL          1         executor: LDS hand-off of successors the producing wave holds
+    ANA_RATE_DIAG           0         executor timing build: per-phase clocks in ctrl[20..47] (ops/rate.diag)
+    ANA_RATE_TIGHT          -1        executor: 2K lanes per match instead of the next power of two (-1 auto)
+    ANA_TELE_FUSED_TAIL     0         fused telemetry only after the executor's chunks are drained
+    ANA_TELE_ROLE           2         fused telemetry: one wave in N aggregates from the start (0 = idle waves)
     ======================  ========  =============================================
+
+    The executor / fused-telemetry knobs reach the launch as ``BatchRater.knobs``
+    (read once per BatchRater, passed to csrc/bindings.cpp ``rate``).
     """
 
     rate_blocks: int = 512
@@ -174,19 +183,25 @@ class EngineConfig:
     checkpoint_dir: Optional[str] = None
     trace: bool = False
     check_rounds: bool = False
+    rate_idle: int = 0
+    rate_local: int = 1
+    rate_diag: int = 0
+    rate_tight: int = -1
+    tele_fused_tail: int = 0
+    tele_role: int = 2
 
-    # read by the native extension itself (csrc/bindings.cpp, kernels), per launch
+    # kernel-implementation A/B switches read by the native extension itself
+    # (csrc/telemetry.hip, kernels.hip, radix_sort.hip) -- experiments, not tuning
     NATIVE_KNOBS = {
-        "ANA_RATE_IDLE": "max s_sleep rounds of an idle executor wave (default 8)",
-        "ANA_RATE_TIGHT": "2K lanes per match instead of the next power of two (-1 auto)",
-        "ANA_RATE_LOCAL": "LDS local hand-off of successors held by the producing wave (default 1)",
-        "ANA_RATE_DIAG": "timing build of the executor: per-phase clocks in ctrl[20..39] (default 0)",
         "ANA_TELE_IMPL": "telemetry aggregation: 1 one-hot MFMA GEMM (default), 0 LDS atomics",
-        "ANA_TELE_FUSED_TAIL": "fused telemetry only after the executor's chunks are drained",
-        "ANA_TELE_ROLE": "fused telemetry: one wave in N aggregates from the start (default 2; 0 = idle waves take tiles)",
         "ANA_SCHED_SMALL": "micro-batch schedule: hash lists (default) or bitonic sort",
         "ANA_SORT_RB / ANA_SORT_NT": "radix-sort tile rows / non-temporal loads (tuning)",
     }
+
+    def rate_knobs(self) -> list:
+        """[idle, local, diag, tight, tele_fused_tail, tele_role] for the native launch."""
+        return [self.rate_idle, self.rate_local, self.rate_diag, self.rate_tight, self.tele_fused_tail,
+                self.tele_role]
 
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "EngineConfig":
@@ -204,4 +219,10 @@ class EngineConfig:
             checkpoint_dir=_env(env, "CHECKPOINT_DIR"),
             trace=(env.get("ANA_TRACE") or "0") not in ("", "0"),
             check_rounds=(env.get("ANA_CHECK_ROUNDS") or "0") not in ("", "0"),
+            rate_idle=int(_env(env, "ANA_RATE_IDLE") or 0),
+            rate_local=int(_env(env, "ANA_RATE_LOCAL") or 1),
+            rate_diag=int(_env(env, "ANA_RATE_DIAG") or 0),
+            rate_tight=int(_env(env, "ANA_RATE_TIGHT") or -1),
+            tele_fused_tail=int(_env(env, "ANA_TELE_FUSED_TAIL") or 0),
+            tele_role=int(_env(env, "ANA_TELE_ROLE") or 2),
         )

@@ -229,9 +229,13 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   }
 }
 
+// knobs (EngineConfig, config.py): [rate_idle, rate_local, rate_diag, rate_tight,
+// tele_fused_tail, tele_role] -- executor / fused-telemetry tuning, per BatchRater
+constexpr size_t kKnobs = 6;
+
 static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& events,
                                              const Tensor& stats, int64_t M, int64_t K,
-                                             const torch::Device& dev) {
+                                             const torch::Device& dev, const std::vector<int64_t>& knobs) {
   ana::TelemetryParams tp{nullptr, nullptr, nullptr, M};
   if (evoff.numel() == 0) return tp;
   check(evoff, "evoff", torch::kInt64, dev);
@@ -244,10 +248,9 @@ static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& 
   tp.events = events.data_ptr<int32_t>();
   tp.stats = stats.data_ptr<float>();
   if (dev.is_cuda()) tp.impl = ana::tele_impl();
-  if (const char* e = std::getenv("ANA_TELE_FUSED_TAIL")) tp.fused_tail = std::atoi(e);  // A/B knob
+  tp.fused_tail = (int32_t)knobs[4];
   // fused: every 2nd wave aggregates first (14.4 -> 11.4 ms per config 4 step, profiles/r2/tele_role_split.log)
-  tp.role_stride = 2;
-  if (const char* e = std::getenv("ANA_TELE_ROLE")) tp.role_stride = std::atoi(e);
+  tp.role_stride = (int32_t)knobs[5];
   return tp;
 }
 
@@ -258,8 +261,9 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
           double tau2, double unknown_sigma, bool record_first_prior, int64_t blocks,
           int64_t epoch, bool host_fp64, Tensor tele_evoff, Tensor tele_events, Tensor tele_stats,
           int64_t progress, int64_t progress_value, int64_t progress_at, int64_t epoch_ptr,
-          int64_t chunk_len, bool ctrl_ready) {
+          int64_t chunk_len, bool ctrl_ready, std::vector<int64_t> knobs) {
   const auto dev = rec.device();
+  TORCH_CHECK(knobs.size() == kKnobs, "knobs must be [idle, local, diag, tight, tele_fused_tail, tele_role]");
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
   check(attrs, "attrs", torch::kFloat32, dev);
@@ -301,20 +305,17 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   TORCH_CHECK(prm.epoch_ptr ? dev.is_cuda() : (epoch >= 1 && epoch <= 255), "epoch must be 1..255");
   prm.epoch = (int32_t)epoch;
   prm.vst = vst.data_ptr<float>();
-  if (const char* e = std::getenv("ANA_RATE_IDLE")) prm.idle_spins = std::atoi(e);  // tuning knob
-  prm.local_handoff = 1;
-  if (const char* e = std::getenv("ANA_RATE_LOCAL")) prm.local_handoff = std::atoi(e);  // A/B knob
-  prm.diag = 0;
-  if (const char* e = std::getenv("ANA_RATE_DIAG")) prm.diag = std::atoi(e);  // timing build
-  prm.tight_groups = -1;
-  if (const char* e = std::getenv("ANA_RATE_TIGHT")) prm.tight_groups = std::atoi(e);
+  prm.idle_spins = (int32_t)knobs[0];
+  prm.local_handoff = (int32_t)knobs[1];
+  prm.diag = (int32_t)knobs[2];
+  prm.tight_groups = (int32_t)knobs[3];
   prm.progress = reinterpret_cast<uint64_t*>((intptr_t)progress);
   prm.progress_value = (uint64_t)progress_value;
   prm.progress_at = progress_at;
   TORCH_CHECK(chunk_len >= 1 && chunk_len <= 64, "chunk_len must be 1..64");
   prm.chunk_len = (int32_t)chunk_len;
   prm.ctrl_ready = ctrl_ready ? 1 : 0;
-  const ana::TelemetryParams tp = telemetry_params(tele_evoff, tele_events, tele_stats, M, K, dev);
+  const ana::TelemetryParams tp = telemetry_params(tele_evoff, tele_events, tele_stats, M, K, dev, knobs);
   if (dev.is_cuda()) {
     check(link, "link", torch::kInt32, dev);
     check(deps, "deps", torch::kInt32, dev);
@@ -405,7 +406,8 @@ int64_t telemetry(Tensor evoff, Tensor events, int64_t K, Tensor stats, Tensor b
   TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
   const int64_t M = evoff.numel() - 1;
   TORCH_CHECK(M >= 0, "evoff must have M + 1 entries");
-  const ana::TelemetryParams tp = telemetry_params(evoff, events, stats, M, K, dev);
+  // standalone: the fused-executor knobs do not apply
+  const ana::TelemetryParams tp = telemetry_params(evoff, events, stats, M, K, dev, {0, 1, 0, -1, 0, 2});
   if (!tp.evoff) return 0;
   if (dev.is_cuda()) {
     check(bad, "bad", torch::kInt32, dev);

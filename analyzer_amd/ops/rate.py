@@ -174,8 +174,10 @@ class BatchRater:
                  blocks: Optional[int] = None):
         self.cfg = cfg or RaterConfig.from_env()
         self.host_fp64 = host_fp64
+        ecfg = EngineConfig.from_env()
         # persistent-grid size of the dataflow launch (4 waves per block)
-        self.blocks = int(blocks or EngineConfig.from_env().rate_blocks)
+        self.blocks = int(blocks or ecfg.rate_blocks)
+        self.knobs = ecfg.rate_knobs()  # executor / fused-telemetry tuning (csrc/bindings.cpp)
         self._vst: Dict[str, torch.Tensor] = {}
         self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
 
@@ -316,7 +318,7 @@ class BatchRater:
                       self.host_fp64, *telemetry,
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
                       epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
-                      self.chunk_len(M, tele), ctrl_ready)
+                      self.chunk_len(M, tele), ctrl_ready, self.knobs)
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out

@@ -8,6 +8,8 @@
 # work after a fault, abort or time limit).
 #
 # tasks:
+#   build      rebuild every extension from source ON THE BOX (build_ext --force, both
+#              libraries), so a session proves the pushed sources compile there
 #   tests      pytest -m gpu (+ smoke)                    gpurun_out/tests/
 #   bench      bench.py config 2, 20 steps, --verify      gpurun_out/bench/
 #   configs    bench.py configs 3, 4 (fused + separate), 5
@@ -50,6 +52,11 @@ run() {  # run NAME SECONDS CMD...: one bounded step, output to gpurun_out/NAME.
 
 for task in "$@"; do
   case $task in
+    build)  # CPU only: hipcc cross-compiles gfx950; the pushed .so files are replaced
+      run build/build 900 $PY -m analyzer_amd.build_ext --force --jobs 16
+      run build/build_diag 900 $PY -m analyzer_amd.build_ext --force --diag --jobs 16
+      run build/import 120 $PY -c "import analyzer_amd.ops.native as n; n.native(); print('native ok')"
+      ;;
     tests)
       run tests/pytest 900 $PY -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
       run tests/smoke 300 $PY -c "import __graft_entry__ as g; g.smoke()"
@@ -242,6 +249,8 @@ EOF
           IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 50000
       run worker/sqlite_python 600 env DATABASE_URI=sqlite:////tmp/wp.db ENGINE=python BATCHSIZE=500 \
           IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 20000
+      # per-stage profiles (scripts/worker_profile.py): columnar serial x2 / pipelined, SQLite, SQLAlchemy
+      run worker/profiles 900 bash scripts/worker_stores.sh
       ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac

@@ -1,3 +1,4 @@
+# Worker throughput per store (scripts/worker_profile.py), run on the GPU box by scripts/gpu.sh worker.
 set -o pipefail
 for i in 1 2; do timeout -k 10 300 python scripts/worker_profile.py --synthetic 400000 --segments 8 --cprofile 0 > gpurun_out/worker_columnar_$i.json 2>&1 || exit 1; echo columnar $(grep -h "matches_per_s" gpurun_out/worker_columnar_$i.json | tr -d "\n "); done
 timeout -k 10 300 python scripts/worker_profile.py --synthetic 200000 --segments 4 --cprofile 0 --pipeline true > gpurun_out/worker_columnar_pipelined.json 2>&1 || exit 1
