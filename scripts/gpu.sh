@@ -55,7 +55,7 @@ for task in "$@"; do
     build)  # CPU only: hipcc cross-compiles gfx950; the pushed .so files are replaced
       run build/build 900 $PY -m analyzer_amd.build_ext --force --jobs 16
       run build/build_diag 900 $PY -m analyzer_amd.build_ext --force --diag --jobs 16
-      run build/import 120 $PY -c "import analyzer_amd.ops.native as n; n.native(); print('native ok')"
+      run build/import 120 $PY -c "from analyzer_amd.ops.native import native; native(); print('native ok')"
       ;;
     tests)
       run tests/pytest 900 $PY -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
