@@ -30,7 +30,7 @@ HIP_SOURCES = ["kernels.hip", "radix_sort.hip", "dataflow.hip", "sweep.hip", "te
 # which the NULL = NaN convention relies on.
 HIP_FLAGS = {n: ["-fapprox-func", "-freciprocal-math", "-fno-signed-zeros"]
              for n in ("dataflow.hip",)}
-CPP_SOURCES = ["host.cpp", "ingest.cpp", "batch_host.cpp", "bindings.cpp"]
+CPP_SOURCES = ["host.cpp", "ingest.cpp", "batch_host.cpp", "telemetry_file.cpp", "bindings.cpp"]
 
 
 def _ext_suffix() -> str:

@@ -96,6 +96,9 @@ class WorkerConfig:
     resident: bool = True
     # new: the run is a benchmark -- synthetic telemetry may be persisted (worker.connect)
     synthetic_telemetry: bool = False
+    # new: DOTELEMETRY event source -- an ANATEL01 file of downloaded events keyed by
+    # match api id (ops/telemetry.TelemetrySource); unset = synthetic events
+    telemetry_source: Optional[str] = None
     # new: skip matches that already carry a rating (trueskill_quality set), so a
     # redelivery after commit-but-before-ack does not rate a match twice.  Off by
     # default: the reference re-rates redelivered matches (worker.py:122-129,194)
@@ -126,6 +129,7 @@ class WorkerConfig:
             dotelemetry=env.get("DOTELEMETRY") == "true",
             telemetry_events=_env(env, "TELEMETRY_EVENTS") or "100,300",
             synthetic_telemetry=env.get("SYNTHETIC_TELEMETRY") == "true",
+            telemetry_source=_env(env, "TELEMETRY_SOURCE"),
             resident=_resident_default(env),
             skip_rated=env.get("SKIP_RATED") == "true",
             pipeline=env.get("PIPELINE") == "true",

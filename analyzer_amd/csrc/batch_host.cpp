@@ -23,6 +23,8 @@
 // fallback the tests compare against.
 #include <torch/extension.h>
 
+#include "key_index.h"
+
 #include <stdint.h>
 
 #include <cmath>
@@ -337,116 +339,44 @@ void batch_stage_players(Tensor keys, Tensor rating, Tensor attr, Tensor out) {
 }
 
 // ---------------------------------------------------------------- key index
-// api id -> store row for a worker batch's match ids.  A Python dict lookup of a
-// fresh string costs ~250 ns on a 10^5..10^6-entry dict: the misses on the
-// table and on the stored key are taken one after the other.  Here a batch of
-// ids is hashed first, every probe slot is prefetched, and then probed, so the
-// misses of different ids overlap.  Open addressing, linear probing; a slot
-// holds the 64-bit hash, the row and the key's place in a byte arena (the key
-// bytes are compared on a hash match).
+// Python binding of ana::KeyMap (key_index.h): keys are str or bytes objects.
+std::string_view key_view(PyObject* o) {
+  char* p = nullptr;
+  Py_ssize_t n = 0;
+  if (PyBytes_Check(o)) {
+    if (PyBytes_AsStringAndSize(o, &p, &n) != 0) throw pybind11::error_already_set();
+    return std::string_view(p, (size_t)n);
+  }
+  const char* u = PyUnicode_AsUTF8AndSize(o, &n);
+  if (!u) throw pybind11::error_already_set();
+  return std::string_view(u, (size_t)n);
+}
+
+std::vector<std::string_view> key_views(const pybind11::list& keys) {
+  std::vector<std::string_view> kv(pybind11::len(keys));
+  for (size_t i = 0; i < kv.size(); ++i) kv[i] = key_view(keys[i].ptr());
+  return kv;
+}
+
 class KeyIndex {
  public:
-  KeyIndex() { rehash(1024); }
-
-  int64_t size() const { return n_; }
+  int64_t size() const { return map_.size(); }
 
   void add(pybind11::list keys, int64_t first_row) {
-    const int64_t k = (int64_t)pybind11::len(keys);
-    if (2 * (n_ + k) > (int64_t)slots_.size()) rehash(next_pow2(4 * (n_ + k)));
-    for (int64_t i = 0; i < k; ++i) {
-      std::string_view key = view(keys[i].ptr());
-      const uint64_t h = hash(key);
-      size_t j = h & mask_;
-      while (slots_[j].len != kEmpty) {
-        if (slots_[j].h == h && key_at(slots_[j]) == key)
-          throw std::invalid_argument("KeyIndex.add: duplicate key " + std::string(key));
-        j = (j + 1) & mask_;
-      }
-      slots_[j] = Slot{h, first_row + i, (uint64_t)arena_.size(), (uint32_t)key.size()};
-      arena_.append(key.data(), key.size());
-      ++n_;
-    }
+    const std::vector<std::string_view> kv = key_views(keys);
+    map_.reserve(map_.size() + (int64_t)kv.size());
+    for (size_t i = 0; i < kv.size(); ++i) map_.add(kv[i], first_row + (int64_t)i);
   }
 
   Tensor lookup(pybind11::list keys) const {
-    const int64_t k = (int64_t)pybind11::len(keys);
-    Tensor out = torch::empty({k}, torch::TensorOptions().dtype(torch::kInt64));
-    int64_t* o = out.data_ptr<int64_t>();
-    std::vector<std::string_view> kv(k);
-    std::vector<uint64_t> hv(k);
-    for (int64_t i = 0; i < k; ++i) {
-      kv[i] = view(keys[i].ptr());
-      hv[i] = hash(kv[i]);
-      __builtin_prefetch(&slots_[hv[i] & mask_]);
-    }
-    for (int64_t i = 0; i < k; ++i) {  // second pass: the key bytes of hash matches
-      const Slot& s = slots_[hv[i] & mask_];
-      if (s.h == hv[i]) __builtin_prefetch(arena_.data() + s.off);
-    }
-    for (int64_t i = 0; i < k; ++i) {
-      size_t j = hv[i] & mask_;
-      o[i] = -1;
-      while (slots_[j].len != kEmpty) {
-        if (slots_[j].h == hv[i] && key_at(slots_[j]) == kv[i]) {
-          o[i] = slots_[j].row;
-          break;
-        }
-        j = (j + 1) & mask_;
-      }
-    }
+    const std::vector<std::string_view> kv = key_views(keys);
+    Tensor out = torch::empty({(int64_t)kv.size()}, torch::TensorOptions().dtype(torch::kInt64));
+    map_.lookup(kv.data(), (int64_t)kv.size(), out.data_ptr<int64_t>());
     return out;
   }
 
  private:
-  static constexpr uint32_t kEmpty = 0xffffffffu;
-  struct Slot {
-    uint64_t h;
-    int64_t row;
-    uint64_t off;
-    uint32_t len;
-  };
-  std::vector<Slot> slots_;
-  std::string arena_;
-  size_t mask_ = 0;
-  int64_t n_ = 0;
-
-  static size_t next_pow2(int64_t v) {
-    size_t p = 1024;
-    while ((int64_t)p < v) p <<= 1;
-    return p;
-  }
-  static uint64_t hash(std::string_view k) {  // FNV-1a 64 + a final avalanche
-    uint64_t h = 1469598103934665603ull;
-    for (unsigned char c : k) h = (h ^ c) * 1099511628211ull;
-    h ^= h >> 33;
-    h *= 0xff51afd7ed558ccdull;
-    h ^= h >> 33;
-    return h;
-  }
-  std::string_view key_at(const Slot& s) const { return std::string_view(arena_.data() + s.off, s.len); }
-  static std::string_view view(PyObject* o) {
-    char* p = nullptr;
-    Py_ssize_t n = 0;
-    if (PyBytes_Check(o)) {
-      if (PyBytes_AsStringAndSize(o, &p, &n) != 0) throw pybind11::error_already_set();
-      return std::string_view(p, (size_t)n);
-    }
-    const char* u = PyUnicode_AsUTF8AndSize(o, &n);
-    if (!u) throw pybind11::error_already_set();
-    return std::string_view(u, (size_t)n);
-  }
-  void rehash(size_t cap) {
-    std::vector<Slot> old;
-    old.swap(slots_);
-    slots_.assign(cap, Slot{0, 0, 0, kEmpty});
-    mask_ = cap - 1;
-    for (const Slot& s : old) {
-      if (s.len == kEmpty) continue;
-      size_t j = s.h & mask_;
-      while (slots_[j].len != kEmpty) j = (j + 1) & mask_;
-      slots_[j] = s;
-    }
-  }
+  ana::KeyMap map_;
 };
 
 }  // namespace

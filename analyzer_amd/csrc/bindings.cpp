@@ -752,10 +752,12 @@ void reset_tags(Tensor state) {
 
 }  // namespace
 
-void register_batch_host(pybind11::module& m);  // batch_host.cpp
+void register_batch_host(pybind11::module& m);      // batch_host.cpp
+void register_telemetry_file(pybind11::module& m);  // telemetry_file.cpp
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_batch_host(m);
+  register_telemetry_file(m);
   m.doc() = "analyzer_amd native engine: gfx950 HIP kernels + C++ host mirror";
   m.def("gen_roster", &gen_roster, "K7: synthetic roster (state [P,16], attrs [P,4])");
   m.def("gen_stream", &gen_stream, "K7: synthetic match stream rec [M, 2K+2]");

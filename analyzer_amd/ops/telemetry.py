@@ -17,12 +17,16 @@ events) -- aligned with the rating outputs ``[M, 2K]``:
 
 Events are 8-B records (slot | type << 8 | 16-bit match tag << 16, value bits)
 grouped by match with CSR offsets ``evoff[M+1]`` (layout: csrc/telemetry_core.h).  ``make_telemetry`` generates them with the
-counter RNG (deterministic per global match index, device or host).
+counter RNG (deterministic per global match index, device or host);
+``TelemetrySource`` reads real events from an ANATEL01 file keyed by match api
+id (``write_telemetry`` / ``jsonl_to_telemetry`` build one from downloaded
+telemetry).
 """
 from __future__ import annotations
 
+import json
 from dataclasses import dataclass
-from typing import NamedTuple, Optional
+from typing import Iterable, List, NamedTuple, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -49,8 +53,76 @@ class Telemetry(NamedTuple):
         return int(self.events.shape[0])
 
 
-def make_telemetry(spec: TelemetrySpec, rec: torch.Tensor, K: int, base: int = 0) -> Telemetry:
-    """Synthetic telemetry for the matches of ``rec`` (global indices base..)."""
+class TelemetrySource:
+    """Real events for DOTELEMETRY: an ANATEL01 file (csrc/telemetry_file.cpp),
+    memory-mapped and keyed by match api id (``TELEMETRY_SOURCE=<path>``).
+    ``for_batch`` gathers a batch's events (pinned on a GPU) in the batch's
+    match order, slots and tags -- matches without telemetry get no events."""
+
+    def __init__(self, path: str):
+        self.path = path
+        self.file = native().TelemetryFile(path)
+
+    @property
+    def num_matches(self) -> int:
+        return int(self.file.num_matches)
+
+    def for_batch(self, ids: Sequence[str], K: int, device) -> Telemetry:
+        device = torch.device(device)
+        evoff, events = self.file.gather(list(ids), int(K), device.type == "cuda")
+        return Telemetry(evoff.to(device, non_blocking=True), events.to(device, non_blocking=True))
+
+
+EVENT_INDEX = {name: k for k, name in enumerate(EVENT_TYPES)}
+
+
+def write_telemetry(path: str, matches: Iterable[Tuple[str, Sequence]]) -> int:
+    """Write an ANATEL01 file from ``(match api id, events)`` pairs, an event
+    being ``(roster, position, type, value)`` -- type an EVENT_TYPES name or
+    index, value a float (ignored for kill / death / assist / other).  Returns
+    the number of events."""
+    ids: List[str] = []
+    off = [0]
+    meta: List[int] = []
+    vals: List[float] = []
+    for mid, evs in matches:
+        ids.append(str(mid))
+        for r, pos, typ, val in evs:
+            t = EVENT_INDEX[typ] if isinstance(typ, str) else int(typ)
+            if not (0 <= int(r) < 16 and 0 <= int(pos) < 16 and 0 <= t < 256):
+                raise ValueError("event (%r, %r, %r) out of range in match %s" % (r, pos, typ, mid))
+            meta.append(int(r) << 4 | int(pos) | t << 8)
+            vals.append(float(val))
+        off.append(len(meta))
+    events = np.empty((len(meta), 2), dtype=np.int32)
+    events[:, 0] = np.asarray(meta, dtype=np.int32)
+    events[:, 1] = np.asarray(vals, dtype=np.float32).view(np.int32)
+    native().write_telemetry_file(path, ids, torch.tensor(off, dtype=torch.int64), torch.from_numpy(events))
+    return len(meta)
+
+
+def jsonl_to_telemetry(src: str, dst: str) -> int:
+    """Convert downloaded telemetry as JSON lines -- ``{"match": api_id,
+    "events": [[roster, position, type, value], ...]}`` per line -- into an
+    ANATEL01 file.  Returns the number of events."""
+    def rows():
+        with open(src) as f:
+            for line in f:
+                if line.strip():
+                    d = json.loads(line)
+                    yield d["match"], d.get("events", ())
+    return write_telemetry(dst, rows())
+
+
+def make_telemetry(spec, rec: torch.Tensor, K: int, base: int = 0,
+                   ids: Optional[Sequence[str]] = None) -> Telemetry:
+    """Telemetry for the matches of ``rec``: from a ``TelemetrySource`` (the
+    matches' api ids ``ids``), else synthetic from a ``TelemetrySpec`` (global
+    match indices base..)."""
+    if isinstance(spec, TelemetrySource):
+        if ids is None or len(ids) != int(rec.shape[0]):
+            raise ValueError("a telemetry source needs the api id of every match")
+        return spec.for_batch(ids, K, rec.device)
     M = int(rec.shape[0])
     counts = native().gen_event_counts(M, spec.seed, spec.min_events, spec.max_events, base, rec.device)
     evoff = torch.zeros(M + 1, dtype=torch.int64, device=rec.device)
@@ -95,3 +167,27 @@ def aggregate_reference(tel: Telemetry, K: int) -> np.ndarray:
     np.add.at(out, (m[ok], slot[ok], feat[ok]), add[ok])
     np.add.at(out, (m, slot, np.full_like(m, 7)), 1.0)
     return out
+
+
+def main(argv=None) -> int:
+    """``python -m analyzer_amd.ops.telemetry convert events.jsonl out.anatel``"""
+    import argparse
+
+    ap = argparse.ArgumentParser(description="telemetry event files (ANATEL01)")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    c = sub.add_parser("convert", help="JSON lines -> ANATEL01")
+    c.add_argument("src")
+    c.add_argument("dst")
+    i = sub.add_parser("info", help="matches and events of an ANATEL01 file")
+    i.add_argument("path")
+    a = ap.parse_args(argv)
+    if a.cmd == "convert":
+        print(json.dumps({"events": jsonl_to_telemetry(a.src, a.dst), "file": a.dst}))
+    else:
+        f = native().TelemetryFile(a.path)
+        print(json.dumps({"matches": int(f.num_matches), "events": int(f.num_events)}))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -82,19 +82,24 @@ class ObjectBatchRater:
         tele = stats = None
         if telemetry is not None:
             from ..ops.telemetry import allocate_stats, make_telemetry
-            tel = make_telemetry(telemetry, rec, K)
+            tel = make_telemetry(telemetry, rec, K, ids=[m.api_id for m in matches])
             stats = allocate_stats(len(matches), K, self.device)
             tele = (tel.evoff, tel.events, stats)
         res = self.rater.rate(roster, rec, K, telemetry=tele)
         self._write_back(matches, res, roster, players, K)
+        status = [int(s) for s in res.status.cpu().tolist()]
         if stats is not None:
-            self._write_stats(matches, stats, K)
-        return [int(s) for s in res.status.cpu().tolist()]
+            self._write_stats(matches, stats, K, status)
+        return status
 
     @staticmethod
-    def _write_stats(matches, stats: torch.Tensor, K: int) -> None:
+    def _write_stats(matches, stats: torch.Tensor, K: int, status) -> None:
+        """participant_stats of every committed match (not the quarantined ones)."""
         st = stats.cpu().double().numpy()
+        bad = set(R.ERROR_STATUSES) | {R.NOT_PROCESSED}
         for i, m in enumerate(matches):
+            if status[i] in bad:
+                continue
             for ri, r in enumerate(list(m.rosters)[:2]):
                 for pos, p in enumerate(r.participants[:K]):
                     vals = dict(zip(STAT_COLUMNS, (float(v) for v in st[i, ri * K + pos])))

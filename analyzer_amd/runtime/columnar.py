@@ -117,6 +117,14 @@ def afk_mask(n: np.ndarray, afk0: np.ndarray, afk1: np.ndarray) -> np.ndarray:
     return mask
 
 
+def stats_mask(status: np.ndarray) -> np.ndarray:
+    """Matches whose telemetry stats are written: every one that is committed
+    (rated, AFK, invalid rosters, unsupported mode) -- not the quarantined ones."""
+    from ..ops import rate as R
+
+    return ~np.isin(status, list(R.ERROR_STATUSES) + [R.NOT_PROCESSED])
+
+
 def touched_players(batch: MatchBatch) -> np.ndarray:
     """Player keys of the batch's rated matches (their final ratings are written)."""
     rated = batch.status == RATED
@@ -436,7 +444,7 @@ class ColumnarSession:
             if stt[i] in (RATED, AFK, INVALID):
                 pt.i_afk[ps] = 0 if stt[i] == RATED else 1
         if b.stats is not None:
-            sel = (stt == RATED)[:, None, None] & (b.part >= 0)
+            sel = stats_mask(stt)[:, None, None] & (b.part >= 0)
             pt.stats[b.part[sel]] = b.stats[sel]
 
     def _write_batch_numpy(self, b: MatchBatch) -> None:
@@ -463,7 +471,8 @@ class ColumnarSession:
         pt.i_rating[p, 2 * mode] = b.m_mu[sel]
         pt.i_rating[p, 2 * mode + 1] = b.m_sig[sel]
         if b.stats is not None:
-            pt.stats[p] = b.stats[sel]
+            ss = stats_mask(stt)[:, None, None] & (b.part >= 0)
+            pt.stats[b.part[ss]] = b.stats[ss]
         if b.final_keys is not None and len(b.final_keys):
             cur = st.players.rating[b.final_keys]
             cols = np.repeat(b.final_tracks, 2, axis=1)  # (mu, sigma) of each touched track

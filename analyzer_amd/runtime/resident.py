@@ -274,7 +274,7 @@ class ResidentBatchRater:
         stats = None
         if telemetry is not None:
             from ..ops.telemetry import allocate_stats, make_telemetry
-            tel = make_telemetry(telemetry, rec, K)
+            tel = make_telemetry(telemetry, rec, K, ids=[m.api_id for m in matches])
             stats = allocate_stats(len(matches), K, self.device)
             res = self._eager(rec, K, (tel.evoff, tel.events, stats))
         else:
@@ -284,7 +284,7 @@ class ResidentBatchRater:
         final = roster.state.index_select(0, idx).cpu().numpy() if rows else None
         st = self._write_back(matches, res, packed, K, row_of, final, rows)
         if stats is not None:
-            _write_stats(matches, stats, K)
+            _write_stats(matches, stats, K, st)
         if self.device.type == "cuda":
             self.rater.check_errors(self.device)
         return st
@@ -345,7 +345,7 @@ class ResidentBatchRater:
         p = PendingBatch(batch, K, pos_t, uniq_t, undo=undo)
         if telemetry is not None:
             from ..ops.telemetry import allocate_stats, make_telemetry
-            tel = make_telemetry(telemetry, rec_t, K)
+            tel = make_telemetry(telemetry, rec_t, K, ids=batch.ids)
             p.stats = allocate_stats(M, K, self.device)
             res = self._eager(rec_t, K, (tel.evoff, tel.events, p.stats))
         else:
@@ -507,9 +507,13 @@ def _to_host(src: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def _write_stats(matches, stats: torch.Tensor, K: int) -> None:
+def _write_stats(matches, stats: torch.Tensor, K: int, status) -> None:
+    """participant_stats of every committed match (not the quarantined ones)."""
     st = stats.cpu().double().numpy()
+    bad = set(R.ERROR_STATUSES) | {R.NOT_PROCESSED}
     for i, m in enumerate(matches):
+        if int(status[i]) in bad:
+            continue
         for ri, r in enumerate(m.rosters[:2]):
             for pos, p in enumerate(r.participants[:K]):
                 vals = dict(zip(STAT_COLUMNS, (float(v) for v in st[i, ri * K + pos])))

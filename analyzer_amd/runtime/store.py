@@ -360,10 +360,13 @@ class SqliteSession(_SessionBase):
             c.executemany("UPDATE participant_items SET any_afk=0, %s=?, %s=? WHERE rowid=?"
                           % (_q(col + "_mu"), _q(col + "_sigma")), rows)
         if b.stats is not None:
-            st8 = b.stats[sel].tolist()
+            from .columnar import stats_mask
+
+            ss = stats_mask(st)[:, None, None] & (b.part >= 0)
+            st8 = b.stats[ss].tolist()
             c.executemany("INSERT OR REPLACE INTO participant_stats VALUES (?, ?, %s)"
                           % ", ".join("?" * len(STAT_COLUMNS)),
-                          [[names[p], names[p]] + v for p, v in zip(ps, st8)])
+                          [[names[p], names[p]] + v for p, v in zip(b.part[ss].tolist(), st8)])
         if b.final_keys is not None and len(b.final_keys):
             pn, prow_of = self.store.player_names, self.store.player_rowid
             f = b.final

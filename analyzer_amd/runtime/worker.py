@@ -35,12 +35,14 @@ Deliberate, documented differences:
   a queue it never declares, which a broker silently drops);
 * ``DOTELEMETRY=true`` (with ``ENGINE=native``) aggregates per-event telemetry
   into ``participant_stats`` in the same launch as the rating (K8 fused mode,
-  BASELINE config 4).  Telemetry is synthetic here: the reference only forwards
-  asset URLs (worker.py:148-161) and this image has no network to fetch them.
-  Synthetic stats are therefore never persisted into a real database: with a
-  ``DATABASE_URI`` other than the in-process ``memory://`` / ``columnar://`` stores, ``connect``
-  refuses ``DOTELEMETRY`` unless ``SYNTHETIC_TELEMETRY=true`` says the run is a
-  benchmark.
+  BASELINE config 4).  The reference only forwards asset URLs
+  (worker.py:148-161); here ``TELEMETRY_SOURCE`` names an ANATEL01 file of the
+  downloaded events keyed by match api id (ops/telemetry.TelemetrySource,
+  ``python -m analyzer_amd.ops.telemetry convert`` builds one from JSON lines).
+  Without it the events are synthetic, and synthetic stats are never persisted
+  into a real database: with a ``DATABASE_URI`` other than the in-process
+  ``memory://`` / ``columnar://`` stores, ``connect`` refuses ``DOTELEMETRY``
+  unless ``SYNTHETIC_TELEMETRY=true`` says the run is a benchmark.
 
 Per-batch counters (matches rated/afk/invalid/unsupported/quarantined, timing)
 are kept in ``stats`` and logged as one JSON line per batch (SURVEY §5 metrics).
@@ -102,18 +104,19 @@ class Worker:
         self.failed_ids: List[str] = []
         self._python_rater = MatchRater(self.rater_cfg)
         self._object_rater = object_rater  # runtime.batch.ObjectBatchRater, built lazily
+        self._tele_source = None
         self._pipe = False
         self._inflight: Optional[_InFlight] = None  # launched, not yet committed / acked
         self._flush = None                          # timer completing it when no batch follows
 
     # ------------------------------------------------------------ connect (W3/W4)
     def connect(self) -> "Worker":
-        if self.cfg.dotelemetry and not self.cfg.synthetic_telemetry:
+        if self.cfg.dotelemetry and not self.cfg.synthetic_telemetry and not self.cfg.telemetry_source:
             uri = self.cfg.database_uri or ""
             if uri and not uri.startswith(("memory:", "columnar:")):  # in-process stores only
-                raise ValueError("DOTELEMETRY aggregates SYNTHETIC telemetry (no real event source "
-                                 "exists yet): refusing to write it into %s; set "
-                                 "SYNTHETIC_TELEMETRY=true for a benchmark run" % uri)
+                raise ValueError("DOTELEMETRY without TELEMETRY_SOURCE aggregates SYNTHETIC telemetry: "
+                                 "refusing to write it into %s; point TELEMETRY_SOURCE at an event "
+                                 "file, or set SYNTHETIC_TELEMETRY=true for a benchmark run" % uri)
         if self.store is None:
             # no DATABASE_URI: an in-process store -- columnar for the native engine
             # (no per-object work at all), the object graph for the Python engine
@@ -428,6 +431,11 @@ class Worker:
     def _telemetry_spec(self, batches_before: Optional[int] = None):
         if not self.cfg.dotelemetry:
             return None
+        if self.cfg.telemetry_source:  # real events, opened once
+            if self._tele_source is None:
+                from ..ops.telemetry import TelemetrySource
+                self._tele_source = TelemetrySource(self.cfg.telemetry_source)
+            return self._tele_source
         from ..ops.telemetry import TelemetrySpec
         lo, hi = (int(x) for x in self.cfg.telemetry_events.split(","))
         before = self.stats.batches if batches_before is None else batches_before

@@ -1,10 +1,12 @@
 """K8 telemetry aggregation: generator, host mirror vs numpy oracle, fused launch
 (CPU here; the device kernels are covered in test_engine_gpu.py)."""
 import numpy as np
+import pytest
 import torch
 
 from analyzer_amd.ops import rate as R
 from analyzer_amd.ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
+from analyzer_amd.runtime.objects import STAT_COLUMNS
 from analyzer_amd.ops.telemetry import (STAT_NAMES, TelemetrySpec, aggregate, aggregate_reference,
                                         allocate_stats, make_telemetry)
 
@@ -86,3 +88,107 @@ def test_strict_attribution_same_tile_other_match():
     bad = native().telemetry(tel.evoff, ev, K, stats, torch.zeros(1, dtype=torch.int32))
     assert bad == 1
     assert stats[2, :, 7].sum() == 1 and stats[3, :, 7].sum() == 2
+
+
+# ------------------------------------------------------------------ real event files
+def _events_for(store, ids, seed=3):
+    """Random downloaded-telemetry events for stored matches: (roster, position,
+    type, value) per event, some matches without any, some events malformed
+    (a third roster's participant, a position beyond the team)."""
+    rng = np.random.default_rng(seed)
+    s = store.session()
+    out, want = [], {}
+    for m in s.load_matches(ids):
+        if rng.random() < 0.15:
+            continue  # no telemetry downloaded for this match
+        evs = []
+        for _ in range(int(rng.integers(0, 40))):
+            r = int(rng.integers(0, 2))
+            parts = m.rosters[r].participants if r < len(m.rosters) else []
+            pos = int(rng.integers(0, len(parts) + (1 if rng.random() < 0.05 else 0))) if parts else 0
+            typ = int(rng.integers(0, 8))
+            val = float(np.float32(rng.uniform(0, 500)))
+            evs.append((r, pos, typ, val))
+            if pos < len(parts):
+                st = want.setdefault(parts[pos].api_id, [0.0] * 8)
+                if typ <= 2:
+                    st[typ] += 1.0
+                elif typ <= 6:
+                    st[typ] += val
+                st[7] += 1.0
+        out.append((m.api_id, evs))
+    s.close()
+    return out, want
+
+
+@pytest.mark.parametrize("uri", ["columnar://", "sqlite:///{tmp}/t.db"])
+def test_worker_aggregates_events_from_a_telemetry_file(tmp_path, uri):
+    """DOTELEMETRY with TELEMETRY_SOURCE: a real store (no SYNTHETIC_TELEMETRY)
+    gets participant_stats aggregated from the events written to the file --
+    round trip file -> worker -> store, per participant."""
+    _telemetry_file_roundtrip(tmp_path, uri)
+
+
+@pytest.mark.gpu
+def test_worker_telemetry_file_on_device(gpu_device, tmp_path):
+    """The same round trip with the fused rating + aggregation launch on the GPU
+    (pinned gather, asynchronous upload)."""
+    _telemetry_file_roundtrip(tmp_path, "columnar://", device_check=True)
+
+
+def _telemetry_file_roundtrip(tmp_path, uri, device_check=False):
+    from analyzer_amd.config import RaterConfig, WorkerConfig
+    from analyzer_amd.ops.telemetry import TelemetrySource, jsonl_to_telemetry
+    from analyzer_amd.runtime import broker as B
+    from analyzer_amd.runtime.source import populate, publish
+    from analyzer_amd.runtime.store import open_store
+    from analyzer_amd.runtime.worker import Worker
+    import json
+
+    uri = uri.format(tmp=tmp_path)
+    store = open_store(uri)
+    ms = populate(store, 60, 40, team_size=3, seed=2)
+    ids = [m if isinstance(m, str) else m.api_id for m in ms]
+    evs, want = _events_for(store, ids)
+    with open(tmp_path / "ev.jsonl", "w") as f:
+        for mid, e in evs:
+            f.write(json.dumps({"match": mid, "events": [list(x) for x in e]}) + "\n")
+    path = str(tmp_path / "ev.anatel")
+    assert jsonl_to_telemetry(str(tmp_path / "ev.jsonl"), path) == sum(len(e) for _, e in evs)
+    assert TelemetrySource(path).num_matches == len(evs)
+    clock = B.ManualClock()
+    cfg = WorkerConfig(batchsize=16, idle_timeout=1.0, engine="native", database_uri=uri, dotelemetry=True,
+                       telemetry_source=path, resident=True)
+    w = Worker(cfg, store=store, broker=B.MemoryBroker(clock), rater_cfg=RaterConfig(), clock=clock)
+    w.connect()
+    publish(w.channel, "analyze", ids)
+    w.start_consuming()
+    assert w.stats.acked == 60
+    if device_check:
+        assert w._batched().device.type == "cuda"
+    s = store.session()
+    n = 0
+    for m in s.load_matches(ids):
+        for p in m.participants:
+            got = s.participant_stats(p.api_id)
+            exp = want.get(p.api_id, [0.0] * 8)
+            assert got is not None, p.api_id
+            np.testing.assert_allclose([got[c] for c in STAT_COLUMNS], exp, rtol=1e-5, atol=1e-3)
+            n += exp[7] > 0
+    assert n > 100
+
+
+def test_synthetic_guard_only_without_a_source(tmp_path):
+    from analyzer_amd.config import WorkerConfig
+    from analyzer_amd.ops.telemetry import write_telemetry
+    from analyzer_amd.runtime import broker as B
+    from analyzer_amd.runtime.worker import Worker
+
+    uri = "sqlite:///" + str(tmp_path / "g.db")
+    with pytest.raises(ValueError, match="SYNTHETIC"):
+        Worker(WorkerConfig(engine="native", database_uri=uri, dotelemetry=True),
+               broker=B.MemoryBroker()).connect()
+    path = str(tmp_path / "e.anatel")
+    write_telemetry(path, [("m0", [(0, 0, "kill", 0.0)])])
+    Worker(WorkerConfig(engine="native", database_uri=uri, dotelemetry=True, telemetry_source=path),
+           broker=B.MemoryBroker()).connect()
