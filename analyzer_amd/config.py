@@ -108,6 +108,9 @@ class WorkerConfig:
     # BATCHSIZE=500 the device part of a batch is ~10 us of a ~1 ms host-bound batch,
     # and the second batch's bookkeeping measured 3-6 % slower (profiles/r3/worker_*)
     pipeline: bool = False
+    # new: fault injection -- these match api ids fail to rate as if their
+    # numerics broke: quarantined (QUARANTINE=true) or failing their batch (false)
+    fault_poison: frozenset = frozenset()
 
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "WorkerConfig":
@@ -133,6 +136,7 @@ class WorkerConfig:
             resident=_resident_default(env),
             skip_rated=env.get("SKIP_RATED") == "true",
             pipeline=env.get("PIPELINE") == "true",
+            fault_poison=frozenset(x for x in (env.get("FAULT_POISON") or "").split(",") if x),
         )
 
     @property

@@ -292,6 +292,7 @@ class Worker:
                     fl.mb = fl.session.load_batch(fl.ids, self.cfg.chunksize)
             # the telemetry seed of the serial worker: batches committed before this one
             seed_batches = self.stats.batches + (1 if self._inflight is not None else 0)
+            self._inject_faults(fl.mb)
             with trace_range("rate", matches=len(fl.mb), engine="native"):
                 fl.pending = self._batched().launch_batch(fl.mb, fl.session.fetch_players,
                                                           telemetry=self._telemetry_spec(seed_batches),
@@ -395,6 +396,8 @@ class Worker:
         for match in matches:
             sp = session.savepoint(match) if self.cfg.quarantine else None
             try:
+                if match.api_id in self.cfg.fault_poison:
+                    raise FloatingPointError("injected fault (FAULT_POISON)")
                 self._python_rater.rate_match(match)
                 counts["rated"] = counts.get("rated", 0) + 1
             except (KeyError, ValueError, FloatingPointError, ZeroDivisionError, IndexError,
@@ -446,9 +449,19 @@ class Worker:
 
         if len(batch) == 0:
             return []
+        self._inject_faults(batch)
         status = self._batched().rate_batch(batch, session.fetch_players, telemetry=self._telemetry_spec(),
                                             stage=getattr(session, "stage_players", None))
         return self._statuses(batch, status, counts)
+
+    def _inject_faults(self, batch) -> None:
+        """FAULT_POISON on a columnar batch: the poisoned matches lose their
+        participants, so the kernels report an empty roster -- a failed match that
+        leaves the state untouched, quarantined like any other."""
+        if self.cfg.fault_poison:
+            for i, mid in enumerate(batch.ids):
+                if mid in self.cfg.fault_poison:
+                    batch.n[i] = 0
 
     def _statuses(self, batch, status, counts) -> List[str]:
         """Count a rated batch's statuses; its quarantined match ids (raises with
@@ -468,8 +481,13 @@ class Worker:
     def _rate_native(self, session, matches, counts) -> List[str]:
         from ..ops import rate as R
 
-        status = self._batched().rate(matches, telemetry=self._telemetry_spec())
         bad = []
+        if self.cfg.fault_poison:  # injected faults: never rated, like a failed match
+            bad = [m.api_id for m in matches if m.api_id in self.cfg.fault_poison]
+            if bad:
+                counts["fault_injected"] = len(bad)
+                matches = [m for m in matches if m.api_id not in self.cfg.fault_poison]
+        status = self._batched().rate(matches, telemetry=self._telemetry_spec()) if matches else []
         for m, s in zip(matches, status):
             name = R.STATUS_NAMES.get(s, str(s))
             counts[name] = counts.get(name, 0) + 1

@@ -264,3 +264,23 @@ def test_native_key_index():
     col, ids = _mixed_store()
     rows = col.match_rows(ids[::-1] + ["missing"])
     assert rows.tolist() == [col.m_index[i] for i in ids[::-1]] + [-1]
+
+
+@pytest.mark.parametrize("quarantine", [True, False])
+def test_fault_injection_poison_matches_python_engine(quarantine):
+    """FAULT_POISON: the named matches fail in both engines -- the same failed
+    queue, failed batches and store contents (SURVEY §5 fault injection)."""
+    poison = frozenset({"m3", "m17", "m40"})
+    wr, ids = run(MemoryStore(), "python", quarantine=quarantine, fault_poison=poison)
+    col = ColumnarStore()
+    wc, _ = run(col, "native", quarantine=quarantine, fault_poison=poison)
+    failed_r = sorted(m.body for m in wr.rabbit.drain("analyze_failed"))
+    failed_c = sorted(m.body for m in wc.rabbit.drain("analyze_failed"))
+    assert failed_c == failed_r
+    if quarantine:
+        assert sorted(failed_r) == sorted(x.encode() for x in poison)
+    assert wc.stats.failed_batches == wr.stats.failed_batches == (0 if quarantine else 3)
+    assert_same(snapshot(col, ids), snapshot(wr.store, ids), 2e-3)
+    wo, _ = run(MemoryStore(), "native", quarantine=quarantine, fault_poison=poison)  # object path
+    assert sorted(m.body for m in wo.rabbit.drain("analyze_failed")) == failed_r
+    assert_same(snapshot(wo.store, ids), snapshot(wr.store, ids), 2e-3)
