@@ -37,10 +37,12 @@ def _ext_suffix() -> str:
     return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 
-def target_path(diag: bool = False) -> Path:
+def target_path(diag: bool = False, variant: str = "") -> Path:
     """The in-tree library: ``_C`` (production) or ``_C_diag`` (``--diag``: also
     the telemetry kernel's diagnostic / tuning variants, ANA_TELE_DEBUG and
     ANA_TELE_SPAN; load it with ANA_NATIVE_LIB)."""
+    if variant:  # experiment builds (--variant): ab/<name>_C.so, loaded with ANA_NATIVE_LIB
+        return PKG.parent / "ab" / (variant + "_C.so")
     return PKG / (("_C_diag" if diag else "_C") + _ext_suffix())
 
 
@@ -65,10 +67,12 @@ def _compile(cmd, src: Path, obj: Path, force: bool) -> str:
     return "built %s" % src.name
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = False, diag: bool = False) -> Path:
-    out = target_path(diag)
-    objdir = BUILD / "diag" if diag else BUILD
-    dflags = ["-DANA_DIAG_BUILD=1"] if diag else []
+def build(force: bool = False, jobs: int = 4, verbose: bool = False, diag: bool = False,
+          variant: str = "", defines=()) -> Path:
+    out = target_path(diag, variant)
+    out.parent.mkdir(parents=True, exist_ok=True)
+    objdir = BUILD / ("variant_" + variant) if variant else BUILD / "diag" if diag else BUILD
+    dflags = (["-DANA_DIAG_BUILD=1"] if diag else []) + ["-D" + d for d in defines]
     sources = [CSRC / n for n in HIP_SOURCES + CPP_SOURCES if (CSRC / n).exists()]
     if not force and out.exists() and out.stat().st_mtime >= max(_deps_mtime(s) for s in sources):
         # the in-tree library is newer than every source: nothing to do (a GPU box
@@ -129,8 +133,12 @@ def main(argv=None) -> int:
     ap.add_argument("--jobs", type=int, default=4)
     ap.add_argument("--diag", action="store_true",
                     help="build _C_diag with the diagnostic kernel variants (scripts/tune_tele.py)")
+    ap.add_argument("--variant", default="",
+                    help="experiment build: ab/<VARIANT>_C.so with --define flags (in-call A/B, gpu.sh ab)")
+    ap.add_argument("--define", action="append", default=[], help="extra -D for the device code")
     args = ap.parse_args(argv)
-    path = build(force=args.force, jobs=args.jobs, verbose=True, diag=args.diag)
+    path = build(force=args.force, jobs=args.jobs, verbose=True, diag=args.diag, variant=args.variant,
+                 defines=args.define)
     print(path)
     return 0
 

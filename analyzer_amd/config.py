@@ -171,7 +171,9 @@ class EngineConfig:
     ANA_RATE_DIAG           0         executor timing build: per-phase clocks in ctrl[20..47] (ops/rate.diag)
     ANA_RATE_TIGHT          -1        executor: 2K lanes per match instead of the next power of two (-1 auto)
     ANA_TELE_FUSED_TAIL     0         fused telemetry only after the executor's chunks are drained
-    ANA_TELE_ROLE           2         fused telemetry: one wave in N aggregates from the start (0 = idle waves)
+    ANA_TELE_ROLE           2         fused telemetry: one wave in N aggregates from the start (0 = idle
+                                      waves; -1 = inline: each lane group folds the events of the match
+                                      it rates)
     ======================  ========  =============================================
 
     The executor / fused-telemetry knobs reach the launch as ``BatchRater.knobs``

@@ -433,12 +433,14 @@ void check_rows(const Tensor& t, const char* name, int64_t P, int64_t cols, cons
 
 // s0: common window start, prior: this rank's prior of the sweep (s0 itself in
 // the first sweep), s: the posterior after the local shard
+// K9 merge: s0 / prior / s2 are base rows [P, 16] = (mu, sigma) of the 8 granules
+// (sweep_core.h kBaseFloats); s is the roster [P, 32]
 void sweep_delta(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma,
                  bool scaled, Tensor buf) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
-  check_rows(s0, "s0", P, ana::kRowFloats, dev);
-  check_rows(prior, "prior", P, ana::kRowFloats, dev);
+  check_rows(s0, "s0 (base rows)", P, ana::kBaseFloats, dev);
+  check_rows(prior, "prior (base rows)", P, ana::kBaseFloats, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
   check_rows(attrs, "attrs", P, 4, dev);
   check_rows(buf, "buf", P, 16, dev);
@@ -456,18 +458,18 @@ void sweep_delta(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor vst, do
   }
 }
 
-// decoded rows to s and, if s2 is non-empty, also to s2
+// decoded rows to s and, if s2 is non-empty, base rows [P, 16] (sweep_core.h) to s2
 void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor s2, Tensor vst,
                  double unknown_sigma, bool scaled) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
-  check_rows(s0, "s0", P, ana::kRowFloats, dev);
+  check_rows(s0, "s0 (base rows)", P, ana::kBaseFloats, dev);
   check_rows(buf, "buf", P, 16, dev);
   check_rows(attrs, "attrs", P, 4, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
   float* p2 = nullptr;
   if (s2.numel()) {
-    check_rows(s2, "s2", P, ana::kRowFloats, dev);
+    check_rows(s2, "s2 (base rows)", P, ana::kBaseFloats, dev);
     p2 = s2.data_ptr<float>();
   }
   check(vst, "vst", torch::kFloat32, dev);
@@ -490,8 +492,8 @@ void sweep_delta_packed(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor 
                         Tensor msg, Tensor cnt) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
-  check_rows(s0, "s0", P, ana::kRowFloats, dev);
-  check_rows(prior, "prior", P, ana::kRowFloats, dev);
+  check_rows(s0, "s0 (base rows)", P, ana::kBaseFloats, dev);
+  check_rows(prior, "prior (base rows)", P, ana::kBaseFloats, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
   check_rows(attrs, "attrs", P, 4, dev);
   TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
@@ -520,7 +522,7 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
                         double unknown_sigma) {
   const auto dev = s.device();
   const int64_t P = s.size(0);
-  check_rows(s0, "s0", P, ana::kRowFloats, dev);
+  check_rows(s0, "s0 (base rows)", P, ana::kBaseFloats, dev);
   TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
                   msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
               "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
@@ -529,7 +531,7 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
   check_rows(s, "state", P, ana::kRowFloats, dev);
   float* p2 = nullptr;
   if (s2.numel()) {
-    check_rows(s2, "s2", P, ana::kRowFloats, dev);
+    check_rows(s2, "s2 (base rows)", P, ana::kBaseFloats, dev);
     p2 = s2.data_ptr<float>();
   }
   check(vst, "vst", torch::kFloat32, dev);

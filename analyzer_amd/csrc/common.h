@@ -37,6 +37,7 @@ namespace ana {
 constexpr int kTracks = 7;        // shared + 6 modes
 constexpr int kGranules = 8;      // 16-B granules per player row
 constexpr int kRowFloats = 32;    // floats per player row (128 B)
+constexpr int kBaseFloats = 16;   // DP merge base row: (mu, sigma) per granule (sweep_core.h)
 // Schedule link of a slot (K5), 4 bytes: the match of the player's next
 // occurrence (kNoMatch: none) | kLinkHasPred if the player occurred earlier in
 // the window.  A match publishes each player's shared granule tagged with that

@@ -55,6 +55,9 @@
 namespace ana {
 
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight
+// K8 inline telemetry: events per match loaded with the batch's granules (more go
+// through a remainder loop after the rating); per group lane ceil(64 / G) 8-B loads
+constexpr int kTeleInline = 64;
 
 // One wave iteration's assignment: per lane, its group's match and the
 // participant's slot facts and granules (section 4 of the executor loop).
@@ -65,13 +68,22 @@ struct Batch {
   bool inr = false, islast = false, own = false, any_dup = false;
   uint32_t lk0 = kNoMatch;  // schedule link (common.h): next match | has-earlier
   v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
+  // K8 inline telemetry (TelemetryParams::role_stride < 0): the match's event count, a
+  // match without state to rate (tele-only: early status in est), its first kTeleInline
+  // events (lane j of the group holds events j, j + G, ...)
+  int64_t toff = 0;
+  int32_t tcnt = 0;
+  bool tonly = false;
+  uint8_t est = kRated;
 };
 
 // TELE: K8 fused telemetry compiled in (the plain rating launch leaves it out,
-// which frees the registers its code pins).  DIAG: the timing build
+// which frees the registers its code pins): 1 = aggregation tiles taken by idle or
+// dedicated waves (one-hot MFMA), 2 = inline, each lane group folds the events of the
+// match it rated (TelemetryParams::role_stride < 0).  DIAG: the timing build
 // (ANA_RATE_DIAG=1) -- every wave clocks its iterations and its wait with
 // s_memrealtime and adds them to ctrl[20..27] at exit (launch_rate).
-template <int K, int G, bool TELE, bool DIAG>
+template <int K, int G, int TELE, bool DIAG>
 __global__ void __launch_bounds__(256)
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
@@ -81,6 +93,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
   constexpr int kH = kHeld;
+  constexpr bool TILES = TELE == 1;  // K8 tiles taken by idle / dedicated waves
+  constexpr bool INL = TELE == 2;    // K8 inline: each group folds its match's events
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
   static_assert(kH == 2 || kH == 4, "readiness reads the held chunks' local counts as one vector");
@@ -91,9 +105,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   __shared__ hvec lloc[kWavesPerBlock][kChunk];
   // this iteration's pick per group, written by the lane holding the match:
   // {match index, slot << 8 | lane in chunk, meta0, meta1, player ids...}
-  constexpr int SP = (4 + S + 3) / 4 * 4;
+  constexpr int SPT = (4 + S + 3) / 4 * 4;  // inline telemetry words: {offset lo, hi, count, 0}
+  constexpr int SP = SPT + (INL ? 4 : 0);
+  // inline event loads per lane: kTeleInline events per group, at most 8 loads per lane
+  constexpr int TT = INL ? ((kTeleInline + G - 1) / G < 8 ? (kTeleInline + G - 1) / G : 8) : 1;
+  // inline telemetry: one stat block [S][8] per group, accumulated with LDS float adds
+  __shared__ __attribute__((aligned(16))) float tstat[kWavesPerBlock][INL ? NG : 1][INL ? S * kStatFeatures : 4];
   __shared__ __attribute__((aligned(16))) int32_t lpick[kWavesPerBlock][NG][SP];  // v4i slots
-  __shared__ float tele[kWavesPerBlock][TELE ? tele_scratch_floats<K>() : 1];  // K8 scratch
+  __shared__ float tele[kWavesPerBlock][TILES ? tele_scratch_floats<K>() : 1];  // K8 scratch
   // each group's output row, assembled here so it leaves as whole 16-B quads
   // (one store instruction writes the rows of every group: full lines, where
   // per-field stores sent 6-7 partial-line writes per match to the fabric)
@@ -135,6 +154,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // registers so the lane that picks a match hands the whole record to its group
   // through one LDS slot (one round trip instead of pick -> meta -> id)
   int32_t hrec[kH][R];
+  int64_t hoff[kH];    // per lane (inline telemetry): first event of match cbase + lane
+  int32_t hcnt[kH];    // ... and its event count
   int32_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
                        // (a window has < 2^28 slots, so match indices fit int32)
   uint64_t pend[kH];   // wave-uniform: stateful matches not yet handed to a group
@@ -148,6 +169,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     for (int k = 0; k < R; ++k) hrec[h][k] = -1;
     dval[h] = kNone;
     need[h] = 0u;
+    hoff[h] = 0;
+    hcnt[h] = 0;
   }
   bool exhausted = false, tk_pending = false;
   unsigned tk = 0;                 // ticket returned to lane 0
@@ -157,10 +180,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // spans from the start -- spread one per (block group, SIMD) so no SIMD and no
   // XCD gets them all -- while the rating waves keep their dependency chains
   // moving; an aggregation wave joins the rating when the events run out.
-  const bool tele_role = TELE && tp.role_stride > 0 && tp.impl != 0;
+  const bool tele_role = TILES && tp.role_stride > 0 && tp.impl != 0;
+  // inline: each lane group folds its match's events into the participants' stats
+  // right after rating it (no tiles, nothing co-runs with the rating)
+  const bool tele_inline = INL && tp.role_stride < 0 && tp.evoff != nullptr;
   const int tele_span = tele_role ? kTeleMaxSpan : kTeleTile;
-  const int64_t tele_tiles = TELE && tp.evoff ? (tp.num_matches + tele_span - 1) / tele_span : 0;
-  bool tele_done = tele_tiles == 0;
+  const int64_t tele_tiles = TILES && tp.evoff ? (tp.num_matches + tele_span - 1) / tele_span : 0;
+  bool tele_done = tele_tiles == 0 || tele_inline;
   auto tele_claim = [&]() -> int64_t {
     unsigned t = 0;
     if (lane == 0)
@@ -169,13 +195,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     return (int64_t)t < tele_tiles ? (int64_t)t : -1;
   };
   auto tele_run = [&](int64_t t) {
-    if constexpr (TELE) {
+    if constexpr (TILES) {
       if (tele_role) telemetry_tile_mfma<K, 0, kTeleMaxSpan>(tp, t, lane, tele[wv], &ctrl[13]);
       else if (tp.impl) telemetry_tile_mfma<K>(tp, t, lane, tele[wv], &ctrl[13]);
       else telemetry_tile<K>(tp, t, lane, tele[wv], &ctrl[13]);
     }
   };
-  if constexpr (TELE) {
+  if constexpr (TILES) {
     if (tele_role) {
       const int b = blockIdx.x, per = tp.role_stride >= 4 ? tp.role_stride / 4 : 1;
       const bool agg = tp.role_stride >= 4   ? (wv == ((b >> 3) & 3) && ((b >> 5) % per) == 0)
@@ -188,6 +214,51 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
     }
   }
+  // K8 inline (software-pipelined): the events of the last rated batch, per lane,
+  // folded by tele_flush in the next iteration (and at exit)
+  v2u tev_prev[TT];
+#pragma unroll
+  for (int t = 0; t < TT; ++t) tev_prev[t] = v2u{0u, 0u};
+  int32_t tp_m = -1, tp_cnt = 0;
+  int64_t tp_off = 0;
+  auto tele_flush = [&]() {
+    if constexpr (INL) {
+      if (tp_m < 0) return;  // this lane's group rated nothing last iteration
+      float* const ts = tstat[wv][g];
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      if (j < S) {
+        reinterpret_cast<v4f*>(ts)[2 * j] = v4f{0.f, 0.f, 0.f, 0.f};
+        reinterpret_cast<v4f*>(ts)[2 * j + 1] = v4f{0.f, 0.f, 0.f, 0.f};
+      }
+      uint32_t nbad = 0;
+      const uint32_t mtag = (uint32_t)tp_m & 0xffffu;
+      auto fold = [&](v2u ev) {
+        const int32_t meta = (int32_t)ev.x;
+        const int slot = event_slot(meta);
+        if (event_tag(meta) != mtag || slot >= S) {  // strict attribution (telemetry_core.h)
+          ++nbad;
+          return;
+        }
+        float add;
+        const int f = event_feature(event_type(meta), __uint_as_float(ev.y), add);
+        if (f >= 0) atomicAdd(&ts[slot * kStatFeatures + f], add);
+        atomicAdd(&ts[slot * kStatFeatures + kStatEvents], 1.f);
+      };
+#pragma unroll
+      for (int t = 0; t < TT; ++t)
+        if (j + G * t < tp_cnt) fold(tev_prev[t]);
+      // events past the loaded ones (rare: > kTeleInline in one match)
+      for (int e = j + G * TT; e < tp_cnt; e += G)
+        fold(__builtin_nontemporal_load(reinterpret_cast<const v2u*>(tp.events + 2 * (tp_off + e))));
+      if (j < S) {  // (the group's LDS writes and reads are the same wave's, in order)
+        v4f* dst = reinterpret_cast<v4f*>(tp.stats + ((int64_t)tp_m * S + j) * kStatFeatures);
+        __builtin_nontemporal_store(reinterpret_cast<const v4f*>(ts)[2 * j], dst);
+        __builtin_nontemporal_store(reinterpret_cast<const v4f*>(ts)[2 * j + 1], dst + 1);
+      }
+      if (nbad) atomicAdd(&ctrl[13], nbad);  // malformed events (none in a valid stream)
+      tp_m = -1;
+    }
+  };
   const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : prm.idle_spins < 0 ? 0u : 8u;
   const int cl = prm.chunk_len;  // matches per ticket (<= kChunk lanes)
   // chunks in the window (hoisted: a 64-bit division is ~130 scalar instructions)
@@ -246,7 +317,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           w[2] = hrec[h][S];
           w[3] = hrec[h][S + 1];
 #pragma unroll
-          for (int k = 0; k < SP - 4; ++k) w[4 + k] = k < S ? hrec[h][k] : -1;
+          for (int k = 0; k < SPT - 4; ++k) w[4 + k] = k < S ? hrec[h][k] : -1;
+          if constexpr (INL) {
+            w[SPT] = (int32_t)(uint32_t)hoff[h];
+            w[SPT + 1] = (int32_t)(hoff[h] >> 32);
+            w[SPT + 2] = hcnt[h];
+            w[SPT + 3] = 0;
+          }
           v4i* dst = reinterpret_cast<v4i*>(&lpick[wv][nassigned + (int)below][0]);
 #pragma unroll
           for (int q = 0; q < SP / 4; ++q) dst[q] = v4i{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]};
@@ -258,8 +335,15 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
     int32_t my_m = 0, my_id = -1;
     uint32_t my_m0 = 0u, my_m1 = 0u;
+    int64_t my_toff = 0;
+    int32_t my_tcnt = 0;
     if (g < nassigned) {  // two LDS reads, one wait
       const v4i pk = *reinterpret_cast<const v4i*>(&lpick[wv][g][0]);
+      if constexpr (INL) {
+        const v4i tk4 = *reinterpret_cast<const v4i*>(&lpick[wv][g][SPT]);
+        my_toff = (int64_t)(((uint64_t)(uint32_t)tk4.y << 32) | (uint32_t)tk4.x);
+        my_tcnt = tk4.z;
+      }
       if (j < S) my_id = lpick[wv][g][4 + j];
       my_m = pk.x;
       my_h = pk.y >> 8;
@@ -292,7 +376,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       nb.n1 = meta_n1(m0);
       nb.rank0 = meta_winner0(m1) ? 0 : 1;
       nb.rank1 = meta_winner1(m1) ? 0 : 1;
-      const bool inr = my_h >= 0 && j < S && rpos < (r0 ? nb.n0 : nb.n1);
+      // inline telemetry: a match without state to rate (AFK, invalid, unsupported,
+      // malformed) still goes through a group, for its events only
+      nb.tonly = INL && ((m1 >> 4) & 1u);
+      nb.est = (uint8_t)(m1 >> 28);
+      nb.tcnt = my_h >= 0 ? my_tcnt : 0;
+      nb.toff = my_toff;
+      const bool inr = my_h >= 0 && j < S && rpos < (r0 ? nb.n0 : nb.n1) && !nb.tonly;
       nb.inr = inr;
       const int32_t id = inr ? my_id : -1;
       nb.id = id;
@@ -329,6 +419,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     int staging = -1;
     int32_t r[R];
     uint32_t lks[S];  // the staged match's links: its readiness count
+    int64_t stoff = 0;  // inline telemetry: the staged match's first event and count
+    int32_t stcnt = 0;
 #pragma unroll
     for (int k = 0; k < R; ++k) r[k] = -1;
 #pragma unroll
@@ -375,11 +467,21 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
             lks[2 * k] = v.x;
             lks[2 * k + 1] = v.y;
           }
+          if (tele_inline) {
+            stoff = tp.evoff[m];
+            stcnt = (int32_t)(tp.evoff[m + 1] - stoff);
+          }
         }
       }
     }
 
     // ---------------------------------------------- (10) rate a batch
+    int32_t row_m = -1;  // ANA_EXP_ROWLATE: the group's output row leaves after the polls
+    (void)row_m;
+    // inline telemetry: the events this iteration's groups load for the next flush
+    v2u tev_next[TT];
+    int32_t tn_m = -1, tn_cnt = 0;
+    int64_t tn_off = 0;
     auto rate_batch = [&](const Batch& bt) {
     int my_h = bt.my_h;
     const int my_bit = bt.my_bit;
@@ -431,7 +533,33 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       if (gstale) my_h = -1;
     }
+    if constexpr (INL) {
+      // K8 inline, software-pipelined: this group's events are LOADED now (HBM, cold)
+      // and folded into its stats one iteration later (tele_flush, after the next
+      // wait), so no rating ever waits for event data; a stale group loads nothing
+      // (it is retried, and aggregated then)
+      if (tele_inline && my_h >= 0) {
+        tn_m = m;
+        tn_cnt = bt.tcnt;
+        tn_off = bt.toff;
+      }
+#pragma unroll
+      for (int t = 0; t < TT; ++t) {
+        const bool okl = tele_inline && my_h >= 0 && j + G * t < bt.tcnt;
+        const int32_t* src = okl ? tp.events + 2 * (bt.toff + j + G * t)
+                                 : reinterpret_cast<const int32_t*>(tp.evoff);
+        tev_next[t] = __builtin_nontemporal_load(reinterpret_cast<const v2u*>(src));
+      }
+    }
     if (my_h >= 0) {
+#if ANA_EXP_DEPLOAD
+      // experiment: a load whose address depends on the gathered granule, needed at
+      // the publish (prices a position-chained successor list)
+      uint32_t dep = (uint32_t)gs.w ^ (uint32_t)id;
+      asm volatile("" : "+v"(dep));
+      const v2u xl = __builtin_amdgcn_raw_buffer_load_b64(
+          rl, own ? (int)(((dep * 2654435761u) & ((1u << 26) - 1u)) * 4u) : kOutOfRange, 0, 16);
+#endif
       const float smu = __int_as_float(gs.x), ssg = __int_as_float(gs.z);
       const float mmu = __int_as_float(gm.x), msg = __int_as_float(gm.z);
       // seed attributes only for players without a shared rating (their first
@@ -474,6 +602,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         rmmu = __shfl(mmu, src);
         rmsg = __shfl(msg, src);
       }
+      if (bt.tonly) gst = bt.est;  // inline telemetry: a stateless match keeps its early status
       if (gst == kRated && (n0 == 0 || n1 == 0)) gst = kErrEmptyRoster;
       float nsm = NAN, nss = NAN, nmm = NAN, nms = NAN, dl = NAN, q = NAN;
       if (gst == kRated) {
@@ -520,6 +649,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       const bool ok = gst == kRated && inr;
       if constexpr (DIAG) d_p[2] = __builtin_amdgcn_s_memrealtime();
+#if ANA_EXP_DEPLOAD
+      asm volatile("; dep %0 %1" :: "v"(xl.x), "v"(xl.y));
+#endif
       if (inr && islast) {  // publish: new values, or the untouched ones on error
         const int off = id * (kRowFloats * 4);
         // shared granule: tagged with the next reader + bumped mode counter;
@@ -576,7 +708,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         lr[4 * S + j] = ok ? nms : NAN;
       }
       if (j == 0) {
-        lr[5 * S] = gst == kRated ? q : NAN;
+        // (AFK / invalid rosters: quality 0 -- only tele-only groups carry those here)
+        lr[5 * S] = gst == kRated ? q : (gst == kAfk || gst == kInvalidRosters) ? 0.f : NAN;
         lr[5 * S + 1] = __uint_as_float((uint32_t)gst);  // the status byte, upper bytes 0
       }
       if (j == (G > 1 ? 1 : 0)) {
@@ -584,6 +717,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         for (int k = 5 * S + 2; k < 4 * OQ; ++k) lr[k] = 0.f;  // row padding
       }
       // (the group's LDS writes and reads are the same wave's, in order)
+#if ANA_EXP_ROWLATE
+      row_m = m;
+#else
 #pragma unroll
       for (int t = 0; t < (OQ + G - 1) / G; ++t) {
         typedef float v4f __attribute__((ext_vector_type(4)));
@@ -591,6 +727,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         if (qd < OQ)
           __builtin_nontemporal_store(reinterpret_cast<const v4f*>(lr)[qd], reinterpret_cast<v4f*>(orm) + qd);
       }
+#endif
     }
     };
 
@@ -612,6 +749,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     if constexpr (DIAG) d_w0 = __builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (DIAG) d_w1 = __builtin_amdgcn_s_memrealtime();
+    if constexpr (INL) {
+      // the previous iteration's event loads retired in the wait above: re-define the
+      // registers here so the compiler's own wait before tele_flush cannot also wait
+      // for the event loads this iteration issues in between
+#pragma unroll
+      for (int t = 0; t < TT; ++t) asm volatile("" : "+v"(tev_prev[t]));
+    }
 
     // ---------------------------------------------- (9) install the staged chunk
     if (staging >= 0) {
@@ -642,33 +786,47 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         }
         r[S + 1] = dup ? (r[S + 1] | 8) : (r[S + 1] & ~8);
       }
+      const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
+      // inline telemetry: a stateless match is handed to a group like any ready one
+      // (its counter needs 0), flagged tele-only (meta1 bit 4) with its status in bits 28..31
+      const bool tonly = tele_inline && mm < M && est != kRated;
+      if (tonly) r[S + 1] = (int32_t)(((uint32_t)r[S + 1] & 0x0fffffffu) | 16u | ((uint32_t)est << 28));
 #pragma unroll
       for (int h = 0; h < kH; ++h)
         if (h == staging) {
 #pragma unroll
           for (int k = 0; k < R; ++k) hrec[h][k] = r[k];
+          hoff[h] = stoff;
+          hcnt[h] = stcnt;
         }
       reinterpret_cast<uint32_t*>(&lloc[wv][lane])[staging] = 0u;
-      const uint8_t est = mm < M ? early_status<K>(r, P) : kRated;
-      if (mm < M && est != kRated) {  // no state, no dependencies: finish it now
+      if (mm < M && est != kRated && !tonly) {  // no state, no dependencies: finish it now
 #pragma unroll
         for (int q = 0; q < 5 * S; ++q) orows[mm * orow + q] = NAN;
         orows[mm * orow + 5 * S] = (est == kAfk || est == kInvalidRosters) ? 0.f : NAN;
         reinterpret_cast<uint8_t*>(orows + mm * orow + 5 * S + 1)[0] = est;
       }
-      const uint64_t pm = __ballot(mm < M && est == kRated);
+      const uint64_t pm = __ballot(mm < M && (est == kRated || tonly));
 #pragma unroll
       for (int h = 0; h < kH; ++h)
         if (h == staging) {
           pend[h] = pm;
           dval[h] = kNone;  // first poll next iteration
-          need[h] = nd;
+          need[h] = tonly ? 0u : nd;  // a tele-only match's links are unwritten
           if (pm == 0ull) cbase[h] = -1;
         }
     }
 
     if constexpr (DIAG) d_p[0] = d_p[1] = d_p[2] = d_p[3] = d_w1;
     rate_batch(nb);
+    if constexpr (INL) {  // fold the previous batch's events, then hand this batch's on
+      tele_flush();
+#pragma unroll
+      for (int t = 0; t < TT; ++t) tev_prev[t] = tev_next[t];
+      tp_m = tn_m;
+      tp_cnt = tn_cnt;
+      tp_off = tn_off;
+    }
     if constexpr (DIAG) {
       if (worked) {
         const uint64_t end = __builtin_amdgcn_s_memrealtime();
@@ -707,7 +865,19 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     for (int h = 0; h < kH; ++h)
       dval[h] = __builtin_amdgcn_raw_buffer_load_b32(rd, ((pend[h] >> lane) & 1ull) ? (cbase[h] + lane) * 4 : kOutOfRange,
                                                      0, 16);
-
+#if ANA_EXP_ROWLATE
+    if (row_m >= 0) {
+      float* const orm = orows + (int64_t)row_m * orow;
+      const float* const lr = lrow[wv][g];
+#pragma unroll
+      for (int t = 0; t < (OQ + G - 1) / G; ++t) {
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const int qd = j + t * G;
+        if (qd < OQ)
+          __builtin_nontemporal_store(reinterpret_cast<const v4f*>(lr)[qd], reinterpret_cast<v4f*>(orm) + qd);
+      }
+    }
+#endif
 
     // ---------------------------------------------- (11) retire finished chunks
     {
@@ -728,6 +898,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 #pragma unroll
     for (int h = 0; h < kH; ++h) held |= cbase[h] >= 0;
     if (exhausted && !held && !tk_pending) {
+      tele_flush();  // inline telemetry: the last batch's events
       if (lane == 0) {  // diagnostics: wave iterations (ctrl[15]), hand-offs (ctrl[26..27])
         __hip_atomic_fetch_add((gu32*)&ctrl[15], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add((gu32*)&ctrl[26], n_local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -752,7 +923,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
             atomicAdd(reinterpret_cast<unsigned long long*>(&ctrl[40 + 2 * q]), (unsigned long long)d_s[q]);
         }
       }
-      if constexpr (TELE) {
+      if constexpr (TILES) {
         while (!tele_done) {  // leftover telemetry tiles
           const int64_t t = tele_claim();
           if (t < 0) tele_done = true;
@@ -785,7 +956,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
             reinterpret_cast<uint8_t*>(orows + (int64_t)(cbase[h] + lane) * orow + 5 * S + 1)[0] = kNotProcessed;
         return;  // give up: the host sees ctrl[1] and raises
       }
-      if constexpr (TELE) {
+      if constexpr (TILES) {
         // nothing ready for a while: aggregate a telemetry tile instead of sleeping
         if (!tele_done && ((!tp.fused_tail && !tele_role) || !held)) {
           const int64_t t = tele_claim();
@@ -845,9 +1016,10 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
                      rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, tp)
 #define ANA_RATE_LAUNCH(k, g)                                      \
   do {                                                             \
-    if (tp.evoff) ANA_RATE_LAUNCH_D(k, g, true, false);            \
-    else if (prm.diag) ANA_RATE_LAUNCH_D(k, g, false, true);       \
-    else ANA_RATE_LAUNCH_D(k, g, false, false);                    \
+    if (tp.evoff && tp.role_stride < 0) ANA_RATE_LAUNCH_D(k, g, 2, false); \
+    else if (tp.evoff) ANA_RATE_LAUNCH_D(k, g, 1, false);          \
+    else if (prm.diag) ANA_RATE_LAUNCH_D(k, g, 0, true);           \
+    else ANA_RATE_LAUNCH_D(k, g, 0, false);                        \
   } while (0)
   switch (K) {
     case 1: ANA_RATE_LAUNCH(1, 2); break;

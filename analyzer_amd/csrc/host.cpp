@@ -236,20 +236,22 @@ int host_rate(int K, bool fp64, const int32_t* rec, float* state, const float* a
 
 namespace ana {
 
+// s0, a, s2: base rows [P][kBaseFloats] (sweep_core.h); s: roster rows [P][32]
 void host_sweep_delta(const float* s0, const float* a, const float* s, const float* attrs,
                       const float* vst, float unknown_sigma, bool scaled, float* buf, int64_t P) {
   for (int64_t p = 0; p < P; ++p)
-    sweep_delta_player(s0 + p * kRowFloats, a + p * kRowFloats, s + p * kRowFloats, attrs + p * 4,
+    sweep_delta_player(s0 + p * kBaseFloats, a + p * kBaseFloats, s + p * kRowFloats, attrs + p * 4,
                        vst, unknown_sigma, scaled, buf + p * 16);
 }
 
 void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                       bool scaled, const float* vst, float unknown_sigma, int64_t P) {
   for (int64_t p = 0; p < P; ++p) {
-    sweep_apply_player(s0 + p * kRowFloats, buf + p * 16, attrs + p * 4, vst, unknown_sigma, scaled,
-                       s + p * kRowFloats);
+    float ob[kBaseFloats];
+    sweep_apply_player(s0 + p * kBaseFloats, buf + p * 16, attrs + p * 4, vst, unknown_sigma, scaled,
+                       s + p * kRowFloats, ob);
     if (s2)
-      for (int k = 0; k < kRowFloats; ++k) s2[p * kRowFloats + k] = s[p * kRowFloats + k];
+      for (int k = 0; k < kBaseFloats; ++k) s2[p * kBaseFloats + k] = ob[k];
   }
 }
 

@@ -337,7 +337,7 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
 // as well costs more than it saves (8.13 -> 8.46 ms).  ANA_LINK_PARTS overrides
 // the count (1 = one pass).
 static int link_parts(int64_t n) {
-  if (const char* e = getenv("ANA_LINK_PARTS")) {
+  if (const char* e = getenv("ANA_LINK_PARTS")) {  // per launch: tests switch it at run time
     const int v = atoi(e);
     if (v >= 1) return v > 16 ? 16 : v;
   }
@@ -481,10 +481,9 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
   // ANA_SORT_RB=10: 10-bit digits (2 passes for <= 2^20 players instead of 3).  Measured
   // on MI355X, 10M 3v3 / 1M players: 3.11 ms vs 1.76 ms for 8-bit digits (1024
   // per-tile runs of ~4 elements scatter the pass's writes) -> off by default.
-  const char* rb_env = getenv("ANA_SORT_RB");
-  const bool wide = bits <= 20 && rb_env && atoi(rb_env) == 10;
-  const char* nt_env = getenv("ANA_SORT_NT");
-  const bool nt = nt_env ? atoi(nt_env) != 0 : false;
+  static const int rb_env = [] { const char* e = getenv("ANA_SORT_RB"); return e ? atoi(e) : 8; }();
+  static const bool nt = [] { const char* e = getenv("ANA_SORT_NT"); return e && atoi(e) != 0; }();
+  const bool wide = bits <= 20 && rb_env == 10;
   switch (K) {
 #define ANA_SORT_CASE(k)                                                                         \
   case k:                                                                                        \

@@ -28,74 +28,125 @@
 
 namespace ana {
 
-// one thread per player, 16-B vector accesses (rows are kRowFloats = 32 floats)
-constexpr int kRowVec = kRowFloats / 4;
+// Layout: EIGHT LANES PER PLAYER, lane t = granule t of the 128-B roster row
+// (tracks 0..6, granule 7 the spare).  Every access is then a whole-wave run of
+// contiguous bytes -- a wave reads 1 KB of roster rows, 512 B of base rows
+// (float2 (mu, sigma) per granule, sweep_core.h kBaseFloats) per instruction, and
+// writes its players' messages as one 224-B run -- where one thread per player
+// touched 64 rows 16 B at a time (8 loads per row, none of them coalesced).  The
+// per-track math is sweep_core.h's (the host mirror runs the same functions);
+// the shared track's start value and the touch fields cross lanes by shuffles
+// within the 8-lane group.  Base rows instead of full start rows: 64 of the 128
+// B per player on every start read and write (-26 % merge traffic).
+constexpr int kLanesPerPlayer = kGranules;  // 8
+constexpr int kRowVec = kRowFloats / 4;      // 16-B vectors per roster row (C2 exchange below)
 
-__device__ __forceinline__ void load_row(const float4* __restrict__ src, int64_t p, float* r) {
-#pragma unroll
-  for (int k = 0; k < kRowVec; ++k) {
-    const float4 x = src[p * kRowVec + k];
-    r[4 * k] = x.x; r[4 * k + 1] = x.y; r[4 * k + 2] = x.z; r[4 * k + 3] = x.w;
-  }
+struct TrackLane {
+  int64_t p;  // player
+  int t;      // granule / track
+  int gbase;  // first lane of the player's group
+};
+
+__device__ __forceinline__ TrackLane track_lane() {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  return TrackLane{gid / kLanesPerPlayer, (int)(gid % kLanesPerPlayer), lane & ~(kLanesPerPlayer - 1)};
 }
 
-// s0: common window start, a: this rank's prior of the sweep (may alias s0),
-// s: posterior after the local window; buf: [P][16] messages
-__global__ void sweep_delta_kernel(const float4* __restrict__ s0, const float4* a0,
-                                   const float4* __restrict__ s, const float4* __restrict__ attrs,
-                                   const float* __restrict__ vst, float unknown_sigma, int scaled,
-                                   float4* __restrict__ buf, int64_t P) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  float c[kRowFloats], a[kRowFloats], b[kRowFloats], o[16];
-  load_row(s0, p, c);
-  if (a0 != s0) load_row(a0, p, a);
-  else
-#pragma unroll
-    for (int k = 0; k < kRowFloats; ++k) a[k] = c[k];
-  load_row(s, p, b);
-  const float4 at = attrs[p];
-  const float attr[4] = {at.x, at.y, at.z, at.w};
-  sweep_delta_player(c, a, b, attr, vst, unknown_sigma, scaled != 0, o);
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    buf[p * 4 + k] = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+// sum over the 8 lanes of a player's group (every lane gets it)
+__device__ __forceinline__ float group8_sum(float x) {
+  x += __shfl_xor(x, 1);
+  x += __shfl_xor(x, 2);
+  x += __shfl_xor(x, 4);
+  return x;
 }
 
-// decoded rows go to s and, when given, also to s2: the final merge of a window
-// writes the next window's common start there (no per-window snapshot copy),
-// a causal re-sweep writes the rank's prior for the next message
-__global__ void sweep_apply_kernel(const float4* __restrict__ s0, const float4* __restrict__ buf,
-                                   const float4* __restrict__ attrs, float4* s, float4* s2,
-                                   const float* __restrict__ vst, float unknown_sigma, int scaled,
-                                   int64_t P) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  float a[kRowFloats], d[16], o[kRowFloats];
-  load_row(s0, p, a);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float4 y = buf[p * 4 + k];
-    d[4 * k] = y.x; d[4 * k + 1] = y.y; d[4 * k + 2] = y.z; d[4 * k + 3] = y.w;
-  }
-  const float4 at = attrs[p];
+__device__ __forceinline__ void lane_seed(const float4* __restrict__ attrs, int64_t p, const float* vst,
+                                          float unknown_sigma, bool& seeded, float& seed_mu,
+                                          float& seed_sig) {
+  const float4 at = attrs[p];  // one 16-B line per group: broadcast
   const float attr[4] = {at.x, at.y, at.z, at.w};
-  sweep_apply_player(a, d, attr, vst, unknown_sigma, scaled != 0, o);
-#pragma unroll
-  for (int k = 0; k < kRowVec; ++k) {
-    const float4 v = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
-    s[p * kRowVec + k] = v;
-    if (s2) s2[p * kRowVec + k] = v;
+  seed_mu = NAN;
+  seed_sig = NAN;
+  seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
+}
+
+// this lane's track message (tracks 0..6) and the player's touch fields (lo, hi)
+__device__ __forceinline__ void lane_delta(const TrackLane& L, const float2* __restrict__ s0,
+                                          const float2* a0, const float4* __restrict__ s,
+                                          const float4* __restrict__ attrs, const float* vst,
+                                          float unknown_sigma, bool scaled, float& dp, float& dt,
+                                          float& lo, float& hi) {
+  const float2 c = s0[L.p * kLanesPerPlayer + L.t];
+  const float2 a = a0 != s0 ? a0[L.p * kLanesPerPlayer + L.t] : c;
+  const float4 b = s[L.p * kLanesPerPlayer + L.t];
+  const float c0mu = __shfl(c.x, L.gbase), c0sg = __shfl(c.y, L.gbase);
+  bool seeded;
+  float seed_mu, seed_sig;
+  lane_seed(attrs, L.p, vst, unknown_sigma, seeded, seed_mu, seed_sig);
+  bool touched = false;
+  dp = dt = 0.f;
+  if (L.t < kTracks)
+    sweep_delta_track(L.t, c.x, c.y, c0mu, c0sg, a.x, a.y, b.x, b.z, seeded, seed_mu, seed_sig, scaled,
+                      dp, dt, touched);
+  const float field = touched ? (float)(1 << (4 * (L.t & 3))) : 0.f;
+  lo = group8_sum(L.t < 4 ? field : 0.f);
+  hi = group8_sum(L.t >= 4 ? field : 0.f);
+}
+
+// decode this lane's track: roster granule {mu, 0, sigma, 0} and base (mu, sigma)
+__device__ __forceinline__ void lane_apply(const TrackLane& L, const float2* __restrict__ s0, float dpi,
+                                          float dtau, uint32_t lo, uint32_t hi,
+                                          const float4* __restrict__ attrs, const float* vst,
+                                          float unknown_sigma, bool scaled, float4* s, float2* s2) {
+  const float2 c = s0[L.p * kLanesPerPlayer + L.t];
+  const float c0mu = __shfl(c.x, L.gbase), c0sg = __shfl(c.y, L.gbase);
+  bool seeded;
+  float seed_mu, seed_sig;
+  lane_seed(attrs, L.p, vst, unknown_sigma, seeded, seed_mu, seed_sig);
+  float mu = c.x, sg = c.y;  // granule 7: the spare floats of the base row
+  if (L.t < kTracks) {
+    const uint32_t touched = L.t < 4 ? (lo >> (4 * L.t)) & 15u : (hi >> (4 * (L.t - 4))) & 15u;
+    sweep_apply_track(L.t, c.x, c.y, c0mu, c0sg, dpi, dtau, touched, seeded, seed_mu, seed_sig, scaled,
+                      mu, sg);
   }
+  s[L.p * kLanesPerPlayer + L.t] = make_float4(mu, 0.f, sg, 0.f);
+  if (s2) s2[L.p * kLanesPerPlayer + L.t] = make_float2(mu, sg);
+}
+
+// s0: base rows of the common window start, a0: this rank's prior of the sweep
+// (base rows; may alias s0), s: roster rows after the local window; buf: [P][16]
+// fp32 messages = a float2 per lane (lane 7: the touch fields)
+__global__ void __launch_bounds__(256)
+sweep_delta_kernel(const float2* __restrict__ s0, const float2* a0, const float4* __restrict__ s,
+                   const float4* __restrict__ attrs, const float* __restrict__ vst, float unknown_sigma,
+                   int scaled, float2* __restrict__ buf, int64_t P) {
+  const TrackLane L = track_lane();
+  if (L.p >= P) return;  // whole groups leave together (grid = 8 lanes per player)
+  float dp, dt, lo, hi;
+  lane_delta(L, s0, a0, s, attrs, vst, unknown_sigma, scaled != 0, dp, dt, lo, hi);
+  buf[L.p * kLanesPerPlayer + L.t] = L.t < kTracks ? make_float2(dp, dt) : make_float2(lo, hi);
+}
+
+// decoded rows go to s and, when given, base rows to s2: the final merge of a
+// window writes the next window's common start there (no per-window snapshot
+// copy), a causal re-sweep writes the rank's prior for the next message
+__global__ void __launch_bounds__(256)
+sweep_apply_kernel(const float2* __restrict__ s0, const float2* __restrict__ buf,
+                   const float4* __restrict__ attrs, float4* s, float2* s2, const float* __restrict__ vst,
+                   float unknown_sigma, int scaled, int64_t P) {
+  const TrackLane L = track_lane();
+  if (L.p >= P) return;
+  const float2 d = buf[L.p * kLanesPerPlayer + L.t];
+  const uint32_t lo = (uint32_t)__shfl(d.x, L.gbase + kTracks), hi = (uint32_t)__shfl(d.y, L.gbase + kTracks);
+  lane_apply(L, s0, d.x, d.y, lo, hi, attrs, vst, unknown_sigma, scaled != 0, s, s2);
 }
 
 // ------------------------------------------------- compressed (fp16 / bf16) messages
-// COMM_DTYPE=bf16/fp16 merges used to write the fp32 [P][16] buffer, convert it
-// into the 16-bit message block + int32 touch counts for the all-reduce, and
-// convert back before decoding: four extra passes over the buffer per bucket.
-// These variants write / read the all-reduce operands directly: msg [P][14] in
-// the 16-bit type (round to nearest even, as torch's .to()), cnt [P][2] int32
-// (the base-16 touch fields, exact integers).
+// COMM_DTYPE=bf16/fp16 merges write / read the all-reduce operands directly:
+// msg [P][14] in the 16-bit type (round to nearest even, as torch's .to()) --
+// lane t < 7 one 4-B word (its track's two halves) --, cnt [P][2] int32 (the
+// base-16 touch fields, exact integers; lane 7).
 // The empty asm pins x as the rounded fp32 message: without it the compiler folds
 // the message's last fma into the conversion (v_fma_mixlo_f16, one rounding
 // instead of two), which is not what the fp32 path + .to() produce on ties.
@@ -117,65 +168,44 @@ __device__ __forceinline__ float from_half_bits(uint32_t b) {
 }
 
 template <typename H>
-__global__ void sweep_delta_packed_kernel(const float4* __restrict__ s0, const float4* a0,
-                                          const float4* __restrict__ s, const float4* __restrict__ attrs,
-                                          const float* __restrict__ vst, float unknown_sigma,
-                                          uint32_t* __restrict__ msg, int2* __restrict__ cnt, int64_t P) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  float c[kRowFloats], a[kRowFloats], b[kRowFloats], o[16];
-  load_row(s0, p, c);
-  if (a0 != s0) load_row(a0, p, a);
+__global__ void __launch_bounds__(256)
+sweep_delta_packed_kernel(const float2* __restrict__ s0, const float2* a0, const float4* __restrict__ s,
+                          const float4* __restrict__ attrs, const float* __restrict__ vst,
+                          float unknown_sigma, uint32_t* __restrict__ msg, int2* __restrict__ cnt, int64_t P) {
+  const TrackLane L = track_lane();
+  if (L.p >= P) return;
+  float dp, dt, lo, hi;
+  lane_delta(L, s0, a0, s, attrs, vst, unknown_sigma, true, dp, dt, lo, hi);
+  if (L.t < kTracks)  // 14 halves = 7 words (28 B per player, contiguous over the wave)
+    msg[L.p * kTracks + L.t] = (uint32_t)to_half_bits<H>(dp) | ((uint32_t)to_half_bits<H>(dt) << 16);
   else
-#pragma unroll
-    for (int k = 0; k < kRowFloats; ++k) a[k] = c[k];
-  load_row(s, p, b);
-  const float4 at = attrs[p];
-  const float attr[4] = {at.x, at.y, at.z, at.w};
-  sweep_delta_player(c, a, b, attr, vst, unknown_sigma, true, o);
-#pragma unroll
-  for (int k = 0; k < 7; ++k)  // 14 halves = 7 words (28 B per player)
-    msg[p * 7 + k] = (uint32_t)to_half_bits<H>(o[2 * k]) | ((uint32_t)to_half_bits<H>(o[2 * k + 1]) << 16);
-  cnt[p] = make_int2((int)o[14], (int)o[15]);
+    cnt[L.p] = make_int2((int)lo, (int)hi);
 }
 
 template <typename H>
-__global__ void sweep_apply_packed_kernel(const float4* __restrict__ s0, const uint32_t* __restrict__ msg,
-                                          const int2* __restrict__ cnt, const float4* __restrict__ attrs,
-                                          float4* s, float4* s2, const float* __restrict__ vst,
-                                          float unknown_sigma, int64_t P) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= P) return;
-  float a[kRowFloats], d[16], o[kRowFloats];
-  load_row(s0, p, a);
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const uint32_t w = msg[p * 7 + k];
-    d[2 * k] = from_half_bits<H>(w & 0xffffu);
-    d[2 * k + 1] = from_half_bits<H>(w >> 16);
-  }
-  const int2 c = cnt[p];
-  d[14] = (float)c.x;
-  d[15] = (float)c.y;
-  const float4 at = attrs[p];
-  const float attr[4] = {at.x, at.y, at.z, at.w};
-  sweep_apply_player(a, d, attr, vst, unknown_sigma, true, o);
-#pragma unroll
-  for (int k = 0; k < kRowVec; ++k) {
-    const float4 v = make_float4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
-    s[p * kRowVec + k] = v;
-    if (s2) s2[p * kRowVec + k] = v;
-  }
+__global__ void __launch_bounds__(256)
+sweep_apply_packed_kernel(const float2* __restrict__ s0, const uint32_t* __restrict__ msg,
+                          const int2* __restrict__ cnt, const float4* __restrict__ attrs, float4* s,
+                          float2* s2, const float* __restrict__ vst, float unknown_sigma, int64_t P) {
+  const TrackLane L = track_lane();
+  if (L.p >= P) return;
+  const uint32_t w = L.t < kTracks ? msg[L.p * kTracks + L.t] : 0u;
+  const int2 c = cnt[L.p];  // broadcast within the group
+  lane_apply(L, s0, from_half_bits<H>(w & 0xffffu), from_half_bits<H>(w >> 16), (uint32_t)c.x,
+             (uint32_t)c.y, attrs, vst, unknown_sigma, true, s, s2);
+}
+
+static dim3 track_grid(int64_t P) {
+  return dim3((unsigned)((P * kLanesPerPlayer + 255) / 256));
 }
 
 int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, const float* attrs,
                               const float* vst, float unknown_sigma, int bf16, void* msg, int32_t* cnt,
                               int64_t P, hipStream_t st) {
   if (P <= 0) return 0;
-  const dim3 grid((unsigned)((P + 255) / 256)), block(256);
   auto args = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, block, 0, st, reinterpret_cast<const float4*>(s0),
-                       reinterpret_cast<const float4*>(a), reinterpret_cast<const float4*>(s),
+    hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
+                       reinterpret_cast<const float2*>(a), reinterpret_cast<const float4*>(s),
                        reinterpret_cast<const float4*>(attrs), vst, unknown_sigma,
                        reinterpret_cast<uint32_t*>(msg), reinterpret_cast<int2*>(cnt), P);
   };
@@ -188,12 +218,11 @@ int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* c
                               const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
                               int64_t P, hipStream_t st) {
   if (P <= 0) return 0;
-  const dim3 grid((unsigned)((P + 255) / 256)), block(256);
   auto args = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, block, 0, st, reinterpret_cast<const float4*>(s0),
+    hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
                        reinterpret_cast<const uint32_t*>(msg), reinterpret_cast<const int2*>(cnt),
                        reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
-                       reinterpret_cast<float4*>(s2), vst, unknown_sigma, P);
+                       reinterpret_cast<float2*>(s2), vst, unknown_sigma, P);
   };
   if (bf16) args(sweep_apply_packed_kernel<__bf16>);
   else args(sweep_apply_packed_kernel<_Float16>);
@@ -204,20 +233,20 @@ int launch_sweep_delta(const float* s0, const float* a, const float* s, const fl
                        const float* vst, float unknown_sigma, int scaled, float* buf, int64_t P,
                        hipStream_t st) {
   if (P <= 0) return 0;
-  hipLaunchKernelGGL(sweep_delta_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(s0), reinterpret_cast<const float4*>(a),
+  hipLaunchKernelGGL(sweep_delta_kernel, track_grid(P), dim3(256), 0, st,
+                     reinterpret_cast<const float2*>(s0), reinterpret_cast<const float2*>(a),
                      reinterpret_cast<const float4*>(s), reinterpret_cast<const float4*>(attrs), vst,
-                     unknown_sigma, scaled, reinterpret_cast<float4*>(buf), P);
+                     unknown_sigma, scaled, reinterpret_cast<float2*>(buf), P);
   return (int)hipGetLastError();
 }
 
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                        const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st) {
   if (P <= 0) return 0;
-  hipLaunchKernelGGL(sweep_apply_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(s0), reinterpret_cast<const float4*>(buf),
+  hipLaunchKernelGGL(sweep_apply_kernel, track_grid(P), dim3(256), 0, st,
+                     reinterpret_cast<const float2*>(s0), reinterpret_cast<const float2*>(buf),
                      reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
-                     reinterpret_cast<float4*>(s2), vst, unknown_sigma, scaled, P);
+                     reinterpret_cast<float2*>(s2), vst, unknown_sigma, scaled, P);
   return (int)hipGetLastError();
 }
 

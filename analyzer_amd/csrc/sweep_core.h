@@ -15,21 +15,21 @@ ANA_HD void nat_params(float mu, float sig, float& pi, float& tau) {
   tau = mu * pi;
 }
 
-// The common base every rank measures its message against, for each track:
-// the window-start value; for a track NULL at window start the prior the
+// The common base every rank measures its message against, for track t: the
+// window-start value (cmu, csg); for a track NULL at window start the prior the
 // reference would give it -- the seed for the shared track, the window-start
-// shared rating (else the seed) for a mode track (rater.py:115-136).  Returns
-// false when the track has no base (NULL and the player cannot be seeded).
-ANA_HD bool track_base(const float* a, int t, bool seeded, float seed_mu, float seed_sig,
-                       float& mu, float& sig) {
-  if (a[4 * t] == a[4 * t]) {
-    mu = a[4 * t];
-    sig = a[4 * t + 2];
+// shared rating (c0mu, c0sg; else the seed) for a mode track (rater.py:115-136).
+// Returns false when the track has no base (NULL and the player cannot be seeded).
+ANA_HD bool track_base(int t, float cmu, float csg, float c0mu, float c0sg, bool seeded, float seed_mu,
+                       float seed_sig, float& mu, float& sig) {
+  if (cmu == cmu) {
+    mu = cmu;
+    sig = csg;
     return true;
   }
-  if (t > 0 && a[0] == a[0]) {
-    mu = a[0];
-    sig = a[2];
+  if (t > 0 && c0mu == c0mu) {
+    mu = c0mu;
+    sig = c0sg;
     return true;
   }
   mu = seed_mu;
@@ -45,88 +45,120 @@ ANA_HD bool track_base(const float* a, int t, bool seeded, float seed_mu, float 
 //         a rating-point-sized mean shift -- small, well-conditioned numbers that
 //         survive an fp16 / bf16 all-reduce (COMM_DTYPE), decoded against the same base B.
 //
-// s: the COMMON window-start row (identical on every rank; it defines the base B
-// of each track), a: the prior this rank rated its shard from in this sweep
-// (== s in the first sweep; the start plus the earlier ranks' messages in a
-// causal re-sweep, parallel/sweep.py), b: the row after the local window.  The
-// message is nat(b) - nat(a), measured against a's value where a has one and
-// against B where the track is NULL in a: prefix sums then telescope, so the
-// start + the messages of ranks 0..r-1 is exactly rank r-1's posterior once
-// every earlier rank rated from its exact prior.  attr/vst/unknown_sigma: seed
-// inputs.  o: 16 floats = message per track + touch fields for tracks that are
-// NULL in a and rated now (base-16 counters, exact in fp32 for <= 15 ranks).
+// The merge keeps its window start and causal priors as BASE rows: float[16] per
+// player, (mu, sigma) of the 8 granules of the roster row (kBaseFloats) -- half the
+// bytes of a roster row, and all a message needs.  The kernels (sweep.hip) run one
+// lane per track on these per-track functions; the host mirror calls the same ones.
+
+// One track t of a player's message.  (cmu, csg): the COMMON window-start value of
+// the track (identical on every rank; with the start's shared value (c0mu, c0sg)
+// and the seed it defines the base B, track_base), (amu, asg): the prior this rank
+// rated its shard from in this sweep (== the start in the first sweep; the start
+// plus the earlier ranks' messages in a causal re-sweep, parallel/sweep.py),
+// (bmu, bsg): the value after the local window.  The message is nat(b) - nat(a),
+// measured against a's value where a has one and against B where the track is NULL
+// in a: prefix sums then telescope, so the start + the messages of ranks 0..r-1 is
+// exactly rank r-1's posterior once every earlier rank rated from its exact prior.
+// touched: the track is NULL in a and rated now (base-16 touch counters,
+// exact in fp32 for <= 15 ranks, make it non-NULL on every rank).
+ANA_HD void sweep_delta_track(int t, float cmu, float csg, float c0mu, float c0sg, float amu, float asg,
+                              float bmu, float bsg, bool seeded, float seed_mu, float seed_sig,
+                              bool scaled, float& dp, float& dt, bool& touched) {
+  dp = 0.f;
+  dt = 0.f;
+  const bool had = amu == amu;
+  const bool changed = had ? (bmu != amu || bsg != asg) : bmu == bmu;
+  float bm, bs;
+  const bool based = track_base(t, cmu, csg, c0mu, c0sg, seeded, seed_mu, seed_sig, bm, bs);
+  if (changed && based) {
+    if (scaled) {  // (pi/pi_B - pi0/pi_B, (pi/pi_B)(mu - mu_B) - (pi0/pi_B)(mu0 - mu_B))
+      const float r1 = bs / bsg;
+      const float r0 = had ? bs / asg : 1.f;
+      dp = r1 * r1 - r0 * r0;
+      dt = r1 * r1 * (bmu - bm) - (had ? r0 * r0 * (amu - bm) : 0.f);
+    } else {
+      float p1, t1, p0, t0;
+      nat_params(bmu, bsg, p1, t1);
+      if (had) nat_params(amu, asg, p0, t0);
+      else nat_params(bm, bs, p0, t0);
+      dp = p1 - p0;
+      dt = t1 - t0;
+    }
+  }
+  touched = !had && bmu == bmu;
+}
+
+// One track t of the decode: (amu, asg) the common window-start value of the track,
+// (a0mu, a0sg) the start's shared value, (dpi, dtau) the summed messages, touched the
+// summed touch count of the track.  Returns the decoded (mu, sigma).
+ANA_HD void sweep_apply_track(int t, float amu, float asg, float a0mu, float a0sg, float dpi, float dtau,
+                              unsigned touched, bool seeded, float seed_mu, float seed_sig, bool scaled,
+                              float& mu, float& sg) {
+  mu = amu;
+  sg = asg;
+  const bool live = amu == amu ? (dpi != 0.f || dtau != 0.f) : touched != 0u;
+  if (!live) return;
+  float bm, bs;
+  const bool based = track_base(t, amu, asg, a0mu, a0sg, seeded, seed_mu, seed_sig, bm, bs);
+  if (!based) return;
+  if (scaled) {  // pi = pi_b (1 + sum r_pi), mu = mu_b + sum r_tau / (1 + sum r_pi)
+    float ratio = 1.f + dpi;
+    ratio = ratio > 1e-6f ? ratio : 1e-6f;
+    mu = bm + dtau / ratio;
+    sg = bs / sqrtf(ratio);
+  } else {
+    float pb, tb;
+    nat_params(bm, bs, pb, tb);
+    float pi = pb + dpi;
+    const float tau = tb + dtau;
+    pi = pi > 1e-12f ? pi : 1e-12f;  // merged precision never below "no information"
+    mu = tau / pi;
+    sg = 1.f / sqrtf(pi);
+  }
+}
+
+// Whole-player forms over base rows (host mirror): s, a: base rows [16] (start,
+// prior), b: roster row [32]; o: 16 floats = message per track + the touch fields.
 ANA_HD void sweep_delta_player(const float* s, const float* a, const float* b, const float* attr,
                                const float* vst, float unknown_sigma, bool scaled, float* o) {
   float seed_mu = NAN, seed_sig = NAN;
   const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
   float touch_lo = 0.f, touch_hi = 0.f;
   for (int t = 0; t < kTracks; ++t) {
-    const float mu0 = a[4 * t], sg0 = a[4 * t + 2], mu = b[4 * t], sg = b[4 * t + 2];
-    float dp = 0.f, dt = 0.f;
-    const bool had = mu0 == mu0;
-    const bool changed = had ? (mu != mu0 || sg != sg0) : mu == mu;
-    float bm, bs;
-    if (changed && track_base(s, t, seeded, seed_mu, seed_sig, bm, bs)) {
-      if (scaled) {  // (pi/pi_B - pi0/pi_B, (pi/pi_B)(mu - mu_B) - (pi0/pi_B)(mu0 - mu_B))
-        const float r1 = bs / sg;
-        const float r0 = had ? bs / sg0 : 1.f;
-        dp = r1 * r1 - r0 * r0;
-        dt = r1 * r1 * (mu - bm) - (had ? r0 * r0 * (mu0 - bm) : 0.f);
-      } else {
-        float p1, t1, p0, t0;
-        nat_params(mu, sg, p1, t1);
-        if (had) nat_params(mu0, sg0, p0, t0);
-        else nat_params(bm, bs, p0, t0);
-        dp = p1 - p0;
-        dt = t1 - t0;
-      }
-    }
-    if (!had && mu == mu) {
+    bool touched;
+    sweep_delta_track(t, s[2 * t], s[2 * t + 1], s[0], s[1], a[2 * t], a[2 * t + 1], b[4 * t],
+                      b[4 * t + 2], seeded, seed_mu, seed_sig, scaled, o[2 * t], o[2 * t + 1], touched);
+    if (touched) {
       if (t < 4) touch_lo += (float)(1 << (4 * t));
       else touch_hi += (float)(1 << (4 * (t - 4)));
     }
-    o[2 * t] = dp;
-    o[2 * t + 1] = dt;
   }
   o[14] = touch_lo;
   o[15] = touch_hi;
 }
 
-// a: common window-start row, d: summed messages (all ranks: the merged window;
-// ranks < r: rank r's prior for a causal re-sweep), attr: player attributes,
-// o: decoded row (tags reset to 0; spare floats copied).
+// a: base row of the common window start, d: summed messages (all ranks: the
+// merged window; ranks < r: rank r's prior for a causal re-sweep); o: the decoded
+// roster row (tags 0; granule 7 from the base row), ob: the same as a base row.
 ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr,
-                               const float* vst, float unknown_sigma, bool scaled, float* o) {
+                               const float* vst, float unknown_sigma, bool scaled, float* o, float* ob) {
   float seed_mu = NAN, seed_sig = NAN;
   const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
   const unsigned lo = (unsigned)d[14], hi = (unsigned)d[15];
-  for (int t = 0; t < kTracks; ++t) {
-    const float mu0 = a[4 * t], sg0 = a[4 * t + 2];
-    const unsigned touched = t < 4 ? (lo >> (4 * t)) & 15u : (hi >> (4 * (t - 4))) & 15u;
-    float mu = mu0, sg = sg0, bm, bs;
-    const bool live = mu0 == mu0 ? (d[2 * t] != 0.f || d[2 * t + 1] != 0.f) : touched != 0u;
-    if (live && track_base(a, t, seeded, seed_mu, seed_sig, bm, bs)) {
-      if (scaled) {  // pi = pi_b (1 + sum r_pi), mu = mu_b + sum r_tau / (1 + sum r_pi)
-        float ratio = 1.f + d[2 * t];
-        ratio = ratio > 1e-6f ? ratio : 1e-6f;
-        mu = bm + d[2 * t + 1] / ratio;
-        sg = bs / sqrtf(ratio);
-      } else {
-        float pb, tb;
-        nat_params(bm, bs, pb, tb);
-        float pi = pb + d[2 * t];
-        const float tau = tb + d[2 * t + 1];
-        pi = pi > 1e-12f ? pi : 1e-12f;  // merged precision never below "no information"
-        mu = tau / pi;
-        sg = 1.f / sqrtf(pi);
-      }
+  for (int g = 0; g < kGranules; ++g) {
+    float mu = a[2 * g], sg = a[2 * g + 1];
+    if (g < kTracks) {
+      const unsigned touched = g < 4 ? (lo >> (4 * g)) & 15u : (hi >> (4 * (g - 4))) & 15u;
+      sweep_apply_track(g, a[2 * g], a[2 * g + 1], a[0], a[1], d[2 * g], d[2 * g + 1], touched, seeded,
+                        seed_mu, seed_sig, scaled, mu, sg);
     }
-    o[4 * t] = mu;
-    o[4 * t + 1] = 0.f;
-    o[4 * t + 2] = sg;
-    o[4 * t + 3] = 0.f;
+    o[4 * g] = mu;
+    o[4 * g + 1] = 0.f;
+    o[4 * g + 2] = sg;
+    o[4 * g + 3] = 0.f;
+    ob[2 * g] = mu;
+    ob[2 * g + 1] = sg;
   }
-  for (int k = 4 * kTracks; k < kRowFloats; ++k) o[k] = (k & 1) ? 0.f : a[k];
 }
 
 }  // namespace ana

@@ -308,17 +308,20 @@ class BatchRater:
             epoch = 1
             ctrl_ready = False
         tele = self.has_telemetry(telemetry)
+        # aggregation tiles need the full grid and whole chunks; inline aggregation
+        # (ANA_TELE_ROLE < 0: each lane group folds its own match's events) does not
+        tiles = tele and self.knobs[5] >= 0
         if not tele:
             none = torch.empty(0, dtype=torch.int64, device=dev)
             telemetry = (none, none.to(torch.int32), none.to(torch.float32))
         native().rate(rec, K, link, deps, roster.state, roster.attrs, fp, out.quality, out.status,
                       out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
                       float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
-                      record, self.grid_blocks(M, tele), epoch,
+                      record, self.grid_blocks(M, tiles), epoch,
                       self.host_fp64, *telemetry,
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
                       epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
-                      self.chunk_len(M, tele), ctrl_ready, self.knobs)
+                      self.chunk_len(M, tiles), ctrl_ready, self.knobs)
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out

@@ -151,7 +151,9 @@ def aggregate(tel: Telemetry, K: int, stats: Optional[torch.Tensor] = None,
 
 
 def aggregate_reference(tel: Telemetry, K: int) -> np.ndarray:
-    """fp64 numpy oracle of the aggregation (well-formed events only)."""
+    """fp64 numpy oracle of the aggregation.  Strict attribution, as the kernels
+    and the host mirror (csrc/telemetry_core.h): an event whose 16-bit match tag
+    does not name the match of its CSR range, or whose slot is >= 2K, is dropped."""
     ev = tel.events.cpu().numpy()
     M = tel.evoff.numel() - 1
     out = np.zeros((M, 2 * K, len(STAT_NAMES)), dtype=np.float64)
@@ -160,6 +162,9 @@ def aggregate_reference(tel: Telemetry, K: int) -> np.ndarray:
     m = np.repeat(np.arange(M, dtype=np.int64), np.diff(tel.evoff.cpu().numpy()))  # CSR position
     slot = ev[:, 0] & 0xFF
     typ = (ev[:, 0] >> 8) & 0xFF
+    tag = (ev[:, 0].astype(np.int64) >> 16) & 0xFFFF
+    good = (tag == (m & 0xFFFF)) & (slot < 2 * K)
+    m, slot, typ, ev = m[good], slot[good], typ[good], ev[good]
     val = ev[:, 1].view(np.float32).astype(np.float64)
     add = np.where(typ <= 2, 1.0, val)
     feat = np.where(typ <= 6, typ, -1)

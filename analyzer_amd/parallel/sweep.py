@@ -58,6 +58,12 @@ from ..ops.native import native
 from .comm import all_reduce_sum, exclusive_scan, world
 
 MAX_RANKS = 15  # touch counts are base-16 fields in fp32 (see csrc/sweep_core.h)
+BASE_FLOATS = 16  # base row: (mu, sigma) per 16-B granule of a roster row
+
+
+def base_rows(state: torch.Tensor) -> torch.Tensor:
+    """Roster rows [P, 32] -> base rows [P, 16]: (mu, sigma) of each granule."""
+    return state.view(state.shape[0], 8, 4)[:, :, 0::2].reshape(state.shape[0], BASE_FLOATS)
 COMM_DTYPES = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloat16}
 
 
@@ -83,8 +89,10 @@ class SweepMerger:
         self.comm_dtype = comm_dtype
         self.scaled = comm_dtype != "fp32"
         f = dict(dtype=torch.float32, device=self.device)
-        self.start = torch.empty((self.P, 32), **f)   # common window start
-        self.prior = None                            # this rank's prior (re-sweeps only)
+        # common window start as BASE rows: (mu, sigma) of the 8 granules, 64 B per
+        # player (csrc/sweep_core.h) -- a message needs nothing else of the row
+        self.start = torch.empty((self.P, BASE_FLOATS), **f)
+        self.prior = None                            # this rank's prior (re-sweeps only; base rows)
         self.buf = torch.empty((self.P, 16), **f)
         # fp16/bf16: merge() writes and reads the all-reduce operands directly
         # (messages [P, 14] in the comm dtype + touch counts [P, 2] int32)
@@ -117,7 +125,7 @@ class SweepMerger:
         (the merge decodes into both), so only the first window -- or one after
         ``invalidate()`` -- copies it."""
         if not self._synced:
-            self.start.copy_(roster.state)
+            self.start.copy_(base_rows(roster.state))
             self._synced = True
         self._sweep = 0
 

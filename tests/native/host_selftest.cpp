@@ -99,13 +99,24 @@ static void run(int K, int64_t P, int64_t M, uint64_t seed) {
 
   // DP merge round trip (raw and base-relative encodings): messages of "after"
   // against "before", then apply, reproduces "after"
+  // (the merge keeps its window start as base rows: (mu, sigma) per granule)
+  std::vector<float> base((size_t)P * kBaseFloats);
+  for (int64_t p = 0; p < P; ++p)
+    for (int g = 0; g < kGranules; ++g) {
+      base[p * kBaseFloats + 2 * g] = state[p * kRowFloats + 4 * g];
+      base[p * kBaseFloats + 2 * g + 1] = state[p * kRowFloats + 4 * g + 2];
+    }
   for (int scaled = 0; scaled < 2; ++scaled) {
-    std::vector<float> buf((size_t)P * 16), merged(state.size()), copy(state.size());
-    host_sweep_delta(state.data(), state.data(), st64.data(), attrs.data(), vst.data(), 500.f, scaled,
+    std::vector<float> buf((size_t)P * 16), merged(state.size()), copy(base.size());
+    host_sweep_delta(base.data(), base.data(), st64.data(), attrs.data(), vst.data(), 500.f, scaled,
                      buf.data(), P);
-    host_sweep_apply(state.data(), buf.data(), attrs.data(), merged.data(), copy.data(), scaled,
+    host_sweep_apply(base.data(), buf.data(), attrs.data(), merged.data(), copy.data(), scaled,
                      vst.data(), 500.f, P);
-    CHECK(memcmp(merged.data(), copy.data(), merged.size() * sizeof(float)) == 0);
+    for (int64_t p = 0; p < P; ++p)  // the base-row copy is the decoded row's (mu, sigma)
+      for (int g = 0; g < kGranules; ++g) {
+        CHECK(memcmp(&merged[p * kRowFloats + 4 * g], &copy[p * kBaseFloats + 2 * g], 4) == 0);
+        CHECK(memcmp(&merged[p * kRowFloats + 4 * g + 2], &copy[p * kBaseFloats + 2 * g + 1], 4) == 0);
+      }
     for (int64_t p = 0; p < P; ++p)
       for (int t = 0; t < kTracks; ++t) {
         const float a = st64[p * kRowFloats + 4 * t], b = merged[p * kRowFloats + 4 * t];

@@ -211,10 +211,12 @@ def test_radix_sort_pairs_stable(gpu_device, n, bits):
 @pytest.mark.parametrize("scaled", [False, True])
 @pytest.mark.parametrize("resweep", [False, True])
 def test_sweep_kernels_match_host(gpu_device, scaled, resweep):
-    """K9 device kernels (messages + decode, dual write) == C++ host mirror on
-    128-B rows; ``resweep``: messages measured from a prior != the start."""
+    """K9 device kernels (messages + decode, dual write; one lane per track over
+    base rows) == C++ host mirror; ``resweep``: messages measured from a prior !=
+    the start."""
     from analyzer_amd.ops.native import native
     from analyzer_amd.models.tiers import vst_table
+    from analyzer_amd.parallel.sweep import base_rows
 
     P = 5000
     start = make_roster(RosterSpec(num_players=P, seed=3, p_rated=0.5))
@@ -226,23 +228,23 @@ def test_sweep_kernels_match_host(gpu_device, scaled, resweep):
     R.BatchRater().rate(after, rec, 3)
     vst = torch.tensor(vst_table(), dtype=torch.float32)
     g = lambda t: t.to(gpu_device)
+    sb, pb = base_rows(start.state).contiguous(), base_rows(prior.state).contiguous()
     bh = torch.empty((P, 16))
-    native().sweep_delta(start.state, prior.state, after.state, start.attrs, vst, 500.0, scaled, bh)
+    native().sweep_delta(sb, pb, after.state, start.attrs, vst, 500.0, scaled, bh)
     bd = torch.empty((P, 16), device=gpu_device)
-    native().sweep_delta(g(start.state), g(prior.state), g(after.state), g(start.attrs), g(vst), 500.0,
-                         scaled, bd)
+    native().sweep_delta(g(sb), g(pb), g(after.state), g(start.attrs), g(vst), 500.0, scaled, bd)
     # scaled messages are (pi/pi_b - pi0/pi_b, ...): a 1-ulp difference in a ratio near 1
     # is a large relative one in the message (they travel as fp16/bf16 anyway)
     np.testing.assert_allclose(bd.cpu().numpy(), bh.numpy(), rtol=1e-3 if scaled else 1e-6,
                                atol=1e-5 if scaled else 1e-9)
-    sh, sh2 = start.state.clone(), torch.zeros_like(start.state)
-    native().sweep_apply(start.state, bh * 2, start.attrs, sh, sh2, vst, 500.0, scaled)
-    sd, sd2 = g(start.state).clone(), torch.zeros_like(g(start.state))
-    native().sweep_apply(g(start.state), g(bh * 2), g(start.attrs), sd, sd2, g(vst), 500.0, scaled)
+    sh, sh2 = start.state.clone(), torch.zeros_like(sb)
+    native().sweep_apply(sb, bh * 2, start.attrs, sh, sh2, vst, 500.0, scaled)
+    sd, sd2 = g(start.state).clone(), torch.zeros_like(g(sb))
+    native().sweep_apply(g(sb), g(bh * 2), g(start.attrs), sd, sd2, g(vst), 500.0, scaled)
     # fp32 (tau / pi, 1 / sqrt(pi)): device fma contraction vs host rounding
     np.testing.assert_allclose(sd.cpu().numpy(), sh.numpy(), rtol=5e-5, atol=1e-6, equal_nan=True)
-    assert torch.equal(sd.nan_to_num(-7), sd2.nan_to_num(-7))
-    assert torch.equal(sh.nan_to_num(-7), sh2.nan_to_num(-7))
+    assert torch.equal(base_rows(sd).nan_to_num(-7), sd2.nan_to_num(-7))
+    assert torch.equal(base_rows(sh).nan_to_num(-7), sh2.nan_to_num(-7))
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
@@ -252,27 +254,30 @@ def test_packed_sweep_kernels_match_fp32_path(gpu_device, dtype):
     conversions, bit for bit."""
     from analyzer_amd.ops.native import native
     from analyzer_amd.models.tiers import vst_table
+    from analyzer_amd.parallel.sweep import base_rows
 
     P = 6000
     start = make_roster(RosterSpec(num_players=P, seed=5, p_rated=0.5), device=gpu_device)
     after = start.clone()
     R.BatchRater().rate(after, make_stream(StreamSpec(team_size=3, seed=6), 20000, P, device=gpu_device), 3)
     vst = torch.tensor(vst_table(), dtype=torch.float32, device=gpu_device)
+    sb = base_rows(start.state).contiguous()
     buf = torch.empty((P, 16), device=gpu_device)
-    native().sweep_delta(start.state, start.state, after.state, start.attrs, vst, 500.0, True, buf)
+    native().sweep_delta(sb, sb, after.state, start.attrs, vst, 500.0, True, buf)
     msg = torch.empty((P, 14), dtype=dtype, device=gpu_device)
     cnt = torch.empty((P, 2), dtype=torch.int32, device=gpu_device)
-    native().sweep_delta_packed(start.state, start.state, after.state, start.attrs, vst, 500.0, msg, cnt)
+    native().sweep_delta_packed(sb, sb, after.state, start.attrs, vst, 500.0, msg, cnt)
     assert torch.equal(msg.view(torch.int16), buf[:, :14].to(dtype).view(torch.int16))
     assert torch.equal(cnt, buf[:, 14:].to(torch.int32))
     msg2, cnt2 = msg * 2, cnt * 2  # a "sum" of two ranks
     joined = torch.cat([msg2.float(), cnt2.float()], dim=1)
-    s_ref, s2_ref = start.state.clone(), torch.zeros_like(start.state)
-    native().sweep_apply(start.state, joined, start.attrs, s_ref, s2_ref, vst, 500.0, True)
-    s_p, s2_p = start.state.clone(), torch.zeros_like(start.state)
-    native().sweep_apply_packed(start.state, msg2, cnt2, start.attrs, s_p, s2_p, vst, 500.0)
+    s_ref, s2_ref = start.state.clone(), torch.zeros_like(sb)
+    native().sweep_apply(sb, joined, start.attrs, s_ref, s2_ref, vst, 500.0, True)
+    s_p, s2_p = start.state.clone(), torch.zeros_like(sb)
+    native().sweep_apply_packed(sb, msg2, cnt2, start.attrs, s_p, s2_p, vst, 500.0)
     assert torch.equal(s_p.nan_to_num(-7), s_ref.nan_to_num(-7))
-    assert torch.equal(s2_p.nan_to_num(-7), s_ref.nan_to_num(-7))
+    assert torch.equal(s2_p.nan_to_num(-7), s2_ref.nan_to_num(-7))
+    assert torch.equal(s2_ref.nan_to_num(-7), base_rows(s_ref).nan_to_num(-7))
 
 
 def test_telemetry_device_generator_and_aggregation(gpu_device):
@@ -378,10 +383,11 @@ def test_telemetry_diagnostic_variants_need_the_diag_library(gpu_device, monkeyp
     assert torch.equal(aggregate(tel, 3), ref)
 
 
-@pytest.mark.parametrize("role", [0, 2, 4, 8])
+@pytest.mark.parametrize("role", [-1, 0, 2, 4, 8])
 def test_fused_rate_telemetry_on_device(gpu_device, monkeypatch, role):
-    """Fused aggregation, idle-wave tiles (role 0) and dedicated aggregation
-    waves (ANA_TELE_ROLE): same stats as the oracle, same ratings as without."""
+    """Fused aggregation: inline in the rating groups (role -1), idle-wave tiles
+    (role 0) and dedicated aggregation waves (ANA_TELE_ROLE): same stats as the
+    oracle, same ratings as without."""
     from analyzer_amd.ops.telemetry import (TelemetrySpec, aggregate_reference, allocate_stats,
                                             make_telemetry)
 
@@ -401,6 +407,39 @@ def test_fused_rate_telemetry_on_device(gpu_device, monkeypatch, role):
     assert torch.equal(ra.s_mu.nan_to_num(-7), rb.s_mu.nan_to_num(-7))
     ref = aggregate_reference(type(tel)(tel.evoff.cpu(), tel.events.cpu()), K)
     np.testing.assert_allclose(stats.cpu().numpy(), ref, rtol=2e-5, atol=0.05)
+
+
+def test_inline_telemetry_edge_cases_on_device(gpu_device, monkeypatch):
+    """Inline aggregation (ANA_TELE_ROLE=-1) on the paths the common case skips:
+    stateless matches (AFK, invalid rosters, unsupported) aggregated by tele-only
+    groups, matches with more events than a group loads with its granules (the
+    remainder loop), 5v5 groups, and malformed events counted, not folded."""
+    from analyzer_amd.ops.telemetry import (TelemetrySpec, aggregate_reference, allocate_stats,
+                                            make_telemetry)
+
+    monkeypatch.setenv("ANA_TELE_ROLE", "-1")
+    for K, lo, hi in ((3, 0, 150), (5, 30, 90)):
+        P, M = 5000, 60000
+        roster = make_roster(RosterSpec(num_players=P, seed=15), device=gpu_device)
+        spec = StreamSpec(team_size=K, seed=16, p_afk=0.1, p_bad_rosters=0.05, p_unsupported=0.05,
+                          p_tie=0.05)
+        rec = make_stream(spec, M, P, K=K, device=gpu_device)
+        tel = make_telemetry(TelemetrySpec(seed=18, min_events=lo, max_events=hi), rec, K)
+        ev = tel.events.clone()
+        ev[::97, 0] ^= 1 << 16  # wrong match tag: malformed
+        stats = allocate_stats(M, K, gpu_device)
+        a, b = roster.clone(), roster.clone()
+        br = R.BatchRater()
+        ra = br.rate(a, rec, K, telemetry=(tel.evoff, ev, stats))
+        nbad = br.telemetry_errors(gpu_device)
+        rb = R.BatchRater().rate(b, rec, K)
+        assert torch.equal(a.state.nan_to_num(-7), b.state.nan_to_num(-7))
+        assert torch.equal(ra.status, rb.status)
+        for f in ("quality", "s_mu", "s_sig", "delta", "m_mu", "m_sig"):
+            assert torch.equal(getattr(ra, f).nan_to_num(-7), getattr(rb, f).nan_to_num(-7)), f
+        ref = aggregate_reference(type(tel)(tel.evoff.cpu(), ev.cpu()), K)
+        np.testing.assert_allclose(stats.cpu().numpy(), ref, rtol=2e-5, atol=0.05)
+        assert nbad == (ev.shape[0] + 96) // 97
 
 
 def test_file_ingest_pipeline_on_device(gpu_device, tmp_path):
