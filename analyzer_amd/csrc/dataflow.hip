@@ -118,6 +118,17 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // per-field stores sent 6-7 partial-line writes per match to the fabric)
   constexpr int OQ = (5 * S + 2 + 3) / 4;
   __shared__ __attribute__((aligned(16))) float lrow[kWavesPerBlock][NG][4 * OQ];
+#if ANA_EXP_VPTR
+  // experiment: per-lane-addressed bases held in VGPR pairs instead of SGPRs (the
+  // kernel spills ~57 SGPRs into VGPR lanes; every readback is a v_readlane)
+#define ANA_VPTR(p) do { uint64_t u_ = (uint64_t)(uintptr_t)(p); asm volatile("" : "+v"(u_)); (p) = (decltype(p))(uintptr_t)u_; } while (0)
+  ANA_VPTR(rec); ANA_VPTR(link); ANA_VPTR(attrs); ANA_VPTR(first_prior); ANA_VPTR(orows);
+  ANA_VPTR(prm.vst);
+#if ANA_EXP_VPTR > 1
+  ANA_VPTR(ctrl);
+#endif
+#undef ANA_VPTR
+#endif
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int j = lane % G;
