@@ -171,9 +171,10 @@ class EngineConfig:
     ANA_RATE_DIAG           0         executor timing build: per-phase clocks in ctrl[20..47] (ops/rate.diag)
     ANA_RATE_TIGHT          -1        executor: 2K lanes per match instead of the next power of two (-1 auto)
     ANA_TELE_FUSED_TAIL     0         fused telemetry only after the executor's chunks are drained
-    ANA_TELE_ROLE           2         fused telemetry: one wave in N aggregates from the start (0 = idle
-                                      waves; -1 = inline: each lane group folds the events of the match
-                                      it rates)
+    ANA_TELE_ROLE           -1        fused telemetry: -1 = inline, each lane group folds the events of
+                                      the match it rates (11.4 ms per config 4 step); N > 0 = one wave in
+                                      N aggregates MFMA tiles from the start (N = 2: 11.7); 0 = idle waves.
+                                      All slower than the separate kernel (10.1; bench default)
     ======================  ========  =============================================
 
     The executor / fused-telemetry knobs reach the launch as ``BatchRater.knobs``
@@ -198,7 +199,7 @@ class EngineConfig:
     rate_diag: int = 0
     rate_tight: int = -1
     tele_fused_tail: int = 0
-    tele_role: int = 2
+    tele_role: int = -1
 
     # kernel-implementation A/B switches read by the native extension itself
     # (csrc/telemetry.hip, kernels.hip, radix_sort.hip) -- experiments, not tuning
@@ -234,5 +235,5 @@ class EngineConfig:
             rate_diag=int(_env(env, "ANA_RATE_DIAG") or 0),
             rate_tight=int(_env(env, "ANA_RATE_TIGHT") or -1),
             tele_fused_tail=int(_env(env, "ANA_TELE_FUSED_TAIL") or 0),
-            tele_role=int(_env(env, "ANA_TELE_ROLE") or 2),
+            tele_role=int(_env(env, "ANA_TELE_ROLE") or -1),
         )

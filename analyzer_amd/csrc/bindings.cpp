@@ -249,7 +249,8 @@ static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& 
   tp.stats = stats.data_ptr<float>();
   if (dev.is_cuda()) tp.impl = ana::tele_impl();
   tp.fused_tail = (int32_t)knobs[4];
-  // fused: every 2nd wave aggregates first (14.4 -> 11.4 ms per config 4 step, profiles/r2/tele_role_split.log)
+  // fused: < 0 inline in the rating groups (default, 11.4 ms per config 4 step); N > 0 one wave
+  // in N aggregates tiles first (N = 2: 14.4 -> 11.4-11.7 ms, profiles/r2/tele_role_split.log)
   tp.role_stride = (int32_t)knobs[5];
   return tp;
 }

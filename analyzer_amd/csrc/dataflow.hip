@@ -986,8 +986,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 }
 
 
-__global__ void __launch_bounds__(64) zero_ctrl_kernel(uint32_t* __restrict__ p, int n) {
-  if ((int)threadIdx.x < n) p[threadIdx.x] = 0u;
+// both control ranges of a launch in one dispatch: [a, a + na) and [b, b + nb)
+__global__ void __launch_bounds__(64) zero_ctrl2_kernel(uint32_t* __restrict__ a, int na,
+                                                        uint32_t* __restrict__ b, int nb) {
+  if ((int)threadIdx.x < na) a[threadIdx.x] = 0u;
+  if ((int)threadIdx.x < nb) b[threadIdx.x] = 0u;
 }
 
 int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, float* state,
@@ -1000,9 +1003,9 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // [20..25], [28..29] timing build (see the kernel), [26] local / [27] global hand-offs
   // one-wave kernel rather than hipMemsetAsync: a 60-B fill at a 4-B offset becomes two
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
-  if (!prm.ctrl_ready) hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, 15);
-  // the diagnostic words are zeroed by every launch (not by the schedule's zeroing)
-  hipLaunchKernelGGL(zero_ctrl_kernel, dim3(1), dim3(64), 0, s, ctrl + 20, 28);
+  // the diagnostic words [20..47] are zeroed by every launch (not by the schedule's zeroing)
+  hipLaunchKernelGGL(zero_ctrl2_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, prm.ctrl_ready ? 0 : 15,
+                     ctrl + 20, 28);
   if (M <= 0) return 0;
   if (prm.chunk_len < 1 || prm.chunk_len > kChunk) return (int)hipErrorInvalidValue;
   if ((int64_t)prm.num_players * kRowFloats * 4 > kOutOfRange) return (int)hipErrorInvalidValue;

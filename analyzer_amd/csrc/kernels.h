@@ -31,9 +31,12 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 // stateful match (next match of its player | kLinkHasPred), from a stable sort
 // of the stream's slots by player fused with the record decode and the links.
 // ws: radix_sort_workspace_bytes(M * 2K) bytes; ka..vb: M * 2K words each.
+// deps [M] (zeroed by the first kernel), ctrl[0..nz) (zeroed), epoch_bump (+1): the
+// schedule's fill work, folded into that kernel (null / 0: skipped)
 int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
                       uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
-                      hipStream_t s);
+                      hipStream_t s, int32_t* deps = nullptr, uint32_t* ctrl = nullptr, int nz = 0,
+                      int32_t* epoch_bump = nullptr);
 // Device levelizer (levels.hip): level[m] = 0 for a match without state, else
 // 1 + the largest level of its players' previous matches -- the exact-DP rounds --
 // as a dataflow over a fresh schedule (link, deps zeroed; deps are consumed).

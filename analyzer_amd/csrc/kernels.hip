@@ -327,18 +327,22 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
     if (bitonic && epoch_bump) hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(1), 0, s, epoch_bump);
     return (int)hipGetLastError();
   }
-  ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 4 * (size_t)nz, s));
-  if (epoch_bump) hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(1), 0, s, epoch_bump);
-  if (n <= 0) return 0;
+  if (n <= 0) {
+    ANA_HIP_CHECK(hipMemsetAsync(overflow, 0, 4 * (size_t)nz, s));
+    if (epoch_bump) hipLaunchKernelGGL(epoch_bump_kernel, dim3(1), dim3(1), 0, s, epoch_bump);
+    return 0;
+  }
   if (n > kMaxSlots || P >= 0x7fffffffLL || K < 1 || K > 5) return (int)hipErrorInvalidValue;
   if (ws_bytes < schedule_workspace_bytes(n, P)) return (int)hipErrorInvalidValue;
-  ANA_HIP_CHECK(hipMemsetAsync(deps, 0, (size_t)M * 4, s));
+  // the counters, the control words and the epoch bump are the first sort kernel's
+  // side duties (radix_sort.hip SchedInit): no fill dispatches in front of the sort
   char* p = static_cast<char*>(ws);
   uint32_t* keys_a = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* vals_a = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* keys_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* vals_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
-  return launch_sched_sort(K, rec, M, (uint32_t)P, keys_a, vals_a, keys_b, vals_b, p, link, s);
+  return launch_sched_sort(K, rec, M, (uint32_t)P, keys_a, vals_a, keys_b, vals_b, p, link, s, deps,
+                           overflow, nz, epoch_bump);
 }
 
 }  // namespace ana

@@ -124,11 +124,21 @@ __device__ __forceinline__ void decode_tile_keys(const int32_t* __restrict__ rec
   }
 }
 
-// KS > 0: keys from the match stream (decode_tile_keys).
+// What the schedule's first kernel also does, so the prepass needs no fill
+// dispatches of its own: zero the window's completion counters (each tile its
+// matches), the control words, and bump the device launch epoch (graph replays).
+struct SchedInit {
+  int32_t* deps = nullptr;       // [M] completion counters
+  uint32_t* ctrl = nullptr;      // ctrl[0..nz) zeroed by block 0
+  int nz = 0;
+  int32_t* epoch_bump = nullptr; // += 1 by block 0
+};
+
+// KS > 0: keys from the match stream (decode_tile_keys), and the SchedInit duties.
 template <int KS, int RB = 8, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
 radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec, uint32_t kend,
-              int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles) {
+              int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles, SchedInit init = {}) {
   constexpr int kR = 1 << RB;
   __shared__ uint32_t hist[kWaves][kR];
   __shared__ uint32_t lkeys[KS > 0 ? kTile : 1];
@@ -136,6 +146,17 @@ radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec
   for (int i = tid; i < kWaves * kR; i += kThreads) (&hist[0][0])[i] = 0u;
   const int64_t tile = xcd_tile(tiles);
   const int64_t base = tile * kTile;
+  if constexpr (KS > 0) {
+    if (init.deps) {  // the matches whose slots start in this tile (every match has its first slot in one)
+      constexpr int S = 2 * KS;
+      const int64_t hi = base + kTile < n ? base + kTile : n;
+      for (int64_t m = (base + S - 1) / S + tid; m < (hi + S - 1) / S; m += kThreads) init.deps[m] = 0;
+    }
+    if (blockIdx.x == 0) {
+      if (tid < init.nz) init.ctrl[tid] = 0u;
+      if (tid == 0 && init.epoch_bump) init.epoch_bump[0] += 1;
+    }
+  }
   if constexpr (KS > 0) decode_tile_keys<KS>(rec, kend, base, n, lkeys);
   __syncthreads();
 #pragma unroll
@@ -427,7 +448,7 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 template <int K, int RB, bool NT>
 static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits, uint32_t* ka,
                          uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* counts,
-                         int64_t tiles, uint32_t* link, hipStream_t s) {
+                         int64_t tiles, uint32_t* link, const SchedInit& init, hipStream_t s) {
   constexpr int S = 2 * K;
   constexpr int kR = 1 << RB;
   uint32_t* totals = counts + tiles * kR;
@@ -437,7 +458,8 @@ static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits,
   for (int shift = 0; shift < bits; shift += RB) {
     const bool first = shift == 0, last = shift + RB >= bits;
     if (first)
-      hipLaunchKernelGGL((radix_upsweep<K, RB, NT>), grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles);
+      hipLaunchKernelGGL((radix_upsweep<K, RB, NT>), grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles,
+                         init);
     else
       hipLaunchKernelGGL((radix_upsweep<0, RB, NT>), grid, block, 0, s, ki, nullptr, kend, n, shift, counts, tiles);
     hipLaunchKernelGGL(radix_rowscan, dim3(kR), block, 0, s, counts, tiles, totals);
@@ -470,7 +492,7 @@ static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits,
 
 int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
                       uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
-                      hipStream_t s) {
+                      hipStream_t s, int32_t* deps, uint32_t* ctrl, int nz, int32_t* epoch_bump) {
   const int64_t n = M * 2 * K;
   if (n <= 0) return 0;
   if (n > kMaxSlots) return (int)hipErrorInvalidValue;
@@ -478,6 +500,11 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
   while (bits < 32 && (1ull << bits) <= (uint64_t)num_players) ++bits;
   const int64_t tiles = (n + kTile - 1) / kTile;
   uint32_t* counts = static_cast<uint32_t*>(ws);
+  SchedInit init;
+  init.deps = deps;
+  init.ctrl = ctrl;
+  init.nz = ctrl ? nz : 0;
+  init.epoch_bump = epoch_bump;
   // ANA_SORT_RB=10: 10-bit digits (2 passes for <= 2^20 players instead of 3).  Measured
   // on MI355X, 10M 3v3 / 1M players: 3.11 ms vs 1.76 ms for 8-bit digits (1024
   // per-tile runs of ~4 elements scatter the pass's writes) -> off by default.
@@ -487,9 +514,9 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
   switch (K) {
 #define ANA_SORT_CASE(k)                                                                         \
   case k:                                                                                        \
-    if (wide) sched_sort_k<k, 10, false>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s); \
-    else if (nt) sched_sort_k<k, 8, true>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s); \
-    else sched_sort_k<k, 8, false>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, s); \
+    if (wide) sched_sort_k<k, 10, false>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    else if (nt) sched_sort_k<k, 8, true>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    else sched_sort_k<k, 8, false>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
     break;
     ANA_SORT_CASE(1) ANA_SORT_CASE(2) ANA_SORT_CASE(3) ANA_SORT_CASE(4) ANA_SORT_CASE(5)
 #undef ANA_SORT_CASE

@@ -79,6 +79,12 @@ class WindowPipeline:
         self._signal = 0
         self._seq = 0
         self.side = self._side_stream() if self.cuda else None
+        # serial prepass + DP merge: the next window's prepass runs on a stream of its
+        # own, beside this window's merge (messages, all-reduce, decode) -- the two
+        # share nothing (the prepass reads records, the merge the roster) -- instead of
+        # between the all-reduce launch and the decode on the main stream
+        self.merge_side = torch.cuda.Stream(self.device) if self.cuda and self.serial else None
+        self._rated: Optional[torch.cuda.Event] = None  # the last rating launch finished
         # ANA_PREPASS_EXCLUSIVE (with ANA_PREPASS_CUS=n): the rating launches go to a
         # stream masked to the other CUs, so the two never share a CU
         self.exec_stream = None
@@ -116,29 +122,30 @@ class WindowPipeline:
         return torch.cuda.Stream(self.device)
 
     def prepare(self, rec: torch.Tensor,
-                produced: Optional[torch.cuda.Event] = None) -> Prepared:
-        """Enqueue the schedule prepass of ``rec`` on the side stream, after the
-        tail of the last enqueued rate launch (tail overlap) and after
+                produced: Optional[torch.cuda.Event] = None, stream=None) -> Prepared:
+        """Enqueue the schedule prepass of ``rec`` on the side stream (or ``stream``),
+        after the tail of the last enqueued rate launch (tail overlap) and after
         ``produced`` (default: everything enqueued on the main stream so far,
         which is where ``rec`` was made)."""
         if not self.cuda:
             return Prepared(rec, None, None)
         tag = "_set%d" % self._set
         main = torch.cuda.current_stream(self.device)
+        side = self.side if stream is None else stream
         if produced is None:
             produced = torch.cuda.Event()
             produced.record(main)
-        with torch.cuda.stream(self.side), trace_range("schedule", window=self.windows_rated + 1):
-            self.side.wait_event(produced)
+        with torch.cuda.stream(side), trace_range("schedule", window=self.windows_rated + 1):
+            side.wait_event(produced)
             if self._signal and self._seq > 0:
                 from ..ops.native import native
 
-                native().stream_wait_value64(self.side.cuda_stream, self._signal, self._seq)
+                native().stream_wait_value64(side.cuda_stream, self._signal, self._seq)
             if self._free[self._set] is not None:  # previous user of this buffer set is done
-                self.side.wait_event(self._free[self._set])
+                side.wait_event(self._free[self._set])
             sched = self.rater.schedule(rec, self.K, self.roster.num_players, tag=tag)
             ready = torch.cuda.Event()
-            ready.record(self.side)
+            ready.record(side)
         used = self._set
         self._set ^= 1
         return Prepared(rec, sched, ready, used)
@@ -187,6 +194,7 @@ class WindowPipeline:
             done.record(main)
             # the buffer set of this schedule is free once this launch finished
             self._free[prep.buffer_set] = done
+            self._rated = done
         if self.merger is not None:
             with trace_range("merge", window=self.windows_rated):
                 self.merger.merge(self.roster, overlap=overlap)
@@ -204,11 +212,12 @@ class WindowPipeline:
             produced = torch.cuda.Event()
             produced.record(torch.cuda.current_stream(self.device))
         if self.serial and self.merger is not None and self.cuda and next_rec is not None:
-            # serial prepass + DP merge: the prepass needs no roster, so it goes onto
-            # the main stream while the merge's all-reduces are on the wire
+            # serial prepass + DP merge: the prepass needs no roster, so it runs on its
+            # own stream from the end of this window's rating on, beside the merge's
+            # message kernels, all-reduces and decodes (never beside the executor)
             held: List[Prepared] = []
-            res = self.rate(prep, overlap=lambda: held.append(self.prepare(next_rec, produced=produced)),
-                            **rate_kwargs)
+            res = self.rate(prep, overlap=lambda: held.append(
+                self.prepare(next_rec, produced=self._rated, stream=self.merge_side)), **rate_kwargs)
             return res, held[0]
         res = self.rate(prep, **rate_kwargs)
         nxt = self.prepare(next_rec, produced=produced) if next_rec is not None else None
