@@ -10,6 +10,8 @@ step() {  # step NAME SECONDS CMD...
   local rc=$?
   if [ $rc -ne 0 ]; then echo "!! $name rc=$rc"; tail -30 gpurun_out/s2c/$name.log; exit $rc; fi
 }
+step tests 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
+tail -2 gpurun_out/s2c/tests.log
 for r in 1 2; do
   for k in 1 8; do
     step merge_k${k}_$r 300 python bench.py --steps 20 --warmup 3 --merges-per-step $k --force-merge
