@@ -207,6 +207,7 @@ class EngineConfig:
         "ANA_TELE_IMPL": "telemetry aggregation: 1 one-hot MFMA GEMM (default), 0 LDS atomics",
         "ANA_SCHED_SMALL": "micro-batch schedule: hash lists (default) or bitonic sort",
         "ANA_SORT_RB / ANA_SORT_NT": "radix-sort tile rows / non-temporal loads (tuning)",
+        "ANA_SCHED_RUNS": "last schedule pass: run-end table (1, default) or digit offsets + fix-up (0)",
     }
 
     def rate_knobs(self) -> list:

@@ -222,11 +222,22 @@ radix_rowscan(uint32_t* __restrict__ counts, int64_t tiles, uint32_t* __restrict
   if (threadIdx.x == 0) totals[blockIdx.x] = carry;
 }
 
+// The two ends of one (tile, digit) run of the schedule's last pass (first and last
+// key / value; kf = kRunEmpty: the tile has no element of that digit).
+struct RunEnds {
+  uint32_t kf, vf, kl, vl;
+};
+constexpr uint32_t kRunEmpty = 0xffffffffu;
+
 // KS > 0: elements come from the match stream (decode_tile_keys).  LINK (the schedule's
 // last pass): instead of writing the sorted pairs, write every slot's link from
 // its neighbours in the LDS-sorted tile -- within a (tile, digit) run they are
 // its global neighbours -- and only the run-boundary pairs, whose outer
 // neighbour lives in another tile (sched_fixup completes those links).
+// bnd (LINK, last pass with nd <= kRunsMaxDigits digits): the boundary pairs go to a
+// [tile][nd] RunEnds table instead of their global sorted positions, so this pass
+// needs no digit offsets -- no upsweep / rowscan in front of it -- and sched_runs_fixup
+// links each run to the nearest non-empty run of its digit in an earlier tile.
 template <int KS, bool LINK, int RB = 8, bool NT = false>
 __global__ void __launch_bounds__(kThreads)
 radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
@@ -234,7 +245,8 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n, int shift,
                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
                 int64_t tiles, int slots_per_match, uint32_t* __restrict__ link,
-                uint32_t vlo = 0u, uint32_t vhi = 0xffffffffu, int bounds = 1) {
+                uint32_t vlo = 0u, uint32_t vhi = 0xffffffffu, int bounds = 1,
+                RunEnds* __restrict__ bnd = nullptr, int nd = 0) {
   constexpr int kR = 1 << RB;
   constexpr int DPT = kR / kThreads;  // digits per thread in the scans
   static_assert(DPT >= 1 && DPT * kThreads == kR, "radix must be a multiple of the block");
@@ -248,7 +260,8 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
   const int64_t tile = xcd_tile(tiles);
   const int64_t base = tile * kTile;
   for (int i = tid; i < kWaves * kR; i += kThreads) (&wcnt[0][0])[i] = 0u;
-  {  // global start of each digit for this tile
+  const bool local_ends = LINK && bnd != nullptr;  // uniform: no global digit offsets needed
+  if (!local_ends) {  // global start of each digit for this tile
     uint32_t v[DPT];
 #pragma unroll
     for (int j = 0; j < DPT; ++j) v[j] = totals[tid * DPT + j];
@@ -317,13 +330,19 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
   }
   __syncthreads();
   const int64_t nvalid = n - base < kTile ? n - base : kTile;
+  if constexpr (LINK) {
+    if (local_ends && bounds && tid < nd) {  // digits without an element in this tile
+      const uint32_t e = tid + 1 < kR ? tstart[tid + 1] : (uint32_t)kTile;
+      if (tstart[tid] == e) bnd[tile * nd + tid].kf = kRunEmpty;
+    }
+  }
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
     const int i = k * kThreads + tid;
     if (i < nvalid) {
       const uint32_t kk = skey[i];
       const uint32_t d = (kk >> shift) & (kR - 1);
-      const int64_t o = (int64_t)gstart[d] + (i - (int64_t)tstart[d]);
+      const int64_t o = local_ends ? 0 : (int64_t)gstart[d] + (i - (int64_t)tstart[d]);
       if constexpr (!LINK) {
         st32<NT>(kout + o, kk);
         st32<NT>(vout + o, sval[i]);
@@ -332,9 +351,17 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
         const bool first = i == (int)tstart[d];
         const bool last = i + 1 == hi || i + 1 >= nvalid;
         const uint32_t v = sval[i];
-        if (bounds && (first || last)) {  // sched_fixup reads the boundary pairs of every run
-          st32<NT>(kout + o, kk);
-          st32<NT>(vout + o, v);
+        if (bounds && (first || last)) {  // the fix-up reads the boundary pairs of every run
+          if (local_ends) {
+            if ((int)d < nd) {  // (pads sort to digit kR - 1, past the schedule's digits)
+              RunEnds* r = bnd + tile * nd + d;
+              if (first) { r->kf = kk; r->vf = v; }
+              if (last) { r->kl = kk; r->vl = v; }
+            }
+          } else {
+            st32<NT>(kout + o, kk);
+            st32<NT>(vout + o, v);
+          }
         }
         if (kk < kend && v >= vlo && v < vhi) {  // this part's slot range (link_parts)
           uint32_t w = (!last && skey[i + 1] == kk) ? sval[i + 1] / (uint32_t)slots_per_match
@@ -357,6 +384,13 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
 // parts 2 x 0.91 ms, its step 13.40 -> 12.56 ms.  Splitting config 2's 240 MB
 // as well costs more than it saves (8.13 -> 8.46 ms).  ANA_LINK_PARTS overrides
 // the count (1 = one pass).
+// ANA_SCHED_RUNS=0: the last pass with digit offsets + sched_fixup (the round-2 path),
+// for A/B; default: the run table (radix_downsweep bnd, sched_runs_fixup)
+static bool local_runs() {  // per schedule: tests switch it at run time
+  const char* e = getenv("ANA_SCHED_RUNS");
+  return !(e && atoi(e) == 0);
+}
+
 static int link_parts(int64_t n) {
   if (const char* e = getenv("ANA_LINK_PARTS")) {  // per launch: tests switch it at run time
     const int v = atoi(e);
@@ -412,6 +446,74 @@ sched_fixup(const uint32_t* __restrict__ kout, const uint32_t* __restrict__ vout
   }
 }
 
+// The last pass's run table -> links across tiles (sched_runs_fixup): the
+// predecessor of the first pair of run (t, d) is the last pair of the nearest
+// non-empty run (t' < t, d).  Segments of kThreads tiles: sched_runs_last finds each
+// segment's last non-empty tile per digit, sched_runs_fixup takes the nearest one
+// before its segment as the carry and a block max-scan of the non-empty tiles inside
+// it.  Grids (segments, nd); nd <= kRunsMaxDigits keeps the table small.
+constexpr int kRunsMaxDigits = 32;
+
+__global__ void __launch_bounds__(kThreads)
+sched_runs_last(const RunEnds* __restrict__ bnd, int64_t tiles, int nd, int32_t* __restrict__ seglast) {
+  __shared__ int32_t wmax[kWaves];
+  const int d = blockIdx.y;
+  const int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  int32_t x = (t < tiles && bnd[t * nd + d].kf != kRunEmpty) ? (int32_t)t : -1;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x = max(x, __shfl_xor(x, off));
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t m = wmax[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) m = max(m, wmax[w]);
+    seglast[(int64_t)d * gridDim.x + blockIdx.x] = m;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+sched_runs_fixup(const RunEnds* __restrict__ bnd, int64_t tiles, int nd, const int32_t* __restrict__ seglast,
+                 uint32_t kend, int slots_per_match, uint32_t* __restrict__ link) {
+  __shared__ int32_t wmax[kWaves];
+  __shared__ int32_t carry_s;
+  const int d = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t seg = blockIdx.x;
+  // carry: the last non-empty tile of digit d before this segment (seglast grows with the segment)
+  if (wv == 0) {
+    int32_t c = -1;
+    for (int64_t q = lane; q < seg; q += 64) c = max(c, seglast[(int64_t)d * gridDim.x + q]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) c = max(c, __shfl_xor(c, off));
+    if (lane == 0) carry_s = c;
+  }
+  const int64_t t = seg * kThreads + threadIdx.x;
+  RunEnds me = {kRunEmpty, 0u, kRunEmpty, 0u};
+  if (t < tiles) me = bnd[t * nd + d];
+  const bool full = me.kf != kRunEmpty;
+  // inclusive max-scan of the non-empty tiles: wave, then across the block's waves
+  int32_t x = full ? (int32_t)t : -1;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(x, off);
+    if (lane >= off) x = max(x, y);
+  }
+  if (lane == 63) wmax[wv] = x;
+  __syncthreads();
+  int32_t before = carry_s;
+  for (int w = 0; w < wv; ++w) before = max(before, wmax[w]);
+  int32_t ex = __shfl_up(x, 1);  // exclusive within the wave
+  ex = lane == 0 ? -1 : ex;
+  const int32_t pred = max(before, ex);
+  if (!full || pred < 0 || me.kf >= kend) return;
+  const RunEnds pr = bnd[(int64_t)pred * nd + d];
+  if (pr.kl != me.kf) return;  // the key starts here: no earlier occurrence
+  // the two boundary links: each word gets its bits from one thread each (atomics on
+  // disjoint fields, so a one-pair run that is both a first and a last is safe)
+  atomicOr(&link[me.vf], kLinkHasPred);
+  atomicAnd(&link[pr.vl], ~kMatchMask | (me.vf / (uint32_t)slots_per_match));
+}
+
 }  // namespace
 
 size_t radix_sort_workspace_bytes(int64_t n) {
@@ -457,6 +559,23 @@ static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits,
   uint32_t *ko = kb, *vo = vb;
   for (int shift = 0; shift < bits; shift += RB) {
     const bool first = shift == 0, last = shift + RB >= bits;
+    // the last pass of a multi-pass sort over few digits (1M players: bits 16..19, 16
+    // digits): run ends in a table, no digit offsets (radix_downsweep bnd)
+    const int nd = bits - shift < RB ? 1 << (bits - shift) : kR;
+    if (last && !first && nd <= kRunsMaxDigits && local_runs()) {
+      RunEnds* bnd = reinterpret_cast<RunEnds*>(counts);  // pass counts are consumed by now
+      const int64_t nseg = (tiles + kThreads - 1) / kThreads;
+      int32_t* seglast = reinterpret_cast<int32_t*>(bnd + tiles * nd);
+      const int parts = link_parts(n);
+      for (int q = 0; q < parts; ++q)
+        hipLaunchKernelGGL((radix_downsweep<0, true, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo,
+                           n, shift, counts, totals, tiles, S, link, (uint32_t)(n * q / parts),
+                           (uint32_t)(n * (q + 1) / parts), q == 0 ? 1 : 0, bnd, nd);
+      const dim3 sgrid((unsigned)nseg, (unsigned)nd);
+      hipLaunchKernelGGL(sched_runs_last, sgrid, block, 0, s, bnd, tiles, nd, seglast);
+      hipLaunchKernelGGL(sched_runs_fixup, sgrid, block, 0, s, bnd, tiles, nd, seglast, kend, S, link);
+      break;
+    }
     if (first)
       hipLaunchKernelGGL((radix_upsweep<K, RB, NT>), grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles,
                          init);

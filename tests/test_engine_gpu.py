@@ -92,6 +92,24 @@ def test_schedule_matches_host(gpu_device, P, M, K):
     np.testing.assert_array_equal(need[rated], deps_h.numpy()[rated])
 
 
+@pytest.mark.parametrize("P,M,K,skew,runs", [(1_000_000, 400_000, 3, 3, "1"), (1_000_000, 400_000, 3, 1, "0"),
+                                             (1_000_000, 400_000, 3, 1, "1"), (5000, 300_000, 5, 2, "1")])
+def test_schedule_run_table_matches_host(gpu_device, P, M, K, skew, runs, monkeypatch):
+    """The last sort pass with run ends in a [tile][digit] table (no digit offsets,
+    sched_runs_fixup) and the round-2 path (ANA_SCHED_RUNS=0): the same links as the
+    host, also on power-law streams where a hot player's runs span many tiles and a
+    sparse player's nearest earlier run lies tiles back."""
+    monkeypatch.setenv("ANA_SCHED_RUNS", runs)
+    rec = make_stream(StreamSpec(team_size=K, seed=P + skew, skew=skew, p_afk=0.05), M, P, K=K)
+    br = R.BatchRater()
+    link_h, deps_h = (t.clone() for t in br.schedule(rec, K, P))
+    link_d, deps_d = br.schedule(rec.to(gpu_device), K, P)
+    slots, first = _stateful_slots(rec.numpy(), K, P)
+    link_d = link_d.cpu().numpy()
+    np.testing.assert_array_equal(link_d[slots], link_h.numpy()[slots])
+    assert int(deps_d.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("P,M,K", [(20, 3000, 3), (70_000, 400_000, 3), (17_000_000, 300_000, 5)])
 def test_schedule_link_parts_match_host(gpu_device, P, M, K, monkeypatch):
     """The link pass split into slot-range parts (ANA_LINK_PARTS; automatic above
