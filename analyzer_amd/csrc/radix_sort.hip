@@ -13,8 +13,10 @@
 //   downsweep per tile: stable rank in wave order (8 ballots -> peer mask),
 //             wave prefixes in LDS, local scatter into an LDS-sorted tile,
 //             then coalesced runs to the global digit offsets.
-// 4096-element tiles (256 threads x 16); 8-bit digits (10-bit ones for the schedule
-// are an opt-in experiment, ANA_SORT_RB: fewer passes but measured slower).
+// 8192-element tiles (512 threads x 16: the per-(tile, digit) runs the downsweeps write
+// average 32 elements, whole 128-B lines; 4096-element tiles measured 0.03-0.04 ms slower
+// per 10M 3v3 prepass, profiles/r3/sort_tile_8192.log); 8-bit digits (10-bit ones for the
+// schedule are an opt-in experiment, ANA_SORT_RB: fewer passes but measured slower).
 //
 // The schedule prepass (launch_sched_sort) fuses both ends: pass 0 computes its
 // keys from the match records, and the last pass writes each slot's link from
@@ -32,7 +34,10 @@ namespace ana {
 
 namespace {
 
-constexpr int kThreads = 256;
+#ifndef ANA_SORT_THREADS
+#define ANA_SORT_THREADS 512  // threads per tile (x 16 items = 8192 elements; 256: 4096, A/B)
+#endif
+constexpr int kThreads = ANA_SORT_THREADS;
 constexpr int kWaves = kThreads / 64;
 constexpr int kItems = 16;
 constexpr int kTile = kThreads * kItems;
@@ -248,8 +253,8 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
                 uint32_t vlo = 0u, uint32_t vhi = 0xffffffffu, int bounds = 1,
                 RunEnds* __restrict__ bnd = nullptr, int nd = 0) {
   constexpr int kR = 1 << RB;
-  constexpr int DPT = kR / kThreads;  // digits per thread in the scans
-  static_assert(DPT >= 1 && DPT * kThreads == kR, "radix must be a multiple of the block");
+  constexpr int DPT = kR >= kThreads ? kR / kThreads : 1;  // digits per thread in the scans
+  static_assert(kR % kThreads == 0 || kThreads % kR == 0, "radix and block must divide");
   __shared__ uint32_t skey[kTile];
   __shared__ uint32_t sval[kTile];
   __shared__ uint32_t wcnt[kWaves][kR];
@@ -264,11 +269,11 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
   if (!local_ends) {  // global start of each digit for this tile
     uint32_t v[DPT];
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) v[j] = totals[tid * DPT + j];
+    for (int j = 0; j < DPT; ++j) v[j] = tid * DPT + j < kR ? totals[tid * DPT + j] : 0u;
     digits_exclusive_scan<DPT>(v, wsum, nullptr);
 #pragma unroll
     for (int j = 0; j < DPT; ++j)
-      gstart[tid * DPT + j] = v[j] + counts[(int64_t)(tid * DPT + j) * tiles + tile];
+      if (tid * DPT + j < kR) gstart[tid * DPT + j] = v[j] + counts[(int64_t)(tid * DPT + j) * tiles + tile];
   }
   if constexpr (KS > 0) decode_tile_keys<KS>(rec, kend, base, n, sval);  // sval: scratch until the scatter
   __syncthreads();
@@ -308,17 +313,20 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
     for (int j = 0; j < DPT; ++j) {
       const int d = tid * DPT + j;
       uint32_t s = 0;
+      if (d < kR) {  // (threads past kR own no digit: they add 0 to the scan)
 #pragma unroll
-      for (int w = 0; w < kWaves; ++w) {
-        const uint32_t c = wcnt[w][d];
-        wcnt[w][d] = s;
-        s += c;
+        for (int w = 0; w < kWaves; ++w) {
+          const uint32_t c = wcnt[w][d];
+          wcnt[w][d] = s;
+          s += c;
+        }
       }
       v[j] = s;
     }
     digits_exclusive_scan<DPT>(v, wsum, nullptr);
 #pragma unroll
-    for (int j = 0; j < DPT; ++j) tstart[tid * DPT + j] = v[j];
+    for (int j = 0; j < DPT; ++j)
+      if (tid * DPT + j < kR) tstart[tid * DPT + j] = v[j];
   }
   __syncthreads();
 #pragma unroll
