@@ -55,6 +55,82 @@ __global__ void __launch_bounds__(256) telemetry_kernel(TelemetryParams tp, uint
   else telemetry_tile<K, D>(tp, t, threadIdx.x & 63, scratch[wv], bad);
 }
 
+// impl 2: ONE LANE PER STAT ROW.  Lane (q, j) of a wave owns the stat row of slot j
+// of the wave's q-th match (64 / 2K matches per wave) and walks that match's whole
+// CSR range, folding the events of its slot: every event is read by the 2K lanes of
+// its match (one broadcast line per instruction), and each lane adds only its own.
+// The row's seven sums live in LDS at a lane-private stride of 9 floats (the
+// feature is per-event data, and a register array indexed by it would be a select
+// chain over all seven), added with ds_add_f32 (IEEE round to nearest, in issue
+// order), the event count in a register.  Sums run in event order
+// per row, the order of the host mirror, so the result is the host's bit for bit
+// (Inf / NaN values included); a malformed event is counted once, by slot 0's lane.
+// 4 events in flight per lane; the loop runs to the longest range of the wave.
+template <int K>
+__global__ void __launch_bounds__(256) telemetry_rows_kernel(TelemetryParams tp, uint32_t* bad) {
+  constexpr int S = 2 * K;
+  constexpr int MPW = 64 / S;   // matches per wave
+  constexpr int kStride = 9;    // LDS floats per lane (8 sums + pad: conflict-free lane stride)
+  constexpr int kAhead = 4;     // event loads in flight per lane
+  __shared__ float rows[256 * kStride];
+  const int lane = threadIdx.x & 63;
+  const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int q = lane / S, slot = lane % S;
+  const int64_t m = task * MPW + q;
+  const bool act = q < MPW && m < tp.num_matches;
+  const int64_t e0 = act ? tp.evoff[m] : 0;
+  const int n = act ? (int)(tp.evoff[m + 1] - e0) : 0;
+  int nmax = n;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) nmax = max(nmax, __shfl_xor(nmax, off));
+  float* const acc = rows + threadIdx.x * kStride;
+#pragma unroll
+  for (int k = 0; k < kStatFeatures - 1; ++k) acc[k] = 0.f;
+  const uint32_t mtag = (uint32_t)m & 0xffffu;
+  float cnt = 0.f;
+  uint32_t nbad = 0;
+  const int32_t* const dummy = reinterpret_cast<const int32_t*>(tp.evoff);
+  for (int i = 0; i < nmax; i += kAhead) {
+    int2 ev[kAhead];
+#pragma unroll
+    for (int u = 0; u < kAhead; ++u) {
+      const bool ok = i + u < n;
+      ev[u] = *reinterpret_cast<const int2*>(ok ? tp.events + 2 * (e0 + i + u) : dummy);
+    }
+#pragma unroll
+    for (int u = 0; u < kAhead; ++u) {
+      if (i + u >= n) continue;
+      const int32_t meta = ev[u].x;
+      const int es = event_slot(meta);
+      const bool good = event_tag(meta) == mtag && es < S;
+      if (!good) {
+        nbad += slot == 0 ? 1u : 0u;
+        continue;
+      }
+      if (es != slot) continue;
+      cnt += 1.f;
+      float add;
+      const int f = event_feature(event_type(meta), __int_as_float(ev[u].y), add);
+      // lane-private LDS word: a ds_add without return -- fire and forget, applied in
+      // issue order, so consecutive events of one feature never wait on a read-back
+      if (f >= 0) atomicAdd(&acc[f], add);
+    }
+  }
+  if (act) {
+    float4* dst = reinterpret_cast<float4*>(tp.stats + (m * S + slot) * kStatFeatures);
+    dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    dst[1] = make_float4(acc[4], acc[5], acc[6], cnt);
+  }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
+template <int K>
+static void launch_tele_rows(const TelemetryParams& tp, uint32_t* bad, hipStream_t s) {
+  constexpr int MPW = 64 / (2 * K);
+  const int64_t tasks = (tp.num_matches + MPW - 1) / MPW;
+  hipLaunchKernelGGL(telemetry_rows_kernel<K>, dim3((unsigned)((tasks + 3) / 4)), dim3(256), 0, s, tp, bad);
+}
+
 int launch_gen_event_counts(const GenEventParams& g, int64_t base, int64_t M, int64_t* counts,
                             hipStream_t s) {
   if (M <= 0) return 0;
@@ -103,6 +179,7 @@ static void launch_tele_k(const TelemetryParams& tp, uint32_t* bad, hipStream_t 
   if (dbg == 2) return launch_tele<K, 2, kTeleTile>(tp, bad, s);
 #endif
   if (impl == 0) return launch_tele<K, 0, kTeleTile>(tp, bad, s);
+  if (impl == 2) return launch_tele_rows<K>(tp, bad, s);
 #if ANA_DIAG_BUILD
   const int d = dbg == 6 ? 6 : dbg == 7 ? 7 : 3;
 #define ANA_TELE_SPAN(sp)                                                                     \
@@ -124,7 +201,7 @@ static void launch_tele_k(const TelemetryParams& tp, uint32_t* bad, hipStream_t 
 
 int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_t s) {
   if (tp.num_matches <= 0) return 0;
-  // ANA_TELE_IMPL: 1 (default) one-hot MFMA, 0 LDS atomics; ANA_TELE_SPAN: matches per
+  // ANA_TELE_IMPL: 1 (default) one-hot MFMA, 0 LDS atomics, 2 one lane per stat row; ANA_TELE_SPAN: matches per
   // wave of the MFMA kernel (16, 32, 63); ANA_TELE_DEBUG (diagnostic, timing only):
   // atomic version 1 = no LDS adds, 2 = no count adds; MFMA version 6 = no MFMA, 7 = decode only
   const char* dbg_env = getenv("ANA_TELE_DEBUG");

@@ -311,10 +311,11 @@ def test_telemetry_device_generator_and_aggregation(gpu_device):
     np.testing.assert_allclose(sd.cpu().numpy(), aggregate_reference(th, K), rtol=2e-5, atol=0.05)
 
 
-@pytest.mark.parametrize("impl", ["1", "0"])
+@pytest.mark.parametrize("impl", ["1", "0", "2"])
 @pytest.mark.parametrize("K", [1, 2, 3, 4, 5])
 def test_telemetry_impls_vs_oracle_edges(gpu_device, monkeypatch, K, impl):
-    """K8 one-hot MFMA (impl 1) and LDS-atomic (impl 0) tiles vs an fp64 oracle:
+    """K8 one-hot MFMA (impl 1), LDS-atomic (impl 0) tiles and one lane per stat
+    row (impl 2, also bit-identical to the host mirror) vs an fp64 oracle:
     every team size (16-row blocks of 8/4/2/2/1 matches), empty matches, a
     partial last tile, malformed events (strict attribution) and non-finite
     values; the host mirror counts the same malformed events."""
@@ -352,6 +353,8 @@ def test_telemetry_impls_vs_oracle_edges(gpu_device, monkeypatch, K, impl):
     assert int(bad.item()) == int((~ok).sum())
     np.testing.assert_allclose(stats.cpu().numpy(), ref, rtol=2e-6, atol=1e-3)
     np.testing.assert_allclose(host.numpy(), ref, rtol=2e-6, atol=1e-3)
+    if impl == "2":  # row sums in event order, as the host mirror: the same bits
+        assert torch.equal(stats.cpu(), host)
 
 
 def test_graph_rater_matches_eager(gpu_device):
