@@ -155,10 +155,11 @@ class EngineConfig:
     variable                default   consumer
     ======================  ========  =============================================
     ANA_RATE_BLOCKS         512       persistent grid of a window launch (ops/rate.py)
-    ANA_PREPASS_AT          0.7       tail overlap point of the next prepass (runtime/engine.py)
+    ANA_PREPASS_AT          0.7       tail overlap point of the next prepass (runtime/engine.py; 0.9 for
+                                      1v1-4v4 windows between DP merges)
     ANA_PREPASS_CUS         0         CU-masked prepass stream, 0 = off (runtime/engine.py)
     ANA_PREPASS_SERIAL      auto      1 prepass on the main stream, 0 tail overlap; auto: serial
-                                      for K <= 4, overlap for 5v5 (runtime/engine.py)
+                                      for K <= 4 without DP merges, overlap otherwise (runtime/engine.py)
     ANA_MERGE_BUCKET_MB     16        sweep-merge bucket size (parallel/sweep.py)
     COMM_DTYPE              fp32      sweep-merge message precision (bench.py, rerate)
     SWEEPS                  1         causal sweeps per window (bench.py, rerate)
@@ -183,6 +184,7 @@ class EngineConfig:
 
     rate_blocks: int = 512
     prepass_at: float = 0.7
+    prepass_at_set: bool = False  # ANA_PREPASS_AT given explicitly (else the engine picks per mode)
     prepass_cus: int = 0
     prepass_exclusive: bool = False  # with prepass_cus: the executor gets the other CUs
     prepass_serial: Optional[bool] = None  # None = auto (WindowPipeline.serial_prepass)
@@ -220,6 +222,7 @@ class EngineConfig:
         return EngineConfig(
             rate_blocks=int(_env(env, "ANA_RATE_BLOCKS") or 512),
             prepass_at=float(_env(env, "ANA_PREPASS_AT") or 0.7) if env.get("ANA_PREPASS_AT") != "0" else 0.0,
+            prepass_at_set=bool(env.get("ANA_PREPASS_AT")),
             prepass_cus=int(_env(env, "ANA_PREPASS_CUS") or 0),
             prepass_exclusive=env.get("ANA_PREPASS_EXCLUSIVE", "0") not in ("", "0", "false"),
             prepass_serial=_tristate(env.get("ANA_PREPASS_SERIAL")),

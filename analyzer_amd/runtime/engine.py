@@ -48,6 +48,7 @@ from ..ops.rate import BatchRater, RateResult, Roster, Schedule
 from ..utils.trace import trace_range
 
 CHUNK = 64  # matches per executor ticket of a window (csrc/dataflow.hip kChunk; BatchRater.chunk_len)
+DP_TAIL_AT = 0.9  # tail-overlap start of the next prepass between DP merges (3v3; see tail_point)
 
 
 @dataclass
@@ -73,9 +74,10 @@ class WindowPipeline:
         self.windows_rated = 0
         # tail overlap: signal word + number of the last enqueued rate launch
         self.ecfg = EngineConfig.from_env()
-        self.serial = self.serial_prepass(self.K, self.ecfg)
+        dp = merger is not None
+        self.serial = self.serial_prepass(self.K, self.ecfg, dp)
         # serial prepass: nothing to overlap, no tail signal
-        self.tail = 0.0 if self.serial else self.ecfg.prepass_at
+        self.tail = 0.0 if self.serial else self.tail_point(self.K, self.ecfg, dp)
         self._signal = 0
         self._seq = 0
         self.side = self._side_stream() if self.cuda else None
@@ -101,12 +103,22 @@ class WindowPipeline:
                 self._signal = native().progress_signal(dev)
 
     @staticmethod
-    def serial_prepass(K: int, ecfg: EngineConfig) -> bool:
+    def serial_prepass(K: int, ecfg: EngineConfig, dp: bool = False) -> bool:
         """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial
-        below 5v5 (see the module docstring for the measurements)."""
+        below 5v5 -- except under DP merges (``dp``), where the windows are short
+        (k per step) and the tail overlap pays (see the module docstring)."""
         if ecfg.prepass_serial is not None:
             return ecfg.prepass_serial
-        return K < 5
+        return K < 5 and not dp
+
+    @staticmethod
+    def tail_point(K: int, ecfg: EngineConfig, dp: bool = False) -> float:
+        """Where the overlapped prepass starts: ``ANA_PREPASS_AT`` if set, else 0.7,
+        and DP_TAIL_AT for 1v1-4v4 windows between merges (measured: config 2 with 8
+        merges per step, profiles/r3/dp_prepass_placement_k8.log)."""
+        if ecfg.prepass_at_set or K >= 5 or not dp:
+            return ecfg.prepass_at
+        return DP_TAIL_AT
 
     def _side_stream(self):
         """Side stream of the prepass; ``ANA_PREPASS_CUS=n`` confines it to n CUs
