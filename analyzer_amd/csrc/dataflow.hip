@@ -118,17 +118,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // per-field stores sent 6-7 partial-line writes per match to the fabric)
   constexpr int OQ = (5 * S + 2 + 3) / 4;
   __shared__ __attribute__((aligned(16))) float lrow[kWavesPerBlock][NG][4 * OQ];
-#if ANA_EXP_VPTR
-  // experiment: per-lane-addressed bases held in VGPR pairs instead of SGPRs (the
-  // kernel spills ~57 SGPRs into VGPR lanes; every readback is a v_readlane)
-#define ANA_VPTR(p) do { uint64_t u_ = (uint64_t)(uintptr_t)(p); asm volatile("" : "+v"(u_)); (p) = (decltype(p))(uintptr_t)u_; } while (0)
-  ANA_VPTR(rec); ANA_VPTR(link); ANA_VPTR(attrs); ANA_VPTR(first_prior); ANA_VPTR(orows);
-  ANA_VPTR(prm.vst);
-#if ANA_EXP_VPTR > 1
-  ANA_VPTR(ctrl);
-#endif
-#undef ANA_VPTR
-#endif
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int j = lane % G;
@@ -487,8 +476,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
 
     // ---------------------------------------------- (10) rate a batch
-    int32_t row_m = -1;  // ANA_EXP_ROWLATE: the group's output row leaves after the polls
-    (void)row_m;
     // inline telemetry: the events this iteration's groups load for the next flush
     v2u tev_next[TT];
     int32_t tn_m = -1, tn_cnt = 0;
@@ -563,14 +550,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
     }
     if (my_h >= 0) {
-#if ANA_EXP_DEPLOAD
-      // experiment: a load whose address depends on the gathered granule, needed at
-      // the publish (prices a position-chained successor list)
-      uint32_t dep = (uint32_t)gs.w ^ (uint32_t)id;
-      asm volatile("" : "+v"(dep));
-      const v2u xl = __builtin_amdgcn_raw_buffer_load_b64(
-          rl, own ? (int)(((dep * 2654435761u) & ((1u << 26) - 1u)) * 4u) : kOutOfRange, 0, 16);
-#endif
       const float smu = __int_as_float(gs.x), ssg = __int_as_float(gs.z);
       const float mmu = __int_as_float(gm.x), msg = __int_as_float(gm.z);
       // seed attributes only for players without a shared rating (their first
@@ -660,9 +639,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       const bool ok = gst == kRated && inr;
       if constexpr (DIAG) d_p[2] = __builtin_amdgcn_s_memrealtime();
-#if ANA_EXP_DEPLOAD
-      asm volatile("; dep %0 %1" :: "v"(xl.x), "v"(xl.y));
-#endif
       if (inr && islast) {  // publish: new values, or the untouched ones on error
         const int off = id * (kRowFloats * 4);
         // shared granule: tagged with the next reader + bumped mode counter;
@@ -728,9 +704,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         for (int k = 5 * S + 2; k < 4 * OQ; ++k) lr[k] = 0.f;  // row padding
       }
       // (the group's LDS writes and reads are the same wave's, in order)
-#if ANA_EXP_ROWLATE
-      row_m = m;
-#else
 #pragma unroll
       for (int t = 0; t < (OQ + G - 1) / G; ++t) {
         typedef float v4f __attribute__((ext_vector_type(4)));
@@ -738,7 +711,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         if (qd < OQ)
           __builtin_nontemporal_store(reinterpret_cast<const v4f*>(lr)[qd], reinterpret_cast<v4f*>(orm) + qd);
       }
-#endif
     }
     };
 
@@ -876,19 +848,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     for (int h = 0; h < kH; ++h)
       dval[h] = __builtin_amdgcn_raw_buffer_load_b32(rd, ((pend[h] >> lane) & 1ull) ? (cbase[h] + lane) * 4 : kOutOfRange,
                                                      0, 16);
-#if ANA_EXP_ROWLATE
-    if (row_m >= 0) {
-      float* const orm = orows + (int64_t)row_m * orow;
-      const float* const lr = lrow[wv][g];
-#pragma unroll
-      for (int t = 0; t < (OQ + G - 1) / G; ++t) {
-        typedef float v4f __attribute__((ext_vector_type(4)));
-        const int qd = j + t * G;
-        if (qd < OQ)
-          __builtin_nontemporal_store(reinterpret_cast<const v4f*>(lr)[qd], reinterpret_cast<v4f*>(orm) + qd);
-      }
-    }
-#endif
 
     // ---------------------------------------------- (11) retire finished chunks
     {
