@@ -82,8 +82,11 @@ def parse(argv=None):
                     help="N > 1: split each GPU's step into this many windows with a sweep merge after "
                          "each (same matches per step; shorter slices cut the sweep-DP error ~linearly, "
                          "profiles/r2/slice_size_accuracy.log).  Default: 1 on one GPU (nothing to "
-                         "merge), 8 for N > 1 (one sweep then keeps Spearman(mu - sigma) >= 0.99 against "
-                         "the exact sequential result at 8 x 10M 3v3 over 1M players)")
+                         "merge), N for N > 1 (largest power of two <= N, at most 8): every rank then "
+                         "misses about the same (N - 1) / N of a step of the others' matches between merges, "
+                         "and one sweep keeps Spearman(mu - sigma) >= 0.99 against the exact sequential "
+                         "result -- 0.9993 / 0.9978 / 0.9948 at N = 2 / 4 / 8 for 10M 3v3 per rank over 1M "
+                         "players (profiles/r3/merges_vs_ranks.log)")
     ap.add_argument("--accuracy", type=int, default=1,
                     help="N > 1: after timing, rank 0 measures the sweep-DP error of this run's "
                          "configuration against the exact sequential rating (parallel/accuracy.py, "
@@ -109,7 +112,10 @@ def parse(argv=None):
         args.ring = min(args.ring, 2)
     if args.merges_per_step is None:
         n = args.gpus if args.gpus is not None else int(os.environ.get("WORLD_SIZE") or 1)
-        args.merges_per_step = 8 if n > 1 and args.config != 4 and args.sweeps <= 1 else 1
+        k = 1
+        while k * 2 <= min(n, 8):
+            k *= 2
+        args.merges_per_step = k if n > 1 and args.config != 4 and args.sweeps <= 1 else 1
     if args.merges_per_step < 1 or args.matches_per_gpu % args.merges_per_step:
         ap.error("--merges-per-step must divide --matches-per-gpu")
     if args.merges_per_step > 1 and args.config == 4:

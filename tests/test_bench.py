@@ -61,8 +61,11 @@ def test_merges_per_step_default_is_accuracy_bounded(monkeypatch):
     sequential result (profiles/r2/slice_size_accuracy.log); causal re-sweeps are
     exact already and keep one window."""
     assert bench.parse([]).merges_per_step == 1
+    # one merge per rank's worth of concurrency: k = the largest power of two <= N (<= 8)
     assert bench.parse(["--gpus", "8"]).merges_per_step == 8
-    assert bench.parse(["--gpus", "2", "--config", "3"]).merges_per_step == 8
+    assert bench.parse(["--gpus", "4"]).merges_per_step == 4
+    assert bench.parse(["--gpus", "6"]).merges_per_step == 4
+    assert bench.parse(["--gpus", "2", "--config", "3"]).merges_per_step == 2
     assert bench.parse(["--gpus", "8", "--sweeps", "8"]).merges_per_step == 1
     assert bench.parse(["--gpus", "8", "--config", "4"]).merges_per_step == 1
     assert bench.parse(["--gpus", "8", "--merges-per-step", "2"]).merges_per_step == 2
