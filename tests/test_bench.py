@@ -56,9 +56,9 @@ def test_merges_per_step():
 
 
 def test_merges_per_step_default_is_accuracy_bounded(monkeypatch):
-    """One GPU has nothing to merge (one window per step); N > 1 merges 8 times per
+    """One GPU has nothing to merge (one window per step); N > 1 merges N times per
     step so that one sweep keeps Spearman(mu - sigma) >= 0.99 against the exact
-    sequential result (profiles/r2/slice_size_accuracy.log); causal re-sweeps are
+    sequential result (profiles/r3/merges_vs_ranks.log); causal re-sweeps are
     exact already and keep one window."""
     assert bench.parse([]).merges_per_step == 1
     # one merge per rank's worth of concurrency: k = the largest power of two <= N (<= 8)
@@ -70,5 +70,5 @@ def test_merges_per_step_default_is_accuracy_bounded(monkeypatch):
     assert bench.parse(["--gpus", "8", "--config", "4"]).merges_per_step == 1
     assert bench.parse(["--gpus", "8", "--merges-per-step", "2"]).merges_per_step == 2
     monkeypatch.setenv("WORLD_SIZE", "4")
-    assert bench.parse([]).merges_per_step == 8
+    assert bench.parse([]).merges_per_step == 4
     assert bench.parse([]).accuracy == 1
