@@ -86,7 +86,9 @@ def parse(argv=None):
                          "misses about the same (N - 1) / N of a step of the others' matches between merges, "
                          "and one sweep keeps Spearman(mu - sigma) >= 0.99 against the exact sequential "
                          "result -- 0.9993 / 0.9978 / 0.9948 at N = 2 / 4 / 8 for 10M 3v3 per rank over 1M "
-                         "players (profiles/r3/merges_vs_ranks.log)")
+                         "players (profiles/r3/merges_vs_ranks.log); 5v5 (config 3) doubles k from N = 4: "
+                         "0.9897 at N = k = 4 but 0.9971 at k = 8, 0.9884 at N = k = 8 but 0.9965 at k = 16 "
+                         "(profiles/r3/merges_vs_ranks_5v5.log)")
     ap.add_argument("--accuracy", type=int, default=1,
                     help="N > 1: after timing, rank 0 measures the sweep-DP error of this run's "
                          "configuration against the exact sequential rating (parallel/accuracy.py, "
@@ -115,6 +117,8 @@ def parse(argv=None):
         k = 1
         while k * 2 <= min(n, 8):
             k *= 2
+        if args.team_size == 5 and n >= 4:
+            k *= 2      # 5v5: 10 appearances a match, twice the merges for the same error
         args.merges_per_step = k if n > 1 and args.config != 4 and args.sweeps <= 1 else 1
     if args.merges_per_step < 1 or args.matches_per_gpu % args.merges_per_step:
         ap.error("--merges-per-step must divide --matches-per-gpu")

@@ -66,6 +66,9 @@ def test_merges_per_step_default_is_accuracy_bounded(monkeypatch):
     assert bench.parse(["--gpus", "4"]).merges_per_step == 4
     assert bench.parse(["--gpus", "6"]).merges_per_step == 4
     assert bench.parse(["--gpus", "2", "--config", "3"]).merges_per_step == 2
+    # 5v5 has 10 appearances a match: twice the merges from N = 4 (merges_vs_ranks_5v5.log)
+    assert bench.parse(["--gpus", "4", "--config", "3"]).merges_per_step == 8
+    assert bench.parse(["--gpus", "8", "--config", "3"]).merges_per_step == 16
     assert bench.parse(["--gpus", "8", "--sweeps", "8"]).merges_per_step == 1
     assert bench.parse(["--gpus", "8", "--config", "4"]).merges_per_step == 1
     assert bench.parse(["--gpus", "8", "--merges-per-step", "2"]).merges_per_step == 2
