@@ -175,7 +175,11 @@ class EngineConfig:
     ANA_TELE_ROLE           -1        fused telemetry: -1 = inline, each lane group folds the events of
                                       the match it rates (11.4 ms per config 4 step); N > 0 = one wave in
                                       N aggregates MFMA tiles from the start (N = 2: 11.7); 0 = idle waves.
-                                      All slower than the separate kernel (10.1; bench default)
+                                      All slower than the separate kernel on 10M windows (10.1)
+    ANA_TELE_FUSE_MAX       262144    inline (fused) telemetry up to this many matches per launch; larger
+                                      launches rate, then run the MFMA kernel (ops/rate.py; crossover
+                                      measured by scripts/tele_batch.py: fused 0.55x separate at 500
+                                      matches, 0.96x at 100k, 1.05x at 1M)
     ======================  ========  =============================================
 
     The executor / fused-telemetry knobs reach the launch as ``BatchRater.knobs``
@@ -202,6 +206,7 @@ class EngineConfig:
     rate_tight: int = -1
     tele_fused_tail: int = 0
     tele_role: int = -1
+    tele_fuse_max: int = 262_144
 
     # kernel-implementation A/B switches read by the native extension itself
     # (csrc/telemetry.hip, kernels.hip, radix_sort.hip) -- experiments, not tuning
@@ -240,4 +245,5 @@ class EngineConfig:
             rate_tight=int(_env(env, "ANA_RATE_TIGHT") or -1),
             tele_fused_tail=int(_env(env, "ANA_TELE_FUSED_TAIL") or 0),
             tele_role=int(_env(env, "ANA_TELE_ROLE") or -1),
+            tele_fuse_max=int(_env(env, "ANA_TELE_FUSE_MAX") or 262_144),
         )

@@ -178,6 +178,9 @@ class BatchRater:
         # persistent-grid size of the dataflow launch (4 waves per block)
         self.blocks = int(blocks or ecfg.rate_blocks)
         self.knobs = ecfg.rate_knobs()  # executor / fused-telemetry tuning (csrc/bindings.cpp)
+        # inline (fused) telemetry up to this many matches per launch, the MFMA kernel after
+        # the rating above (scripts/tele_batch.py, profiles/r3/tele_fused_vs_separate_by_batch.log)
+        self.tele_fuse_max = int(ecfg.tele_fuse_max)
         self._vst: Dict[str, torch.Tensor] = {}
         self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
 
@@ -186,6 +189,22 @@ class BatchRater:
         """One definition of "this launch aggregates telemetry" for every caller
         that sizes chunks (rate(), runtime/engine.py's tail signal)."""
         return telemetry is not None and telemetry[0].numel() > 0
+
+    def tiles(self, telemetry, M: int) -> bool:
+        """Does a launch of M matches with ``telemetry`` aggregate in MFMA tiles of
+        its own waves (ANA_TELE_ROLE >= 0), which need the full grid and 64-match
+        chunks?  Inline aggregation (the default) and launches past
+        ``tele_fuse_max`` (aggregated by the kernel after the rating) do not."""
+        return self.has_telemetry(telemetry) and self.knobs[5] >= 0
+
+    def fuses(self, telemetry, M: int) -> bool:
+        """Is ``telemetry`` aggregated inside the rating launch of M matches?  Tiles
+        always are; inline aggregation up to ``tele_fuse_max`` matches.  Above it the
+        standalone MFMA kernel runs after the rating on the same stream: inline costs
+        each rating iteration its event loads and LDS adds, which a latency-bound
+        window pays on every dependency level (10M 3v3: 11.1 ms fused vs 9.9 ms
+        separate), while a worker batch is launch-bound (500 matches: 44 vs 80 us)."""
+        return self.has_telemetry(telemetry) and (self.knobs[5] >= 0 or M <= self.tele_fuse_max)
 
     def chunk_len(self, M: int, telemetry: bool = False) -> int:
         """Matches per executor ticket: 64 (one per lane) for windows, shorter
@@ -307,10 +326,13 @@ class BatchRater:
             link = deps = ctrl = torch.empty(0, dtype=torch.int32)
             epoch = 1
             ctrl_ready = False
-        tele = self.has_telemetry(telemetry)
         # aggregation tiles need the full grid and whole chunks; inline aggregation
         # (ANA_TELE_ROLE < 0: each lane group folds its own match's events) does not
-        tiles = tele and self.knobs[5] >= 0
+        tiles = self.tiles(telemetry, M)
+        after = None
+        if self.has_telemetry(telemetry) and not self.fuses(telemetry, M) and dev.type == "cuda":
+            after, telemetry = telemetry, None  # the MFMA kernel after the rating (fuses())
+        tele = self.has_telemetry(telemetry)
         if not tele:
             none = torch.empty(0, dtype=torch.int64, device=dev)
             telemetry = (none, none.to(torch.int32), none.to(torch.float32))
@@ -322,6 +344,11 @@ class BatchRater:
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
                       epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
                       self.chunk_len(M, tiles), ctrl_ready, self.knobs)
+        if after is not None:
+            # same stream, after the rating; malformed events count into ctrl[13] as in
+            # the fused launch (zeroed by this launch, read by telemetry_errors)
+            evoff, events, stats = after
+            native().telemetry(evoff, events, K, stats, ctrl[13:14])
         if check and dev.type == "cuda":
             self.check_errors(dev)
         return out

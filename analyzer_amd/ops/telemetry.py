@@ -11,9 +11,12 @@ events) -- aligned with the rating outputs ``[M, 2K]``:
   one-hot GEMM on the matrix cores -- or LDS float atomics, ANA_TELE_IMPL=0 --
   and coalesced stat stores; csrc/telemetry.hip, telemetry_dev.h);
 * ``BatchRater.rate(..., telemetry=(evoff, events, stats))`` runs it INSIDE the
-  dataflow launch: waves with no ready match aggregate telemetry tiles instead
-  of sleeping, so a latency-bound rating absorbs the bandwidth-bound
-  aggregation (the fused streaming mode).
+  dataflow launch (the fused streaming mode): each lane group folds the events
+  of the match it just rated (inline, default), or aggregation waves take
+  MFMA tiles (ANA_TELE_ROLE >= 0).  Inline fusion holds up to
+  ANA_TELE_FUSE_MAX matches per launch -- a 500-match worker batch takes 45 us
+  fused against 80 us for rating + kernel -- and above that the call runs
+  ``aggregate``'s kernel after the rating instead (``BatchRater.fuses``).
 
 Events are 8-B records (slot | type << 8 | 16-bit match tag << 16, value bits)
 grouped by match with CSR offsets ``evoff[M+1]`` (layout: csrc/telemetry_core.h).  ``make_telemetry`` generates them with the

@@ -176,7 +176,7 @@ class WindowPipeline:
         if self._signal:
             self._seq += 1
             M = int(prep.rec.shape[0])
-            cl = self.rater.chunk_len(M, self.rater.has_telemetry(telemetry))
+            cl = self.rater.chunk_len(M, self.rater.tiles(telemetry, M))
             at = int(self.tail * ((M + cl - 1) // cl))
             progress = (self._signal, self._seq, at)
         with trace_range("rate", window=self.windows_rated, matches=int(prep.rec.shape[0])):

@@ -68,10 +68,12 @@ def parse(argv=None):
                     help="player activity: floor(u^skew * P); 1 = uniform (headline), 2 = quadratic, "
                          "3 = cubic (SURVEY H1: ~585k dependency levels per 10M window)")
     ap.add_argument("--events", default="20,60", help="config 4: min,max telemetry events per match")
-    ap.add_argument("--telemetry-mode", default="separate", choices=["overlap", "fused", "separate"],
-                    help="config 4: overlap = the MFMA aggregation kernel co-runs with the rating "
-                         "launch on its own stream; fused = executor waves aggregate in their idle "
-                         "time; separate = aggregation after the rating on the same stream")
+    ap.add_argument("--telemetry-mode", default="auto", choices=["auto", "overlap", "fused", "separate"],
+                    help="config 4: auto = the rating launch takes the telemetry and fuses it up to "
+                         "ANA_TELE_FUSE_MAX matches (worker batches), the MFMA kernel after it above "
+                         "(10M windows; scripts/tele_batch.py); fused = always inline in the rating "
+                         "groups; separate = the MFMA kernel after the rating on the same stream; "
+                         "overlap = the MFMA kernel co-runs with the rating on its own stream")
     ap.add_argument("--comm-dtype", default=None, choices=["fp32", "fp16", "bf16"],
                     help="sweep-merge message precision (N > 1; default COMM_DTYPE, else bf16 for one "
                          "sweep -- at 8 x 10M the compressed messages leave the sweep error unchanged, "
@@ -211,6 +213,8 @@ def main(argv=None) -> int:
     windows = [make_stream(spec, Mw, P, K=K, base=(w * world + rank) * Mw, device=dev)
                for w in range(n_windows)]
     rater = BatchRater()
+    if args.telemetry_mode == "fused":
+        rater.tele_fuse_max = 1 << 62  # inline at any launch size
     out = RateResult.allocate(Mw, K, dev)
     tele = stats = None
     if args.config == 4:
@@ -346,6 +350,10 @@ def main(argv=None) -> int:
                   "1M-player roster, streaming")
         extra = {"events_per_match": n_events / M, "events_per_s": world * n_events / (ms / 1000.0),
                  "telemetry_mode": args.telemetry_mode}
+        if args.telemetry_mode == "auto":
+            t0w = tele[0]
+            extra["telemetry_path"] = ("fused (inline)" if rater.fuses((t0w.evoff, t0w.events, stats), Mw)
+                                       else "MFMA kernel after the rating (launch > ANA_TELE_FUSE_MAX)")
     if rank == 0:
         print(json.dumps({
             "metric": metric,

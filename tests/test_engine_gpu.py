@@ -413,6 +413,7 @@ def test_fused_rate_telemetry_on_device(gpu_device, monkeypatch, role):
                                             make_telemetry)
 
     monkeypatch.setenv("ANA_TELE_ROLE", str(role))
+    monkeypatch.setenv("ANA_TELE_FUSE_MAX", str(1 << 30))  # inline even past the default threshold
 
     K, P, M = 3, 20000, 400000
     roster = make_roster(RosterSpec(num_players=P, seed=5), device=gpu_device)
@@ -430,15 +431,19 @@ def test_fused_rate_telemetry_on_device(gpu_device, monkeypatch, role):
     np.testing.assert_allclose(stats.cpu().numpy(), ref, rtol=2e-5, atol=0.05)
 
 
-def test_inline_telemetry_edge_cases_on_device(gpu_device, monkeypatch):
+@pytest.mark.parametrize("fuse_max", [1 << 30, 0])
+def test_inline_telemetry_edge_cases_on_device(gpu_device, monkeypatch, fuse_max):
     """Inline aggregation (ANA_TELE_ROLE=-1) on the paths the common case skips:
     stateless matches (AFK, invalid rosters, unsupported) aggregated by tele-only
     groups, matches with more events than a group loads with its granules (the
-    remainder loop), 5v5 groups, and malformed events counted, not folded."""
+    remainder loop), 5v5 groups, and malformed events counted, not folded.
+    ``fuse_max`` 0: the same launch past ANA_TELE_FUSE_MAX, where BatchRater.rate
+    runs the MFMA kernel after the rating -- same stats, ratings and error count."""
     from analyzer_amd.ops.telemetry import (TelemetrySpec, aggregate_reference, allocate_stats,
                                             make_telemetry)
 
     monkeypatch.setenv("ANA_TELE_ROLE", "-1")
+    monkeypatch.setenv("ANA_TELE_FUSE_MAX", str(fuse_max))
     for K, lo, hi in ((3, 0, 150), (5, 30, 90)):
         P, M = 5000, 60000
         roster = make_roster(RosterSpec(num_players=P, seed=15), device=gpu_device)

@@ -192,3 +192,22 @@ def test_synthetic_guard_only_without_a_source(tmp_path):
     write_telemetry(path, [("m0", [(0, 0, "kill", 0.0)])])
     Worker(WorkerConfig(engine="native", database_uri=uri, dotelemetry=True, telemetry_source=path),
            broker=B.MemoryBroker()).connect()
+
+
+def test_fuse_threshold_policy(monkeypatch):
+    """Inline (fused) aggregation up to ANA_TELE_FUSE_MAX matches per launch, the
+    MFMA kernel after the rating above it (scripts/tele_batch.py crossover);
+    aggregation tiles (ANA_TELE_ROLE >= 0) are always fused."""
+    import torch
+    from analyzer_amd.ops import rate as R
+
+    t = (torch.zeros(3, dtype=torch.int64), torch.zeros(0, 2, dtype=torch.int32), torch.zeros(0))
+    br = R.BatchRater()
+    assert br.tele_fuse_max == 262_144
+    assert br.fuses(t, 500) and br.fuses(t, 262_144) and not br.fuses(t, 10_000_000)
+    assert not br.tiles(t, 500) and not br.fuses(None, 500)
+    monkeypatch.setenv("ANA_TELE_FUSE_MAX", "1000")
+    assert not R.BatchRater().fuses(t, 1001)
+    monkeypatch.setenv("ANA_TELE_ROLE", "2")
+    br = R.BatchRater()
+    assert br.tiles(t, 10_000_000) and br.fuses(t, 10_000_000)
