@@ -37,6 +37,7 @@ import torch
 from .native import native
 
 STAT_NAMES = ("kills", "deaths", "assists", "damage", "gold", "farm", "healing", "events")
+HOST_COUNTS_MAX = 1 << 16  # make_telemetry: per-match event counts on the host up to this many matches
 EVENT_TYPES = ("kill", "death", "assist", "damage", "gold", "farm", "heal", "other")
 
 
@@ -127,10 +128,21 @@ def make_telemetry(spec, rec: torch.Tensor, K: int, base: int = 0,
             raise ValueError("a telemetry source needs the api id of every match")
         return spec.for_batch(ids, K, rec.device)
     M = int(rec.shape[0])
-    counts = native().gen_event_counts(M, spec.seed, spec.min_events, spec.max_events, base, rec.device)
-    evoff = torch.zeros(M + 1, dtype=torch.int64, device=rec.device)
-    torch.cumsum(counts, 0, out=evoff[1:])
-    E = int(evoff[-1].item())
+    if rec.is_cuda and M <= HOST_COUNTS_MAX:
+        # a worker batch: the counts (counter RNG, same values as the device kernel) on
+        # the host, so sizing the events needs no device sync -- an .item() here would
+        # wait for every batch still in flight on the stream
+        counts = native().gen_event_counts(M, spec.seed, spec.min_events, spec.max_events, base,
+                                           torch.device("cpu"))
+        off = torch.zeros(M + 1, dtype=torch.int64)
+        torch.cumsum(counts, 0, out=off[1:])
+        E = int(off[-1])
+        evoff = off.pin_memory().to(rec.device, non_blocking=True)
+    else:
+        counts = native().gen_event_counts(M, spec.seed, spec.min_events, spec.max_events, base, rec.device)
+        evoff = torch.zeros(M + 1, dtype=torch.int64, device=rec.device)
+        torch.cumsum(counts, 0, out=evoff[1:])
+        E = int(evoff[-1].item())
     events = torch.empty((E, 2), dtype=torch.int32, device=rec.device)
     native().gen_events(rec, K, evoff, spec.seed, spec.min_events, spec.max_events, base, events)
     return Telemetry(evoff, events)

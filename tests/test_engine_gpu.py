@@ -675,3 +675,17 @@ def test_exact_dp_round_check_on_device(gpu_device):
     bad[M // 2:] = bad[M // 2]  # the second half collapses into one round
     plan = RoundPlan(bad, 4)
     assert check_rounds(rec, K, plan, P) == check_rounds(rec.cpu(), K, plan, P) >= 0
+
+
+def test_make_telemetry_host_counts_match_device(gpu_device, monkeypatch):
+    """Worker-sized batches size their synthetic events from host-side counts (no
+    device sync); the events equal the device-counted path bit for bit."""
+    from analyzer_amd.ops import telemetry as T
+
+    K, P, M = 3, 5000, 1500
+    rec = make_stream(StreamSpec(team_size=K, seed=41), M, P, K=K, device=gpu_device)
+    spec = T.TelemetrySpec(seed=9, min_events=20, max_events=60)
+    a = T.make_telemetry(spec, rec, K, base=1234)
+    monkeypatch.setattr(T, "HOST_COUNTS_MAX", 0)
+    b = T.make_telemetry(spec, rec, K, base=1234)
+    assert torch.equal(a.evoff, b.evoff) and torch.equal(a.events, b.events)
