@@ -189,6 +189,12 @@ def main(argv=None) -> int:
     backend = EngineConfig.from_env().dist_backend
     ngpu = torch.cuda.device_count()
     local = local % ngpu if backend != "nccl" and ngpu else local
+    if backend != "nccl" and ngpu and world > ngpu and not os.environ.get("ANA_RATE_BLOCKS"):
+        # ranks sharing a card: size each persistent grid to its share of the card, so
+        # every rank's launch is resident at once (full 512-block grids from 4-8
+        # processes get time-sliced and trip the executor's 5-s no-progress watchdog;
+        # profiles/r3/dp_gloo_rehearsals_k_default.log)
+        os.environ["ANA_RATE_BLOCKS"] = str(max(16, 512 // -(-world // ngpu)))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
