@@ -295,8 +295,10 @@ class BatchRater:
         """Rate every match of ``rec`` in order, updating ``roster`` in place.
 
         ``telemetry`` = (evoff [M+1] int64, events [E,2] int32, stats [M,2K,8] f32):
-        per-participant telemetry is aggregated into ``stats`` in the same launch
-        (K8 fused streaming mode: idle dataflow waves take telemetry tiles).
+        per-participant telemetry is aggregated into ``stats`` -- in the same launch
+        up to ``tele_fuse_max`` matches (K8 fused streaming mode: each lane group folds
+        the events of the match it rates), by the MFMA kernel right after it above
+        (``fuses``).
         ``progress`` = (signal address, launch number, chunk index): the tail
         signal of runtime/engine.py (device only).  ``epoch_dev``: a device int32
         tensor holding the launch epoch (graph replays, ops/graph.py), bumped by
