@@ -66,6 +66,7 @@ for task in "$@"; do
       ;;
     configs)
       run bench/config3 400 $PY bench.py --config 3 --steps 10 --warmup 2 --check
+      run bench/config4_auto 400 $PY bench.py --config 4 --steps 10 --warmup 2
       run bench/config4_fused 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode fused
       run bench/config4_separate 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode separate
       run bench/config5 400 $PY bench.py --config 5 --steps 10 --warmup 2 --check
