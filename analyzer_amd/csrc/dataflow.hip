@@ -54,6 +54,13 @@
 
 namespace ana {
 
+#ifndef ANA_LROW_PAD
+#define ANA_LROW_PAD 0
+#endif
+// extra floats per group's LDS output row (A/B: a stride of 32 floats puts the 8 groups'
+// same-column writes on one bank)
+constexpr int kLrowPad = ANA_LROW_PAD;
+
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight
 // K8 inline telemetry: events per match loaded with the batch's granules (more go
 // through a remainder loop after the rating); per group lane ceil(64 / G) 8-B loads
@@ -117,7 +124,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // (one store instruction writes the rows of every group: full lines, where
   // per-field stores sent 6-7 partial-line writes per match to the fabric)
   constexpr int OQ = (5 * S + 2 + 3) / 4;
-  __shared__ __attribute__((aligned(16))) float lrow[kWavesPerBlock][NG][4 * OQ];
+  __shared__ __attribute__((aligned(16))) float lrow[kWavesPerBlock][NG][4 * OQ + kLrowPad];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int j = lane % G;
