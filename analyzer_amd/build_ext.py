@@ -68,7 +68,7 @@ def _compile(cmd, src: Path, obj: Path, force: bool) -> str:
 
 
 def build(force: bool = False, jobs: int = 4, verbose: bool = False, diag: bool = False,
-          variant: str = "", defines=()) -> Path:
+          variant: str = "", defines=(), hip_flags=()) -> Path:
     out = target_path(diag, variant)
     out.parent.mkdir(parents=True, exist_ok=True)
     objdir = BUILD / ("variant_" + variant) if variant else BUILD / "diag" if diag else BUILD
@@ -90,7 +90,7 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False, diag: bool 
             continue
         obj = objdir / (name + ".o")
         cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC",
-               "-I" + str(CSRC)] + HIP_FLAGS.get(name, []) + dflags + ["-c", str(src), "-o", str(obj)]
+               "-I" + str(CSRC)] + HIP_FLAGS.get(name, []) + dflags + list(hip_flags) + ["-c", str(src), "-o", str(obj)]
         tasks.append((cmd, src, obj))
         objs.append(obj)
     for name in CPP_SOURCES:
@@ -136,8 +136,10 @@ def main(argv=None) -> int:
     ap.add_argument("--variant", default="",
                     help="experiment build: ab/<VARIANT>_C.so with --define flags (in-call A/B, gpu.sh ab)")
     ap.add_argument("--define", action="append", default=[], help="extra -D for the device code")
+    ap.add_argument("--hip-flag", action="append", default=[],
+                    help="extra hipcc flag for the HIP sources (experiment builds)")
     args = ap.parse_args(argv)
-    path = build(force=args.force, jobs=args.jobs, verbose=True, diag=args.diag, variant=args.variant,
+    path = build(force=args.force, jobs=args.jobs, verbose=True, diag=args.diag, variant=args.variant, hip_flags=args.hip_flag,
                  defines=args.define)
     print(path)
     return 0

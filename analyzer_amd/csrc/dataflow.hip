@@ -54,6 +54,11 @@
 
 namespace ana {
 
+#ifdef ANA_WAVES_PER_EU  // A/B: occupancy hint (min, max waves per SIMD) for register use / scheduling
+#define ANA_EXEC_ATTR __attribute__((amdgpu_waves_per_eu(ANA_WAVES_PER_EU)))
+#else
+#define ANA_EXEC_ATTR
+#endif
 #ifndef ANA_LROW_PAD
 #define ANA_LROW_PAD 0
 #endif
@@ -91,7 +96,7 @@ struct Batch {
 // (ANA_RATE_DIAG=1) -- every wave clocks its iterations and its wait with
 // s_memrealtime and adds them to ctrl[20..27] at exit (launch_rate).
 template <int K, int G, int TELE, bool DIAG>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) ANA_EXEC_ATTR
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
                      float* __restrict__ first_prior, float* __restrict__ orows, int64_t orow,
