@@ -132,6 +132,18 @@ def parse(argv=None):
     return args
 
 
+def shared_card_blocks(world: int, ngpu: int, backend: str) -> int:
+    """Executor grid for ranks that share a card (gloo rehearsals with more ranks than
+    GPUs): each rank's persistent grid is sized to its share of the 512 blocks, so every
+    rank's launch is resident at once -- full grids from 4-8 processes get time-sliced
+    and trip the executor's 5-s no-progress watchdog
+    (profiles/r3/dp_gloo_rehearsals_k_default.log).  0 = one rank per GPU (the default
+    grid)."""
+    if backend == "nccl" or not ngpu or world <= ngpu:
+        return 0
+    return max(16, 512 // -(-world // ngpu))
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -189,12 +201,9 @@ def main(argv=None) -> int:
     backend = EngineConfig.from_env().dist_backend
     ngpu = torch.cuda.device_count()
     local = local % ngpu if backend != "nccl" and ngpu else local
-    if backend != "nccl" and ngpu and world > ngpu and not os.environ.get("ANA_RATE_BLOCKS"):
-        # ranks sharing a card: size each persistent grid to its share of the card, so
-        # every rank's launch is resident at once (full 512-block grids from 4-8
-        # processes get time-sliced and trip the executor's 5-s no-progress watchdog;
-        # profiles/r3/dp_gloo_rehearsals_k_default.log)
-        os.environ["ANA_RATE_BLOCKS"] = str(max(16, 512 // -(-world // ngpu)))
+    blocks = shared_card_blocks(world, ngpu, backend)
+    if blocks and not os.environ.get("ANA_RATE_BLOCKS"):
+        os.environ["ANA_RATE_BLOCKS"] = str(blocks)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:

@@ -75,3 +75,15 @@ def test_merges_per_step_default_is_accuracy_bounded(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "4")
     assert bench.parse([]).merges_per_step == 4
     assert bench.parse([]).accuracy == 1
+
+
+def test_shared_card_blocks():
+    """Ranks sharing a card (gloo rehearsal) split the executor grid; one rank per GPU
+    (RCCL, or world <= GPUs) keeps the default."""
+    assert bench.shared_card_blocks(8, 8, "nccl") == 0
+    assert bench.shared_card_blocks(8, 1, "nccl") == 0
+    assert bench.shared_card_blocks(2, 2, "gloo") == 0
+    assert bench.shared_card_blocks(2, 1, "gloo") == 256
+    assert bench.shared_card_blocks(8, 1, "gloo") == 64
+    assert bench.shared_card_blocks(6, 2, "gloo") == 170
+    assert bench.shared_card_blocks(64, 1, "gloo") == 16
