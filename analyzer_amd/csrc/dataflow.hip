@@ -54,18 +54,6 @@
 
 namespace ana {
 
-#ifdef ANA_WAVES_PER_EU  // A/B: occupancy hint (min, max waves per SIMD) for register use / scheduling
-#define ANA_EXEC_ATTR __attribute__((amdgpu_waves_per_eu(ANA_WAVES_PER_EU)))
-#else
-#define ANA_EXEC_ATTR
-#endif
-#ifndef ANA_LROW_PAD
-#define ANA_LROW_PAD 0
-#endif
-// extra floats per group's LDS output row (A/B: a stride of 32 floats puts the 8 groups'
-// same-column writes on one bank)
-constexpr int kLrowPad = ANA_LROW_PAD;
-
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight
 // K8 inline telemetry: events per match loaded with the batch's granules (more go
 // through a remainder loop after the rating); per group lane ceil(64 / G) 8-B loads
@@ -96,7 +84,7 @@ struct Batch {
 // (ANA_RATE_DIAG=1) -- every wave clocks its iterations and its wait with
 // s_memrealtime and adds them to ctrl[20..27] at exit (launch_rate).
 template <int K, int G, int TELE, bool DIAG>
-__global__ void __launch_bounds__(256) ANA_EXEC_ATTR
+__global__ void __launch_bounds__(256)
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
                      float* __restrict__ first_prior, float* __restrict__ orows, int64_t orow,
@@ -129,7 +117,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // (one store instruction writes the rows of every group: full lines, where
   // per-field stores sent 6-7 partial-line writes per match to the fabric)
   constexpr int OQ = (5 * S + 2 + 3) / 4;
-  __shared__ __attribute__((aligned(16))) float lrow[kWavesPerBlock][NG][4 * OQ + kLrowPad];
+  __shared__ __attribute__((aligned(16))) float lrow[kWavesPerBlock][NG][4 * OQ];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int j = lane % G;

@@ -31,26 +31,6 @@ ANA_HD void vw_win(T t, T& v, T& w) {
     v = u + h;
     w = v * h;
   } else {
-#if defined(ANA_VW_FAST) && defined(__HIP_DEVICE_COMPILE__)
-    if constexpr (sizeof(T) == 4) {
-      // A/B: erfc(z) = tau exp(-z^2 + Q(tau)), tau = 1 / (1 + |z| / 2), relative
-      // error < 1.2e-7 for z >= 0 (the Chebyshev-fitted erfc).  For t <= 0 the
-      // Gaussian factors of pdf / cdf cancel: v = sqrt(2/pi) (1 + |z|/2) exp(-Q);
-      // for t > 0, cdf = 1 - erfc(|z|) / 2 >= 1/2 needs no such care.
-      const T z = fabsf(t) * (T)0.70710678118654752;
-      const T u = (T)1 + (T)0.5 * z;
-      const T tau = (T)1 / u;
-      const T q = (T)-1.26551223 + tau * ((T)1.00002368 + tau * ((T)0.37409196 + tau * ((T)0.09678418 +
-                  tau * ((T)-0.18628806 + tau * ((T)0.27886807 + tau * ((T)-1.13520398 +
-                  tau * ((T)1.48851587 + tau * ((T)-0.82215223 + tau * (T)0.17087277))))))));
-      const T vneg = (T)0.79788456080286536 * u * __expf(-q);
-      const T g = expf(-z * z);  // full-precision exp: its argument reaches -100
-      const T vpos = (T)0.39894228040143268 * g / ((T)1 - (T)0.5 * tau * g * __expf(q));
-      v = t <= (T)0 ? vneg : vpos;
-      w = v * (v + t);
-      return;
-    }
-#endif
     // cdf(t) >= 2.8e-7 here, so erfc keeps full relative precision and the
     // plain pdf/cdf ratio is as accurate as the erfcx form (which costs ~70
     // VGPRs in ocml); pdf underflow for t > 13 gives the exact v = w = 0 limit.
