@@ -46,6 +46,7 @@
 #include "dataflow_dev.h"
 #include "kernels.h"
 #include "rate_core.h"
+#include "rate_dev.h"
 #include "telemetry_dev.h"
 
 #ifndef ANA_HELD
@@ -597,36 +598,15 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       float nsm = NAN, nss = NAN, nmm = NAN, nms = NAN, dl = NAN, q = NAN;
       if (gst == kRated) {
         if constexpr (DIAG) d_p[1] = __builtin_amdgcn_s_memrealtime();
-        const float sgn = r0 ? 1.f : -1.f;
-        const float s_c2 = group_sum<G>(inr ? pss * pss + tau2 : 0.f, j, gbase);
-        const float s_d = group_sum<G>(inr ? sgn * pms : 0.f, j, gbase);
-        const float m_d = group_sum<G>(inr ? sgn * pmm : 0.f, j, gbase);
-        const float m_q = group_sum<G>(inr ? psm * psm : 0.f, j, gbase);
-        const int n = n0 + n1;
-        const float nb2 = (float)n * beta2;
-        const float m_c2 = m_q + (float)n * tau2;
-        q = quality_from_sums<float>(n, m_q, m_d, beta2);
-        UpdCoef<float> ks, km;
-        if constexpr (G == 8 || G == 16) {
-          // the two tracks' coefficients in the two halves of the group (one erfc/exp
-          // per lane instead of two), swapped across with a mirror DPP move
-          constexpr int kMirror = G == 8 ? 0x141 : 0x140;
-          const bool sh = j < G / 2;
-          const UpdCoef<float> k =
-              update_coef<float>(sh ? s_d : m_d, nb2 + (sh ? s_c2 : m_c2), rank0, rank1);
-          UpdCoef<float> o;
-          o.a0 = dpp_mov<kMirror>(k.a0);
-          o.a1 = dpp_mov<kMirror>(k.a1);
-          o.wf = dpp_mov<kMirror>(k.wf);
-          o.c2 = dpp_mov<kMirror>(k.c2);
-          ks = sh ? k : o;
-          km = sh ? o : k;
-        } else {
-          ks = update_coef<float>(s_d, nb2 + s_c2, rank0, rank1);
-          km = update_coef<float>(m_d, nb2 + m_c2, rank0, rank1);
-        }
-        apply_coef<float>(ks, r0, pms, pss, tau2, nsm, nss);
-        apply_coef<float>(km, r0, pmm, psm, tau2, nmm, nms);
+        // both tracks as one packed pair (rate_dev.h): roster sign times winner side
+        const float lsg = (r0 == (rank0 <= rank1)) ? 1.f : -1.f;
+        f2 nm2, ns2;
+        rate_pair<G>(f2{pms, pmm}, f2{pss, psm}, inr, lsg, n0 + n1, rank0 == rank1, beta2, tau2, j,
+                     gbase, nm2, ns2, q);
+        nsm = nm2.x;
+        nmm = nm2.y;
+        nss = ns2.x;
+        nms = ns2.y;
         const bool bad_num = inr && !(isfinite(nsm) && isfinite(nss) && isfinite(nmm) &&
                                       isfinite(nms) && isfinite(q));
         if ((__ballot(bad_num) & gmask) != 0ull) gst = kErrNumeric;

@@ -162,6 +162,8 @@ class _Cols:
 
 
 class ColumnarStore:
+    columnar_batches = True  # sessions build MatchBatch columns (load_batch / fetch_players)
+
     """The reference's tables as numpy columns (see the module doc)."""
 
     # a session writes only at commit and a batch's load reads match structure and

@@ -152,6 +152,14 @@ class ResidentRoster:
                 n += 1
         return n
 
+    def reset(self) -> None:
+        """Forget every cached player (RESIDENT=false on a columnar store: each batch
+        re-reads its players from the store, so other replicas' commits are seen).
+        The rows are reused from 0; the tensors stay where they are."""
+        self.rows.clear()
+        self.by_key[:] = -1
+        self.n = 0
+
     def _grow(self, need: int) -> None:
         cap = self.capacity
         while cap < need:

@@ -17,12 +17,26 @@ rater (ENGINE=native) rate them unchanged.
 Selected by ``STORE_BACKEND=sqlalchemy`` (with a sqlite URL), a
 ``sqlalchemy+<url>`` URI, or any URL scheme other than memory/columnar/sqlite
 (runtime/store.open_store).
+
+**Columnar batches (ENGINE=native).**  ``SqlAlchemySession.load_batch`` builds the
+worker's ``MatchBatch`` (runtime/columnar.py) from four SQLAlchemy Core SELECTs per
+batch -- matches ordered by ``created_at``, their rosters, their participants, the
+participants' item rows -- with no ORM object at all; ``fetch_players`` reads the
+stored ratings of the players the device roster has not seen; ``commit`` writes the
+batch back as ``executemany`` UPDATEs keyed by primary key (match quality,
+participant shared rating and delta, item ``any_afk`` + mode rating, the players'
+final tracks) plus the ``participant_stats`` rows of DOTELEMETRY.  Only Core
+constructs with bound parameters, so a MySQL URL takes the same statements.  Row
+order follows what the reference's relationship loaders see (no ORDER BY on the
+child tables: the database's order within a roster), so the columnar and the
+object paths rate the same team lists (tests/test_worker.py).
 """
 from __future__ import annotations
 
-from typing import Iterable, Iterator, List, Optional
+from typing import Dict, Iterable, Iterator, List, Optional
 
-from sqlalchemy import create_engine, insert, select, text
+import numpy as np
+from sqlalchemy import bindparam, create_engine, insert, select, text
 from sqlalchemy.ext.automap import automap_base
 from sqlalchemy.orm import relationship, selectinload, sessionmaker
 
@@ -32,6 +46,8 @@ from .store import (ITEM_WRITE_COLS, PARTICIPANT_WRITE_COLS, PLAYER_RATING_COLS,
                     _restore_match, _restore_player, _snap_match, _snap_player)
 
 class SqlAlchemyStore:
+    columnar_batches = True  # sessions build MatchBatch columns (load_batch / fetch_players)
+
     def __init__(self, uri: str, create_schema: bool = False):
         self.uri = uri
         kw = {"pool_recycle": 3600}
@@ -70,6 +86,21 @@ class SqlAlchemyStore:
         self.tables = Base.metadata.tables
         self.Session = sessionmaker(bind=self.engine, autoflush=False)
         self.commits = 0
+        # integer keys of player api ids (columnar batches, device-resident roster rows)
+        self.player_keys: Dict[str, int] = {}
+        self.player_names: List[str] = []
+        self._stmts: Dict[tuple, object] = {}
+
+    def update_stmt(self, table: str, cols: tuple, key: str = "api_id"):
+        """``UPDATE table SET cols WHERE key = :k_key`` with positional-free bound
+        names (5v5_* columns start with a digit), cached per column set."""
+        st = self._stmts.get((table, cols, key))
+        if st is None:
+            t = self.tables[table]
+            st = (t.update().where(t.c[key] == bindparam("k_key"))
+                  .values({c: bindparam("k%d" % i) for i, c in enumerate(cols)}))
+            self._stmts[(table, cols, key)] = st
+        return st
 
     # ------------------------------------------------------------- loading (synthetic data)
     def _insert(self, table: str, rows: List[dict]) -> None:
@@ -126,7 +157,187 @@ class SqlAlchemySession:
         self.db = store.Session()
         self._snaps = {}  # id(match) -> snapshot for rollback of the in-memory objects
         self._players = {}
+        self._batches: List = []  # columnar batches, written at commit
         self.closed = False
+
+    # ------------------------------------------------------------- columnar batches
+    def load_batch(self, ids: Iterable[str], chunksize: int = 100):
+        """The batch as columns (runtime/columnar.MatchBatch) from Core SELECTs:
+        no ORM objects, one statement per table and 500 keys."""
+        from .columnar import MODE_INDEX, UNSUPPORTED, MatchBatch, afk_mask
+
+        st = self.store
+        t = st.tables
+        Mt, Rt, Pt, It = t["match"], t["roster"], t["participant"], t["participant_items"]
+        conn = self.db.connection()
+        ids = list(set(ids))
+        heads: List[tuple] = []
+        for chunk in _chunks(ids, 500):
+            heads += conn.execute(select(Mt.c.api_id, Mt.c.game_mode, Mt.c.created_at)
+                                  .where(Mt.c.api_id.in_(chunk)).order_by(Mt.c.created_at.asc())).all()
+        if len(ids) > 500:  # merge the chunks as ORDER BY would (NULL first, as MySQL / SQLite)
+            heads.sort(key=lambda r: (r[2] is not None, r[2] if r[2] is not None else 0))
+        mids = [h[0] for h in heads]
+        pos = {m: i for i, m in enumerate(mids)}
+        rosters: List[List[tuple]] = [[] for _ in mids]
+        parts: Dict[str, List[tuple]] = {}
+        for chunk in _chunks(mids, 500):
+            for r in conn.execute(select(Rt.c.api_id, Rt.c.match_api_id, Rt.c.winner)
+                                  .where(Rt.c.match_api_id.in_(chunk))):
+                rosters[pos[r[1]]].append(r)
+            for p in conn.execute(select(Pt.c.api_id, Pt.c.roster_api_id, Pt.c.player_api_id, Pt.c.went_afk)
+                                  .where(Pt.c.match_api_id.in_(chunk))):
+                parts.setdefault(p[1], []).append(p)
+        pids = [p[0] for ps in parts.values() for p in ps]
+        item_of: Dict[str, object] = {}
+        for chunk in _chunks(pids, 500):
+            for it in conn.execute(select(It.c.api_id, It.c.participant_api_id)
+                                   .where(It.c.participant_api_id.in_(chunk))):
+                item_of.setdefault(it[1], it[0])  # participant_items[0]
+        M = len(mids)
+        nr = np.array([len(r) for r in rosters], dtype=np.int64)
+        n = np.zeros((M, 2), dtype=np.int64)
+        for i, rs in enumerate(rosters):
+            for ri in range(min(2, len(rs))):
+                n[i, ri] = len(parts.get(rs[ri][0], ()))
+        K = int(max(1, n.max() if M else 1))
+        player = np.full((M, 2, K), -1, dtype=np.int64)
+        part = np.full((M, 2, K), -1, dtype=np.int64)
+        afk = np.zeros((M, 2, K), dtype=bool)
+        winner = np.zeros((M, 2), dtype=bool)
+        keys, names = st.player_keys, st.player_names
+        pnames: List[str] = []
+        items: List[object] = []
+        extra: Dict[int, List[int]] = {}
+        afk23 = np.zeros(M, dtype=bool)
+        for i, rs in enumerate(rosters):
+            for ri, r in enumerate(rs):
+                ps = parts.get(r[0], ())
+                if ri >= 2:
+                    ext = extra.setdefault(i, [])
+                    for p in ps:
+                        ext.append(len(pnames))
+                        pnames.append(p[0])
+                        items.append(item_of.get(p[0]))
+                        afk23[i] |= p[3] == 1
+                    continue
+                winner[i, ri] = r[2] is not None and bool(r[2])
+                for k, p in enumerate(ps):
+                    k_ = keys.get(p[2])
+                    if k_ is None:
+                        k_ = keys[p[2]] = len(names)
+                        names.append(p[2])
+                    player[i, ri, k] = k_
+                    part[i, ri, k] = len(pnames)
+                    pnames.append(p[0])
+                    items.append(item_of.get(p[0]))
+                    afk[i, ri, k] = p[3] == 1
+        mask = afk_mask(n, afk[:, 0], afk[:, 1]) | np.where(afk23, np.int64(1) << 23, 0)
+        mode = np.array([MODE_INDEX.get(h[1], UNSUPPORTED) for h in heads], dtype=np.int64)
+        b = MatchBatch(ids=mids, mode=mode, nrosters=nr, n=n, winner=winner, afk=mask, player=player,
+                       part=part, player_names=pnames, extra_parts=extra)
+        b.item_keys = items
+        self._batches.append(b)
+        return b
+
+    def fetch_players(self, keys):
+        """Stored (ratings [n, 14], attributes [n, 3]) of integer player keys."""
+        Pl = self.store.tables["player"]
+        names = [self.store.player_names[int(k)] for k in keys]
+        cols = [Pl.c[c] for c in ("api_id", "rank_points_ranked", "rank_points_blitz", "skill_tier")
+                + PLAYER_RATING_COLS]
+        conn = self.db.connection()
+        got = {}
+        for chunk in _chunks(names, 500):
+            for row in conn.execute(select(*cols).where(Pl.c.api_id.in_(chunk))):
+                got[row[0]] = row[1:]
+        att = np.full((len(names), 3), np.nan)
+        rat = np.full((len(names), 14), np.nan)
+        for i, a in enumerate(names):
+            row = got.get(a)
+            if row is not None:
+                vals = np.array([np.nan if v is None else float(v) for v in row])
+                att[i], rat[i] = vals[:3], vals[3:]
+        return rat, att
+
+    def _write_batch(self, b) -> None:
+        """The batch's results as executemany UPDATEs keyed by primary key."""
+        from .columnar import AFK, INVALID, RATED, stats_mask
+
+        if b.status is None:
+            return
+        st = self.store
+        conn = self.db.connection()
+        stt = b.status
+        rated = stt == RATED
+        afkm = (stt == AFK) | (stt == INVALID)
+
+        def run(table, cols, rows, key="api_id"):
+            if rows:
+                conn.execute(st.update_stmt(table, cols, key),
+                             [dict(zip(["k%d" % i for i in range(len(cols))] + ["k_key"], r)) for r in rows])
+
+        run("match", ("trueskill_quality",),
+            [(float(b.quality[i]), b.ids[i]) for i in np.nonzero(rated)[0].tolist()] +
+            [(0.0, b.ids[i]) for i in np.nonzero(afkm)[0].tolist()])
+        items = b.item_keys
+        flag = []  # any_afk: every participant of AFK / invalid matches (all rosters)
+        for i in np.nonzero(afkm)[0].tolist():
+            for p in b.part[i][b.part[i] >= 0].tolist() + b.extra_parts.get(i, []):
+                flag.append((1, items[p]))
+        for i in np.nonzero(rated)[0].tolist():  # rosters beyond the second of rated matches
+            for p in b.extra_parts.get(i, []):
+                flag.append((0, items[p]))
+        run("participant_items", ("any_afk",), [f for f in flag if f[1] is not None])
+        sel = rated[:, None, None] & (b.part >= 0)
+        ps = b.part[sel].tolist()
+        names = b.player_names
+        run("participant", ("trueskill_mu", "trueskill_sigma", "trueskill_delta"),
+            [(a, s_, d, names[p]) for a, s_, d, p in zip(b.s_mu[sel].tolist(), b.s_sig[sel].tolist(),
+                                                            b.delta[sel].tolist(), ps)])
+        mode = np.broadcast_to(b.mode[:, None, None], b.part.shape)[sel].tolist()
+        by_mode: Dict[int, list] = {}
+        for md, a, s_, p in zip(mode, b.m_mu[sel].tolist(), b.m_sig[sel].tolist(), ps):
+            if items[p] is not None:  # any_afk = False and the mode rating at once
+                by_mode.setdefault(md, []).append((0, a, s_, items[p]))
+        for md, rows in by_mode.items():
+            col = TRACK_COLUMNS[1 + md]
+            run("participant_items", ("any_afk", col + "_mu", col + "_sigma"), rows)
+        if b.stats is not None:
+            self._write_stats(b, stats_mask(stt)[:, None, None] & (b.part >= 0))
+        if b.final_keys is not None and len(b.final_keys):
+            pn, f = st.player_names, b.final
+            groups: Dict[tuple, list] = {}  # one UPDATE per set of touched tracks
+            for u, k in enumerate(b.final_keys.tolist()):
+                tracks = tuple(np.nonzero(b.final_tracks[u])[0].tolist())
+                vals = []
+                for tr in tracks:
+                    mu, sg = f[u, 2 * tr], f[u, 2 * tr + 1]
+                    vals += [None if mu != mu else float(mu), None if sg != sg else float(sg)]
+                groups.setdefault(tracks, []).append(vals + [pn[int(k)]])
+            for tracks, rows in groups.items():
+                run("player", tuple(TRACK_COLUMNS[tr] + s for tr in tracks for s in ("_mu", "_sigma")), rows)
+
+    def _write_stats(self, b, sel) -> None:
+        """participant_stats rows (DOTELEMETRY): UPDATE the participants' existing
+        rows, INSERT the others keyed by the participant api id -- no dialect
+        specific upsert."""
+        St = self.store.tables["participant_stats"]
+        conn = self.db.connection()
+        names = b.player_names
+        vals = {names[p]: v for p, v in zip(b.part[sel].tolist(), b.stats[sel].tolist())}
+        have = set()
+        keys = list(vals)
+        for chunk in _chunks(keys, 500):
+            have.update(r[0] for r in conn.execute(select(St.c.participant_api_id)
+                                                   .where(St.c.participant_api_id.in_(chunk))))
+        upd = [list(vals[k]) + [k] for k in keys if k in have]
+        if upd:
+            conn.execute(self.store.update_stmt("participant_stats", STAT_COLUMNS, "participant_api_id"),
+                         [dict(zip(["k%d" % i for i in range(len(STAT_COLUMNS))] + ["k_key"], r)) for r in upd])
+        new = [dict(api_id=k, participant_api_id=k, **dict(zip(STAT_COLUMNS, vals[k]))) for k in keys if k not in have]
+        if new:
+            conn.execute(insert(St), new)
 
     def load_matches(self, ids: Iterable[str], chunksize: int = 100) -> Iterator:
         """The reference's batch query (worker.py:176-191), SQLAlchemy 2.0 spelling,
@@ -136,9 +347,10 @@ class SqlAlchemySession:
         participant items to lazy loading, so rating a match then issues one
         SELECT per item list, per deferred participant column group and per
         deferred player column (5v5 tracks, skill_tier): ~17 queries per 3v3
-        match, measured 99 matches/s on sqlite:///file with ENGINE=native
-        (profiles/r3/worker_stores.log).  Same rows and values, six queries per
-        chunk instead."""
+        match, measured 99 matches/s on sqlite:///file with ENGINE=native before
+        this eager loading (profiles/r3/worker_sqla_native.json).  Same rows and
+        values, six queries per chunk instead.  ENGINE=native takes ``load_batch``
+        (columns, no objects) instead of this path."""
         s = self.store
         M, R, P = s.Match, s.Roster, s.Participant
         q = (select(M).where(M.api_id.in_(list(set(ids)))).order_by(M.created_at.asc())
@@ -162,12 +374,16 @@ class SqlAlchemySession:
             _restore_player(pl, snap)
 
     def commit(self) -> None:
+        for b in self._batches:
+            self._write_batch(b)
+        self._batches.clear()
         self.db.commit()
         self.store.commits += 1
         self._snaps.clear()
         self._players.clear()
 
     def rollback(self) -> None:
+        self._batches.clear()
         self.db.rollback()
         for m, snap in self._snaps.values():
             _restore_match(m, snap)
@@ -194,6 +410,12 @@ class SqlAlchemySession:
     def __exit__(self, *exc):
         self.close()
         return False
+
+
+def _chunks(seq, n: int):
+    seq = list(seq)
+    for i in range(0, len(seq), n):
+        yield seq[i:i + n]
 
 
 __all__ = ["SqlAlchemyStore", "SqlAlchemySession", "PARTICIPANT_WRITE_COLS"]

@@ -63,6 +63,7 @@ SCHEMA = [
     "roster_api_id TEXT, player_api_id TEXT, skill_tier INTEGER, went_afk INTEGER, "
     "trueskill_mu REAL, trueskill_sigma REAL, trueskill_delta REAL)",
     "CREATE INDEX IF NOT EXISTS participant_match ON participant(match_api_id)",
+    "CREATE INDEX IF NOT EXISTS participant_roster ON participant(roster_api_id)",
     "CREATE TABLE IF NOT EXISTS participant_items (api_id TEXT PRIMARY KEY, "
     "participant_api_id TEXT, any_afk INTEGER, %s)" % ", ".join("%s REAL" % _q(c) for c in ITEM_RATING_COLS),
     "CREATE INDEX IF NOT EXISTS items_participant ON participant_items(participant_api_id)",
@@ -498,6 +499,8 @@ class SqliteSession(_SessionBase):
 
 
 class SqliteStore:
+    columnar_batches = True  # sessions build MatchBatch columns (load_batch / fetch_players)
+
     def __init__(self, path: str = ":memory:"):
         self.path = path
         self.conn = sqlite3.connect(path)

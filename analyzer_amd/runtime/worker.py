@@ -35,7 +35,8 @@ Deliberate, documented differences:
   a queue it never declares, which a broker silently drops);
 * ``DOTELEMETRY=true`` (with ``ENGINE=native``) aggregates per-event telemetry
   into ``participant_stats`` in the same launch as the rating (K8 fused mode,
-  BASELINE config 4).  The reference only forwards asset URLs
+  BASELINE config 4), on every store (on the reflected SQLAlchemy store through
+  its columnar batch path).  The reference only forwards asset URLs
   (worker.py:148-161); here ``TELEMETRY_SOURCE`` names an ANATEL01 file of the
   downloaded events keyed by match api id (ops/telemetry.TelemetrySource,
   ``python -m analyzer_amd.ops.telemetry convert`` builds one from JSON lines).
@@ -122,9 +123,12 @@ class Worker:
             # (no per-object work at all), the object graph for the Python engine
             uri = self.cfg.database_uri or ("columnar://" if self.cfg.engine == "native" else None)
             self.store = open_store(uri)
-        if self.cfg.dotelemetry and type(self.store).__name__ == "SqlAlchemyStore":
-            raise ValueError("DOTELEMETRY writes participant_stats through the memory, columnar and "
-                             "sqlite stores only")
+        if (self.cfg.dotelemetry and type(self.store).__name__ == "SqlAlchemyStore"
+                and not (self.cfg.engine == "native" and not self.cfg.skip_rated)):
+            # the reflected store's participant_stats are written by the columnar batch
+            # path (runtime/sqla.py load_batch / commit); its ORM relationships are read-only
+            raise ValueError("DOTELEMETRY on a SQLAlchemy store needs the columnar path "
+                             "(ENGINE=native, SKIP_RATED=false)")
         if self.rabbit is None:
             self.rabbit = B.connect(self.cfg.rabbitmq_uri, clock=self.clock)
         ch = self.rabbit.channel()
@@ -349,9 +353,11 @@ class Worker:
         quarantined: List[str] = []
         counts: Dict[str, int] = {}
         try:
-            if (self.cfg.engine == "native" and self.cfg.resident and not self.cfg.skip_rated
-                    and hasattr(session, "load_batch")):
-                # columnar path: no per-object work (runtime/columnar.py)
+            if self.cfg.engine == "native" and not self.cfg.skip_rated and hasattr(session, "load_batch"):
+                # columnar path: no per-object work (runtime/columnar.py); without
+                # RESIDENT the batch's players are all re-read from the store
+                if not self.cfg.resident:
+                    self._batched().resident.reset()
                 with trace_range("load", ids=len(ids)):
                     mb = session.load_batch(ids, self.cfg.chunksize)
                 with trace_range("rate", matches=len(mb), engine="native"):
@@ -422,7 +428,7 @@ class Worker:
         if self._object_rater is None:
             from ..ops.rate import BatchRater
 
-            if self.cfg.resident:
+            if self.cfg.resident or getattr(self.store, "columnar_batches", False):
                 from .resident import ResidentBatchRater
                 self._object_rater = ResidentBatchRater(BatchRater(self.rater_cfg),
                                                         capacity=self.cfg.batchsize)

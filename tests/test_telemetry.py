@@ -121,11 +121,12 @@ def _events_for(store, ids, seed=3):
     return out, want
 
 
-@pytest.mark.parametrize("uri", ["columnar://", "sqlite:///{tmp}/t.db"])
+@pytest.mark.parametrize("uri", ["columnar://", "sqlite:///{tmp}/t.db", "sqlalchemy+sqlite:///{tmp}/sa.db"])
 def test_worker_aggregates_events_from_a_telemetry_file(tmp_path, uri):
     """DOTELEMETRY with TELEMETRY_SOURCE: a real store (no SYNTHETIC_TELEMETRY)
     gets participant_stats aggregated from the events written to the file --
-    round trip file -> worker -> store, per participant."""
+    round trip file -> worker -> store, per participant; the reflected
+    SQLAlchemy store through its columnar batch path (runtime/sqla.py)."""
     _telemetry_file_roundtrip(tmp_path, uri)
 
 

@@ -370,6 +370,59 @@ def test_sqlalchemy_store_worker_matches_memory_store(tmp_path, engine):
     s.close()
 
 
+def _table_rows(store):
+    from sqlalchemy import text
+    out = {}
+    with store.engine.connect() as c:
+        for t in ("match", "participant", "participant_items", "player"):
+            out[t] = [tuple(r) for r in c.execute(text("SELECT * FROM %s ORDER BY api_id" % t))]
+    return out
+
+
+def test_sqlalchemy_columnar_path_writes_the_object_paths_rows(tmp_path, monkeypatch):
+    """ENGINE=native on the reflected store takes the columnar batch path (Core
+    SELECTs, executemany UPDATEs by primary key); it writes exactly the rows the
+    ORM object path writes -- every table, every column -- over a stream with
+    AFK, ties, uneven / invalid rosters, unsupported modes and a quarantined
+    (tier-30) player."""
+    from analyzer_amd.ops.synth import RosterSpec, StreamSpec
+    from analyzer_amd.runtime.sqla import SqlAlchemySession
+
+    stream = StreamSpec(team_size=3, seed=4, p_unsupported=0.1, p_uneven=0.1, p_bad_rosters=0.05,
+                        p_tie=0.1, p_afk=0.1)
+    roster = RosterSpec(num_players=25, seed=3, p_tier_bad=0.3, p_rated=0.3, p_rp_ranked=0.1, p_rp_blitz=0.05)
+    stores, workers = [], []
+    loads = []
+    orig = SqlAlchemySession.load_batch
+    monkeypatch.setattr(SqlAlchemySession, "load_batch",
+                        lambda self, *a, **k: loads.append(1) or orig(self, *a, **k))
+    for name, columnar in (("col.db", True), ("obj.db", False)):
+        store = _sqla(tmp_path, name)
+        clock = B.ManualClock()
+        if not columnar:  # the ORM object path: sessions without the columnar interface
+            monkeypatch.delattr(SqlAlchemySession, "load_batch")
+        cfg = WorkerConfig(batchsize=16, chunksize=3, idle_timeout=1.0, engine="native", resident=False)
+        ms = populate(store, 80, 25, team_size=3, seed=3, stream=stream, roster=roster)
+        w = Worker(cfg, store=store, broker=B.MemoryBroker(clock), rater_cfg=RaterConfig(), clock=clock)
+        w.connect()
+        publish(w.channel, "analyze", [m.api_id for m in ms])
+        w.start_consuming()
+        stores.append(store)
+        workers.append(w)
+        if columnar:
+            assert loads, "the columnar path was not taken"
+            n_loads = len(loads)
+    assert len(loads) == n_loads  # the object path never builds columnar batches
+    a, b = workers
+    assert a.stats.acked == b.stats.acked and a.stats.quarantined == b.stats.quarantined > 0
+    assert a.failed_ids == b.failed_ids
+    ra, rb = _table_rows(stores[0]), _table_rows(stores[1])
+    for t in ra:
+        assert len(ra[t]) == len(rb[t]) > 0, t
+        for x, y in zip(ra[t], rb[t]):
+            assert x == y, (t, x, y)
+
+
 def test_sqlalchemy_store_rollback_and_quarantine(tmp_path):
     store = _sqla(tmp_path)
     w, ms, _ = make_worker(n=8, batch=8, quarantine=False, store=store)
