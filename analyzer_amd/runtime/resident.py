@@ -102,8 +102,8 @@ class ResidentRoster:
         if base + k > self.capacity:
             self._grow(base + k)
         dev = buf.to(self.device, non_blocking=True)
-        self.roster.state[base:base + k].copy_(dev[:, :32])
-        self.roster.attrs[base:base + k].copy_(dev[:, 32:])
+        _copy_rows(self.roster.state[base:base + k], dev[:, :32])
+        _copy_rows(self.roster.attrs[base:base + k], dev[:, 32:])
         self.n = base + k
 
     def _upload_arrays(self, vals: np.ndarray, attrs: np.ndarray) -> None:
@@ -278,7 +278,7 @@ class ResidentBatchRater:
         rec = encode(matches, row_of, K).to(self.device, non_blocking=True)
         roster = self.resident.roster
         idx = torch.tensor(rows, dtype=torch.int64).to(self.device, non_blocking=True)
-        self._undo = (idx, roster.state.index_select(0, idx)) if rows else None
+        self._undo = (idx, _gather_rows(roster.state, idx)) if rows else None
         stats = None
         if telemetry is not None:
             from ..ops.telemetry import allocate_stats, make_telemetry
@@ -289,7 +289,7 @@ class ResidentBatchRater:
             g = self._graph(K, len(matches)) if self.use_graphs else None
             res = g.rate(rec) if g is not None else self._eager(rec, K, None)
         packed = res.packed.cpu().numpy() if res.packed is not None else None
-        final = roster.state.index_select(0, idx).cpu().numpy() if rows else None
+        final = _gather_rows(roster.state, idx).cpu().numpy() if rows else None
         st = self._write_back(matches, res, packed, K, row_of, final, rows)
         if stats is not None:
             _write_stats(matches, stats, K, st)
@@ -348,7 +348,7 @@ class ResidentBatchRater:
             rec_t = rec_c.to(self.device, non_blocking=True)
             roster = res_.roster
             idx = rows_t.to(self.device, non_blocking=True)
-            undo = (idx, roster.state.index_select(0, idx)) if rows_t.numel() else None
+            undo = (idx, _gather_rows(roster.state, idx)) if rows_t.numel() else None
         self._undo = undo
         p = PendingBatch(batch, K, pos_t, uniq_t, undo=undo)
         if telemetry is not None:
@@ -363,7 +363,7 @@ class ResidentBatchRater:
         # outputs, the players' final rows and the error flags: asynchronous
         # copies into pinned buffers, one event to wait on
         p.packed = _to_host(res.packed)
-        p.final = _to_host(roster.state.index_select(0, idx)) if rows_t.numel() else None
+        p.final = _to_host(_gather_rows(roster.state, idx)) if rows_t.numel() else None
         if self.device.type == "cuda":
             p.flags = _to_host(self.rater.error_flags(self.device))
             if p.stats is not None:
@@ -423,7 +423,7 @@ class ResidentBatchRater:
             # no launch's epoch ever matches, as unpack_rows does
             saved = saved.clone()
             saved[:, 1::2] = 0.0
-            self.resident.roster.state.index_copy_(0, idx, saved)
+            _scatter_rows(self.resident.roster.state, idx, saved)
         if self._undo is undo:
             self._undo = None
 
@@ -503,6 +503,29 @@ class PendingBatch:
     def __init__(self, batch, K: int, pos=None, uniq=None, undo=None):
         self.batch, self.K, self.pos, self.uniq, self.undo = batch, K, pos, uniq, undo
         self.packed = self.final = self.flags = self.stats = self.event = None
+
+
+# Row gathers / scatters / copies of the roster.  On the CPU (the host mirror) they go
+# through numpy: torch's intra-op pool wakes every thread for a few thousand 128-B
+# rows, which measured 30-120 ms per call on an 8-core host against 0.1 ms in numpy.
+def _gather_rows(t: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    if t.device.type == "cpu":
+        return torch.from_numpy(t.numpy()[idx.numpy()])
+    return t.index_select(0, idx)
+
+
+def _scatter_rows(t: torch.Tensor, idx: torch.Tensor, rows: torch.Tensor) -> None:
+    if t.device.type == "cpu":
+        t.numpy()[idx.numpy()] = rows.numpy()
+    else:
+        t.index_copy_(0, idx, rows)
+
+
+def _copy_rows(dst: torch.Tensor, src: torch.Tensor) -> None:
+    if dst.device.type == "cpu" and src.device.type == "cpu":
+        dst.numpy()[...] = src.numpy()
+    else:
+        dst.copy_(src)
 
 
 def _to_host(src: torch.Tensor) -> torch.Tensor:

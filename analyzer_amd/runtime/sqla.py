@@ -36,7 +36,7 @@ from __future__ import annotations
 from typing import Dict, Iterable, Iterator, List, Optional
 
 import numpy as np
-from sqlalchemy import bindparam, create_engine, insert, select, text
+from sqlalchemy import bindparam, create_engine, event, insert, select, text
 from sqlalchemy.ext.automap import automap_base
 from sqlalchemy.orm import relationship, selectinload, sessionmaker
 
@@ -54,6 +54,15 @@ class SqlAlchemyStore:
         if not uri.startswith("sqlite"):
             kw["pool_size"] = 1  # worker.py:44
         self.engine = create_engine(uri, **kw)
+        if uri.startswith("sqlite") and ":memory:" not in uri and uri.rstrip("/") not in ("sqlite:", "sqlite:/"):
+            # a sqlite FILE gets the stdlib store's settings (runtime/store.SqliteStore):
+            # write-ahead log + NORMAL sync, every committed batch survives a process crash
+            @event.listens_for(self.engine, "connect")
+            def _sqlite_pragmas(dbapi_conn, _rec):
+                c = dbapi_conn.cursor()
+                c.execute("PRAGMA journal_mode=WAL")
+                c.execute("PRAGMA synchronous=NORMAL")
+                c.close()
         if create_schema:
             with self.engine.begin() as c:
                 for ddl in SCHEMA:
@@ -91,16 +100,24 @@ class SqlAlchemyStore:
         self.player_names: List[str] = []
         self._stmts: Dict[tuple, object] = {}
 
-    def update_stmt(self, table: str, cols: tuple, key: str = "api_id"):
-        """``UPDATE table SET cols WHERE key = :k_key`` with positional-free bound
-        names (5v5_* columns start with a digit), cached per column set."""
-        st = self._stmts.get((table, cols, key))
-        if st is None:
-            t = self.tables[table]
-            st = (t.update().where(t.c[key] == bindparam("k_key"))
-                  .values({c: bindparam("k%d" % i) for i, c in enumerate(cols)}))
-            self._stmts[(table, cols, key)] = st
-        return st
+    def sql(self, key: tuple, build, names: List[str]):
+        """A Core statement compiled once for this engine's dialect: (SQL text,
+        parameter order, bound names).  The columnar path runs it on the DBAPI
+        cursor, so the dialect's SQL and paramstyle come from SQLAlchemy without its
+        per-row parameter and result processing (two thirds of a batch's store
+        time through ``Connection.execute``)."""
+        c = self._stmts.get(key)
+        if c is None:
+            comp = build().compile(dialect=self.engine.dialect)
+            if self.engine.dialect.positional:
+                at = {n: i for i, n in enumerate(names)}
+                order = [at[n] for n in comp.positiontup]
+                order = None if order == list(range(len(names))) else order
+                c = (comp.string, "positional", order, names)
+            else:
+                c = (comp.string, "named", None, names)
+            self._stmts[key] = c
+        return c
 
     # ------------------------------------------------------------- loading (synthetic data)
     def _insert(self, table: str, rows: List[dict]) -> None:
@@ -161,39 +178,55 @@ class SqlAlchemySession:
         self.closed = False
 
     # ------------------------------------------------------------- columnar batches
+    def _cursor(self):
+        """A DBAPI cursor on the session's connection (the session's transaction)."""
+        return self.db.connection().connection.dbapi_connection.cursor()
+
+    def _select_in(self, cur, table: str, cols: tuple, key: str, values: List, order_by=None) -> List[tuple]:
+        """``SELECT cols FROM table WHERE key IN (values)``, 500 bound values per
+        statement (one compiled statement per chunk length)."""
+        out: List[tuple] = []
+        for chunk in _chunks(sorted(values), 500):  # key order: neighbouring index pages
+            n = len(chunk)
+
+            def build(n=n):
+                t = self.store.tables[table]
+                q = select(*[t.c[c] for c in cols]).where(t.c[key].in_([bindparam("i%d" % k) for k in range(n)]))
+                return q.order_by(t.c[order_by].asc()) if order_by else q
+            c = self.store.sql(("in", table, cols, key, order_by, n), build, ["i%d" % k for k in range(n)])
+            _execute(cur, c, [chunk])
+            out += cur.fetchall()
+        return out
+
     def load_batch(self, ids: Iterable[str], chunksize: int = 100):
-        """The batch as columns (runtime/columnar.MatchBatch) from Core SELECTs:
-        no ORM objects, one statement per table and 500 keys."""
+        """The batch as columns (runtime/columnar.MatchBatch) from four SELECTs per
+        500 keys: no ORM objects, no per-row SQLAlchemy processing."""
         from .columnar import MODE_INDEX, UNSUPPORTED, MatchBatch, afk_mask
 
         st = self.store
-        t = st.tables
-        Mt, Rt, Pt, It = t["match"], t["roster"], t["participant"], t["participant_items"]
-        conn = self.db.connection()
+        cur = self._cursor()
         ids = list(set(ids))
-        heads: List[tuple] = []
-        for chunk in _chunks(ids, 500):
-            heads += conn.execute(select(Mt.c.api_id, Mt.c.game_mode, Mt.c.created_at)
-                                  .where(Mt.c.api_id.in_(chunk)).order_by(Mt.c.created_at.asc())).all()
+        heads = self._select_in(cur, "match", ("api_id", "game_mode", "created_at"), "api_id", ids,
+                                order_by="created_at")
         if len(ids) > 500:  # merge the chunks as ORDER BY would (NULL first, as MySQL / SQLite)
             heads.sort(key=lambda r: (r[2] is not None, r[2] if r[2] is not None else 0))
         mids = [h[0] for h in heads]
         pos = {m: i for i, m in enumerate(mids)}
         rosters: List[List[tuple]] = [[] for _ in mids]
+        # no ORDER BY on the child tables: the database's order, as the reference's
+        # relationship loaders see it (worker.py:176-191)
+        for r in self._select_in(cur, "roster", ("api_id", "match_api_id", "winner"), "match_api_id", mids):
+            rosters[pos[r[1]]].append(r)
         parts: Dict[str, List[tuple]] = {}
-        for chunk in _chunks(mids, 500):
-            for r in conn.execute(select(Rt.c.api_id, Rt.c.match_api_id, Rt.c.winner)
-                                  .where(Rt.c.match_api_id.in_(chunk))):
-                rosters[pos[r[1]]].append(r)
-            for p in conn.execute(select(Pt.c.api_id, Pt.c.roster_api_id, Pt.c.player_api_id, Pt.c.went_afk)
-                                  .where(Pt.c.match_api_id.in_(chunk))):
-                parts.setdefault(p[1], []).append(p)
+        for p in self._select_in(cur, "participant", ("api_id", "roster_api_id", "player_api_id", "went_afk"),
+                                 "match_api_id", mids):
+            parts.setdefault(p[1], []).append(p)
         pids = [p[0] for ps in parts.values() for p in ps]
         item_of: Dict[str, object] = {}
-        for chunk in _chunks(pids, 500):
-            for it in conn.execute(select(It.c.api_id, It.c.participant_api_id)
-                                   .where(It.c.participant_api_id.in_(chunk))):
-                item_of.setdefault(it[1], it[0])  # participant_items[0]
+        for it in self._select_in(cur, "participant_items", ("api_id", "participant_api_id"),
+                                  "participant_api_id", pids):
+            item_of.setdefault(it[1], it[0])  # participant_items[0]
+        cur.close()
         M = len(mids)
         nr = np.array([len(r) for r in rosters], dtype=np.int64)
         n = np.zeros((M, 2), dtype=np.int64)
@@ -242,23 +275,29 @@ class SqlAlchemySession:
 
     def fetch_players(self, keys):
         """Stored (ratings [n, 14], attributes [n, 3]) of integer player keys."""
-        Pl = self.store.tables["player"]
         names = [self.store.player_names[int(k)] for k in keys]
-        cols = [Pl.c[c] for c in ("api_id", "rank_points_ranked", "rank_points_blitz", "skill_tier")
-                + PLAYER_RATING_COLS]
-        conn = self.db.connection()
-        got = {}
-        for chunk in _chunks(names, 500):
-            for row in conn.execute(select(*cols).where(Pl.c.api_id.in_(chunk))):
-                got[row[0]] = row[1:]
-        att = np.full((len(names), 3), np.nan)
-        rat = np.full((len(names), 14), np.nan)
-        for i, a in enumerate(names):
-            row = got.get(a)
-            if row is not None:
-                vals = np.array([np.nan if v is None else float(v) for v in row])
-                att[i], rat[i] = vals[:3], vals[3:]
-        return rat, att
+        cols = ("api_id", "rank_points_ranked", "rank_points_blitz", "skill_tier") + PLAYER_RATING_COLS
+        cur = self._cursor()
+        got = {row[0]: row[1:] for row in self._select_in(cur, "player", cols, "api_id", names)}
+        cur.close()
+        nan = float("nan")
+        vals = np.array([[nan if v is None else v for v in got.get(a, (None,) * 17)] for a in names],
+                        dtype=np.float64).reshape(len(names), 17)
+        return vals[:, 3:], vals[:, :3]
+
+    def _update(self, cur, table: str, cols: tuple, rows: List[tuple], key: str = "api_id") -> None:
+        """executemany ``UPDATE table SET cols WHERE key = ?`` of (values..., key) rows."""
+        if not rows:
+            return
+        names = ["k%d" % i for i in range(len(cols))] + ["k_key"]
+
+        def build():
+            t = self.store.tables[table]
+            return (t.update().where(t.c[key] == bindparam("k_key"))
+                    .values({c: bindparam("k%d" % i) for i, c in enumerate(cols)}))
+        # in key order: consecutive rows touch neighbouring index pages
+        rows = sorted(rows, key=_last)
+        _execute(cur, self.store.sql(("upd", table, cols, key), build, names), rows, many=True)
 
     def _write_batch(self, b) -> None:
         """The batch's results as executemany UPDATEs keyed by primary key."""
@@ -267,34 +306,28 @@ class SqlAlchemySession:
         if b.status is None:
             return
         st = self.store
-        conn = self.db.connection()
+        cur = self._cursor()
         stt = b.status
         rated = stt == RATED
         afkm = (stt == AFK) | (stt == INVALID)
-
-        def run(table, cols, rows, key="api_id"):
-            if rows:
-                conn.execute(st.update_stmt(table, cols, key),
-                             [dict(zip(["k%d" % i for i in range(len(cols))] + ["k_key"], r)) for r in rows])
-
-        run("match", ("trueskill_quality",),
-            [(float(b.quality[i]), b.ids[i]) for i in np.nonzero(rated)[0].tolist()] +
-            [(0.0, b.ids[i]) for i in np.nonzero(afkm)[0].tolist()])
+        ri, ai = np.nonzero(rated)[0].tolist(), np.nonzero(afkm)[0].tolist()
+        self._update(cur, "match", ("trueskill_quality",),
+                     [(q, b.ids[i]) for i, q in zip(ri, b.quality[rated].tolist())] + [(0.0, b.ids[i]) for i in ai])
         items = b.item_keys
         flag = []  # any_afk: every participant of AFK / invalid matches (all rosters)
-        for i in np.nonzero(afkm)[0].tolist():
+        for i in ai:
             for p in b.part[i][b.part[i] >= 0].tolist() + b.extra_parts.get(i, []):
                 flag.append((1, items[p]))
-        for i in np.nonzero(rated)[0].tolist():  # rosters beyond the second of rated matches
+        for i in ri:  # rosters beyond the second of rated matches
             for p in b.extra_parts.get(i, []):
                 flag.append((0, items[p]))
-        run("participant_items", ("any_afk",), [f for f in flag if f[1] is not None])
+        self._update(cur, "participant_items", ("any_afk",), [f for f in flag if f[1] is not None])
         sel = rated[:, None, None] & (b.part >= 0)
         ps = b.part[sel].tolist()
         names = b.player_names
-        run("participant", ("trueskill_mu", "trueskill_sigma", "trueskill_delta"),
-            [(a, s_, d, names[p]) for a, s_, d, p in zip(b.s_mu[sel].tolist(), b.s_sig[sel].tolist(),
-                                                            b.delta[sel].tolist(), ps)])
+        self._update(cur, "participant", ("trueskill_mu", "trueskill_sigma", "trueskill_delta"),
+                     list(zip(b.s_mu[sel].tolist(), b.s_sig[sel].tolist(), b.delta[sel].tolist(),
+                              [names[p] for p in ps])))
         mode = np.broadcast_to(b.mode[:, None, None], b.part.shape)[sel].tolist()
         by_mode: Dict[int, list] = {}
         for md, a, s_, p in zip(mode, b.m_mu[sel].tolist(), b.m_sig[sel].tolist(), ps):
@@ -302,42 +335,43 @@ class SqlAlchemySession:
                 by_mode.setdefault(md, []).append((0, a, s_, items[p]))
         for md, rows in by_mode.items():
             col = TRACK_COLUMNS[1 + md]
-            run("participant_items", ("any_afk", col + "_mu", col + "_sigma"), rows)
+            self._update(cur, "participant_items", ("any_afk", col + "_mu", col + "_sigma"), rows)
         if b.stats is not None:
-            self._write_stats(b, stats_mask(stt)[:, None, None] & (b.part >= 0))
+            self._write_stats(cur, b, stats_mask(stt)[:, None, None] & (b.part >= 0))
         if b.final_keys is not None and len(b.final_keys):
-            pn, f = st.player_names, b.final
-            groups: Dict[tuple, list] = {}  # one UPDATE per set of touched tracks
-            for u, k in enumerate(b.final_keys.tolist()):
-                tracks = tuple(np.nonzero(b.final_tracks[u])[0].tolist())
-                vals = []
-                for tr in tracks:
-                    mu, sg = f[u, 2 * tr], f[u, 2 * tr + 1]
-                    vals += [None if mu != mu else float(mu), None if sg != sg else float(sg)]
-                groups.setdefault(tracks, []).append(vals + [pn[int(k)]])
-            for tracks, rows in groups.items():
-                run("player", tuple(TRACK_COLUMNS[tr] + s for tr in tracks for s in ("_mu", "_sigma")), rows)
+            pn = st.player_names
+            ft = np.asarray(b.final_tracks, dtype=bool)
+            code = ft.astype(np.int64).dot(np.int64(1) << np.arange(ft.shape[1], dtype=np.int64))
+            for c in np.unique(code).tolist():  # one UPDATE per set of touched tracks
+                u = np.nonzero(code == c)[0]
+                tracks = [t for t in range(ft.shape[1]) if (c >> t) & 1]
+                v = b.final[u][:, [x for t in tracks for x in (2 * t, 2 * t + 1)]]
+                vo = v.astype(object)
+                vo[np.isnan(v)] = None  # NULL
+                self._update(cur, "player", tuple(TRACK_COLUMNS[t] + s for t in tracks for s in ("_mu", "_sigma")),
+                             [tuple(r) + (pn[k],) for r, k in zip(vo.tolist(), b.final_keys[u].tolist())])
+        cur.close()
 
-    def _write_stats(self, b, sel) -> None:
+    def _write_stats(self, cur, b, sel) -> None:
         """participant_stats rows (DOTELEMETRY): UPDATE the participants' existing
         rows, INSERT the others keyed by the participant api id -- no dialect
         specific upsert."""
-        St = self.store.tables["participant_stats"]
-        conn = self.db.connection()
         names = b.player_names
         vals = {names[p]: v for p, v in zip(b.part[sel].tolist(), b.stats[sel].tolist())}
-        have = set()
         keys = list(vals)
-        for chunk in _chunks(keys, 500):
-            have.update(r[0] for r in conn.execute(select(St.c.participant_api_id)
-                                                   .where(St.c.participant_api_id.in_(chunk))))
-        upd = [list(vals[k]) + [k] for k in keys if k in have]
-        if upd:
-            conn.execute(self.store.update_stmt("participant_stats", STAT_COLUMNS, "participant_api_id"),
-                         [dict(zip(["k%d" % i for i in range(len(STAT_COLUMNS))] + ["k_key"], r)) for r in upd])
-        new = [dict(api_id=k, participant_api_id=k, **dict(zip(STAT_COLUMNS, vals[k]))) for k in keys if k not in have]
+        have = {r[0] for r in self._select_in(cur, "participant_stats", ("participant_api_id",),
+                                              "participant_api_id", keys)}
+        self._update(cur, "participant_stats", STAT_COLUMNS,
+                     [tuple(vals[k]) + (k,) for k in keys if k in have], key="participant_api_id")
+        new = [(k, k) + tuple(vals[k]) for k in keys if k not in have]
         if new:
-            conn.execute(insert(St), new)
+            cols = ("api_id", "participant_api_id") + STAT_COLUMNS
+            names_ = ["v%d" % i for i in range(len(cols))]
+
+            def build():
+                t = self.store.tables["participant_stats"]
+                return insert(t).values({c: bindparam(n) for c, n in zip(cols, names_)})
+            _execute(cur, self.store.sql(("ins", "participant_stats"), build, names_), new, many=True)
 
     def load_matches(self, ids: Iterable[str], chunksize: int = 100) -> Iterator:
         """The reference's batch query (worker.py:176-191), SQLAlchemy 2.0 spelling,
@@ -410,6 +444,25 @@ class SqlAlchemySession:
     def __exit__(self, *exc):
         self.close()
         return False
+
+
+def _last(row):
+    return row[-1]
+
+
+def _execute(cur, compiled, rows: List[tuple], many: bool = False) -> None:
+    """Run a ``SqlAlchemyStore.sql`` statement with tuple rows in bound-name order."""
+    text_, style, order, names = compiled
+    if style == "named":
+        params = [dict(zip(names, r)) for r in rows]
+    elif order is not None:
+        params = [tuple(r[i] for i in order) for r in rows]
+    else:
+        params = rows if isinstance(rows, list) else list(rows)
+    if many:
+        cur.executemany(text_, params)
+    else:
+        cur.execute(text_, params[0])
 
 
 def _chunks(seq, n: int):
