@@ -10,10 +10,14 @@ the repository snapshot to the GPU box and is what the tests load.
 from __future__ import annotations
 
 import argparse
+import hashlib
+import json
 import os
+import socket
 import subprocess
 import sys
 import sysconfig
+import time
 from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
@@ -67,6 +71,48 @@ def _compile(cmd, src: Path, obj: Path, force: bool) -> str:
     return "built %s" % src.name
 
 
+def _host_id() -> str:
+    """This machine: host name + kernel boot id (the image -- and with it
+    /etc/machine-id and often the host name -- is the same here and on a GPU box)."""
+    try:
+        boot = Path("/proc/sys/kernel/random/boot_id").read_text().strip()[:8]
+    except OSError:  # pragma: no cover
+        boot = "?"
+    return "%s/%s" % (socket.gethostname(), boot)
+
+
+def _hipcc_version() -> str:
+    try:
+        res = subprocess.run(["hipcc", "--version"], capture_output=True, text=True, timeout=120)
+        return " | ".join(ln.strip() for ln in res.stdout.splitlines() if "version" in ln.lower())
+    except Exception as e:  # pragma: no cover - no toolchain
+        return "unavailable: %s" % e
+
+
+def source_digest(dflags=(), hip_flags=()) -> str:
+    """sha256 over every source and header of the extension, the device flags and
+    this file (which holds the compile commands)."""
+    h = hashlib.sha256()
+    files = sorted(set(CSRC.glob("*.h")) | {CSRC / n for n in HIP_SOURCES + CPP_SOURCES} | {Path(__file__)})
+    for f in files:
+        if f.exists():
+            h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    h.update(repr((ARCH, sorted(HIP_FLAGS.items()), list(dflags), list(hip_flags))).encode())
+    return h.hexdigest()
+
+
+def stamp_path(out: Path) -> Path:
+    """``<library>.build.json``: what the library next to it was built from, where."""
+    return out.with_name(out.name.split(".")[0] + ".build.json")
+
+
+def read_stamp(out: Path) -> dict:
+    try:
+        return json.loads(stamp_path(out).read_text())
+    except (OSError, ValueError):
+        return {}
+
+
 def build(force: bool = False, jobs: int = 4, verbose: bool = False, diag: bool = False,
           variant: str = "", defines=(), hip_flags=()) -> Path:
     out = target_path(diag, variant)
@@ -74,12 +120,28 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False, diag: bool 
     objdir = BUILD / ("variant_" + variant) if variant else BUILD / "diag" if diag else BUILD
     dflags = (["-DANA_DIAG_BUILD=1"] if diag else []) + ["-D" + d for d in defines]
     sources = [CSRC / n for n in HIP_SOURCES + CPP_SOURCES if (CSRC / n).exists()]
-    if not force and out.exists() and out.stat().st_mtime >= max(_deps_mtime(s) for s in sources):
-        # the in-tree library is newer than every source: nothing to do (a GPU box
-        # that got the tree without build/ objects must not recompile it)
+    digest = source_digest(dflags, hip_flags)
+    hipcc = _hipcc_version()
+    stamp = read_stamp(out)
+    # provenance: the library is current only if its stamp names these exact sources,
+    # this compiler and THIS host -- a library that travelled from another machine (the
+    # container build on a GPU box) is rebuilt from source, so a box build proves the
+    # sources compile there
+    current = (out.exists() and stamp.get("sources_sha256") == digest and stamp.get("hipcc") == hipcc
+               and stamp.get("host") == _host_id())
+    if not force and current:
         if verbose:
-            print("up-to-date", out, flush=True)
+            print("up-to-date", out, "(stamp %s, built on %s)" % (digest[:12], stamp.get("host")), flush=True)
         return out
+    if not force and (not stamp or stamp.get("host") != _host_id() or stamp.get("hipcc") != hipcc):
+        force = True  # objects here may belong to another build: compile every source
+        if verbose:
+            print("stamp %s: rebuilding every source" % (
+                "missing" if not stamp else "from host %s" % stamp.get("host")
+                if stamp.get("host") != _host_id() else "of another hipcc"), flush=True)
+    elif not force and verbose:
+        print("sources changed since stamp %s: rebuilding what changed" % str(stamp.get("sources_sha256"))[:12],
+              flush=True)
     incs, libs = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     objs = []
@@ -118,6 +180,10 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False, diag: bool 
             raise RuntimeError("link failed:\n%s\n%s" % (res.stdout, res.stderr))
         if verbose:
             print("linked", out, flush=True)
+    stamp_path(out).write_text(json.dumps({
+        "library": out.name, "sources_sha256": digest, "hipcc": hipcc, "host": _host_id(),
+        "arch": ARCH, "sources": [s_.name for s_ in sources], "defines": dflags,
+        "built_at": time.strftime("%Y-%m-%dT%H:%M:%S%z")}, indent=1) + "\n")
     return out
 
 

@@ -300,10 +300,8 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
   const int64_t n = M * 2 * K;
   if (n > 0 && n <= kSmallSched && P < 0x7fffffffLL && K >= 1 && K <= 5) {
     const int e = n <= 2048 ? 2 : n <= 4096 ? 4 : 8;  // elements per thread
-    static const bool bitonic = [] {
-      const char* v = getenv("ANA_SCHED_SMALL");
-      return v && v[0] == 'b';
-    }();
+    const char* small_e = getenv("ANA_SCHED_SMALL");  // per schedule (A/B in one process)
+    const bool bitonic = small_e && small_e[0] == 'b';
     switch (K) {
 #define ANA_SMALL_CASE(k)                                                                            \
   case k:                                                                                            \

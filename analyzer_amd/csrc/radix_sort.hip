@@ -637,8 +637,12 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
   // ANA_SORT_RB=10: 10-bit digits (2 passes for <= 2^20 players instead of 3).  Measured
   // on MI355X, 10M 3v3 / 1M players: 3.11 ms vs 1.76 ms for 8-bit digits (1024
   // per-tile runs of ~4 elements scatter the pass's writes) -> off by default.
-  static const int rb_env = [] { const char* e = getenv("ANA_SORT_RB"); return e ? atoi(e) : 8; }();
-  static const bool nt = [] { const char* e = getenv("ANA_SORT_NT"); return e && atoi(e) != 0; }();
+  // read per schedule, like ANA_SCHED_RUNS / ANA_LINK_PARTS: A/B runs and tests switch
+  // them inside one process
+  const char* rb_e = getenv("ANA_SORT_RB");
+  const char* nt_e = getenv("ANA_SORT_NT");
+  const int rb_env = rb_e ? atoi(rb_e) : 8;
+  const bool nt = nt_e && atoi(nt_e) != 0;
   const bool wide = bits <= 20 && rb_env == 10;
   switch (K) {
 #define ANA_SORT_CASE(k)                                                                         \

@@ -108,16 +108,26 @@ class TelemetryFile {
     n_ = h.n;
     E_ = h.E;
     if (n_ < 0 || E_ < 0 || h.id_bytes < 0) fail("bad header");
-    const size_t need = sizeof(Header) + 2 * 8 * ((size_t)n_ + 1) + (size_t)h.id_bytes + 8 * (size_t)E_;
-    if (need > size_) fail("truncated");
+    // every header term is bounded by the file size before it is added, so a corrupt
+    // header cannot wrap the size check (the index arrays and events are mapped reads)
+    const size_t avail = size_ - sizeof(Header);
+    if ((uint64_t)n_ >= avail / 16) fail("truncated");  // two int64 arrays of n + 1
+    const size_t idx = 16 * ((size_t)n_ + 1);
+    if ((uint64_t)h.id_bytes > avail - idx) fail("truncated");
+    if ((uint64_t)E_ > (avail - idx - (size_t)h.id_bytes) / 8) fail("truncated");
     evoff_ = reinterpret_cast<const int64_t*>(base_ + sizeof(Header));
     const int64_t* id_off = evoff_ + n_ + 1;
     const char* ids = reinterpret_cast<const char*>(id_off + n_ + 1);
     events_ = reinterpret_cast<const int32_t*>(ids + h.id_bytes);
     if (evoff_[0] != 0 || evoff_[n_] != E_) fail("bad event offsets");
+    if (id_off[0] != 0) fail("bad index");
     map_.reserve(n_);
     for (int64_t i = 0; i < n_; ++i) {
-      if (evoff_[i] > evoff_[i + 1] || id_off[i] > id_off[i + 1] || id_off[i + 1] > h.id_bytes) fail("bad index");
+      // evoff_ runs 0 .. E_ and is non-decreasing, so every event range lies inside the
+      // file; id_off likewise inside the id bytes
+      if (evoff_[i] > evoff_[i + 1] || evoff_[i + 1] > E_ || id_off[i] > id_off[i + 1] ||
+          id_off[i + 1] > h.id_bytes)
+        fail("bad index");
       try {
         map_.add(std::string_view(ids + id_off[i], (size_t)(id_off[i + 1] - id_off[i])), i);
       } catch (const std::invalid_argument&) {

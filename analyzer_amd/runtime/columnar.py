@@ -204,7 +204,11 @@ class ColumnarStore:
             self._mkey = native().KeyIndex()
         k = len(self._mkey)
         if k < len(self.m_ids):
-            self._mkey.add(self.m_ids[k:], k)
+            try:
+                self._mkey.add(self.m_ids[k:], k)
+            except Exception:
+                self._mkey = None  # rebuilt from m_ids on the next lookup, never left short
+                raise
         return self._mkey.lookup(ids).numpy()
 
     # ------------------------------------------------------------- loading
@@ -284,6 +288,10 @@ class ColumnarStore:
         n0, n1, nr = (m0 >> 8) & 0xff, (m0 >> 16) & 0xff, (m0 >> 24) & 0xff
         afkm = (m1 >> 8) & 0xffffff
         mids = ["%s%d" % (prefix, base + i) for i in range(M)]
+        # reject duplicates before anything is written (add_matches does too): the
+        # native match index (match_rows) must stay in step with m_ids
+        if len(set(mids)) != M or any(a in self.m_index for a in mids):
+            raise ValueError("add_stream: a match api id is already stored (prefix %r, base %d)" % (prefix, base))
         # rosters: the first two carry players, any further ones are empty
         r_first = self.rosters.n + np.concatenate([[0], np.cumsum(nr)[:-1]])
         nparts = n0 + n1

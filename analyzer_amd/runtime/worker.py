@@ -289,6 +289,7 @@ class Worker:
             fl = _InFlight(batch, t0)
             fl.ids = batch.match_ids()
             self.stats.messages += len(batch)
+        undo_before = None
         try:
             if fl.session is None:
                 fl.session = self.store.session()
@@ -297,13 +298,22 @@ class Worker:
             # the telemetry seed of the serial worker: batches committed before this one
             seed_batches = self.stats.batches + (1 if self._inflight is not None else 0)
             self._inject_faults(fl.mb)
+            undo_before = getattr(self._batched(), "_undo", None)
             with trace_range("rate", matches=len(fl.mb), engine="native"):
                 fl.pending = self._batched().launch_batch(fl.mb, fl.session.fetch_players,
                                                           telemetry=self._telemetry_spec(seed_batches),
                                                           stage=getattr(fl.session, "stage_players", None))
         except Exception as e:
-            fl.session.rollback()
-            fl.session.close()
+            if fl.session is not None:
+                fl.session.rollback()
+                fl.session.close()
+            # a launch that failed after its undo snapshot (e.g. in the copies back)
+            # must not leave its updates in the device roster: the serial path's
+            # process() rolls them back the same way
+            rater = self._object_rater
+            undo = getattr(rater, "_undo", None)
+            if undo is not None and undo is not undo_before and hasattr(rater, "rollback"):
+                rater.rollback()  # this batch's snapshot, never the batch still in flight
             fl.error, fl.pending = e, None
         fl.seconds += time.perf_counter() - t0
         return fl

@@ -92,14 +92,21 @@ def test_schedule_matches_host(gpu_device, P, M, K):
     np.testing.assert_array_equal(need[rated], deps_h.numpy()[rated])
 
 
-@pytest.mark.parametrize("P,M,K,skew,runs", [(1_000_000, 400_000, 3, 3, "1"), (1_000_000, 400_000, 3, 1, "0"),
-                                             (1_000_000, 400_000, 3, 1, "1"), (5000, 300_000, 5, 2, "1")])
-def test_schedule_run_table_matches_host(gpu_device, P, M, K, skew, runs, monkeypatch):
+@pytest.mark.parametrize("P,M,K,skew,runs,rb", [(1_000_000, 400_000, 3, 3, "1", "8"),
+                                                (1_000_000, 400_000, 3, 1, "0", "8"),
+                                                (1_000_000, 400_000, 3, 1, "1", "8"),
+                                                (5000, 300_000, 5, 2, "1", "8"),
+                                                (5000, 300_000, 3, 2, "1", "10"),
+                                                (300_000, 400_000, 3, 1, "1", "10")])
+def test_schedule_run_table_matches_host(gpu_device, P, M, K, skew, runs, rb, monkeypatch):
     """The last sort pass with run ends in a [tile][digit] table (no digit offsets,
     sched_runs_fixup) and the round-2 path (ANA_SCHED_RUNS=0): the same links as the
     host, also on power-law streams where a hot player's runs span many tiles and a
-    sparse player's nearest earlier run lies tiles back."""
+    sparse player's nearest earlier run lies tiles back.  ANA_SORT_RB=10 (10-bit
+    digits, read per schedule): a small roster's single pass (<= 1024 digits) and a
+    two-pass one, both through the run table."""
     monkeypatch.setenv("ANA_SCHED_RUNS", runs)
+    monkeypatch.setenv("ANA_SORT_RB", rb)
     rec = make_stream(StreamSpec(team_size=K, seed=P + skew, skew=skew, p_afk=0.05), M, P, K=K)
     br = R.BatchRater()
     link_h, deps_h = (t.clone() for t in br.schedule(rec, K, P))
