@@ -349,6 +349,8 @@ def main(argv=None) -> int:
                     "spearman_mu_minus_sigma": sh.get("spearman_mu_minus_sigma"),
                     "sigma_ratio_p01_p99": [sh.get("sigma_ratio_p01"), sh.get("sigma_ratio_p99")],
                     "records_dmu_median": st.get("records_shared_mu", {}).get("dmu_median"),
+                    "records_dmu_p99": st.get("records_shared_mu", {}).get("dmu_p99"),
+                    "records_dmu_max": st.get("records_shared_mu", {}).get("dmu_max"),
                     "seconds": round(time.perf_counter() - t_acc, 2)}
     if world > 1:
         dist.barrier()  # the other ranks wait for rank 0's untimed accuracy pass

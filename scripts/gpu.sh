@@ -34,6 +34,9 @@
 #   telepmc    rocprofv3 counters of the standalone telemetry aggregation
 #   rerate     config 5 end to end: 1B matches / 10M players, checkpoint + kill + resume
 #   worker     streaming worker on the device (ENGINE=native), memory + sqlite stores
+#   workersql  the worker on the reflected SQLAlchemy store (columnar batch path), sqlite file
+#   dpacc      sweep-DP accuracy table (ranks x merges per step) incl. per-participant records
+#   dpcost     one-GPU DP step price: plain vs forced merges at k = 8 / 16
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -252,6 +255,29 @@ EOF
           IDLE_TIMEOUT=0.01 $PY worker.py --synthetic 20000
       # per-stage profiles (scripts/worker_profile.py): columnar serial x2 / pipelined, SQLite, SQLAlchemy
       run worker/profiles 900 bash scripts/worker_stores.sh
+      ;;
+    dpacc)  # sweep-DP accuracy incl. the per-participant records, (ranks x merges per step), 3v3 bench shape
+      run dpacc/table 900 $PY scripts/merges_vs_ranks.py ${DPACC_PAIRS:-2x2,4x4,4x8,8x8,8x16}
+      cat gpurun_out/dpacc/table.log
+      ;;
+    dpcost)  # one-GPU price of the DP step: plain vs forced merges at k = 8 / 16 (interleaved rounds)
+      for r in 1 2; do
+        run dpcost/plain_$r 300 $PY bench.py --steps 10 --warmup 2
+        for k in ${DPCOST_K:-8 16}; do
+          run dpcost/k${k}_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step $k
+        done
+      done
+      for f in gpurun_out/dpcost/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
+      ;;
+    workersql)  # the streaming worker on the reflected SQLAlchemy store (sqlite file), native engine
+      rm -f /tmp/wsa*.db*
+      run workersql/sqla_native 600 $PY scripts/worker_profile.py --synthetic 100000 --cprofile 0 \
+          --store "sqlalchemy+sqlite:////tmp/wsa1.db" --engine native
+      RESIDENT=true run workersql/sqla_native_resident 600 $PY scripts/worker_profile.py --synthetic 100000 \
+          --cprofile 0 --store "sqlalchemy+sqlite:////tmp/wsa2.db" --engine native
+      run workersql/sqlite_native 600 $PY scripts/worker_profile.py --synthetic 100000 --cprofile 0 \
+          --store "sqlite:////tmp/wsa3.db" --engine native
+      grep -h -o '"matches_per_s": [0-9.]*' gpurun_out/workersql/*.log
       ;;
     *) echo "unknown task $task"; exit 2 ;;
   esac
