@@ -42,8 +42,9 @@ __device__ __forceinline__ f2 exp2_2(f2 x) {
 //   t >  0:  v = phi D / (D - phi), D = a + h,  v + t = v + a
 // h is a rational function of s = a / (a + 4) times 1 / (a + 4): bounded on
 // [0, inf), decaying as 1/a, never overflowing.  Coefficients: least-squares fit of
-// relative error (scripts/fit_vw.py); fp32 evaluation vs fp64: relative error of v
-// and w <= 8e-7 wherever v > 1e-3 (max 4e-6 for t in (6, 15), where v < 1e-9).
+// relative error (scripts/fit_vw.py; tests/test_rate_dev_vw.py checks them against
+// 50-digit mpmath); fp32 evaluation vs fp64: relative error of v and w <= 8.4e-7 for
+// t < 4, 2.4e-6 for t in [4, 6) and 9e-6 for t in [6, 15), where v < 2e-5 / 1e-9.
 // A tie (equal ranks) takes the eps -> 0 draw limit v = -t, w = 1.
 __device__ __forceinline__ void vw_pair(f2 t, bool tie, f2& v, f2& w) {
   constexpr float kK = 4.f;

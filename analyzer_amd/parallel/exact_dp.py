@@ -1,5 +1,9 @@
 """Exact data-parallel rating by conflict-free rounds.
 
+A CORRECTNESS ORACLE, not a scaling mode: no bench / worker / re-rate path selects it.
+Depth x exchange latency bounds any exact multi-GPU mode above one GPU rating the
+window alone (docs/EXACT_MULTI_GPU.md: 7.26 s vs 3.8 ms on a 1M-match window).
+
 Exact chronological semantics (/root/reference/worker.py:176,191-192) allow
 parallelism only between matches that share no player.  The levelizer (K5: on
 the device a dataflow over the rating's own schedule, csrc/levels.hip; on the

@@ -108,6 +108,10 @@ class SweepMerger:
             mb = EngineConfig.from_env().merge_bucket_mb
             row_bytes = 16 * 4 if not self.scaled else 14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4
             bucket_rows = int(mb * (1 << 20)) // row_bytes if mb > 0 else self.P
+        if self.world <= 1:
+            # one rank (force): no collective to overlap, so one bucket -- two launches
+            # per merge instead of two per 16 MB
+            bucket_rows = self.P
         self.bucket_rows = max(1, min(int(bucket_rows), max(self.P, 1)))
         self.windows = 0
         self._synced = False   # start == the roster as the last merge left it
