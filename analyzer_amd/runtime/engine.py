@@ -62,7 +62,7 @@ class Prepared:
 class WindowPipeline:
     """Rate consecutive windows against one roster, prepass overlapped."""
 
-    def __init__(self, rater: BatchRater, roster: Roster, K: int, merger=None):
+    def __init__(self, rater: BatchRater, roster: Roster, K: int, merger=None, signal_at: float = 0.0):
         self.rater = rater
         self.roster = roster
         self.K = int(K)
@@ -76,8 +76,10 @@ class WindowPipeline:
         self.ecfg = EngineConfig.from_env()
         dp = merger is not None
         self.serial = self.serial_prepass(self.K, self.ecfg, dp)
-        # serial prepass: nothing to overlap, no tail signal
-        self.tail = 0.0 if self.serial else self.tail_point(self.K, self.ecfg, dp)
+        # serial prepass: nothing to overlap, no tail signal -- unless a caller wants the
+        # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail)
+        self.tail = (float(signal_at) if signal_at > 0 else 0.0) if self.serial else \
+            self.tail_point(self.K, self.ecfg, dp)
         self._signal = 0
         self._seq = 0
         self.side = self._side_stream() if self.cuda else None
@@ -132,6 +134,16 @@ class WindowPipeline:
             handle = native().cu_masked_stream(self.device.index or 0, n)
             return torch.cuda.ExternalStream(handle, device=self.device)
         return torch.cuda.Stream(self.device)
+
+    def wait_tail(self, stream) -> bool:
+        """Make ``stream`` wait until the last enqueued rating launch reached its tail
+        (the fraction ``self.tail`` of its chunks claimed); False without a signal."""
+        if not (self.cuda and self._signal and self._seq > 0):
+            return False
+        from ..ops.native import native
+
+        native().stream_wait_value64(stream.cuda_stream, self._signal, self._seq)
+        return True
 
     def prepare(self, rec: torch.Tensor,
                 produced: Optional[torch.cuda.Event] = None, stream=None) -> Prepared:

@@ -68,12 +68,15 @@ def parse(argv=None):
                     help="player activity: floor(u^skew * P); 1 = uniform (headline), 2 = quadratic, "
                          "3 = cubic (SURVEY H1: ~585k dependency levels per 10M window)")
     ap.add_argument("--events", default="20,60", help="config 4: min,max telemetry events per match")
-    ap.add_argument("--telemetry-mode", default="auto", choices=["auto", "overlap", "fused", "separate"],
+    ap.add_argument("--telemetry-mode", default="auto", choices=["auto", "overlap", "fused", "separate", "tail"],
                     help="config 4: auto = the rating launch takes the telemetry and fuses it up to "
                          "ANA_TELE_FUSE_MAX matches (worker batches), the MFMA kernel after it above "
                          "(10M windows; scripts/tele_batch.py); fused = always inline in the rating "
                          "groups; separate = the MFMA kernel after the rating on the same stream; "
-                         "overlap = the MFMA kernel co-runs with the rating on its own stream")
+                         "overlap = the MFMA kernel co-runs with the rating on its own stream; "
+                         "tail = the MFMA kernel of window i starts on its own stream once the rating of "
+                         "window i has claimed ANA_TELE_TAIL_AT (default 0.9) of its chunks, beside its "
+                         "drain and the next prepass, and the next rating waits for it")
     ap.add_argument("--comm-dtype", default=None, choices=["fp32", "fp16", "bf16"],
                     help="sweep-merge message precision (N > 1; default COMM_DTYPE, else bf16 for one "
                          "sweep -- at 8 x 10M the compressed messages leave the sweep error unchanged, "
@@ -241,12 +244,19 @@ def main(argv=None) -> int:
         n_events = sum(t.num_events for t in tele) / n_windows
     merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge)
               if world > 1 or args.force_merge else None)
-    pipe = WindowPipeline(rater, roster, K, merger=merger)
+    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or 0.9) if tele is not None and \
+        args.telemetry_mode == "tail" else 0.0
+    pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     torch.cuda.synchronize()
     prepared = {0: pipe.prepare(windows[0])}
 
     tstream = None
+    ttail = None
+    if tele is not None and args.telemetry_mode == "tail":
+        ttail = torch.cuda.Stream(dev)
+        if not pipe._signal:
+            raise SystemExit("--telemetry-mode tail needs hipStreamWaitValue64 on this device")
     if tele is not None and args.telemetry_mode == "overlap":
         # ANA_TELE_CUS=n: the co-running aggregation confined to n CUs (HIP CU mask),
         # so it takes bandwidth without slowing every executor wave
@@ -262,6 +272,21 @@ def main(argv=None) -> int:
         # rate window i, then the prepass of window i+1 on the side stream behind
         # its tail (every timed step carries exactly one prepass and one rating)
         nxt = windows[(i + 1) % n_windows]
+        if ttail is not None:
+            # the telemetry of window i beside the tail of its rating and the next
+            # prepass; rating i + 1 waits for it (no co-run with a full executor)
+            main = torch.cuda.current_stream(dev)
+            if i > 0:
+                main.wait_stream(ttail)
+            produced = torch.cuda.Event()
+            produced.record(main)
+            res_prep = pipe.step(prepared.pop(i), nxt, out=out)
+            ttail.wait_event(produced)
+            pipe.wait_tail(ttail)
+            with torch.cuda.stream(ttail):
+                aggregate(tele[i % n_windows], K, stats)
+            prepared[i + 1] = res_prep[1]
+            return
         if tstream is not None:
             # window i's telemetry co-runs with its rating; the step ends when both have
             main = torch.cuda.current_stream(dev)

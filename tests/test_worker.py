@@ -612,9 +612,30 @@ def test_python_fallback_forgets_resident_rows():
     assert again[0] == 3  # re-uploaded into a fresh row
 
 
-def _columnar_run(pipeline, quarantine=True, poison=True, fail_commit_at=None, **flags):
-    """The columnar native worker over 120 matches in batches of 16 (PIPELINE on/off)."""
+def _columnar_run(pipeline, quarantine=True, poison=True, fail_commit_at=None, fail_launch_at=None,
+                  monkeypatch=None, **flags):
+    """The columnar native worker over 120 matches in batches of 16 (PIPELINE on/off).
+    ``fail_launch_at``: the launch of that batch raises after its undo snapshot was
+    taken (in the copies back)."""
     import numpy as np
+
+    if fail_launch_at is not None:
+        from analyzer_amd.runtime import resident
+
+        real_launch = resident.ResidentBatchRater.launch_batch
+        calls = [0]
+
+        def launch(self, *a, **k):
+            calls[0] += 1
+            if calls[0] == fail_launch_at:
+                real_to_host = resident._to_host
+
+                def boom(src):
+                    resident._to_host = real_to_host
+                    raise RuntimeError("injected copy-back failure")
+                resident._to_host = boom
+            return real_launch(self, *a, **k)
+        monkeypatch.setattr(resident.ResidentBatchRater, "launch_batch", launch)
 
     from analyzer_amd.runtime.columnar import ColumnarSession, ColumnarStore
     from analyzer_amd.runtime.source import populate
@@ -649,16 +670,17 @@ def _columnar_run(pipeline, quarantine=True, poison=True, fail_commit_at=None, *
 
 
 @pytest.mark.parametrize("case", [dict(), dict(quarantine=False), dict(fail_commit_at=(3, 5)),
-                                  dict(poison=False, dotelemetry=True, telemetry_events="3,7")])
-def test_pipelined_worker_is_the_serial_worker(case):
+                                  dict(poison=False, dotelemetry=True, telemetry_events="3,7"),
+                                  dict(fail_launch_at=3)])
+def test_pipelined_worker_is_the_serial_worker(case, monkeypatch):
     """Two batches in flight give bit-identical store contents, failed queue and
     counters to the one-batch-at-a-time worker -- including whole-batch failures
     (QUARANTINE=false, a failing commit), where the later batch is rolled back on
     the device and launched again."""
     import numpy as np
 
-    ws, ss, fs = _columnar_run(False, **case)
-    wp, sp, fp = _columnar_run(True, **case)
+    ws, ss, fs = _columnar_run(False, monkeypatch=monkeypatch, **case)
+    wp, sp, fp = _columnar_run(True, monkeypatch=monkeypatch, **case)
     assert fp == fs
     for k in ("batches", "failed_batches", "messages", "matches", "quarantined", "acked", "nacked"):
         assert getattr(wp.stats, k) == getattr(ws.stats, k), k
@@ -667,5 +689,5 @@ def test_pipelined_worker_is_the_serial_worker(case):
                       ("players", ("rating",))):
         for c in cols:
             assert np.array_equal(getattr(getattr(sp, tab), c), getattr(getattr(ss, tab), c), equal_nan=True), (tab, c)
-    if case.get("quarantine") is False or case.get("fail_commit_at"):
+    if case.get("quarantine") is False or case.get("fail_commit_at") or case.get("fail_launch_at"):
         assert ws.stats.failed_batches > 0
