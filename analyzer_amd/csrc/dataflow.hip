@@ -56,6 +56,10 @@
 namespace ana {
 
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight
+#ifndef ANA_EARLY_NOTIFY
+#define ANA_EARLY_NOTIFY 0
+#endif
+constexpr bool kEarlyNotify = ANA_EARLY_NOTIFY != 0;
 // K8 inline telemetry: events per match loaded with the batch's granules (more go
 // through a remainder loop after the rating); per group lane ceil(64 / G) 8-B loads
 constexpr int kTeleInline = 64;
@@ -481,6 +485,30 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     v2u tev_next[TT];
     int32_t tn_m = -1, tn_cnt = 0;
     int64_t tn_off = 0;
+    // release the successor of a published player: an LDS count when this wave holds
+    // it (assigned next iteration), else its global completion counter.  The
+    // successor verifies the granule tags, so no store wait precedes the notify.
+    auto notify = [&](uint32_t succ) {
+      if (succ == kNoMatch) return;
+      int lh = -1;
+      int32_t lcb = 0;
+      if (local_ok) {
+#pragma unroll
+        for (int h = 0; h < kH; ++h)
+          if (cbase[h] >= 0 && (int32_t)succ >= cbase[h] && (int32_t)succ < cbase[h] + cl) {
+            lh = h;
+            lcb = cbase[h];
+          }
+      }
+      if (lh >= 0) {  // held by this wave: release it through LDS, next iteration
+        atomicAdd(reinterpret_cast<uint32_t*>(&lloc[wv][(int32_t)succ - lcb]) + lh, 1u);
+      } else {
+        __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const uint64_t lb = __ballot(lh >= 0);
+      n_local += (uint32_t)__popcll(lb);
+      n_global += (uint32_t)__popcll(__ballot(true) & ~lb);
+    };
     auto rate_batch = [&](const Batch& bt) {
     int my_h = bt.my_h;
     const int my_bit = bt.my_bit;
@@ -531,6 +559,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         pend[h] |= uniform64(back);
       }
       if (gstale) my_h = -1;
+    }
+    if constexpr (kEarlyNotify) {
+      // early notify (experiment): the successors learn of this match before it is
+      // rated; a reader that arrives before the publish sees the old tags and retries
+      if (my_h >= 0 && inr && islast) notify(lk0 & kMatchMask);
     }
     if constexpr (INL) {
       // K8 inline, software-pipelined: this group's events are LOADED now (HBM, cold)
@@ -634,27 +667,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         __builtin_amdgcn_raw_buffer_store_b128(
             ok ? granule(nsm, stag, nss, succ) : granule(rsmu, stag, rssg, succ),
             rs, off, 0, 16);
-        if (succ != kNoMatch) {  // the successor verifies the tags, so no store wait
-          int lh = -1;
-          int32_t lcb = 0;
-          if (local_ok) {
-#pragma unroll
-            for (int h = 0; h < kH; ++h)
-              if (cbase[h] >= 0 && (int32_t)succ >= cbase[h] && (int32_t)succ < cbase[h] + cl) {
-                lh = h;
-                lcb = cbase[h];
-              }
-          }
-          if (lh >= 0) {  // held by this wave: release it through LDS, next iteration
-            atomicAdd(reinterpret_cast<uint32_t*>(&lloc[wv][(int32_t)succ - lcb]) + lh, 1u);
-          } else {
-            __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-          }
-          const uint64_t lb = __ballot(lh >= 0);
-          n_local += (uint32_t)__popcll(lb);
-          n_global += (uint32_t)__popcll(__ballot(true) & ~lb);
-        }
+        if (!kEarlyNotify) notify(lk0 & kMatchMask);
       }
       if constexpr (DIAG) d_p[3] = __builtin_amdgcn_s_memrealtime();
       if (ok && prm.record_first_prior && own) {
@@ -721,6 +734,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
 
     // ---------------------------------------------- (9) install the staged chunk
+    int64_t early_m = -1;   // a staged match with an early status: its row, after the rating
+    uint8_t early_est = kRated;
     if (staging >= 0) {
       int64_t cb = 0;
 #pragma unroll
@@ -763,11 +778,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           hcnt[h] = stcnt;
         }
       reinterpret_cast<uint32_t*>(&lloc[wv][lane])[staging] = 0u;
-      if (mm < M && est != kRated && !tonly) {  // no state, no dependencies: finish it now
-#pragma unroll
-        for (int q = 0; q < 5 * S; ++q) orows[mm * orow + q] = NAN;
-        orows[mm * orow + 5 * S] = (est == kAfk || est == kInvalidRosters) ? 0.f : NAN;
-        reinterpret_cast<uint8_t*>(orows + mm * orow + 5 * S + 1)[0] = est;
+      // no state, no dependencies: its output row is written after this iteration's
+      // rating (early_row), so the rating's waits never include these stores
+      if (mm < M && est != kRated && !tonly) {
+        early_m = mm;
+        early_est = est;
       }
       const uint64_t pm = __ballot(mm < M && (est == kRated || tonly));
 #pragma unroll
@@ -782,6 +797,21 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
 
     if constexpr (DIAG) d_p[0] = d_p[1] = d_p[2] = d_p[3] = d_w1;
     rate_batch(nb);
+    if (early_m >= 0) {  // the staged chunk's early-status matches: one full-line row each
+      typedef float v4f __attribute__((ext_vector_type(4)));
+      const float qv = (early_est == kAfk || early_est == kInvalidRosters) ? 0.f : NAN;
+      v4f* dst = reinterpret_cast<v4f*>(orows + early_m * orow);
+#pragma unroll
+      for (int q = 0; q < OQ; ++q) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int pos = 4 * q + i;
+          v[i] = pos < 5 * S ? NAN : pos == 5 * S ? qv : pos == 5 * S + 1 ? __uint_as_float((uint32_t)early_est) : 0.f;
+        }
+        __builtin_nontemporal_store(v4f{v[0], v[1], v[2], v[3]}, dst + q);
+      }
+    }
     if constexpr (INL) {  // fold the previous batch's events, then hand this batch's on
       tele_flush();
 #pragma unroll

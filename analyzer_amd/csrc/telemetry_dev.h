@@ -167,6 +167,12 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   for (int i = lane; i < kTeleRelOffset / 16; i += 64)  // both operand sets start zero
     reinterpret_cast<uint4*>(lds)[i] = make_uint4(0, 0, 0, 0);
   tele_lds_fence();
+  // B^T row 0 (the count column) is 1.0 for EVERY event position, kept for the whole
+  // span: an event outside the rows (malformed, past the span) has an all-zero A
+  // column, so only attributed events count -- no store + undo of it per event
+  if (lane < 2 * kTeleChunk)
+    tele_st16(lds + (lane >> 5) * kTeleSetBytes + kTeleBOffset + 2 * (lane & 31), kOne);
+  tele_lds_fence();
   auto bound = [&](int j) { return __builtin_amdgcn_readlane(roff, j); };
   const int ne = __builtin_amdgcn_readfirstlane(bound(nm));
   const int t = lane & 31, half = lane >> 5;
@@ -271,8 +277,7 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
     uint8_t* bcol = mine_set + kTeleBOffset + 2 * t;
     uint8_t* arow = mine_set + lr * kTeleRowBytes + 2 * t;
     const bool in_a = ok && lr < kTeleARows;
-    if (ok) {
-      tele_st16(bcol, kOne);  // column 0: count
+    if (ok) {  // (column 0, the count, is a constant 1.0 row: see above)
       if (col >= 0) {
         tele_st16(bcol + col * kTeleRowBytes, p0);
         if (col >= 4) {
@@ -293,7 +298,6 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
     }
     tele_lds_fence();
     if (ok) {
-      tele_st16(bcol, 0);
       if (col >= 0) {
         tele_st16(bcol + col * kTeleRowBytes, 0);
         if (col >= 4) {
