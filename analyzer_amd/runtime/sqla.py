@@ -62,6 +62,8 @@ class SqlAlchemyStore:
                 c = dbapi_conn.cursor()
                 c.execute("PRAGMA journal_mode=WAL")
                 c.execute("PRAGMA synchronous=NORMAL")
+                c.execute("PRAGMA cache_size=-262144")  # 256 MB of page cache (default 8 MB)
+                c.execute("PRAGMA mmap_size=1073741824")
                 c.close()
         if create_schema:
             with self.engine.begin() as c:
