@@ -552,6 +552,66 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
                         s.data_ptr<float>(), p2, true, vst.data_ptr<float>(), (float)unknown_sigma, P);
 }
 
+// lagged merge boundary (parallel/sweep.py lag): c, y base rows [P, 16] (in/out), s the
+// roster [P, 32] (in/out), buf [P, 16] fp32: the summed messages in (has_sum), this
+// rank's message out
+void sweep_lag(Tensor c, Tensor buf, Tensor y, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma,
+               bool scaled, bool has_sum) {
+  const auto dev = s.device();
+  const int64_t P = s.size(0);
+  check_rows(c, "c (base rows)", P, ana::kBaseFloats, dev);
+  check_rows(buf, "buf", P, 16, dev);
+  check_rows(y, "y (base rows)", P, ana::kBaseFloats, dev);
+  check_rows(s, "state", P, ana::kRowFloats, dev);
+  check_rows(attrs, "attrs", P, 4, dev);
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_sweep_lag(c.data_ptr<float>(), buf.data_ptr<float>(), y.data_ptr<float>(),
+                                    s.data_ptr<float>(), attrs.data_ptr<float>(), vst.data_ptr<float>(),
+                                    (float)unknown_sigma, scaled ? 1 : 0, has_sum ? 1 : 0, P, stream_of(s)),
+              "sweep_lag");
+    return;
+  }
+  ana::host_sweep_lag(c.data_ptr<float>(), buf.data_ptr<float>(), y.data_ptr<float>(), s.data_ptr<float>(),
+                      attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, scaled, has_sum, P);
+}
+
+// the same over compressed operands msg [P, 14] bf16/fp16 + cnt [P, 2] int32 (scaled);
+// the CPU path goes through the fp32 host mirror and torch's conversions
+void sweep_lag_packed(Tensor c, Tensor msg, Tensor cnt, Tensor y, Tensor s, Tensor attrs, Tensor vst,
+                      double unknown_sigma, bool has_sum) {
+  const auto dev = s.device();
+  const int64_t P = s.size(0);
+  check_rows(c, "c (base rows)", P, ana::kBaseFloats, dev);
+  TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
+                  msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
+              "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
+  check_rows(cnt, "cnt", P, 2, dev, torch::kInt32);
+  check_rows(y, "y (base rows)", P, ana::kBaseFloats, dev);
+  check_rows(s, "state", P, ana::kRowFloats, dev);
+  check_rows(attrs, "attrs", P, 4, dev);
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_sweep_lag_packed(c.data_ptr<float>(), msg.data_ptr(), cnt.data_ptr<int32_t>(),
+                                           msg.scalar_type() == torch::kBFloat16 ? 1 : 0, y.data_ptr<float>(),
+                                           s.data_ptr<float>(), attrs.data_ptr<float>(), vst.data_ptr<float>(),
+                                           (float)unknown_sigma, has_sum ? 1 : 0, P, stream_of(s)),
+              "sweep_lag_packed");
+    return;
+  }
+  Tensor buf = torch::zeros({P, 16}, s.options());
+  if (has_sum) {
+    buf.slice(1, 0, 14).copy_(msg);
+    buf.slice(1, 14, 16).copy_(cnt);
+  }
+  ana::host_sweep_lag(c.data_ptr<float>(), buf.data_ptr<float>(), y.data_ptr<float>(), s.data_ptr<float>(),
+                      attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, true, has_sum, P);
+  msg.copy_(buf.slice(1, 0, 14));
+  cnt.copy_(buf.slice(1, 14, 16));
+}
+
 // ------------------------------------------------------------- C2 exchange
 // rec: the rank's slice of one round [m, 2K+2]; status: its per-match status
 // (any row stride); out: [cap, 33] float entries, cap >= m * 2K
@@ -740,6 +800,18 @@ void epoch_bump(Tensor e) {
   check_hip(ana::launch_epoch_bump(e.data_ptr<int32_t>(), stream_of(e)), "epoch_bump");
 }
 
+void warm_rows(Tensor state, Tensor sink) {
+  const auto dev = state.device();
+  check(state, "state", torch::kFloat32, dev);
+  check(sink, "sink", torch::kInt32, dev);
+  TORCH_CHECK(state.dim() == 2 && state.size(1) == ana::kRowFloats, "state must be [P, 32]");
+  TORCH_CHECK(sink.numel() >= 256, "sink needs 256 words");
+  if (!dev.is_cuda()) return;  // nothing to warm on the host
+  check_hip(ana::launch_warm_rows(state.data_ptr<float>(), state.size(0),
+                                  reinterpret_cast<uint32_t*>(sink.data_ptr<int32_t>()), stream_of(state)),
+            "warm_rows");
+}
+
 void reset_tags(Tensor state) {
   const auto dev = state.device();
   check(state, "state", torch::kFloat32, dev);
@@ -778,6 +850,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sweep_apply", &sweep_apply, "K9: decode summed messages against the common start (-> s, s2)");
   m.def("sweep_delta_packed", &sweep_delta_packed, "K9: messages straight into bf16/fp16 + int32 all-reduce operands");
   m.def("sweep_apply_packed", &sweep_apply_packed, "K9: decode bf16/fp16 + int32 summed messages (-> s, s2)");
+  m.def("sweep_lag", &sweep_lag, "K9: one-window-late merge boundary (fp32 operands)");
+  m.def("sweep_lag_packed", &sweep_lag_packed, "K9: one-window-late merge boundary (bf16/fp16 + int32 operands)");
   m.def("pack_rows", &pack_rows, "C2: changed rows of a round slice -> fixed-capacity [cap, 33] entries");
   m.def("check_round", &check_round, "C2 race detector: one round's matches share no player (flag |= 1)");
   m.def("unpack_rows", &unpack_rows, "C2: write gathered entries (id >= 0) into the roster, tags zeroed");
@@ -799,6 +873,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stream_wait_value64", &stream_wait_value64, "hipStreamWaitValue64(stream, ptr, >= value)");
   m.def("can_wait_value", &can_wait_value, "hipDeviceAttributeCanUseStreamWaitValue");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
+  m.def("warm_rows", &warm_rows, "read every roster row once (cache warm-up before a rating launch)");
   m.def("epoch_bump", &epoch_bump, "device launch epoch += 1 (graph replays)");
   m.attr("ROW_FLOATS") = ana::kRowFloats;
   m.attr("N_TRACKS") = ana::kTracks;

@@ -255,4 +255,11 @@ void host_sweep_apply(const float* s0, const float* buf, const float* attrs, flo
   }
 }
 
+void host_sweep_lag(float* c, float* buf, float* y, float* x, const float* attrs, const float* vst,
+                    float unknown_sigma, bool scaled, bool has_sum, int64_t P) {
+  for (int64_t p = 0; p < P; ++p)
+    sweep_lag_player(c + p * kBaseFloats, has_sum ? buf + p * 16 : nullptr, y + p * kBaseFloats,
+                     x + p * kRowFloats, attrs + p * 4, vst, unknown_sigma, scaled, buf + p * 16);
+}
+
 }  // namespace ana

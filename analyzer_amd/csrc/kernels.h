@@ -16,6 +16,9 @@ int launch_gen_roster(const GenRosterParams& g, float* state, float* attrs, hipS
 int launch_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M, hipStream_t s);
 
 int launch_reset_tags(float* state, int64_t P, hipStream_t s);
+// read every roster row once (Infinity Cache warm-up in front of a rating launch);
+// sink: >= 256 words, written only under a condition that is never true in practice
+int launch_warm_rows(const float* state, int64_t P, uint32_t* sink, hipStream_t s);
 // e[0] += 1 on the stream (the device epoch of graph replays, RateParams::epoch_ptr)
 int launch_epoch_bump(int32_t* e, hipStream_t s);
 
@@ -89,6 +92,13 @@ int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, c
 int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
                               const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
                               int64_t P, hipStream_t st);
+// lagged merge boundary (sweep_core.h sweep_lag_player): c: common base rows (in/out),
+// buf / msg+cnt: summed messages in (has_sum) and this rank's message out, y: base rows
+// of the rank's window start (in/out), x: roster rows (in/out)
+int launch_sweep_lag(float* c, float* buf, float* y, float* x, const float* attrs, const float* vst,
+                     float unknown_sigma, int scaled, int has_sum, int64_t P, hipStream_t st);
+int launch_sweep_lag_packed(float* c, void* msg, int32_t* cnt, int bf16, float* y, float* x, const float* attrs,
+                            const float* vst, float unknown_sigma, int has_sum, int64_t P, hipStream_t st);
 // C2 exact-DP exchange (sweep.hip): fixed-capacity [cap][33] entries of changed rows
 int launch_pack_rows(const int32_t* rec, int K, int64_t m, const uint8_t* status, int64_t sstride,
                      const float* state, float* out, int64_t cap, hipStream_t st);

@@ -96,6 +96,32 @@ int launch_reset_tags(float* state, int64_t P, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Read every roster row once, so the rating launch behind it finds them in the
+// Infinity Cache instead of HBM (the prepass in front of it streams several
+// hundred MB through that cache).  The loads feed an xor whose only use is a
+// store under a condition the host makes false (`never`), so they stay.
+__global__ void __launch_bounds__(256) warm_rows_kernel(const uint4* __restrict__ rows, int64_t n,
+                                                        uint32_t never, uint32_t* __restrict__ sink) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint4 v = rows[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == never) sink[threadIdx.x] = acc;
+}
+
+int launch_warm_rows(const float* state, int64_t P, uint32_t* sink, hipStream_t s) {
+  const int64_t n = P * kGranules;
+  if (n <= 0) return 0;
+  // 8 granules per thread at 1M players: 1024 workgroups, 4 per CU
+  const int64_t want = (n + 256 * 8 - 1) / (256 * 8);
+  const unsigned blocks = (unsigned)(want < 1 ? 1 : (want > 4096 ? 4096 : want));
+  hipLaunchKernelGGL(warm_rows_kernel, dim3(blocks), dim3(256), 0, s,
+                     reinterpret_cast<const uint4*>(state), n, 0x5a5a5a5au, sink);
+  return (int)hipGetLastError();
+}
+
 // Device-side launch epoch of a captured graph: one bump per replay, before the
 // rate launch that reads it (the host resets the tags and the counter before 255).
 __global__ void epoch_bump_kernel(int32_t* e) { e[0] += 1; }

@@ -89,6 +89,7 @@ class WindowPipeline:
         # between the all-reduce launch and the decode on the main stream
         self.merge_side = torch.cuda.Stream(self.device) if self.cuda and self.serial else None
         self._rated: Optional[torch.cuda.Event] = None  # the last rating launch finished
+        self._warm_sink: Optional[torch.Tensor] = None  # ANA_ROSTER_WARM scratch word block
         # ANA_PREPASS_EXCLUSIVE (with ANA_PREPASS_CUS=n): the rating launches go to a
         # stream masked to the other CUs, so the two never share a CU
         self.exec_stream = None
@@ -145,6 +146,17 @@ class WindowPipeline:
         native().stream_wait_value64(stream.cuda_stream, self._signal, self._seq)
         return True
 
+    def _warm(self) -> None:
+        """``ANA_ROSTER_WARM``: read the roster rows once on the main stream, behind the
+        prepass that streamed the window's sort through the Infinity Cache, so the
+        executor's first gathers of each player hit that cache (scripts/tune_rate.py
+        --touch measured the effect, profiles/r4/touch_warm_roster.log)."""
+        from ..ops.native import native
+
+        if self._warm_sink is None:
+            self._warm_sink = torch.zeros(256, dtype=torch.int32, device=self.device)
+        native().warm_rows(self.roster.state, self._warm_sink)
+
     def prepare(self, rec: torch.Tensor,
                 produced: Optional[torch.cuda.Event] = None, stream=None) -> Prepared:
         """Enqueue the schedule prepass of ``rec`` on the side stream (or ``stream``),
@@ -191,6 +203,8 @@ class WindowPipeline:
             cl = self.rater.chunk_len(M, self.rater.tiles(telemetry, M))
             at = int(self.tail * ((M + cl - 1) // cl))
             progress = (self._signal, self._seq, at)
+        if self.ecfg.roster_warm and self.cuda:
+            self._warm()
         with trace_range("rate", window=self.windows_rated, matches=int(prep.rec.shape[0])):
             if self.exec_stream is not None:
                 self.exec_stream.wait_stream(main)
@@ -247,6 +261,13 @@ class WindowPipeline:
         nxt = self.prepare(next_rec, produced=produced) if next_rec is not None else None
         return res, nxt
 
+    def finish(self) -> None:
+        """End of a run of windows: a lagged DP merge applies its last summed messages
+        (parallel/sweep.py ``flush``), so every rank holds the common roster."""
+        if self.merger is not None and getattr(self.merger, "lag", False):
+            with trace_range("flush", window=self.windows_rated):
+                self.merger.flush(self.roster)
+
     def run(self, windows: Iterable[torch.Tensor], out: Optional[RateResult] = None,
             on_result: Optional[Callable[[int, RateResult], None]] = None) -> int:
         """Rate every window in order; the prepass of window i+1 overlaps window i."""
@@ -266,4 +287,5 @@ class WindowPipeline:
             if on_result is not None:
                 on_result(n, res)
             n += 1
+        self.finish()
         return n

@@ -70,8 +70,8 @@ def parse(argv=None):
     ap.add_argument("--events", default="20,60", help="config 4: min,max telemetry events per match")
     ap.add_argument("--telemetry-mode", default="auto", choices=["auto", "overlap", "fused", "separate", "tail"],
                     help="config 4: auto = the rating launch takes the telemetry and fuses it up to "
-                         "ANA_TELE_FUSE_MAX matches (worker batches), the MFMA kernel after it above "
-                         "(10M windows; scripts/tele_batch.py); fused = always inline in the rating "
+                         "ANA_TELE_FUSE_MAX matches (worker batches; scripts/tele_batch.py), above that "
+                         "(10M windows) the MFMA kernel as in tail, from 0.8; fused = always inline in the rating "
                          "groups; separate = the MFMA kernel after the rating on the same stream; "
                          "overlap = the MFMA kernel co-runs with the rating on its own stream; "
                          "tail = the MFMA kernel of window i starts on its own stream once the rating of "
@@ -101,6 +101,11 @@ def parse(argv=None):
     ap.add_argument("--force-merge", action="store_true",
                     help="N = 1: run the merge kernels after every window anyway (messages + decode, "
                          "no collective) -- prices the DP merge's device work against --merges-per-step")
+    ap.add_argument("--merge-lag", type=int, default=int(os.environ.get("ANA_MERGE_LAG") or 0), choices=[0, 1],
+                    help="1: one-window-late merge (parallel/sweep.py lag) -- window b's all-reduce runs "
+                         "under window b+1's rating instead of in front of it, for one window of extra "
+                         "staleness (the accuracy block reports it); the last sum is applied inside the "
+                         "timed region")
     ap.add_argument("--sweeps", type=int, default=EngineConfig.from_env().sweeps,
                     help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
                          "N = exact sequential semantics (parallel/sweep.py)")
@@ -129,6 +134,8 @@ def parse(argv=None):
         ap.error("--merges-per-step must divide --matches-per-gpu")
     if args.merges_per_step > 1 and args.config == 4:
         ap.error("--merges-per-step is for the rating configs (2, 3, 5)")
+    if args.merge_lag and args.sweeps > 1:
+        ap.error("--merge-lag runs one sweep per window")
     if args.comm_dtype is None:
         one_sweep = "fp16" if args.config == 5 else "bf16"
         args.comm_dtype = os.environ.get("COMM_DTYPE") or (one_sweep if args.sweeps <= 1 else "fp32")
@@ -242,10 +249,27 @@ def main(argv=None) -> int:
         tele = [make_telemetry(tspec, windows[w], K, base=(w * world + rank) * M) for w in range(n_windows)]
         stats = allocate_stats(M, K, dev)
         n_events = sum(t.num_events for t in tele) / n_windows
-    merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge)
+    merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge,
+                          lag=bool(args.merge_lag))
               if world > 1 or args.force_merge else None)
-    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or 0.9) if tele is not None and \
-        args.telemetry_mode == "tail" else 0.0
+    auto_mode = args.telemetry_mode == "auto"
+    tele_path = None
+    if tele is not None and auto_mode:
+        tele_path = "fused (inline)"
+    if tele is not None and auto_mode and not rater.fuses((tele[0].evoff, tele[0].events, stats), Mw):
+        tele_path = "MFMA kernel after the rating (launch > ANA_TELE_FUSE_MAX)"
+        # window-sized launches: the MFMA kernel after the rating, started on its own
+        # stream once the rating has claimed 0.8 of its chunks (beside the drain and
+        # the next prepass): 9.69 ms against 9.85 for the kernel behind the rating
+        # (profiles/r4/telemetry_count_row_and_tail.log); needs hipStreamWaitValue64
+        from analyzer_amd.ops.native import native as _native
+
+        if _native().can_wait_value(dev.index or 0):
+            args.telemetry_mode = "tail"
+            tele_path = ("MFMA kernel on its own stream from %s of the rating's chunks (launch > "
+                         "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.8"))
+    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.8 if auto_mode else 0.9)) \
+        if tele is not None and args.telemetry_mode == "tail" else 0.0
     pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     torch.cuda.synchronize()
@@ -306,6 +330,7 @@ def main(argv=None) -> int:
 
     for i in range(args.warmup * sub):
         step(i)
+    pipe.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -315,6 +340,7 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     for i in range(args.warmup * sub, total_windows):
         step(i)
+    pipe.finish()  # lagged merge: the last window's sum applied (timed: it is part of the work)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -365,7 +391,8 @@ def main(argv=None) -> int:
 
         t_acc = time.perf_counter()
         tab = accuracy_run(world, P, Mw, sub, [args.sweeps], device=dev, team_size=K, seed=args.seed,
-                           comm_dtype=args.comm_dtype, p_rated=RosterSpec().p_rated, warm_windows=1)
+                           comm_dtype=args.comm_dtype, p_rated=RosterSpec().p_rated, warm_windows=1,
+                           lag=bool(args.merge_lag))
         st = tab["sweeps"][str(args.sweeps)]
         sh = st["tracks"].get("shared", {})
         accuracy = {"vs": "exact sequential rating of the same %d x %d matches (one step)" % (world, M),
@@ -391,11 +418,9 @@ def main(argv=None) -> int:
         metric = ("matches/sec rated + telemetry aggregated (whole node), 3v3 TrueSkill, "
                   "1M-player roster, streaming")
         extra = {"events_per_match": n_events / M, "events_per_s": world * n_events / (ms / 1000.0),
-                 "telemetry_mode": args.telemetry_mode}
-        if args.telemetry_mode == "auto":
-            t0w = tele[0]
-            extra["telemetry_path"] = ("fused (inline)" if rater.fuses((t0w.evoff, t0w.events, stats), Mw)
-                                       else "MFMA kernel after the rating (launch > ANA_TELE_FUSE_MAX)")
+                 "telemetry_mode": "auto" if auto_mode else args.telemetry_mode}
+        if auto_mode:
+            extra["telemetry_path"] = tele_path
     if rank == 0:
         print(json.dumps({
             "metric": metric,
@@ -433,6 +458,7 @@ def main(argv=None) -> int:
                 "skew": args.skew,
                 "comm_dtype": args.comm_dtype if world > 1 or args.force_merge else None,
                 "force_merge": bool(args.force_merge),
+                "merge_lag": bool(args.merge_lag) if world > 1 or args.force_merge else None,
                 "sweeps": args.sweeps if world > 1 else None,
                 **extra,
             },

@@ -41,7 +41,8 @@ def main():
     ap.add_argument("--pattern", default="random", choices=["random", "serial", "disjoint"])
     ap.add_argument("--touch", default="0",
                     help="1: read the whole roster after the prepass, untimed, so the launch starts with "
-                         "its rows warm in the Infinity Cache (comma list to A/B)")
+                         "its rows warm in the Infinity Cache; 2: the same with the native warm_rows "
+                         "kernel inside the timed launch (ANA_ROSTER_WARM); comma list to A/B")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     P, M, K = args.players, args.matches, args.team_size
@@ -54,6 +55,7 @@ def main():
                           + torch.arange(2 * K, dtype=torch.int32, device=dev)[None, :])
     out = RateResult.allocate(M, K, dev)
     results = {}
+    sink = torch.zeros(256, dtype=torch.int32, device=dev)  # --touch 2 scratch
     combos = [(int(b), int(i), int(t), int(lo), int(d), int(sp)) for b in args.blocks.split(",")
               for i in args.idle.split(",") for t in args.tight.split(",")
               for lo in args.local.split(",") for d in args.diag.split(",") for sp in args.touch.split(",")]
@@ -63,7 +65,7 @@ def main():
             os.environ["ANA_RATE_IDLE"] = str(idle)
             os.environ["ANA_RATE_LOCAL"] = str(loc)
             os.environ["ANA_RATE_DIAG"] = str(dg)
-            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg) + ("/touch" if sp else "")
+            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg) + ("/touch%d" % sp if sp else "")
             roster = make_roster(RosterSpec(num_players=P, seed=1, p_rated=args.rated,
                                             p_mode_rated=args.rated), device=dev)
             br = BatchRater(blocks=b)
@@ -73,7 +75,11 @@ def main():
             sched = br.schedule(rec, K, P)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            if sp:  # roster rows warm in the Infinity Cache (untimed)
+            if sp == 2:  # the engine's warm-up kernel, timed with the launch
+                from analyzer_amd.ops.native import native
+
+                native().warm_rows(roster.state, sink)
+            elif sp:  # roster rows warm in the Infinity Cache (untimed)
                 float(roster.state.sum())
                 torch.cuda.synchronize()
                 t0 += time.perf_counter() - t1

@@ -334,3 +334,66 @@ def _exact_checked(rank, size, P, M, K, seed):
 def test_exact_dp_with_round_check(tmp_path):
     res = run_ranks(_exact_checked, 2, tmp_path, 40, 300, 3, 9)
     assert len(res) == 2
+
+
+# ------------------------------------------------ one-window-late merge (lag)
+def _lagged(rank, size, P, M, K, seed, windows, comm_dtype, bucket_rows):
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.parallel.sweep import SweepMerger
+    from analyzer_amd.runtime.engine import WindowPipeline
+
+    roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
+    spec = StreamSpec(team_size=K, seed=seed + 1)
+    merger = SweepMerger(P, "cpu", comm_dtype=comm_dtype, lag=True, bucket_rows=bucket_rows)
+    pipe = WindowPipeline(BatchRater(), roster, K, merger=merger)
+    recs = [make_stream(spec, M, P, K=K, base=(w * size + rank) * M) for w in range(windows)]
+    outs = []
+    pipe.run(recs, on_result=lambda i, res: outs.append(res.s_mu.clone()))
+    return {"state": roster.state, "s_mu": outs[-1], "windows": merger.windows}
+
+
+@pytest.mark.parametrize("comm_dtype,bucket_rows", [("fp32", None), ("bf16", 37)])
+def test_lagged_merge_equals_simulation(tmp_path, comm_dtype, bucket_rows):
+    """The one-window-late merge over gloo (async all-reduce waited for at the next
+    boundary, flushed at the end of the run; ragged row buckets) gives every rank
+    the same roster, equal to the one-process simulation of parallel/accuracy.py, and
+    its error against the exact sequential result stays a sweep-DP-sized one."""
+    from analyzer_amd.ops.rate import BatchRater, Roster
+    from analyzer_amd.parallel.accuracy import compare, simulate_lagged_dp
+
+    P, M, K, seed, size, windows = 300, 500, 3, 23, 2, 4
+    res = run_ranks(_lagged, size, tmp_path, P, M, K, seed, windows, comm_dtype, bucket_rows)
+    for r in res:
+        assert r["windows"] == windows
+        assert torch.equal(r["state"].nan_to_num(-7), res[0]["state"].nan_to_num(-7))
+    spec = StreamSpec(team_size=K, seed=seed + 1)
+    start = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
+    sets = [[make_stream(spec, M, P, K=K, base=(w * size + r) * M) for r in range(size)] for w in range(windows)]
+    sim = start.clone()
+    sim_out = simulate_lagged_dp(BatchRater(), sim, sets, K, comm_dtype=comm_dtype)
+    got = res[0]["state"]
+    assert torch.equal(torch.isnan(got[:, 0::4]), torch.isnan(sim.state[:, 0::4]))
+    ok = ~torch.isnan(sim.state[:, 0::4])
+    # two-rank sums are order-independent; bf16 sums of two operands may round once
+    tol = 1e-3 if comm_dtype == "fp32" else 2.0
+    assert float((got[:, 0::4][ok] - sim.state[:, 0::4][ok]).abs().max()) < tol
+    d = (res[-1]["s_mu"] - sim_out[-1].s_mu).abs()
+    assert float(d[~torch.isnan(d)].max()) < tol
+    exact = start.clone()
+    for shards in sets:
+        for sh in shards:
+            BatchRater().rate(exact, sh, K)
+    sh = compare(Roster(got, start.attrs), exact)["tracks"]["shared"]
+    assert sh["null_mismatch"] == 0 and sh["spearman_mu_minus_sigma"] > 0.97, sh
+
+
+def test_lagged_merge_one_rank_is_exact():
+    """One rank (bench --force-merge): the lagged boundary restarts every window from
+    exactly the rank's own posterior, so the run equals plain sequential rating up to
+    the natural-parameter round trip -- fresh (NULL) tracks included."""
+    from analyzer_amd.parallel.accuracy import run
+
+    t = run(ranks=1, players=800, matches_per_rank=3000, windows=4, sweeps=[1], lag=True)
+    for name, tr in t["sweeps"]["1"]["tracks"].items():
+        assert tr["null_mismatch"] == 0 and tr["dmu_max"] < 5e-3, (name, tr)
+    assert t["sweeps"]["1"]["records_shared_mu"]["dmu_max"] < 5e-3

@@ -165,3 +165,16 @@ def test_prepass_placement_knob():
     assert WindowPipeline.tail_point(3, auto, dp=True) == 0.9 and WindowPipeline.tail_point(5, auto, dp=True) == 0.7
     assert WindowPipeline.tail_point(3, EngineConfig.from_env({"ANA_PREPASS_AT": "0.5"}), dp=True) == 0.5
     assert WindowPipeline.tail_point(3, auto) == 0.7
+    assert not auto.roster_warm and EngineConfig.from_env({"ANA_ROSTER_WARM": "1"}).roster_warm
+
+
+def test_warm_rows_host_is_a_no_op():
+    """warm_rows on a host roster checks its operands and changes nothing."""
+    from analyzer_amd.ops.native import native
+
+    roster = make_roster(RosterSpec(num_players=64, seed=5))
+    before = roster.state.clone()
+    native().warm_rows(roster.state, torch.zeros(256, dtype=torch.int32))
+    assert torch.equal(roster.state.nan_to_num(-7), before.nan_to_num(-7))
+    with pytest.raises(RuntimeError):
+        native().warm_rows(roster.state, torch.zeros(8, dtype=torch.int32))
