@@ -210,7 +210,7 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   if (dev.is_cuda()) {
     check(workspace, "workspace", torch::kUInt8, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
-    TORCH_CHECK(ctrl.numel() >= 48, "ctrl must have 48 entries");
+    TORCH_CHECK(ctrl.numel() >= 52, "ctrl must have 52 entries");
     const size_t need = ana::schedule_workspace_bytes(M * 2 * K, num_players);
     TORCH_CHECK((size_t)workspace.numel() >= need, "workspace too small: need ", need, " bytes");
     check_hip(ana::launch_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
@@ -230,8 +230,8 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
 }
 
 // knobs (EngineConfig, config.py): [rate_idle, rate_local, rate_diag, rate_tight,
-// tele_fused_tail, tele_role] -- executor / fused-telemetry tuning, per BatchRater
-constexpr size_t kKnobs = 6;
+// tele_fused_tail, tele_role, rate_spec] -- executor / fused-telemetry tuning, per BatchRater
+constexpr size_t kKnobs = 7;
 
 static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& events,
                                              const Tensor& stats, int64_t M, int64_t K,
@@ -264,7 +264,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
           int64_t progress, int64_t progress_value, int64_t progress_at, int64_t epoch_ptr,
           int64_t chunk_len, bool ctrl_ready, std::vector<int64_t> knobs) {
   const auto dev = rec.device();
-  TORCH_CHECK(knobs.size() == kKnobs, "knobs must be [idle, local, diag, tight, tele_fused_tail, tele_role]");
+  TORCH_CHECK(knobs.size() == kKnobs, "knobs must be [idle, local, diag, tight, tele_fused_tail, tele_role, spec]");
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
   check(attrs, "attrs", torch::kFloat32, dev);
@@ -310,6 +310,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   prm.local_handoff = (int32_t)knobs[1];
   prm.diag = (int32_t)knobs[2];
   prm.tight_groups = (int32_t)knobs[3];
+  prm.speculate = (int32_t)knobs[6];
   prm.progress = reinterpret_cast<uint64_t*>((intptr_t)progress);
   prm.progress_value = (uint64_t)progress_value;
   prm.progress_at = progress_at;
@@ -323,7 +324,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
     check(ctrl, "ctrl", torch::kInt32, dev);
     TORCH_CHECK(link.numel() == M * S * ana::kLinkWords, "link must be [M, 2K]");
     TORCH_CHECK(deps.numel() == M, "deps must have M entries");
-    TORCH_CHECK(ctrl.numel() >= 48, "ctrl must have 48 entries");
+    TORCH_CHECK(ctrl.numel() >= 52, "ctrl must have 52 entries");
     TORCH_CHECK(blocks >= 1 && blocks <= 65535, "blocks must be 1..65535");
     // the executor writes packed rows; other layouts go through a packed buffer
     const bool packed = out.s_sig == out.s_mu + S && out.delta == out.s_mu + 2 * S &&

@@ -71,6 +71,7 @@ struct Batch {
   int my_h = -1, my_bit = 0, mode = 0, n0 = 0, n1 = 0, rank0 = 1, rank1 = 1, first = 0, prevdup = -1;
   int32_t id = -1;
   bool inr = false, islast = false, own = false, any_dup = false;
+  bool spec = false;  // taken one dependency short (ANA_RATE_SPEC): rated only if its granules are fresh
   uint32_t lk0 = kNoMatch;  // schedule link (common.h): next match | has-earlier
   v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
   // K8 inline telemetry (TelemetryParams::role_stride < 0): the match's event count, a
@@ -147,8 +148,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_progress = 0;
   const bool local_ok = prm.local_handoff != 0;
-  // hand-off statistics (wave-uniform counts, added to ctrl[26..27] at exit)
-  uint32_t n_local = 0, n_global = 0;
+  const bool spec_on = prm.speculate != 0;
+  // hand-off statistics (wave-uniform counts, added to ctrl[26..27] at exit); stale
+  // reads retried (ctrl[14]), speculative groups and those of them still stale (ctrl[48..49])
+  uint32_t n_local = 0, n_global = 0, n_stale = 0, n_spec = 0, n_spec_stale = 0;
   // timing build: clocks of the iterations that rated something, split at the wait
   uint64_t d_issue = 0, d_wait = 0, d_after = 0, d_it0 = 0;
   uint64_t d_t[4] = {0, 0, 0, 0}, d_p[5] = {0, 0, 0, 0, 0};  // after-phase split (timing build)
@@ -274,12 +277,14 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // ---------------------------------------------- (2) readiness from the last poll
     // one unconditional LDS read: a free slot's stale count is masked by pend = 0,
     // and without local hand-off the counts stay 0
-    uint64_t ready[kH];
+    uint64_t ready[kH], near[kH];
     {
       const hvec lv = lloc[wv][lane];
 #pragma unroll
-      for (int h = 0; h < kH; ++h)
+      for (int h = 0; h < kH; ++h) {
         ready[h] = __ballot(dval[h] != kNone && dval[h] + lv[h] == need[h]) & pend[h];
+        near[h] = spec_on ? __ballot(dval[h] != kNone && dval[h] + lv[h] + 1u == need[h]) & pend[h] : 0ull;
+      }
       if constexpr (DIAG) {
         uint32_t nn = 0, np = 0;
 #pragma unroll
@@ -308,9 +313,18 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // rarely has more ready matches than groups (2-3.4 per iteration on the
     // bench), so age order buys nothing measurable.
     int my_h = -1, my_bit = 0, nassigned = 0;
+    bool my_spec = false;
+    // Speculation (ANA_RATE_SPEC): groups left over after the ready matches take
+    // matches one dependency short at the last poll.  Their granules are gathered
+    // like any others; the freshness check below (the tags of the last writers) is
+    // exactly the readiness test, so one whose last producer has published since
+    // the poll is rated now -- a poll round trip and an iteration early -- and one
+    // whose producer has not goes back to pending like a stale read.
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
     for (int h = 0; h < kH; ++h) {
-      const uint64_t rdy = ready[h];
+      const uint64_t rdy = pass == 0 ? ready[h] : near[h];
       if (rdy != 0ull && nassigned < NG) {
         const uint32_t below = __builtin_amdgcn_mbcnt_hi(
             (uint32_t)(rdy >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rdy, 0u));
@@ -318,7 +332,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         if (mine) {
           int32_t w[SP];
           w[0] = cbase[h] + lane;
-          w[1] = (h << 8) | lane;
+          w[1] = (pass << 16) | (h << 8) | lane;
           w[2] = hrec[h][S];
           w[3] = hrec[h][S + 1];
 #pragma unroll
@@ -336,7 +350,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         const uint64_t taken = __ballot(mine);
         pend[h] &= ~taken;
         nassigned += __popcll(taken);
+        if (pass == 1) n_spec += (uint32_t)__popcll(taken);
       }
+    }
     }
     int32_t my_m = 0, my_id = -1;
     uint32_t my_m0 = 0u, my_m1 = 0u;
@@ -351,8 +367,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       }
       if (j < S) my_id = lpick[wv][g][4 + j];
       my_m = pk.x;
-      my_h = pk.y >> 8;
+      my_h = (pk.y >> 8) & 255;
       my_bit = pk.y & 255;
+      my_spec = (pk.y >> 16) & 1;
       my_m0 = (uint32_t)pk.z;
       my_m1 = (uint32_t)pk.w;
     }
@@ -375,6 +392,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       const int mode = meta_mode(m0);
       nb.my_h = my_h;
       nb.my_bit = my_bit;
+      nb.spec = my_spec;
       nb.m = m;
       nb.mode = mode;
       nb.n0 = meta_n0(m0);
@@ -545,10 +563,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     }
     const uint64_t stale_lanes = __ballot(!fresh);
     if (stale_lanes) {
-      if (lane == 0)  // diagnostics: stale reads retried (ctrl[14])
-        __hip_atomic_fetch_add((gu32*)&ctrl[14], (unsigned)__popcll(stale_lanes), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
       const bool gstale = (stale_lanes & gmask) != 0ull;
+      // diagnostics (ctrl[14], [49] at exit): stale groups, and the speculative ones among them
+      const uint64_t leads = __ballot(gstale && j == 0);
+      n_stale += (uint32_t)__popcll(leads);
+      n_spec_stale += (uint32_t)__popcll(leads & __ballot(bt.spec));
 #pragma unroll
       for (int h = 0; h < kH; ++h) {
         uint64_t back = 0ull;
@@ -883,6 +902,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         __hip_atomic_fetch_add((gu32*)&ctrl[15], iter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add((gu32*)&ctrl[26], n_local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add((gu32*)&ctrl[27], n_global, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n_stale) __hip_atomic_fetch_add((gu32*)&ctrl[14], n_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n_spec) __hip_atomic_fetch_add((gu32*)&ctrl[48], n_spec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n_spec_stale)
+          __hip_atomic_fetch_add((gu32*)&ctrl[49], n_spec_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (DIAG) {
           // iterations that rated something: [20] count, [21] groups assigned, and
           // 100 MHz s_memrealtime ticks [22..23] issue (top of the loop -> the wait),
@@ -969,12 +992,13 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] retired chunks, [4..11] tickets,
   // [12] telemetry tile ticket, [13] malformed telemetry events, [14] stale reads retried,
   // [15] wave iterations; [16..18] sticky OR of [0..2] over launches (host clears);
-  // [20..25], [28..29] timing build (see the kernel), [26] local / [27] global hand-offs
+  // [20..25], [28..29] timing build (see the kernel), [26] local / [27] global hand-offs,
+  // [48] speculative groups, [49] of them stale (ANA_RATE_SPEC)
   // one-wave kernel rather than hipMemsetAsync: a 60-B fill at a 4-B offset becomes two
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
-  // the diagnostic words [20..47] are zeroed by every launch (not by the schedule's zeroing)
+  // the diagnostic words [20..51] are zeroed by every launch (not by the schedule's zeroing)
   hipLaunchKernelGGL(zero_ctrl2_kernel, dim3(1), dim3(64), 0, s, ctrl + 1, prm.ctrl_ready ? 0 : 15,
-                     ctrl + 20, 28);
+                     ctrl + 20, 32);
   if (M <= 0) return 0;
   if (prm.chunk_len < 1 || prm.chunk_len > kChunk) return (int)hipErrorInvalidValue;
   if ((int64_t)prm.num_players * kRowFloats * 4 > kOutOfRange) return (int)hipErrorInvalidValue;

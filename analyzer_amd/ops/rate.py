@@ -30,7 +30,7 @@ from .native import native
 RATED, AFK, INVALID_ROSTERS, UNSUPPORTED_MODE = 0, 1, 2, 3
 ERR_SEED, ERR_SIGMA, ERR_EMPTY_ROSTER, ERR_NUMERIC, ERR_BAD_RECORD = 4, 5, 6, 7, 8
 NOT_PROCESSED = 255
-CTRL_WORDS = 48  # executor control words (csrc/dataflow.hip launch_rate)
+CTRL_WORDS = 52  # executor control words (csrc/dataflow.hip launch_rate)
 STATUS_NAMES = {RATED: "rated", AFK: "afk", INVALID_ROSTERS: "invalid_rosters",
                 UNSUPPORTED_MODE: "unsupported_mode", ERR_SEED: "error_seed",
                 ERR_SIGMA: "error_sigma", ERR_EMPTY_ROSTER: "error_empty_roster",
@@ -393,7 +393,10 @@ class BatchRater:
                 "local_handoffs": c[26], "global_handoffs": c[27],
                 # held matches one dependency short of ready / pending, per worked iteration
                 "near_ready_per_worked_iteration": c[30] / worked if worked else 0.0,
-                "pending_per_worked_iteration": c[31] / worked if worked else 0.0}
+                "pending_per_worked_iteration": c[31] / worked if worked else 0.0,
+                # ANA_RATE_SPEC: one-short matches given to idle groups, and those whose
+                # granules were not fresh yet (returned to pending)
+                "speculative_groups": c[48], "speculative_stale": c[49], "stale_retries": c[14]}
 
     def telemetry_errors(self, device) -> int:
         """Malformed telemetry events seen by the last fused launch (syncs)."""

@@ -181,16 +181,19 @@ def test_device_repeat_launch_deterministic(gpu_device):
 @pytest.mark.parametrize("K,P,M,skew", [(3, 16, 4000, 1), (3, 100000, 1000000, 1), (5, 2000, 200000, 1),
                                         (3, 100000, 300000, 3)])
 def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K, P, M, skew):
-    """The LDS local hand-off (ANA_RATE_LOCAL) and the timing build
-    (ANA_RATE_DIAG) change only WHEN a match runs, never its result: all three
-    executors give the same bits, and hot chains (16 players, skewed activity)
-    actually take the local path."""
+    """The LDS local hand-off (ANA_RATE_LOCAL), speculation (ANA_RATE_SPEC: idle
+    groups take one-short matches and rate those whose granules are fresh) and the
+    timing build (ANA_RATE_DIAG) change only WHEN a match runs, never its result:
+    every executor gives the same bits, hot chains (16 players, skewed activity)
+    actually take the local path, and speculation rates some matches early."""
     rs = RosterSpec(num_players=P, seed=P + 3)
     rec = make_stream(StreamSpec(team_size=K, seed=M + 1, skew=skew), M, P, K=K, device=gpu_device)
     outs = []
-    for local, diag in (("0", "0"), ("1", "0"), ("1", "1")):
+    for local, diag, spec in (("0", "0", "0"), ("1", "0", "0"), ("1", "1", "0"), ("1", "0", "1"),
+                              ("0", "1", "1")):
         monkeypatch.setenv("ANA_RATE_LOCAL", local)
         monkeypatch.setenv("ANA_RATE_DIAG", diag)
+        monkeypatch.setenv("ANA_RATE_SPEC", spec)
         ro = make_roster(rs, device=gpu_device)
         rater = R.BatchRater()
         res = rater.rate(ro, rec, K)
@@ -200,9 +203,13 @@ def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K
             assert nl == 0
         elif P <= 16 or skew > 1:
             assert nl > 0, (nl, ng)
+        d = rater.diag(gpu_device)
         if diag == "1":
-            d = rater.diag(gpu_device)
             assert d["worked_iterations"] > 0 and d["wait_us"] > 0.0 and d["after_us"] > 0.0, d
+        if spec == "1" and M >= 100000:
+            assert d["speculative_groups"] > d["speculative_stale"], d  # some rated early
+        elif spec == "0":
+            assert d["speculative_groups"] == 0, d
         outs.append((ro.state.cpu(), res.s_mu.cpu(), res.status.cpu(), res.quality.cpu()))
     for b in outs[1:]:
         a = outs[0]
