@@ -90,6 +90,9 @@ class WindowPipeline:
         self.merge_side = torch.cuda.Stream(self.device) if self.cuda and self.serial else None
         self._rated: Optional[torch.cuda.Event] = None  # the last rating launch finished
         self._warm_sink: Optional[torch.Tensor] = None  # ANA_ROSTER_WARM scratch word block
+        # roster warm-up before each launch: ANA_ROSTER_WARM, auto = between DP merges
+        # (k short windows per step, where the rows' first reads dominate)
+        self.warm = self.ecfg.roster_warm if self.ecfg.roster_warm is not None else dp
         # ANA_PREPASS_EXCLUSIVE (with ANA_PREPASS_CUS=n): the rating launches go to a
         # stream masked to the other CUs, so the two never share a CU
         self.exec_stream = None
@@ -150,7 +153,9 @@ class WindowPipeline:
         """``ANA_ROSTER_WARM``: read the roster rows once on the main stream, behind the
         prepass that streamed the window's sort through the Infinity Cache, so the
         executor's first gathers of each player hit that cache (scripts/tune_rate.py
-        --touch measured the effect, profiles/r4/touch_warm_roster.log)."""
+        --touch measured the effect, profiles/r4/touch_warm_roster.log; in the pipeline:
+        profiles/r4/roster_warm_and_lag.log).  A window over a roster that was just
+        rated in full gains nothing; the short windows between DP merges do."""
         from ..ops.native import native
 
         if self._warm_sink is None:
@@ -203,7 +208,7 @@ class WindowPipeline:
             cl = self.rater.chunk_len(M, self.rater.tiles(telemetry, M))
             at = int(self.tail * ((M + cl - 1) // cl))
             progress = (self._signal, self._seq, at)
-        if self.ecfg.roster_warm and self.cuda:
+        if self.warm and self.cuda:
             self._warm()
         with trace_range("rate", window=self.windows_rated, matches=int(prep.rec.shape[0])):
             if self.exec_stream is not None:
