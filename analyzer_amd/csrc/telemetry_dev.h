@@ -354,4 +354,185 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   if (bad) atomicAdd(bad_events, bad);
 }
 
+// impl 3: the same one-hot GEMM with the fragments built in REGISTERS.  Each lane
+// decodes its event once (as above) into two words in LDS -- {row | column + 1 << 10 |
+// p2 << 16, p0 | p1 << 16} -- and every lane then reads the 8 records of its MFMA
+// k-group (lanes 16 fg .. 16 fg + 15 read the same 64 B: broadcast, conflict-free) and
+// builds its A fragment (1.0 where the event's row is the lane's row of the tile) and
+// its B fragment (the event's bf16 part for the lane's column) with compares and
+// selects.  Where impl 1 scatters b16 operands into LDS tiles at event-chosen rows
+// (2.55 bank-conflict cycles per LDS instruction, an undo per store, 23 LDS
+// instructions per 64 events), this is one 8-B store and 4-8 broadcast 16-B reads per
+// 64 events, for ~4x the VALU work of the scatter.
+// LDS of one impl-3 wave: [16][17] float stage, 64 decoded events, span + 1 CSR offsets
+constexpr int kTeleRegsFloats = 16 * 17 + 64 * 2 + kTeleMaxSpan + 5;
+template <int K, int SPAN = kTeleMaxSpan>
+__device__ __forceinline__ void telemetry_tile_regs(const TelemetryParams& tp, int64_t tile, int lane,
+                                                    float* lds_f, uint32_t* bad_events) {
+  constexpr int S = 2 * K;
+  constexpr int NB = kTeleMfmaLoads;
+  constexpr uint32_t kOne = 0x3f80;  // bf16 1.0
+  constexpr int kStageBytes = 16 * 17 * 4;
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_f);
+  float* st = reinterpret_cast<float*>(lds);                              // [16][17] output stage
+  uint2* recs = reinterpret_cast<uint2*>(lds + kStageBytes);              // [64] decoded events
+  int32_t* rel = reinterpret_cast<int32_t*>(lds + kStageBytes + 64 * 8);  // span CSR, relative
+  tile = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(tile >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)tile));
+  static_assert(SPAN >= 1 && SPAN <= kTeleMaxSpan, "span must fit the lanes");
+  static_assert(SPAN * S < 1023, "rows are 10-bit in the decoded record (1023 = none)");
+  const int64_t m0 = tile * SPAN;
+  const int nm = (int)(tp.num_matches - m0 < SPAN ? tp.num_matches - m0 : SPAN);
+  const int64_t off = lane <= nm ? tp.evoff[m0 + lane] : 0;
+  const int64_t e0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off >> 32), 0) << 32) |
+                               (uint32_t)__builtin_amdgcn_readlane((int)off, 0));
+  const int32_t roff = (int32_t)(off - e0);
+  tele_lds_fence();
+  if (lane <= nm) rel[lane] = roff;
+  tele_lds_fence();
+  const int ne = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(roff, nm));
+  const int fr = lane & 15, fg = lane >> 4;  // fragment row / column, k-group
+  const int2* __restrict__ evs = reinterpret_cast<const int2*>(tp.events) + e0;
+  tele_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  int c = 0;
+  const int nrows = nm * S;
+  float* dst = tp.stats + m0 * S * kStatFeatures;
+  auto shift = [&]() {  // row tile c is final: store it through the stage, slide by one
+    tele_lds_fence();
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st[(4 * fg + j) * 17 + fr] = acc0[j];
+    tele_lds_fence();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int o = lane + 64 * h;
+      const float* r = st + (o >> 3) * 17;
+      const int f = o & 7;
+      const bool split = f >= 3 && f < kStatEvents;
+      const int c0 = f < 3 ? f + 1 : split ? 3 * f - 5 : 0;
+      const float v = split ? (r[c0] + r[c0 + 1]) + r[c0 + 2] : r[c0];
+      if (16 * c + (o >> 3) < nrows) dst[16 * c * kStatFeatures + o] = v;
+    }
+    tele_lds_fence();
+    acc0 = acc1;
+    acc1 = tele_f32x4{0.f, 0.f, 0.f, 0.f};
+    ++c;
+  };
+  // A fragment of row tile tl: bf16 1.0 at k = i where the i-th event of this lane's
+  // k-group lies on row 16 tl + fr
+  auto a_frag = [&](const uint32_t (&row)[8], int tl) {
+    const uint32_t want = (uint32_t)(16 * tl + fr);
+    uint32_t w[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      w[p] = (row[2 * p] == want ? kOne : 0u) | (row[2 * p + 1] == want ? kOne << 16 : 0u);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  };
+  uint32_t bad = 0;
+  bool nonfinite = false;
+  auto match_at = [&](int pos) {
+    return (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(lane < nm && roff <= pos)) - 1;
+  };
+  const int elast = ne > 0 ? ne - 1 : 0;
+  for (int pr = 0; pr < ne; pr += 64 * NB) {
+    int2 ev[NB];
+#pragma unroll
+    for (int q = 0; q < NB; ++q) ev[q] = evs[min(pr + 64 * q + lane, elast)];
+#pragma unroll
+  for (int q = 0; q < NB; ++q) {
+    const int pb = pr + 64 * q;
+    if (pb >= ne) break;
+    const int2 cur = ev[q];
+    const int n1 = ne - pb - kTeleChunk;
+    const int ms0 = match_at(pb);
+    const int me0 = match_at((n1 > 0 ? pb + kTeleChunk : ne) - 1);
+    const int ms1 = n1 > 0 ? match_at(pb + kTeleChunk) : me0;
+    const int me1 = n1 > 0 ? match_at(pb + kTeleChunk + (n1 < kTeleChunk ? n1 : kTeleChunk) - 1) : me0;
+    const int ilo0 = (ms0 * S) >> 4, ihi0 = ((me0 + 1) * S - 1) >> 4;
+    const int ilo1 = (ms1 * S) >> 4, ihi1 = ((me1 + 1) * S - 1) >> 4;
+    // decode this lane's event (as impl 1)
+    const int e = pb + lane;
+    const int xw = (int)((event_tag(cur.x) - (uint32_t)(m0 & 0xffff)) & 0xffffu);
+    const int seg = xw >= nm ? nm - 1 : xw;
+    const int slot = event_slot(cur.x);
+    const int r0 = rel[seg], r1e = rel[seg + 1];
+    const bool ok = e < ne && xw == seg && slot < S && e >= r0 && e < r1e;
+    bad += (e < ne && !ok) ? 1u : 0u;
+    const int type = event_type(cur.x);
+    const float value = __int_as_float(cur.y);
+    const bool counted = ok && type < 3;
+    const bool summed = ok && type >= 3 && type <= 6;
+    const bool finite = __builtin_isfinite(value);
+    nonfinite |= summed && !finite;
+    const bool split = summed && finite;
+    const int col = counted ? type + 1 : split ? 3 * type - 5 : -1;
+    const uint32_t hb = __float_as_uint(value) & 0xffff0000u;
+    const float rv = value - __uint_as_float(hb);
+    const uint32_t mb = __float_as_uint(rv) & 0xffff0000u;
+    const uint32_t p0 = counted ? kOne : split ? hb >> 16 : 0u;
+    const uint32_t p1 = split ? mb >> 16 : 0u;
+    const uint32_t p2 = split ? __float_as_uint(rv - __uint_as_float(mb)) >> 16 : 0u;
+    // an unattributed event gets row 1023 (no tile row): its A column stays zero
+    const uint32_t row = ok ? (uint32_t)(seg * S + slot) : 1023u;
+    tele_lds_fence();
+    recs[lane] = make_uint2(row | ((uint32_t)(col + 1) << 10) | (p2 << 16), p0 | (p1 << 16));
+    tele_lds_fence();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && n1 <= 0) break;
+      // the 8 records of this lane's k-group in chunk h: 64 B, four 16-B reads
+      const uint4* src = reinterpret_cast<const uint4*>(recs + 32 * h + 8 * fg);
+      uint32_t ra[8], rb[8];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const uint4 x = src[v];
+        ra[2 * v] = x.x;
+        rb[2 * v] = x.y;
+        ra[2 * v + 1] = x.z;
+        rb[2 * v + 1] = x.w;
+      }
+      uint32_t rw[8], bw[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rw[i] = ra[i] & 1023u;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        uint32_t h2[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int i = 2 * p + u;
+          // column fr takes p0 / p1 / p2 at offsets 0 / 1 / 2 from the event's column
+          const int d = fr - ((int)((ra[i] >> 10) & 31u) - 1);
+          const uint32_t v = d == 0 ? (rb[i] & 0xffffu) : d == 1 ? (rb[i] >> 16) : d == 2 ? (ra[i] >> 16) : 0u;
+          h2[u] = fr == 0 ? kOne : v;  // column 0: the event count
+        }
+        bw[p] = h2[0] | (h2[1] << 16);
+      }
+      const uint4 b = make_uint4(bw[0], bw[1], bw[2], bw[3]);
+      const int ilo = h ? ilo1 : ilo0, ihi = h ? ihi1 : ihi0;
+      while (c < ilo) shift();
+      acc0 = tele_mfma(a_frag(rw, c), b, acc0);
+      if (ihi > c) acc1 = tele_mfma(a_frag(rw, c + 1), b, acc1);
+      while (ihi > c + 1) {  // rare: the chunk reaches a third row tile
+        shift();
+        acc1 = tele_mfma(a_frag(rw, c + 1), b, acc1);
+      }
+    }
+  }
+  }
+  while (16 * c < nrows) shift();  // the last live tiles and any tiles without events
+  if (__builtin_amdgcn_ballot_w64(nonfinite)) {
+    // rare slow path: add the span's Inf/NaN values on top of the stored sums
+    __threadfence();
+    for (int e = lane; e < ne; e += 64) {
+      const int2 x = evs[e];
+      const int xm = (int)((event_tag(x.x) - (uint32_t)(m0 & 0xffff)) & 0xffffu);
+      const int slot = event_slot(x.x);
+      if (xm >= nm || slot >= S || e < rel[xm] || e >= rel[xm + 1]) continue;
+      float add;
+      const int f = event_feature(event_type(x.x), __int_as_float(x.y), add);
+      if (f >= 3 && !__builtin_isfinite(add)) atomicAdd(dst + (xm * S + slot) * kStatFeatures + f, add);
+    }
+  }
+  if (bad) atomicAdd(bad_events, bad);
+}
+
 }  // namespace ana

@@ -376,11 +376,12 @@ def test_telemetry_device_generator_and_aggregation(gpu_device):
     np.testing.assert_allclose(sd.cpu().numpy(), aggregate_reference(th, K), rtol=2e-5, atol=0.05)
 
 
-@pytest.mark.parametrize("impl", ["1", "0", "2"])
+@pytest.mark.parametrize("impl", ["1", "0", "2", "3"])
 @pytest.mark.parametrize("K", [1, 2, 3, 4, 5])
 def test_telemetry_impls_vs_oracle_edges(gpu_device, monkeypatch, K, impl):
-    """K8 one-hot MFMA (impl 1), LDS-atomic (impl 0) tiles and one lane per stat
-    row (impl 2, also bit-identical to the host mirror) vs an fp64 oracle:
+    """K8 one-hot MFMA (impl 1; impl 3 builds the same fragments in registers and
+    must give impl 1's bits), LDS-atomic (impl 0) tiles and one lane per stat row
+    (impl 2, also bit-identical to the host mirror) vs an fp64 oracle:
     every team size (16-row blocks of 8/4/2/2/1 matches), empty matches, a
     partial last tile, malformed events (strict attribution) and non-finite
     values; the host mirror counts the same malformed events."""
@@ -420,6 +421,13 @@ def test_telemetry_impls_vs_oracle_edges(gpu_device, monkeypatch, K, impl):
     np.testing.assert_allclose(host.numpy(), ref, rtol=2e-6, atol=1e-3)
     if impl == "2":  # row sums in event order, as the host mirror: the same bits
         assert torch.equal(stats.cpu(), host)
+    if impl == "3":  # the same MFMA operands as impl 1, in the same order: the same bits
+        monkeypatch.setenv("ANA_TELE_IMPL", "1")
+        s1 = torch.full_like(stats, -1.0)
+        aggregate(Telemetry(tel.evoff.to(gpu_device), ev.to(gpu_device)), K, s1,
+                  torch.zeros(1, dtype=torch.int32, device=gpu_device))
+        torch.cuda.synchronize()
+        assert torch.equal(stats.view(torch.int32), s1.view(torch.int32))
 
 
 def test_graph_rater_matches_eager(gpu_device):
