@@ -39,6 +39,47 @@ namespace ana {
 // within the 8-lane group.  Base rows instead of full start rows: 64 of the 128
 // B per player on every start read and write (-26 % merge traffic).
 constexpr int kLanesPerPlayer = kGranules;  // 8
+
+// The window-start base rows and the message operands are touched once per merge:
+// non-temporal accesses keep them from evicting the roster, which the next rating
+// launch reads from the Infinity Cache (ANA_MERGE_NT=0 at build time: plain accesses).
+#ifndef ANA_MERGE_NT
+#define ANA_MERGE_NT 1
+#endif
+typedef float merge_f2 __attribute__((ext_vector_type(2)));
+typedef int merge_i2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t merge_ld(const uint32_t* p) {
+  if constexpr (ANA_MERGE_NT != 0) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+__device__ __forceinline__ float2 merge_ld(const float2* p) {
+  if constexpr (ANA_MERGE_NT != 0) {
+    const merge_f2 v = __builtin_nontemporal_load(reinterpret_cast<const merge_f2*>(p));
+    return make_float2(v.x, v.y);
+  } else {
+    return *p;
+  }
+}
+__device__ __forceinline__ int2 merge_ld(const int2* p) {
+  if constexpr (ANA_MERGE_NT != 0) {
+    const merge_i2 v = __builtin_nontemporal_load(reinterpret_cast<const merge_i2*>(p));
+    return make_int2(v.x, v.y);
+  } else {
+    return *p;
+  }
+}
+__device__ __forceinline__ void merge_st(uint32_t* p, uint32_t v) {
+  if constexpr (ANA_MERGE_NT != 0) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ void merge_st(float2* p, float2 v) {
+  if constexpr (ANA_MERGE_NT != 0) __builtin_nontemporal_store(merge_f2{v.x, v.y}, reinterpret_cast<merge_f2*>(p));
+  else *p = v;
+}
+__device__ __forceinline__ void merge_st(int2* p, int2 v) {
+  if constexpr (ANA_MERGE_NT != 0) __builtin_nontemporal_store(merge_i2{v.x, v.y}, reinterpret_cast<merge_i2*>(p));
+  else *p = v;
+}
 constexpr int kRowVec = kRowFloats / 4;      // 16-B vectors per roster row (C2 exchange below)
 
 struct TrackLane {
@@ -77,7 +118,7 @@ __device__ __forceinline__ void lane_delta(const TrackLane& L, const float2* __r
                                           const float4* __restrict__ attrs, const float* vst,
                                           float unknown_sigma, bool scaled, float& dp, float& dt,
                                           float& lo, float& hi) {
-  const float2 c = s0[L.p * kLanesPerPlayer + L.t];
+  const float2 c = merge_ld(s0 + L.p * kLanesPerPlayer + L.t);
   const float2 a = a0 != s0 ? a0[L.p * kLanesPerPlayer + L.t] : c;
   const float4 b = s[L.p * kLanesPerPlayer + L.t];
   const float c0mu = __shfl(c.x, L.gbase), c0sg = __shfl(c.y, L.gbase);
@@ -99,7 +140,7 @@ __device__ __forceinline__ void lane_apply(const TrackLane& L, const float2* __r
                                           float dtau, uint32_t lo, uint32_t hi,
                                           const float4* __restrict__ attrs, const float* vst,
                                           float unknown_sigma, bool scaled, float4* s, float2* s2) {
-  const float2 c = s0[L.p * kLanesPerPlayer + L.t];
+  const float2 c = merge_ld(s0 + L.p * kLanesPerPlayer + L.t);
   const float c0mu = __shfl(c.x, L.gbase), c0sg = __shfl(c.y, L.gbase);
   bool seeded;
   float seed_mu, seed_sig;
@@ -111,7 +152,7 @@ __device__ __forceinline__ void lane_apply(const TrackLane& L, const float2* __r
                       mu, sg);
   }
   s[L.p * kLanesPerPlayer + L.t] = make_float4(mu, 0.f, sg, 0.f);
-  if (s2) s2[L.p * kLanesPerPlayer + L.t] = make_float2(mu, sg);
+  if (s2) merge_st(s2 + L.p * kLanesPerPlayer + L.t, make_float2(mu, sg));
 }
 
 // s0: base rows of the common window start, a0: this rank's prior of the sweep
@@ -177,9 +218,9 @@ sweep_delta_packed_kernel(const float2* __restrict__ s0, const float2* a0, const
   float dp, dt, lo, hi;
   lane_delta(L, s0, a0, s, attrs, vst, unknown_sigma, true, dp, dt, lo, hi);
   if (L.t < kTracks)  // 14 halves = 7 words (28 B per player, contiguous over the wave)
-    msg[L.p * kTracks + L.t] = (uint32_t)to_half_bits<H>(dp) | ((uint32_t)to_half_bits<H>(dt) << 16);
+    merge_st(msg + L.p * kTracks + L.t, (uint32_t)to_half_bits<H>(dp) | ((uint32_t)to_half_bits<H>(dt) << 16));
   else
-    cnt[L.p] = make_int2((int)lo, (int)hi);
+    merge_st(cnt + L.p, make_int2((int)lo, (int)hi));
 }
 
 template <typename H>
@@ -189,8 +230,8 @@ sweep_apply_packed_kernel(const float2* __restrict__ s0, const uint32_t* __restr
                           float2* s2, const float* __restrict__ vst, float unknown_sigma, int64_t P) {
   const TrackLane L = track_lane();
   if (L.p >= P) return;
-  const uint32_t w = L.t < kTracks ? msg[L.p * kTracks + L.t] : 0u;
-  const int2 c = cnt[L.p];  // broadcast within the group
+  const uint32_t w = L.t < kTracks ? merge_ld(msg + L.p * kTracks + L.t) : 0u;
+  const int2 c = merge_ld(cnt + L.p);  // broadcast within the group
   lane_apply(L, s0, from_half_bits<H>(w & 0xffffu), from_half_bits<H>(w >> 16), (uint32_t)c.x,
              (uint32_t)c.y, attrs, vst, unknown_sigma, true, s, s2);
 }
