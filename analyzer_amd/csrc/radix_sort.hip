@@ -57,15 +57,16 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t tiles) {
 // a prepass that co-runs with the dataflow executor does not evict the roster
 // the executor keeps in the Infinity Cache.  Opt-in (ANA_SORT_NT=1): measured on
 // MI355X the prepass slows 1.75 -> 4.35 ms (the digit runs lose L2 write
-// combining) and the bench step 8.1 -> 9.2 ms.
-template <bool NT>
+// combining) and the bench step 8.1 -> 9.2 ms.  ANA_SORT_NT=2: non-temporal loads
+// only (each pass streams its input once; the scattered stores keep L2 combining).
+template <int NT>
 __device__ __forceinline__ uint32_t ld32(const uint32_t* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
+  if constexpr (NT >= 1) return __builtin_nontemporal_load(p);
   else return *p;
 }
-template <bool NT>
+template <int NT>
 __device__ __forceinline__ void st32(uint32_t* p, uint32_t v) {
-  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  if constexpr (NT == 1) __builtin_nontemporal_store(v, p);
   else *p = v;
 }
 
@@ -140,7 +141,7 @@ struct SchedInit {
 };
 
 // KS > 0: keys from the match stream (decode_tile_keys), and the SchedInit duties.
-template <int KS, int RB = 8, bool NT = false>
+template <int KS, int RB = 8, int NT = 0>
 __global__ void __launch_bounds__(kThreads)
 radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec, uint32_t kend,
               int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles, SchedInit init = {}) {
@@ -243,7 +244,7 @@ constexpr uint32_t kRunEmpty = 0xffffffffu;
 // [tile][nd] RunEnds table instead of their global sorted positions, so this pass
 // needs no digit offsets -- no upsweep / rowscan in front of it -- and sched_runs_fixup
 // links each run to the nearest non-empty run of its digit in an earlier tile.
-template <int KS, bool LINK, int RB = 8, bool NT = false>
+template <int KS, bool LINK, int RB = 8, int NT = 0>
 __global__ void __launch_bounds__(kThreads)
 radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                 const int32_t* __restrict__ rec, uint32_t kend,
@@ -557,7 +558,7 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 // both ends -- the first pass reads the records (no key array is written), the
 // last pass writes links instead of sorted pairs, then sched_fixup.  RB-bit
 // digits (8; 10 as an experiment).
-template <int K, int RB, bool NT>
+template <int K, int RB, int NT>
 static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits, uint32_t* ka,
                          uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* counts,
                          int64_t tiles, uint32_t* link, const SchedInit& init, hipStream_t s) {
@@ -642,14 +643,15 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
   const char* rb_e = getenv("ANA_SORT_RB");
   const char* nt_e = getenv("ANA_SORT_NT");
   const int rb_env = rb_e ? atoi(rb_e) : 8;
-  const bool nt = nt_e && atoi(nt_e) != 0;
+  const int nt = nt_e ? atoi(nt_e) : 0;
   const bool wide = bits <= 20 && rb_env == 10;
   switch (K) {
 #define ANA_SORT_CASE(k)                                                                         \
   case k:                                                                                        \
-    if (wide) sched_sort_k<k, 10, false>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
-    else if (nt) sched_sort_k<k, 8, true>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
-    else sched_sort_k<k, 8, false>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    if (wide) sched_sort_k<k, 10, 0>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    else if (nt == 1) sched_sort_k<k, 8, 1>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    else if (nt == 2) sched_sort_k<k, 8, 2>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    else sched_sort_k<k, 8, 0>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
     break;
     ANA_SORT_CASE(1) ANA_SORT_CASE(2) ANA_SORT_CASE(3) ANA_SORT_CASE(4) ANA_SORT_CASE(5)
 #undef ANA_SORT_CASE
