@@ -82,6 +82,35 @@ def all_reduce_sum(t: torch.Tensor, group=None, async_op: bool = False):
     return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
 
 
+def time_all_reduce(t: torch.Tensor, group=None, iters: int = 3) -> float:
+    """Milliseconds per SUM all-reduce of ``t`` (one untimed warm-up, then the mean
+    of ``iters``), the MAX over ranks -- so every rank takes the same decision from
+    it.  A collective: every rank of the group must call it.  ``t`` is overwritten."""
+    _, size = world(group)
+    if size <= 1:
+        return 0.0
+    all_reduce_sum(t, group)
+    if t.is_cuda:
+        torch.cuda.synchronize(t.device)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            all_reduce_sum(t, group)
+        b.record()
+        torch.cuda.synchronize(t.device)
+        ms = a.elapsed_time(b) / iters
+    else:
+        import time
+
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            all_reduce_sum(t, group)
+        ms = (time.perf_counter() - t0) * 1e3 / iters
+    m = torch.tensor([ms], dtype=torch.float64, device=t.device if not _staged(t, group) else "cpu")
+    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+    return float(m.item())
+
+
 def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, torch.device]:
     """Initialise the default group from the torchrun environment (no-op for one
     process).  Returns (rank, world_size, device)."""

@@ -76,6 +76,12 @@ class WindowPipeline:
         self.ecfg = EngineConfig.from_env()
         dp = merger is not None
         self.serial = self.serial_prepass(self.K, self.ecfg, dp)
+        # DP over real collectives: the placement depends on what one merge's
+        # all-reduce costs on this interconnect (probe_placement)
+        self.allreduce_probe_ms: Optional[float] = None
+        if dp and self.cuda and self.ecfg.prepass_serial is None and self.K < 5 and \
+                getattr(merger, "world", 1) > 1 and not getattr(merger, "lag", False):
+            self.serial = self.probe_placement(merger, self.ecfg)
         # serial prepass: nothing to overlap, no tail signal -- unless a caller wants the
         # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail)
         self.tail = (float(signal_at) if signal_at > 0 else 0.0) if self.serial else \
@@ -116,6 +122,24 @@ class WindowPipeline:
         if ecfg.prepass_serial is not None:
             return ecfg.prepass_serial
         return K < 5 and not dp
+
+    def probe_placement(self, merger, ecfg: EngineConfig) -> bool:
+        """1v1-4v4 windows between DP merges: serial placement (the next prepass on its
+        own stream beside the merge's all-reduces) or the tail overlap.  On one GPU
+        (forced merges, no collective) the tail wins by ~0.04 ms per window
+        (profiles/r3/dp_prepass_placement_k8.log: 9.54 vs 9.87 ms per 8 windows), but
+        there the all-reduce takes no time; with N ranks it is exposed in the tail
+        placement and runs under the 0.2-ms prepass in the serial one.  So time one
+        merge's all-reduce on this group (the max over ranks, identical everywhere)
+        and go serial when it exceeds ANA_DP_SERIAL_AR_US (default 40 us)."""
+        from ..parallel.comm import time_all_reduce
+
+        buf = torch.zeros(max(1, int(merger.comm_bytes) // 2), dtype=torch.bfloat16, device=self.device)
+        ms = time_all_reduce(buf, getattr(merger, "group", None))
+        del buf
+        self.allreduce_probe_ms = ms
+        thr = float(os.environ.get("ANA_DP_SERIAL_AR_US") or 40.0) / 1000.0
+        return ms > thr
 
     @staticmethod
     def tail_point(K: int, ecfg: EngineConfig, dp: bool = False) -> float:

@@ -370,7 +370,11 @@ def main(argv=None) -> int:
         # are in flight (serial placement); "allreduce" is what stays exposed after it
         merge_ms = {"snapshot": 0.0, "messages": mm[0], "allreduce": mm[1], "apply": mm[2],
                     "total": sum(mm[:3]), "prepass_overlap": mm[3], "bytes_per_rank": merger.comm_bytes,
-                    "buckets": len(merger.buckets())}
+                    "buckets": len(merger.buckets()),
+                    # where the next window's prepass ran: beside the merge (serial) or in
+                    # the rating's tail; chosen from a timed all-reduce for N > 1
+                    "prepass_placement": "beside the merge" if pipe.serial else "rating tail %.2f" % pipe.tail,
+                    "allreduce_probe_ms": pipe.allreduce_probe_ms}
     flags = rater.sticky_flags(dev).cpu()
     if int(flags.sum()):
         raise RuntimeError("dataflow error flags set during the benchmark: %s" % flags.tolist())

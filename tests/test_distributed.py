@@ -397,3 +397,21 @@ def test_lagged_merge_one_rank_is_exact():
     for name, tr in t["sweeps"]["1"]["tracks"].items():
         assert tr["null_mismatch"] == 0 and tr["dmu_max"] < 5e-3, (name, tr)
     assert t["sweeps"]["1"]["records_shared_mu"]["dmu_max"] < 5e-3
+
+
+def _probe(rank, size):
+    from analyzer_amd.parallel.comm import time_all_reduce
+
+    t = torch.ones(1 << 16) * (rank + 1)
+    ms = time_all_reduce(t)
+    return {"ms": torch.tensor([ms], dtype=torch.float64)}
+
+
+def test_all_reduce_probe_agrees_across_ranks(tmp_path):
+    """The DP placement probe (runtime/engine.py probe_placement) times a merge-sized
+    all-reduce; every rank gets the same (max) time, so every rank takes the same
+    prepass placement."""
+    res = run_ranks(_probe, 3, tmp_path)
+    assert float(res[0]["ms"]) > 0.0
+    for r in res[1:]:
+        assert torch.equal(r["ms"], res[0]["ms"])
