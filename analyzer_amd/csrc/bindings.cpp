@@ -195,7 +195,7 @@ std::tuple<Tensor, int64_t> levels_device(Tensor rec, int64_t K, int64_t num_pla
 }
 
 void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
-              Tensor workspace, Tensor ctrl, bool zero_ctrl, int64_t epoch_bump_ptr) {
+              Tensor workspace, Tensor ctrl, bool zero_ctrl, int64_t epoch_bump_ptr, int64_t sort_nt) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(link, "link", torch::kInt32, dev);
@@ -219,7 +219,7 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
                                    (size_t)workspace.numel(),
                                    reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()),
                                    stream_of(rec), zero_ctrl,
-                                   reinterpret_cast<int32_t*>((intptr_t)epoch_bump_ptr)),
+                                   reinterpret_cast<int32_t*>((intptr_t)epoch_bump_ptr), (int)sort_nt),
               "schedule");
   } else {
     TORCH_CHECK(ana::host_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,

@@ -39,7 +39,7 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
                       uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
                       hipStream_t s, int32_t* deps = nullptr, uint32_t* ctrl = nullptr, int nz = 0,
-                      int32_t* epoch_bump = nullptr);
+                      int32_t* epoch_bump = nullptr, int sort_nt = -1);
 // Device levelizer (levels.hip): level[m] = 0 for a match without state, else
 // 1 + the largest level of its players' previous matches -- the exact-DP rounds --
 // as a dataflow over a fresh schedule (link, deps zeroed; deps are consumed).
@@ -54,7 +54,7 @@ int launch_levels(int K, const int32_t* rec, const uint32_t* link, int32_t* deps
 // overflow: zeroed (reserved for schedule error reporting)
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s,
-                    bool zero_ctrl = false, int32_t* epoch_bump = nullptr);
+                    bool zero_ctrl = false, int32_t* epoch_bump = nullptr, int sort_nt = -1);
 
 // out must be the packed layout (one row per match: [s_mu | s_sig | delta |
 // m_mu | m_sig][2K], quality, status byte), else hipErrorInvalidValue.

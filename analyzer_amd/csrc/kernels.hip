@@ -319,7 +319,7 @@ sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uin
 
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s,
-                    bool zero_ctrl, int32_t* epoch_bump) {
+                    bool zero_ctrl, int32_t* epoch_bump, int sort_nt) {
   // zero_ctrl: also zero the executor's control words (overflow = ctrl[0], ctrl[1..15]) for
   // a rate launch that follows on this stream and then skips its own zeroing dispatch
   const int nz = zero_ctrl ? 16 : 1;
@@ -366,7 +366,7 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
   uint32_t* keys_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* vals_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   return launch_sched_sort(K, rec, M, (uint32_t)P, keys_a, vals_a, keys_b, vals_b, p, link, s, deps,
-                           overflow, nz, epoch_bump);
+                           overflow, nz, epoch_bump, sort_nt);
 }
 
 }  // namespace ana

@@ -622,7 +622,8 @@ static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits,
 
 int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
                       uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
-                      hipStream_t s, int32_t* deps, uint32_t* ctrl, int nz, int32_t* epoch_bump) {
+                      hipStream_t s, int32_t* deps, uint32_t* ctrl, int nz, int32_t* epoch_bump,
+                      int sort_nt) {
   const int64_t n = M * 2 * K;
   if (n <= 0) return 0;
   if (n > kMaxSlots) return (int)hipErrorInvalidValue;
@@ -643,7 +644,8 @@ int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players
   const char* rb_e = getenv("ANA_SORT_RB");
   const char* nt_e = getenv("ANA_SORT_NT");
   const int rb_env = rb_e ? atoi(rb_e) : 8;
-  const int nt = nt_e ? atoi(nt_e) : 0;
+  // sort_nt >= 0: the caller's choice (WindowPipeline: loads-only between DP merges)
+  const int nt = nt_e ? atoi(nt_e) : sort_nt >= 0 ? sort_nt : 0;
   const bool wide = bits <= 20 && rb_env == 10;
   switch (K) {
 #define ANA_SORT_CASE(k)                                                                         \

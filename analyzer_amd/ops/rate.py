@@ -260,7 +260,7 @@ class BatchRater:
     # ------------------------------------------------------------- schedule
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
                  tag: str = "", zero_ctrl: bool = False,
-                 epoch_bump: Optional[torch.Tensor] = None) -> Schedule:
+                 epoch_bump: Optional[torch.Tensor] = None, sort_nt: int = -1) -> Schedule:
         """Dependency structure of a window (K5): per slot the match of its
         player's next occurrence and whether it occurred earlier (``link``), and
         per match the completion counter ``deps`` (see ``Schedule``).  The device
@@ -270,7 +270,9 @@ class BatchRater:
         schedule also zeroes the executor's control words for the launch that
         follows it on the same stream -- never from a side stream, where a rate
         launch may be using them.  ``epoch_bump``: a device int32 launch epoch
-        (graph replays) the schedule increments, saving the bump its own dispatch."""
+        (graph replays) the schedule increments, saving the bump its own dispatch.
+        ``sort_nt``: non-temporal accesses of the radix sort (0 none, 1 all, 2 loads
+        only; -1: ANA_SORT_NT or none) -- ANA_SORT_NT, when set, wins."""
         M = rec.shape[0]
         dev = rec.device
         link = self._buffer(dev, "link" + tag, M * 2 * K, torch.int32).view(M, 2 * K)
@@ -284,7 +286,7 @@ class BatchRater:
             ctrl = torch.empty(0, dtype=torch.int32)
         bump = epoch_bump.data_ptr() if epoch_bump is not None and rec.is_cuda else 0
         native().schedule(rec, K, num_players, link, deps, ws, ctrl, bool(zero_ctrl and rec.is_cuda),
-                          bump)
+                          bump, int(sort_nt))
         return Schedule(link, deps)
 
     # ----------------------------------------------------------------- rate

@@ -86,6 +86,11 @@ class WindowPipeline:
         # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail)
         self.tail = (float(signal_at) if signal_at > 0 else 0.0) if self.serial else \
             self.tail_point(self.K, self.ecfg, dp)
+        # a prepass in the rating's tail between DP merges streams its sort input with
+        # non-temporal loads (ANA_SORT_NT=2), so it evicts less of the roster the
+        # executor's drain reads: eight 1.25M windows with forced merges 9.03 vs 9.30 ms
+        # (profiles/r4/merge_nt_and_sort_nt.log); a whole window gains nothing (8.00 vs 7.98)
+        self.sort_nt = 2 if dp and not self.serial else -1
         self._signal = 0
         self._seq = 0
         self.side = self._side_stream() if self.cuda else None
@@ -208,7 +213,7 @@ class WindowPipeline:
                 native().stream_wait_value64(side.cuda_stream, self._signal, self._seq)
             if self._free[self._set] is not None:  # previous user of this buffer set is done
                 side.wait_event(self._free[self._set])
-            sched = self.rater.schedule(rec, self.K, self.roster.num_players, tag=tag)
+            sched = self.rater.schedule(rec, self.K, self.roster.num_players, tag=tag, sort_nt=self.sort_nt)
             ready = torch.cuda.Event()
             ready.record(side)
         used = self._set
