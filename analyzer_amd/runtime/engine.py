@@ -79,7 +79,7 @@ class WindowPipeline:
         # DP over real collectives: the placement depends on what one merge's
         # all-reduce costs on this interconnect (probe_placement)
         self.allreduce_probe_ms: Optional[float] = None
-        if dp and self.cuda and self.ecfg.prepass_serial is None and self.K < 5 and \
+        if dp and self.cuda and self.ecfg.prepass_serial is None and \
                 getattr(merger, "world", 1) > 1 and not getattr(merger, "lag", False):
             self.serial = self.probe_placement(merger, self.ecfg)
         # serial prepass: nothing to overlap, no tail signal -- unless a caller wants the
@@ -129,8 +129,9 @@ class WindowPipeline:
         return K < 5 and not dp
 
     def probe_placement(self, merger, ecfg: EngineConfig) -> bool:
-        """1v1-4v4 windows between DP merges: serial placement (the next prepass on its
-        own stream beside the merge's all-reduces) or the tail overlap.  On one GPU
+        """Windows between DP merges: serial placement (the next prepass on its own
+        stream beside the merge's all-reduces) or the tail overlap (5v5 too: between
+        merges its windows are short, k = 16 at N = 8, and so is their prepass).  On one GPU
         (forced merges, no collective) the tail wins by ~0.04 ms per window
         (profiles/r3/dp_prepass_placement_k8.log: 9.54 vs 9.87 ms per 8 windows), but
         there the all-reduce takes no time; with N ranks it is exposed in the tail
