@@ -40,12 +40,14 @@ namespace ana {
 // B per player on every start read and write (-26 % merge traffic).
 constexpr int kLanesPerPlayer = kGranules;  // 8
 
-// The window-start base rows and the message operands are touched once per merge.
-// ANA_MERGE_NT=1 (build time) gives them non-temporal accesses, to keep the roster in
-// the Infinity Cache for the next rating; measured neutral (eight forced merges per
-// step 9.33 vs 9.29-9.30 ms, profiles/r4/merge_nt_and_sort_nt.log), so plain by default.
+// The window-start base rows and the message operands are touched once per merge:
+// non-temporal accesses keep them from displacing the roster, which the next rating
+// reads from the Infinity Cache.  It pays together with the loads-only non-temporal
+// sort of the prepass in the rating's tail (runtime/engine.py sort_nt): eight forced
+// merges per step 9.08-9.13 ms with both, 9.32-9.40 with either one or neither
+// (profiles/r4/merge_nt_and_sort_nt.log).  ANA_MERGE_NT=0 (build time): plain accesses.
 #ifndef ANA_MERGE_NT
-#define ANA_MERGE_NT 0
+#define ANA_MERGE_NT 1
 #endif
 typedef float merge_f2 __attribute__((ext_vector_type(2)));
 typedef int merge_i2 __attribute__((ext_vector_type(2)));

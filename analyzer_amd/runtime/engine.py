@@ -86,11 +86,12 @@ class WindowPipeline:
         # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail)
         self.tail = (float(signal_at) if signal_at > 0 else 0.0) if self.serial else \
             self.tail_point(self.K, self.ecfg, dp)
-        # a prepass in the rating's tail between DP merges streams its sort input with
-        # non-temporal loads (ANA_SORT_NT=2), so it evicts less of the roster the
-        # executor's drain reads: eight 1.25M windows with forced merges 9.03 vs 9.30 ms
-        # (profiles/r4/merge_nt_and_sort_nt.log); a whole window gains nothing (8.00 vs 7.98)
-        self.sort_nt = 2 if dp and not self.serial else -1
+        # a prepass in the rating's tail streams its sort input with non-temporal loads
+        # (ANA_SORT_NT=2), so it evicts less of the roster the executor's drain reads:
+        # eight 1.25M windows with forced merges 9.08-9.13 vs 9.32-9.40 ms (with the merge
+        # kernels' non-temporal operands), config 3 20.15-20.18 vs 20.26-20.34 ms; a serial
+        # prepass gains nothing (config 2: 8.00 vs 7.98; profiles/r4/merge_nt_and_sort_nt.log)
+        self.sort_nt = 2 if not self.serial else -1
         self._signal = 0
         self._seq = 0
         self.side = self._side_stream() if self.cuda else None
