@@ -81,7 +81,7 @@ class WindowPipeline:
         self.allreduce_probe_ms: Optional[float] = None
         if dp and self.cuda and self.ecfg.prepass_serial is None and \
                 getattr(merger, "world", 1) > 1 and not getattr(merger, "lag", False):
-            self.serial = self.probe_placement(merger, self.ecfg)
+            self.serial = self.probe_placement(merger)
         # serial prepass: nothing to overlap, no tail signal -- unless a caller wants the
         # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail)
         self.tail = (float(signal_at) if signal_at > 0 else 0.0) if self.serial else \
@@ -129,7 +129,7 @@ class WindowPipeline:
             return ecfg.prepass_serial
         return K < 5 and not dp
 
-    def probe_placement(self, merger, ecfg: EngineConfig) -> bool:
+    def probe_placement(self, merger) -> bool:
         """Windows between DP merges: serial placement (the next prepass on its own
         stream beside the merge's all-reduces) or the tail overlap (5v5 too: between
         merges its windows are short, k = 16 at N = 8, and so is their prepass).  On one GPU
