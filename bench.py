@@ -71,7 +71,7 @@ def parse(argv=None):
     ap.add_argument("--telemetry-mode", default="auto", choices=["auto", "overlap", "fused", "separate", "tail"],
                     help="config 4: auto = the rating launch takes the telemetry and fuses it up to "
                          "ANA_TELE_FUSE_MAX matches (worker batches; scripts/tele_batch.py), above that "
-                         "(10M windows) the MFMA kernel as in tail, from 0.8; fused = always inline in the rating "
+                         "(10M windows) the MFMA kernel as in tail, from 0.4; fused = always inline in the rating "
                          "groups; separate = the MFMA kernel after the rating on the same stream; "
                          "overlap = the MFMA kernel co-runs with the rating on its own stream; "
                          "tail = the MFMA kernel of window i starts on its own stream once the rating of "
@@ -263,17 +263,18 @@ def main(argv=None) -> int:
         tele_path = "fused (inline)"
     if tele is not None and auto_mode and not rater.fuses((tele[0].evoff, tele[0].events, stats), Mw):
         tele_path = "MFMA kernel after the rating (launch > ANA_TELE_FUSE_MAX)"
-        # window-sized launches: the MFMA kernel after the rating, started on its own
-        # stream once the rating has claimed 0.8 of its chunks (beside the drain and
-        # the next prepass): 9.69 ms against 9.85 for the kernel behind the rating
-        # (profiles/r4/telemetry_count_row_and_tail.log); needs hipStreamWaitValue64
+        # window-sized launches: the MFMA kernel on its own stream, started once the
+        # rating has claimed 0.4 of its chunks (beside the rest of the rating, its drain
+        # and the next prepass): 9.54-9.56 ms against 9.67-9.70 from 0.8 and 9.85 for the
+        # kernel behind the rating (profiles/r4/config4_tail_point_and_c3_warm.log,
+        # telemetry_count_row_and_tail.log); needs hipStreamWaitValue64
         from analyzer_amd.ops.native import native as _native
 
         if _native().can_wait_value(dev.index or 0):
             args.telemetry_mode = "tail"
             tele_path = ("MFMA kernel on its own stream from %s of the rating's chunks (launch > "
-                         "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.8"))
-    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.8 if auto_mode else 0.9)) \
+                         "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.4"))
+    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.4 if auto_mode else 0.9)) \
         if tele is not None and args.telemetry_mode == "tail" else 0.0
     pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
