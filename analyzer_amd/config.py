@@ -165,6 +165,10 @@ class EngineConfig:
                                       on between DP merges (short windows: k = 8 forced merges 9.30 vs
                                       9.53 ms), off for whole windows (8.02 either way)
     ANA_MERGE_BUCKET_MB     16        sweep-merge bucket size (parallel/sweep.py)
+    ANA_DP_SERIAL_AR_US     40        DP with N > 1 ranks: the next prepass runs beside the merge when one
+                                      merge-sized all-reduce (timed when the pipeline is built, max over
+                                      ranks) takes longer than this, else in the rating's tail
+                                      (runtime/engine.py probe_placement)
     COMM_DTYPE              fp32      sweep-merge message precision (bench.py, rerate)
     SWEEPS                  1         causal sweeps per window (bench.py, rerate)
     ANA_DIST_BACKEND        nccl      process group backend (gloo: N ranks on one GPU)
