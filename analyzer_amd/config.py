@@ -179,8 +179,6 @@ class EngineConfig:
     ANA_RATE_LOCAL          1         executor: LDS hand-off of successors the producing wave holds
     ANA_RATE_DIAG           0         executor timing build: per-phase clocks in ctrl[20..47] (ops/rate.diag)
     ANA_RATE_TIGHT          -1        executor: 2K lanes per match instead of the next power of two (-1 auto)
-    ANA_RATE_SPEC           0         executor: idle lane groups take matches one dependency short of
-                                      ready and rate them when their granules are already fresh
     ANA_TELE_FUSED_TAIL     0         fused telemetry only after the executor's chunks are drained
     ANA_TELE_ROLE           -1        fused telemetry: -1 = inline, each lane group folds the events of
                                       the match it rates (11.4 ms per config 4 step); N > 0 = one wave in
@@ -215,7 +213,6 @@ class EngineConfig:
     rate_local: int = 1
     rate_diag: int = 0
     rate_tight: int = -1
-    rate_spec: int = 0
     tele_fused_tail: int = 0
     tele_role: int = -1
     tele_fuse_max: int = 262_144
@@ -230,9 +227,9 @@ class EngineConfig:
     }
 
     def rate_knobs(self) -> list:
-        """[idle, local, diag, tight, tele_fused_tail, tele_role, spec] for the native launch."""
+        """[idle, local, diag, tight, tele_fused_tail, tele_role] for the native launch."""
         return [self.rate_idle, self.rate_local, self.rate_diag, self.rate_tight, self.tele_fused_tail,
-                self.tele_role, self.rate_spec]
+                self.tele_role]
 
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "EngineConfig":
@@ -256,7 +253,6 @@ class EngineConfig:
             rate_local=int(_env(env, "ANA_RATE_LOCAL") or 1),
             rate_diag=int(_env(env, "ANA_RATE_DIAG") or 0),
             rate_tight=int(_env(env, "ANA_RATE_TIGHT") or -1),
-            rate_spec=int(_env(env, "ANA_RATE_SPEC") or 0),
             tele_fused_tail=int(_env(env, "ANA_TELE_FUSED_TAIL") or 0),
             tele_role=int(_env(env, "ANA_TELE_ROLE") or -1),
             tele_fuse_max=int(_env(env, "ANA_TELE_FUSE_MAX") or 262_144),

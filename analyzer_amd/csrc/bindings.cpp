@@ -230,8 +230,8 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
 }
 
 // knobs (EngineConfig, config.py): [rate_idle, rate_local, rate_diag, rate_tight,
-// tele_fused_tail, tele_role, rate_spec] -- executor / fused-telemetry tuning, per BatchRater
-constexpr size_t kKnobs = 7;
+// tele_fused_tail, tele_role] -- executor / fused-telemetry tuning, per BatchRater
+constexpr size_t kKnobs = 6;
 
 static ana::TelemetryParams telemetry_params(const Tensor& evoff, const Tensor& events,
                                              const Tensor& stats, int64_t M, int64_t K,
@@ -264,7 +264,7 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
           int64_t progress, int64_t progress_value, int64_t progress_at, int64_t epoch_ptr,
           int64_t chunk_len, bool ctrl_ready, std::vector<int64_t> knobs) {
   const auto dev = rec.device();
-  TORCH_CHECK(knobs.size() == kKnobs, "knobs must be [idle, local, diag, tight, tele_fused_tail, tele_role, spec]");
+  TORCH_CHECK(knobs.size() == kKnobs, "knobs must be [idle, local, diag, tight, tele_fused_tail, tele_role]");
   check(rec, "rec", torch::kInt32, dev);
   check(state, "state", torch::kFloat32, dev);
   check(attrs, "attrs", torch::kFloat32, dev);
@@ -310,7 +310,6 @@ void rate(Tensor rec, int64_t K, Tensor link, Tensor deps, Tensor state, Tensor 
   prm.local_handoff = (int32_t)knobs[1];
   prm.diag = (int32_t)knobs[2];
   prm.tight_groups = (int32_t)knobs[3];
-  prm.speculate = (int32_t)knobs[6];
   prm.progress = reinterpret_cast<uint64_t*>((intptr_t)progress);
   prm.progress_value = (uint64_t)progress_value;
   prm.progress_at = progress_at;

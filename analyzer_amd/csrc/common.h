@@ -86,8 +86,6 @@ struct RateParams {
                                // through an LDS counter, not the global one (ANA_RATE_LOCAL, default 1)
   int32_t diag;                // dataflow: 1 = the timing build (ANA_RATE_DIAG): wait/iteration
                                // clocks in ctrl[20..27]
-  int32_t speculate;           // dataflow: idle groups take matches one dependency short of ready
-                               // and rate them if their granules are already fresh (ANA_RATE_SPEC)
   // Tail signal: once chunks from progress_at on are being claimed (every
   // earlier chunk is claimed, the launch is in its tail), waves store
   // progress_value to *progress (signal memory a side stream waits on with

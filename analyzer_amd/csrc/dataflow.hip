@@ -56,10 +56,6 @@
 namespace ana {
 
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight
-#ifndef ANA_EARLY_NOTIFY
-#define ANA_EARLY_NOTIFY 0
-#endif
-constexpr bool kEarlyNotify = ANA_EARLY_NOTIFY != 0;
 // K8 inline telemetry: events per match loaded with the batch's granules (more go
 // through a remainder loop after the rating); per group lane ceil(64 / G) 8-B loads
 constexpr int kTeleInline = 64;
@@ -71,7 +67,6 @@ struct Batch {
   int my_h = -1, my_bit = 0, mode = 0, n0 = 0, n1 = 0, rank0 = 1, rank1 = 1, first = 0, prevdup = -1;
   int32_t id = -1;
   bool inr = false, islast = false, own = false, any_dup = false;
-  bool spec = false;  // taken one dependency short (ANA_RATE_SPEC): rated only if its granules are fresh
   uint32_t lk0 = kNoMatch;  // schedule link (common.h): next match | has-earlier
   v4i gs = {0, 0, 0, 0}, gm = {0, 0, 0, 0};
   // K8 inline telemetry (TelemetryParams::role_stride < 0): the match's event count, a
@@ -148,10 +143,9 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_progress = 0;
   const bool local_ok = prm.local_handoff != 0;
-  const bool spec_on = prm.speculate != 0;
   // hand-off statistics (wave-uniform counts, added to ctrl[26..27] at exit); stale
-  // reads retried (ctrl[14]), speculative groups and those of them still stale (ctrl[48..49])
-  uint32_t n_local = 0, n_global = 0, n_stale = 0, n_spec = 0, n_spec_stale = 0;
+  // reads retried (ctrl[14])
+  uint32_t n_local = 0, n_global = 0, n_stale = 0;
   // timing build: clocks of the iterations that rated something, split at the wait
   uint64_t d_issue = 0, d_wait = 0, d_after = 0, d_it0 = 0;
   uint64_t d_t[4] = {0, 0, 0, 0}, d_p[5] = {0, 0, 0, 0, 0};  // after-phase split (timing build)
@@ -277,14 +271,12 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // ---------------------------------------------- (2) readiness from the last poll
     // one unconditional LDS read: a free slot's stale count is masked by pend = 0,
     // and without local hand-off the counts stay 0
-    uint64_t ready[kH], near[kH];
+    uint64_t ready[kH];
     {
       const hvec lv = lloc[wv][lane];
 #pragma unroll
-      for (int h = 0; h < kH; ++h) {
+      for (int h = 0; h < kH; ++h)
         ready[h] = __ballot(dval[h] != kNone && dval[h] + lv[h] == need[h]) & pend[h];
-        near[h] = spec_on ? __ballot(dval[h] != kNone && dval[h] + lv[h] + 1u == need[h]) & pend[h] : 0ull;
-      }
       if constexpr (DIAG) {
         uint32_t nn = 0, np = 0;
 #pragma unroll
@@ -312,19 +304,13 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // oldest chunk first) sat on every hop.  Chunks go in slot order: a wave
     // rarely has more ready matches than groups (2-3.4 per iteration on the
     // bench), so age order buys nothing measurable.
+    // (Speculatively assigning matches one dependency short to idle groups was
+    // measured slower -- 5 % of them fresh, window +3 %, profiles/r4/executor_speculation.log
+    // -- and removed in round 5.)
     int my_h = -1, my_bit = 0, nassigned = 0;
-    bool my_spec = false;
-    // Speculation (ANA_RATE_SPEC): groups left over after the ready matches take
-    // matches one dependency short at the last poll.  Their granules are gathered
-    // like any others; the freshness check below (the tags of the last writers) is
-    // exactly the readiness test, so one whose last producer has published since
-    // the poll is rated now -- a poll round trip and an iteration early -- and one
-    // whose producer has not goes back to pending like a stale read.
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
     for (int h = 0; h < kH; ++h) {
-      const uint64_t rdy = pass == 0 ? ready[h] : near[h];
+      const uint64_t rdy = ready[h];
       if (rdy != 0ull && nassigned < NG) {
         const uint32_t below = __builtin_amdgcn_mbcnt_hi(
             (uint32_t)(rdy >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rdy, 0u));
@@ -332,7 +318,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         if (mine) {
           int32_t w[SP];
           w[0] = cbase[h] + lane;
-          w[1] = (pass << 16) | (h << 8) | lane;
+          w[1] = (h << 8) | lane;
           w[2] = hrec[h][S];
           w[3] = hrec[h][S + 1];
 #pragma unroll
@@ -350,9 +336,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         const uint64_t taken = __ballot(mine);
         pend[h] &= ~taken;
         nassigned += __popcll(taken);
-        if (pass == 1) n_spec += (uint32_t)__popcll(taken);
       }
-    }
     }
     int32_t my_m = 0, my_id = -1;
     uint32_t my_m0 = 0u, my_m1 = 0u;
@@ -369,7 +353,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       my_m = pk.x;
       my_h = (pk.y >> 8) & 255;
       my_bit = pk.y & 255;
-      my_spec = (pk.y >> 16) & 1;
       my_m0 = (uint32_t)pk.z;
       my_m1 = (uint32_t)pk.w;
     }
@@ -392,7 +375,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       const int mode = meta_mode(m0);
       nb.my_h = my_h;
       nb.my_bit = my_bit;
-      nb.spec = my_spec;
       nb.m = m;
       nb.mode = mode;
       nb.n0 = meta_n0(m0);
@@ -564,10 +546,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     const uint64_t stale_lanes = __ballot(!fresh);
     if (stale_lanes) {
       const bool gstale = (stale_lanes & gmask) != 0ull;
-      // diagnostics (ctrl[14], [49] at exit): stale groups, and the speculative ones among them
-      const uint64_t leads = __ballot(gstale && j == 0);
-      n_stale += (uint32_t)__popcll(leads);
-      n_spec_stale += (uint32_t)__popcll(leads & __ballot(bt.spec));
+      // diagnostics (ctrl[14] at exit): stale groups
+      n_stale += (uint32_t)__popcll(__ballot(gstale && j == 0));
 #pragma unroll
       for (int h = 0; h < kH; ++h) {
         uint64_t back = 0ull;
@@ -578,11 +558,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         pend[h] |= uniform64(back);
       }
       if (gstale) my_h = -1;
-    }
-    if constexpr (kEarlyNotify) {
-      // early notify (experiment): the successors learn of this match before it is
-      // rated; a reader that arrives before the publish sees the old tags and retries
-      if (my_h >= 0 && inr && islast) notify(lk0 & kMatchMask);
     }
     if constexpr (INL) {
       // K8 inline, software-pipelined: this group's events are LOADED now (HBM, cold)
@@ -686,7 +661,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         __builtin_amdgcn_raw_buffer_store_b128(
             ok ? granule(nsm, stag, nss, succ) : granule(rsmu, stag, rssg, succ),
             rs, off, 0, 16);
-        if (!kEarlyNotify) notify(lk0 & kMatchMask);
+        notify(lk0 & kMatchMask);
       }
       if constexpr (DIAG) d_p[3] = __builtin_amdgcn_s_memrealtime();
       if (ok && prm.record_first_prior && own) {
@@ -903,9 +878,6 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
         __hip_atomic_fetch_add((gu32*)&ctrl[26], n_local, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_add((gu32*)&ctrl[27], n_global, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (n_stale) __hip_atomic_fetch_add((gu32*)&ctrl[14], n_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n_spec) __hip_atomic_fetch_add((gu32*)&ctrl[48], n_spec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (n_spec_stale)
-          __hip_atomic_fetch_add((gu32*)&ctrl[49], n_spec_stale, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if constexpr (DIAG) {
           // iterations that rated something: [20] count, [21] groups assigned, and
           // 100 MHz s_memrealtime ticks [22..23] issue (top of the loop -> the wait),
@@ -992,8 +964,7 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // ctrl[0] = schedule flag (kept), [1] timeout, [2] protocol, [3] retired chunks, [4..11] tickets,
   // [12] telemetry tile ticket, [13] malformed telemetry events, [14] stale reads retried,
   // [15] wave iterations; [16..18] sticky OR of [0..2] over launches (host clears);
-  // [20..25], [28..29] timing build (see the kernel), [26] local / [27] global hand-offs,
-  // [48] speculative groups, [49] of them stale (ANA_RATE_SPEC)
+  // [20..25], [28..29] timing build (see the kernel), [26] local / [27] global hand-offs
   // one-wave kernel rather than hipMemsetAsync: a 60-B fill at a 4-B offset becomes two
   // runtime fill dispatches (~4.7 us each on a 500-match micro-batch, profiles/)
   // the diagnostic words [20..51] are zeroed by every launch (not by the schedule's zeroing)

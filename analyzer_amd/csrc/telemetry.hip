@@ -46,14 +46,21 @@ gen_events_kernel(GenEventParams g, int64_t base, const int32_t* __restrict__ re
 // of the atomic version, 6 / 7 = of the MFMA version (ANA_TELE_DEBUG)
 template <int K, int D, int SPAN>
 __global__ void __launch_bounds__(256) telemetry_kernel(TelemetryParams tp, uint32_t* bad) {
+#if ANA_DIAG_BUILD
   // impl 3 (D 10) needs only its stage, decoded records and CSR: 1.9 KB per wave
   __shared__ float scratch[4][D == 10 ? kTeleRegsFloats : tele_scratch_floats<K>()];
+#else
+  __shared__ float scratch[4][tele_scratch_floats<K>()];
+#endif
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t tiles = (tp.num_matches + SPAN - 1) / SPAN;
   const int64_t t = (int64_t)blockIdx.x * 4 + wv;
   if (t >= tiles) return;
+#if ANA_DIAG_BUILD
   if constexpr (D == 10) telemetry_tile_regs<K, SPAN>(tp, t, threadIdx.x & 63, scratch[wv], bad);
-  else if constexpr (D >= 3) telemetry_tile_mfma<K, D - 3, SPAN>(tp, t, threadIdx.x & 63, scratch[wv], bad);
+  else
+#endif
+  if constexpr (D >= 3) telemetry_tile_mfma<K, D - 3, SPAN>(tp, t, threadIdx.x & 63, scratch[wv], bad);
   else telemetry_tile<K, D>(tp, t, threadIdx.x & 63, scratch[wv], bad);
 }
 
@@ -182,8 +189,8 @@ static void launch_tele_k(const TelemetryParams& tp, uint32_t* bad, hipStream_t 
 #endif
   if (impl == 0) return launch_tele<K, 0, kTeleTile>(tp, bad, s);
   if (impl == 2) return launch_tele_rows<K>(tp, bad, s);
-  if (impl == 3) return launch_tele<K, 10, kTeleMaxSpan>(tp, bad, s);
 #if ANA_DIAG_BUILD
+  if (impl == 3) return launch_tele<K, 10, kTeleMaxSpan>(tp, bad, s);
   const int d = dbg == 6 ? 6 : dbg == 7 ? 7 : 3;
 #define ANA_TELE_SPAN(sp)                                                                     \
   if (span == sp) {                                                                           \
@@ -204,8 +211,8 @@ static void launch_tele_k(const TelemetryParams& tp, uint32_t* bad, hipStream_t 
 
 int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_t s) {
   if (tp.num_matches <= 0) return 0;
-  // ANA_TELE_IMPL: 1 (default) one-hot MFMA, 0 LDS atomics, 2 one lane per stat row, 3 one-hot MFMA
-  // with register-built fragments (telemetry_tile_regs); ANA_TELE_SPAN: matches per
+  // ANA_TELE_IMPL: 1 (default) one-hot MFMA, 0 LDS atomics, 2 one lane per stat row, 3 (diagnostic
+  // library only) one-hot MFMA with register-built fragments (telemetry_tile_regs); ANA_TELE_SPAN: matches per
   // wave of the MFMA kernel (16, 32, 63); ANA_TELE_DEBUG (diagnostic, timing only):
   // atomic version 1 = no LDS adds, 2 = no count adds; MFMA version 6 = no MFMA, 7 = decode only
   const char* dbg_env = getenv("ANA_TELE_DEBUG");
@@ -216,7 +223,7 @@ int launch_telemetry(int K, const TelemetryParams& tp, uint32_t* bad, hipStream_
 #if !ANA_DIAG_BUILD
   // diagnostic / tuning variants are not in this library: refuse instead of
   // silently timing the production kernel under their name
-  if (dbg != 0 || span != kTeleMaxSpan) return (int)hipErrorNotSupported;
+  if (dbg != 0 || span != kTeleMaxSpan || impl == 3) return (int)hipErrorNotSupported;
 #endif
   switch (K) {
     case 1: launch_tele_k<1>(tp, bad, s, impl, dbg, span); break;

@@ -354,6 +354,7 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   if (bad) atomicAdd(bad_events, bad);
 }
 
+#if ANA_DIAG_BUILD  // measured slower (3.94 vs 1.82 ms, profiles/r4/telemetry_register_fragments.log): diagnostic library only
 // impl 3: the same one-hot GEMM with the fragments built in REGISTERS.  Each lane
 // decodes its event once (as above) into two words in LDS -- {row | column + 1 << 10 |
 // p2 << 16, p0 | p1 << 16} -- and every lane then reads the 8 records of its MFMA
@@ -534,5 +535,6 @@ __device__ __forceinline__ void telemetry_tile_regs(const TelemetryParams& tp, i
   }
   if (bad) atomicAdd(bad_events, bad);
 }
+#endif  // ANA_DIAG_BUILD
 
 }  // namespace ana

@@ -396,9 +396,7 @@ class BatchRater:
                 # held matches one dependency short of ready / pending, per worked iteration
                 "near_ready_per_worked_iteration": c[30] / worked if worked else 0.0,
                 "pending_per_worked_iteration": c[31] / worked if worked else 0.0,
-                # ANA_RATE_SPEC: one-short matches given to idle groups, and those whose
-                # granules were not fresh yet (returned to pending)
-                "speculative_groups": c[48], "speculative_stale": c[49], "stale_retries": c[14]}
+                "stale_retries": c[14]}
 
     def telemetry_errors(self, device) -> int:
         """Malformed telemetry events seen by the last fused launch (syncs)."""

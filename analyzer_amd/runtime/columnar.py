@@ -162,9 +162,9 @@ class _Cols:
 
 
 class ColumnarStore:
-    columnar_batches = True  # sessions build MatchBatch columns (load_batch / fetch_players)
-
     """The reference's tables as numpy columns (see the module doc)."""
+
+    columnar_batches = True  # sessions build MatchBatch columns (load_batch / fetch_players)
 
     # a session writes only at commit and a batch's load reads match structure and
     # the stored ratings of players no earlier batch touched, so the pipelined

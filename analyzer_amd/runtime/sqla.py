@@ -42,7 +42,7 @@ from sqlalchemy.orm import relationship, selectinload, sessionmaker
 
 from ..config import TRACK_COLUMNS
 from .objects import STAT_COLUMNS
-from .store import (ITEM_WRITE_COLS, PARTICIPANT_WRITE_COLS, PLAYER_RATING_COLS, SCHEMA, Asset,
+from .store import (ITEM_WRITE_COLS, PARTICIPANT_WRITE_COLS, PLAYER_RATING_COLS, SCHEMA, Asset, match_order,
                     _restore_match, _restore_player, _snap_match, _snap_player)
 
 class SqlAlchemyStore:
@@ -194,7 +194,7 @@ class SqlAlchemySession:
             def build(n=n):
                 t = self.store.tables[table]
                 q = select(*[t.c[c] for c in cols]).where(t.c[key].in_([bindparam("i%d" % k) for k in range(n)]))
-                return q.order_by(t.c[order_by].asc()) if order_by else q
+                return q.order_by(*[t.c[c].asc() for c in order_by]) if order_by else q
             c = self.store.sql(("in", table, cols, key, order_by, n), build, ["i%d" % k for k in range(n)])
             _execute(cur, c, [chunk])
             out += cur.fetchall()
@@ -208,10 +208,13 @@ class SqlAlchemySession:
         st = self.store
         cur = self._cursor()
         ids = list(set(ids))
+        # ORDER BY created_at as the reference (worker.py:176), with api_id breaking ties so
+        # that matches created at the same instant come out in one order on every path:
+        # the chunked statements here, their merge below, and load_matches' single query
         heads = self._select_in(cur, "match", ("api_id", "game_mode", "created_at"), "api_id", ids,
-                                order_by="created_at")
+                                order_by=("created_at", "api_id"))
         if len(ids) > 500:  # merge the chunks as ORDER BY would (NULL first, as MySQL / SQLite)
-            heads.sort(key=lambda r: (r[2] is not None, r[2] if r[2] is not None else 0))
+            heads.sort(key=lambda r: match_order(r[0], r[2]))
         mids = [h[0] for h in heads]
         pos = {m: i for i, m in enumerate(mids)}
         rosters: List[List[tuple]] = [[] for _ in mids]
@@ -389,7 +392,7 @@ class SqlAlchemySession:
         (columns, no objects) instead of this path."""
         s = self.store
         M, R, P = s.Match, s.Roster, s.Participant
-        q = (select(M).where(M.api_id.in_(list(set(ids)))).order_by(M.created_at.asc())
+        q = (select(M).where(M.api_id.in_(list(set(ids)))).order_by(M.created_at.asc(), M.api_id.asc())
              .options(selectinload(M.rosters).selectinload(R.participants)
                       .options(selectinload(P.player), selectinload(P.participant_items)),
                       selectinload(M.participants))

@@ -70,9 +70,20 @@ SCHEMA = [
     "CREATE TABLE IF NOT EXISTS participant_stats (api_id TEXT PRIMARY KEY, "
     "participant_api_id TEXT, kills REAL, deaths REAL, assists REAL, damage REAL, "
     "gold REAL, farm REAL, healing REAL, events REAL)",
+    # DOTELEMETRY commits look rows up and UPDATE them by participant (runtime/sqla.py
+    # _write_stats); a reflected database needs the same index for the same reason
+    "CREATE INDEX IF NOT EXISTS stats_participant ON participant_stats(participant_api_id)",
     "CREATE TABLE IF NOT EXISTS asset (api_id TEXT PRIMARY KEY, match_api_id TEXT, url TEXT)",
     "CREATE INDEX IF NOT EXISTS asset_match ON asset(match_api_id)",
 ]
+
+
+def match_order(api_id: str, created_at) -> tuple:
+    """Sort key of a batch: ``ORDER BY created_at ASC`` as the reference
+    (/root/reference/worker.py:176), NULL first as MySQL / SQLite order it, and the
+    api id breaking ties, so every store rates matches created at the same instant in
+    one order (runtime/sqla.py issues the same ORDER BY created_at, api_id)."""
+    return (created_at is not None, created_at if created_at is not None else 0.0, api_id)
 
 
 # ---------------------------------------------------------------- snapshots
@@ -163,7 +174,7 @@ class MemorySession(_SessionBase):
 
     def load_matches(self, ids: Iterable[str], chunksize: int = 100) -> Iterator[Match]:
         found = [self.store.matches[i] for i in set(ids) if i in self.store.matches]
-        found.sort(key=lambda m: m.created_at)
+        found.sort(key=lambda m: match_order(m.api_id, m.created_at))
         for m in found:
             self._track(m)
             yield m
@@ -233,7 +244,7 @@ class SqliteSession(_SessionBase):
             heads += self.conn.execute(
                 "SELECT api_id, game_mode, created_at FROM match WHERE api_id IN (%s)"
                 % ", ".join("?" * len(chunk)), chunk).fetchall()
-        heads.sort(key=lambda r: (r[2] is None, r[2]))
+        heads.sort(key=lambda r: match_order(r[0], r[2]))
         mids = [h[0] for h in heads]
         pos = {m: i for i, m in enumerate(mids)}
         rosters: List[List[tuple]] = [[] for _ in mids]
@@ -406,7 +417,7 @@ class SqliteSession(_SessionBase):
             heads += self.conn.execute(
                 "SELECT api_id, game_mode, created_at, trueskill_quality FROM match "
                 "WHERE api_id IN (%s)" % ", ".join("?" * len(chunk)), chunk).fetchall()
-        heads.sort(key=lambda r: (r[2] is None, r[2]))
+        heads.sort(key=lambda r: match_order(r[0], r[2]))
         # yield_per(chunksize): relationships are loaded one chunk of matches at a time
         for chunk in _chunks(heads, max(1, int(chunksize))):
             for m in self._build(chunk):

@@ -503,7 +503,15 @@ class Worker:
             if bad:
                 counts["fault_injected"] = len(bad)
                 matches = [m for m in matches if m.api_id not in self.cfg.fault_poison]
-        status = self._batched().rate(matches, telemetry=self._telemetry_spec()) if matches else []
+        rater = self._batched()
+        res = getattr(rater, "resident", None)
+        if res is not None and not self.cfg.resident:
+            # a ResidentBatchRater on a columnar-capable store without RESIDENT (the
+            # object path: SKIP_RATED, or a store without load_batch): the device rows
+            # cached by api id would go stale against other replicas' commits, so the
+            # batch's players are re-read from its objects, as ObjectBatchRater does
+            res.reset()
+        status = rater.rate(matches, telemetry=self._telemetry_spec()) if matches else []
         for m, s in zip(matches, status):
             name = R.STATUS_NAMES.get(s, str(s))
             counts[name] = counts.get(name, 0) + 1

@@ -276,12 +276,6 @@ def main(argv=None) -> int:
                          "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.4"))
     tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.4 if auto_mode else 0.9)) \
         if tele is not None and args.telemetry_mode == "tail" else 0.0
-    if os.environ.get("ANA_MAIN_PRIORITY") == "high":
-        # experiment: rating and merge kernels on a high-priority queue, so the CP
-        # dispatches their workgroups ahead of a co-running prepass on the side stream
-        hp = torch.cuda.Stream(dev, priority=-1)
-        hp.wait_stream(torch.cuda.current_stream(dev))
-        torch.cuda.set_stream(hp)
     pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     torch.cuda.synchronize()

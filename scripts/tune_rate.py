@@ -39,7 +39,6 @@ def main():
     ap.add_argument("--rated", type=float, default=1.0,
                     help="fraction of players with stored ratings (1.0 = steady state, no seeding)")
     ap.add_argument("--pattern", default="random", choices=["random", "serial", "disjoint"])
-    ap.add_argument("--spec", default="0", help="ANA_RATE_SPEC values to A/B (comma list)")
     ap.add_argument("--touch", default="0",
                     help="1: read the whole roster after the prepass, untimed, so the launch starts with "
                          "its rows warm in the Infinity Cache; 2: the same with the native warm_rows "
@@ -57,18 +56,16 @@ def main():
     out = RateResult.allocate(M, K, dev)
     results = {}
     sink = torch.zeros(256, dtype=torch.int32, device=dev)  # --touch 2 scratch
-    combos = [(int(b), int(i), int(t), int(lo), int(d), int(sp), int(sc)) for b in args.blocks.split(",")
+    combos = [(int(b), int(i), int(t), int(lo), int(d), int(sp)) for b in args.blocks.split(",")
               for i in args.idle.split(",") for t in args.tight.split(",")
-              for lo in args.local.split(",") for d in args.diag.split(",") for sp in args.touch.split(",")
-              for sc in args.spec.split(",")]
+              for lo in args.local.split(",") for d in args.diag.split(",") for sp in args.touch.split(",")]
     for rnd in range(args.rounds):
-        for b, idle, tg, loc, dg, sp, sc in combos:
-            os.environ["ANA_RATE_SPEC"] = str(sc)
+        for b, idle, tg, loc, dg, sp in combos:
             os.environ["ANA_RATE_TIGHT"] = str(tg)
             os.environ["ANA_RATE_IDLE"] = str(idle)
             os.environ["ANA_RATE_LOCAL"] = str(loc)
             os.environ["ANA_RATE_DIAG"] = str(dg)
-            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg) + ("/touch%d" % sp if sp else "") + ("/spec" if sc else "")
+            key = "b%d/i%d/t%d/local%d/diag%d" % (b, idle, tg, loc, dg) + ("/touch%d" % sp if sp else "")
             roster = make_roster(RosterSpec(num_players=P, seed=1, p_rated=args.rated,
                                             p_mode_rated=args.rated), device=dev)
             br = BatchRater(blocks=b)
@@ -98,8 +95,6 @@ def main():
                     " hand-offs local %d global %d" % (rnd, key, (t1 - t0) * 1e3, (t2 - t1) * 1e3, stale,
                                                        d["wave_iterations"], M / max(d["wave_iterations"], 1),
                                                        d["local_handoffs"], d["global_handoffs"]))
-            if sc:
-                line += " spec %d (stale %d)" % (d["speculative_groups"], d["speculative_stale"])
             if dg:
                 line += " | worked iterations %d (%.2f matches each): issue %.3f + wait %.3f + after %.3f us" % (
                     d["worked_iterations"], d["matches_per_worked_iteration"], d["issue_us"], d["wait_us"],

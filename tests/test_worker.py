@@ -255,6 +255,40 @@ def test_sqlite_store_roundtrip(tmp_path):
     reopened.close()
 
 
+def test_native_object_path_sees_other_replicas_commits():
+    """RESIDENT=false, SKIP_RATED=true on a columnar-capable store: the native engine
+    takes the object path with a ResidentBatchRater.  Its device rows must not
+    outlive the batch: a player another replica rated between two batches is read
+    back from the store, as the Python engine reads it (worker.py:441)."""
+    final = {}
+    for engine in ("python", "native"):
+        store = SqliteStore(":memory:")
+        w, matches, clock = make_worker(n=16, players=8, batch=8, engine=engine, store=store,
+                                        skip_rated=True, resident=False, seed=11)
+        ids = [m.api_id for m in sorted(matches, key=lambda m: m.created_at)]
+        publish(w.channel, "analyze", ids[:8])
+        w.rabbit.process_data_events()
+        assert w.stats.batches == 1
+        # another replica commits new ratings of every player between the batches
+        store.conn.execute("UPDATE player SET trueskill_mu = 2222.0, trueskill_sigma = 123.0 "
+                           "WHERE trueskill_mu IS NOT NULL")
+        store.conn.commit()
+        publish(w.channel, "analyze", ids[8:])
+        w.rabbit.process_data_events()
+        assert w.stats.batches == 2 and w.channel.acked == 16
+        final[engine] = store.conn.execute(
+            "SELECT api_id, trueskill_mu, trueskill_sigma FROM player ORDER BY api_id").fetchall()
+    py, nat = final["python"], final["native"]
+    assert [r[0] for r in py] == [r[0] for r in nat]
+    moved = 0
+    for (_, a, s), (_, b, t) in zip(py, nat):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert abs(a - b) < 2e-3 and abs(s - t) < 2e-3
+            moved += a != 2222.0
+    assert moved > 0  # the second batch rated players from the updated rows
+
+
 def test_env_config_names_and_defaults():
     cfg = WorkerConfig.from_env({})
     assert (cfg.batchsize, cfg.chunksize, cfg.idle_timeout, cfg.queue) == (500, 100, 1.0, "analyze")
@@ -332,6 +366,24 @@ def test_sqlalchemy_store_reflects_and_wires_relationships(tmp_path):
     assert p.roster[0].api_id == m.rosters[0].api_id and p.match[0].api_id == m.api_id
     assert s.assets(m.api_id)[0].url.startswith("https://telemetry.invalid/")
     s.close()
+
+
+def test_created_at_ties_break_by_api_id_on_every_sql_path(tmp_path):
+    """Matches created at the same instant come out in one order -- created_at, then
+    api_id -- from the ORM query, the chunked columnar SELECTs (> 500 ids) and the
+    stdlib SQLite store alike (runtime/sqla.py load_batch)."""
+    for store in (_sqla(tmp_path), SqliteStore(":memory:")):
+        players, ms = synth_objects(620, 400, team_size=3, seed=4)
+        for m in ms:  # three instants, ids interleaved across the chunk boundaries
+            m.created_at = float(int(m.api_id[1:]) % 3)
+        store.add_players(players)
+        store.add_matches(ms)
+        exp = [m.api_id for m in sorted(ms, key=lambda m: (m.created_at, m.api_id))]
+        ids = [m.api_id for m in ms][::-1]
+        s = store.session()
+        assert [m.api_id for m in s.load_matches(ids)] == exp
+        assert list(s.load_batch(ids).ids) == exp
+        s.close()
 
 
 @pytest.mark.parametrize("engine", ["python", "native"])
