@@ -98,6 +98,10 @@ def parse(argv=None):
                     help="N > 1: after timing, rank 0 measures the sweep-DP error of this run's "
                          "configuration against the exact sequential rating (parallel/accuracy.py, "
                          "N ranks simulated on its GPU) and reports it in the JSON line (0 = skip)")
+    ap.add_argument("--step-prepass", type=int, default=-1, choices=[-1, 0, 1],
+                    help="merges per step > 1: 1 = ONE schedule prepass per step over its k windows "
+                         "(links cut at the window boundaries, runtime/engine.py step_windows), 0 = a "
+                         "prepass per window (rounds 2-4), -1 = auto (1 unless --merge-lag)")
     ap.add_argument("--force-merge", action="store_true",
                     help="N = 1: run the merge kernels after every window anyway (messages + decode, "
                          "no collective) -- prices the DP merge's device work against --merges-per-step")
@@ -238,10 +242,20 @@ def main(argv=None) -> int:
     Mw = M // sub                        # matches per window and GPU
     roster = make_roster(RosterSpec(num_players=P, seed=args.seed), device=dev)
     spec = StreamSpec(team_size=K, seed=args.seed + 1, skew=args.skew)
+    # one prepass per step over its k windows (engine.step_windows) -- the unit of the
+    # timed loop is then a step, not a window
+    step_prepass = sub > 1 and args.config != 4 and (
+        args.step_prepass == 1 or (args.step_prepass < 0 and not args.merge_lag))
     n_windows = max(1, min(args.ring, (args.steps + args.warmup) * sub))
     total_windows = (args.steps + args.warmup) * sub
-    windows = [make_stream(spec, Mw, P, K=K, base=(w * world + rank) * Mw, device=dev)
-               for w in range(n_windows)]
+    if step_prepass:  # a ring of whole steps: window w of rank r as before, k windows per step
+        n_windows = max(1, min(args.ring, args.steps + args.warmup))
+        total_windows = args.steps + args.warmup
+        windows = [torch.cat([make_stream(spec, Mw, P, K=K, base=((s * sub + i) * world + rank) * Mw,
+                                          device=dev) for i in range(sub)]) for s in range(n_windows)]
+    else:
+        windows = [make_stream(spec, Mw, P, K=K, base=(w * world + rank) * Mw, device=dev)
+                   for w in range(n_windows)]
     rater = BatchRater()
     if args.telemetry_mode == "fused":
         rater.tele_fuse_max = 1 << 62  # inline at any launch size
@@ -279,7 +293,7 @@ def main(argv=None) -> int:
     pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     torch.cuda.synchronize()
-    prepared = {0: pipe.prepare(windows[0])}
+    prepared = {0: pipe.prepare(windows[0], window=Mw if step_prepass else 0)}
 
     tstream = None
     ttail = None
@@ -302,6 +316,9 @@ def main(argv=None) -> int:
         # rate window i, then the prepass of window i+1 on the side stream behind
         # its tail (every timed step carries exactly one prepass and one rating)
         nxt = windows[(i + 1) % n_windows]
+        if step_prepass:  # step i: its k windows with a merge after each, then step i+1's prepass
+            _, prepared[i + 1] = pipe.step_windows(prepared.pop(i), nxt, out=out)
+            return
         if ttail is not None:
             # the telemetry of window i beside the tail of its rating and the next
             # prepass; rating i + 1 waits for it (no co-run with a full executor)
@@ -334,7 +351,8 @@ def main(argv=None) -> int:
             _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out,
                                            telemetry=(t.evoff, t.events, stats))
 
-    for i in range(args.warmup * sub):
+    per = 1 if step_prepass else sub  # loop units per step
+    for i in range(args.warmup * per):
         step(i)
     pipe.finish()
     torch.cuda.synchronize()
@@ -344,7 +362,7 @@ def main(argv=None) -> int:
     if merger is not None:
         merger.timing = True  # stage events on the main stream (no syncs)
     t0 = time.perf_counter()
-    for i in range(args.warmup * sub, total_windows):
+    for i in range(args.warmup * per, total_windows):
         step(i)
     pipe.finish()  # lagged merge: the last window's sum applied (timed: it is part of the work)
     torch.cuda.synchronize()
@@ -375,7 +393,9 @@ def main(argv=None) -> int:
                     # where the next window's prepass ran: beside the merge (serial) or in
                     # the rating's tail; chosen from a timed all-reduce for N > 1
                     "prepass_placement": "beside the merge" if pipe.serial else "rating tail %.2f" % pipe.tail,
-                    "allreduce_probe_ms": pipe.allreduce_probe_ms}
+                    "allreduce_probe_ms": pipe.allreduce_probe_ms,
+                    # one schedule prepass per step over its k windows, or one per window
+                    "prepass_per": "step" if step_prepass else "window"}
     flags = rater.sticky_flags(dev).cpu()
     if int(flags.sum()):
         raise RuntimeError("dataflow error flags set during the benchmark: %s" % flags.tolist())

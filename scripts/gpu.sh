@@ -37,6 +37,8 @@
 #   workersql  the worker on the reflected SQLAlchemy store (columnar batch path), sqlite file
 #   dpacc      sweep-DP accuracy table (ranks x merges per step) incl. per-participant records
 #   dpcost     one-GPU DP step price: plain vs forced merges at k = 8 / 16
+#   dpstep     the same with one prepass per step (tail / serial placement, k = 8 / 16 / 32)
+#   gtest      a subset of the GPU tests (GTEST_K = pytest -k expression)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -59,6 +61,9 @@ for task in "$@"; do
       run build/build 900 $PY -m analyzer_amd.build_ext --force --jobs 16
       run build/build_diag 900 $PY -m analyzer_amd.build_ext --force --diag --jobs 16
       run build/import 120 $PY -c "from analyzer_amd.ops.native import native; native(); print('native ok')"
+      ;;
+    gtest)
+      run gtest/pytest 600 $PY -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${GTEST_K}"
       ;;
     tests)
       run tests/pytest 900 $PY -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
@@ -268,6 +273,21 @@ EOF
         done
       done
       for f in gpurun_out/dpcost/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
+      ;;
+    dpstep)  # one-GPU DP step price with ONE prepass per step (engine.step_windows) vs one per window,
+             # tail and serial placements, k = 8 / 16 / 32 (interleaved rounds)
+      for r in 1 2; do
+        run dpstep/plain_$r 300 $PY bench.py --steps 10 --warmup 2
+        for k in ${DPSTEP_K:-8 16 32}; do
+          run dpstep/k${k}_step_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step $k
+          ANA_PREPASS_SERIAL=1 run dpstep/k${k}_step_serial_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge \
+              --merges-per-step $k
+        done
+        run dpstep/k8_window_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step 8 --step-prepass 0
+        ANA_PREPASS_PIECES=0 run dpstep/k8_whole_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge \
+            --merges-per-step 8
+      done
+      for f in gpurun_out/dpstep/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
       ;;
     workersql)  # the streaming worker on the reflected SQLAlchemy store (sqlite file), native engine
       rm -f /tmp/wsa*.db*

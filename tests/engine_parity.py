@@ -96,3 +96,21 @@ def status_of(res) -> dict:
 
 def as_torch(x):
     return torch.as_tensor(x)
+
+
+def _stateful_slots(rec: np.ndarray, K: int, P: int):
+    """[M, 2K] bool: slots of matches that rate (the slots the schedule links) and
+    [M, 2K] bool: the first slot of each distinct player of such a match."""
+    S = 2 * K
+    ids, m0, m1 = rec[:, :S], rec[:, S].astype(np.int64), rec[:, S + 1].astype(np.int64)
+    n0, n1 = (m0 >> 8) & 0xFF, (m0 >> 16) & 0xFF
+    pos = np.array([j if j < K else j - K for j in range(S)])
+    inr = pos[None, :] < np.where(np.arange(S)[None, :] < K, n0[:, None], n1[:, None])
+    bad = (n0 > K) | (n1 > K) | (inr & ((ids < 0) | (ids >= P))).any(1)
+    rated = ((m0 & 0xFF) < 6) & ~bad & ((m0 >> 24) == 2) & (((m1 >> 2) & 1) == 0)
+    slots = rated[:, None] & inr
+    first = slots.copy()
+    for j in range(S):
+        for i in range(j):
+            first[:, j] &= ~(slots[:, i] & (ids[:, i] == ids[:, j]))
+    return slots, first
