@@ -506,10 +506,19 @@ void sweep_delta(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor vst, do
   }
 }
 
+// clamps: int32 [1] (empty: not counted) += the decoded tracks whose merged precision
+// hit the floor (sweep_core.h sweep_apply_track); the merger raises on it
+static uint32_t* clamp_ptr(const c10::optional<Tensor>& c, const torch::Device& dev) {
+  if (!c.has_value() || !c->defined() || c->numel() == 0) return nullptr;
+  check(*c, "clamps", torch::kInt32, dev);
+  return reinterpret_cast<uint32_t*>(c->data_ptr<int32_t>());
+}
+
 // decoded rows to s and, if s2 is non-empty, base rows [P, 16] (sweep_core.h) to s2
 void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor s2, Tensor vst,
-                 double unknown_sigma, bool scaled) {
+                 double unknown_sigma, bool scaled, const c10::optional<Tensor>& clamps) {
   const auto dev = s.device();
+  uint32_t* cl = clamp_ptr(clamps, dev);
   const int64_t P = s.size(0);
   check_rows(s0, "s0 (base rows)", P, ana::kBaseFloats, dev);
   check_rows(buf, "buf", P, 16, dev);
@@ -525,12 +534,12 @@ void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor s2, Tenso
   if (dev.is_cuda()) {
     check_hip(ana::launch_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(),
                                       attrs.data_ptr<float>(), s.data_ptr<float>(), p2,
-                                      vst.data_ptr<float>(), (float)unknown_sigma, scaled ? 1 : 0, P,
+                                      vst.data_ptr<float>(), (float)unknown_sigma, scaled ? 1 : 0, P, cl,
                                       stream_of(s)), "sweep_apply");
   } else {
     ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
                           s.data_ptr<float>(), p2, scaled, vst.data_ptr<float>(),
-                          (float)unknown_sigma, P);
+                          (float)unknown_sigma, P, cl);
   }
 }
 
@@ -567,8 +576,9 @@ void sweep_delta_packed(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor 
 }
 
 void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor s, Tensor s2, Tensor vst,
-                        double unknown_sigma) {
+                        double unknown_sigma, const c10::optional<Tensor>& clamps) {
   const auto dev = s.device();
+  uint32_t* cl = clamp_ptr(clamps, dev);
   const int64_t P = s.size(0);
   check_rows(s0, "s0 (base rows)", P, ana::kBaseFloats, dev);
   TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
@@ -588,7 +598,7 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
     check_hip(ana::launch_sweep_apply_packed(s0.data_ptr<float>(), msg.data_ptr(), cnt.data_ptr<int32_t>(),
                                              msg.scalar_type() == torch::kBFloat16 ? 1 : 0,
                                              attrs.data_ptr<float>(), s.data_ptr<float>(), p2,
-                                             vst.data_ptr<float>(), (float)unknown_sigma, P, stream_of(s)),
+                                             vst.data_ptr<float>(), (float)unknown_sigma, P, cl, stream_of(s)),
               "sweep_apply_packed");
     return;
   }
@@ -596,67 +606,7 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
   buf.slice(1, 0, 14).copy_(msg);
   buf.slice(1, 14, 16).copy_(cnt);
   ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
-                        s.data_ptr<float>(), p2, true, vst.data_ptr<float>(), (float)unknown_sigma, P);
-}
-
-// lagged merge boundary (parallel/sweep.py lag): c, y base rows [P, 16] (in/out), s the
-// roster [P, 32] (in/out), buf [P, 16] fp32: the summed messages in (has_sum), this
-// rank's message out
-void sweep_lag(Tensor c, Tensor buf, Tensor y, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma,
-               bool scaled, bool has_sum) {
-  const auto dev = s.device();
-  const int64_t P = s.size(0);
-  check_rows(c, "c (base rows)", P, ana::kBaseFloats, dev);
-  check_rows(buf, "buf", P, 16, dev);
-  check_rows(y, "y (base rows)", P, ana::kBaseFloats, dev);
-  check_rows(s, "state", P, ana::kRowFloats, dev);
-  check_rows(attrs, "attrs", P, 4, dev);
-  check(vst, "vst", torch::kFloat32, dev);
-  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
-  if (dev.is_cuda()) {
-    check_hip(ana::launch_sweep_lag(c.data_ptr<float>(), buf.data_ptr<float>(), y.data_ptr<float>(),
-                                    s.data_ptr<float>(), attrs.data_ptr<float>(), vst.data_ptr<float>(),
-                                    (float)unknown_sigma, scaled ? 1 : 0, has_sum ? 1 : 0, P, stream_of(s)),
-              "sweep_lag");
-    return;
-  }
-  ana::host_sweep_lag(c.data_ptr<float>(), buf.data_ptr<float>(), y.data_ptr<float>(), s.data_ptr<float>(),
-                      attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, scaled, has_sum, P);
-}
-
-// the same over compressed operands msg [P, 14] bf16/fp16 + cnt [P, 2] int32 (scaled);
-// the CPU path goes through the fp32 host mirror and torch's conversions
-void sweep_lag_packed(Tensor c, Tensor msg, Tensor cnt, Tensor y, Tensor s, Tensor attrs, Tensor vst,
-                      double unknown_sigma, bool has_sum) {
-  const auto dev = s.device();
-  const int64_t P = s.size(0);
-  check_rows(c, "c (base rows)", P, ana::kBaseFloats, dev);
-  TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
-                  msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
-              "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
-  check_rows(cnt, "cnt", P, 2, dev, torch::kInt32);
-  check_rows(y, "y (base rows)", P, ana::kBaseFloats, dev);
-  check_rows(s, "state", P, ana::kRowFloats, dev);
-  check_rows(attrs, "attrs", P, 4, dev);
-  check(vst, "vst", torch::kFloat32, dev);
-  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
-  if (dev.is_cuda()) {
-    check_hip(ana::launch_sweep_lag_packed(c.data_ptr<float>(), msg.data_ptr(), cnt.data_ptr<int32_t>(),
-                                           msg.scalar_type() == torch::kBFloat16 ? 1 : 0, y.data_ptr<float>(),
-                                           s.data_ptr<float>(), attrs.data_ptr<float>(), vst.data_ptr<float>(),
-                                           (float)unknown_sigma, has_sum ? 1 : 0, P, stream_of(s)),
-              "sweep_lag_packed");
-    return;
-  }
-  Tensor buf = torch::zeros({P, 16}, s.options());
-  if (has_sum) {
-    buf.slice(1, 0, 14).copy_(msg);
-    buf.slice(1, 14, 16).copy_(cnt);
-  }
-  ana::host_sweep_lag(c.data_ptr<float>(), buf.data_ptr<float>(), y.data_ptr<float>(), s.data_ptr<float>(),
-                      attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, true, has_sum, P);
-  msg.copy_(buf.slice(1, 0, 14));
-  cnt.copy_(buf.slice(1, 14, 16));
+                        s.data_ptr<float>(), p2, true, vst.data_ptr<float>(), (float)unknown_sigma, P, cl);
 }
 
 // ------------------------------------------------------------- C2 exchange
@@ -901,11 +851,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("telemetry", &telemetry, "K8: per-participant telemetry aggregation [M, 2K, 8]");
   m.attr("STAT_FEATURES") = ana::kStatFeatures;
   m.def("sweep_delta", &sweep_delta, "K9: per-rank natural-parameter messages for the DP merge");
-  m.def("sweep_apply", &sweep_apply, "K9: decode summed messages against the common start (-> s, s2)");
+  m.def("sweep_apply", &sweep_apply, "K9: decode summed messages against the common start (-> s, s2)",
+        py::arg("s0"), py::arg("buf"), py::arg("attrs"), py::arg("s"), py::arg("s2"), py::arg("vst"),
+        py::arg("unknown_sigma"), py::arg("scaled"), py::arg("clamps") = py::none());
   m.def("sweep_delta_packed", &sweep_delta_packed, "K9: messages straight into bf16/fp16 + int32 all-reduce operands");
-  m.def("sweep_apply_packed", &sweep_apply_packed, "K9: decode bf16/fp16 + int32 summed messages (-> s, s2)");
-  m.def("sweep_lag", &sweep_lag, "K9: one-window-late merge boundary (fp32 operands)");
-  m.def("sweep_lag_packed", &sweep_lag_packed, "K9: one-window-late merge boundary (bf16/fp16 + int32 operands)");
+  m.def("sweep_apply_packed", &sweep_apply_packed, "K9: decode bf16/fp16 + int32 summed messages (-> s, s2)",
+        py::arg("s0"), py::arg("msg"), py::arg("cnt"), py::arg("attrs"), py::arg("s"), py::arg("s2"), py::arg("vst"),
+        py::arg("unknown_sigma"), py::arg("clamps") = py::none());
   m.def("pack_rows", &pack_rows, "C2: changed rows of a round slice -> fixed-capacity [cap, 33] entries");
   m.def("check_round", &check_round, "C2 race detector: one round's matches share no player (flag |= 1)");
   m.def("unpack_rows", &unpack_rows, "C2: write gathered entries (id >= 0) into the roster, tags zeroed");

@@ -255,21 +255,14 @@ void host_sweep_delta(const float* s0, const float* a, const float* s, const flo
 }
 
 void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
-                      bool scaled, const float* vst, float unknown_sigma, int64_t P) {
+                      bool scaled, const float* vst, float unknown_sigma, int64_t P, uint32_t* clamps) {
   for (int64_t p = 0; p < P; ++p) {
     float ob[kBaseFloats];
     sweep_apply_player(s0 + p * kBaseFloats, buf + p * 16, attrs + p * 4, vst, unknown_sigma, scaled,
-                       s + p * kRowFloats, ob);
+                       s + p * kRowFloats, ob, clamps);
     if (s2)
       for (int k = 0; k < kBaseFloats; ++k) s2[p * kBaseFloats + k] = ob[k];
   }
-}
-
-void host_sweep_lag(float* c, float* buf, float* y, float* x, const float* attrs, const float* vst,
-                    float unknown_sigma, bool scaled, bool has_sum, int64_t P) {
-  for (int64_t p = 0; p < P; ++p)
-    sweep_lag_player(c + p * kBaseFloats, has_sum ? buf + p * 16 : nullptr, y + p * kBaseFloats,
-                     x + p * kRowFloats, attrs + p * 4, vst, unknown_sigma, scaled, buf + p * 16);
 }
 
 }  // namespace ana

@@ -32,10 +32,7 @@ int host_rate(int K, bool fp64, const int32_t* rec, float* state, const float* a
 namespace ana {
 void host_sweep_delta(const float* s0, const float* a, const float* s, const float* attrs,
                       const float* vst, float unknown_sigma, bool scaled, float* buf, int64_t P);
+// clamps (nullable): += decoded tracks whose merged precision hit the floor (sweep_core.h)
 void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
-                      bool scaled, const float* vst, float unknown_sigma, int64_t P);
-// lagged merge boundary (sweep_core.h sweep_lag_player); buf [P][16]: summed messages in
-// (has_sum), this rank's message out
-void host_sweep_lag(float* c, float* buf, float* y, float* x, const float* attrs, const float* vst,
-                    float unknown_sigma, bool scaled, bool has_sum, int64_t P);
+                      bool scaled, const float* vst, float unknown_sigma, int64_t P, uint32_t* clamps = nullptr);
 }  // namespace ana

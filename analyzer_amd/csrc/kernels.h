@@ -117,23 +117,18 @@ namespace ana {
 int launch_sweep_delta(const float* s0, const float* a, const float* s, const float* attrs,
                        const float* vst, float unknown_sigma, int scaled, float* buf, int64_t P,
                        hipStream_t st);
-// decoded rows to s and (s2 != nullptr) s2
+// decoded rows to s and (s2 != nullptr) s2; clamps (nullable): += decoded tracks whose
+// merged precision hit the floor (sweep_core.h sweep_apply_track), here and below
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
-                       const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st);
+                       const float* vst, float unknown_sigma, int scaled, int64_t P, uint32_t* clamps,
+                       hipStream_t st);
 // compressed merges: msg [P][14] bf16 (bf16 != 0) or fp16 + cnt [P][2] int32
 int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, const float* attrs,
                               const float* vst, float unknown_sigma, int bf16, void* msg, int32_t* cnt,
                               int64_t P, hipStream_t st);
 int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
                               const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
-                              int64_t P, hipStream_t st);
-// lagged merge boundary (sweep_core.h sweep_lag_player): c: common base rows (in/out),
-// buf / msg+cnt: summed messages in (has_sum) and this rank's message out, y: base rows
-// of the rank's window start (in/out), x: roster rows (in/out)
-int launch_sweep_lag(float* c, float* buf, float* y, float* x, const float* attrs, const float* vst,
-                     float unknown_sigma, int scaled, int has_sum, int64_t P, hipStream_t st);
-int launch_sweep_lag_packed(float* c, void* msg, int32_t* cnt, int bf16, float* y, float* x, const float* attrs,
-                            const float* vst, float unknown_sigma, int has_sum, int64_t P, hipStream_t st);
+                              int64_t P, uint32_t* clamps, hipStream_t st);
 // C2 exact-DP exchange (sweep.hip): fixed-capacity [cap][33] entries of changed rows
 int launch_pack_rows(const int32_t* rec, int K, int64_t m, const uint8_t* status, int64_t sstride,
                      const float* state, float* out, int64_t cap, hipStream_t st);

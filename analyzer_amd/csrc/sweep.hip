@@ -97,6 +97,14 @@ __device__ __forceinline__ TrackLane track_lane() {
   return TrackLane{gid / kLanesPerPlayer, (int)(gid % kLanesPerPlayer), lane & ~(kLanesPerPlayer - 1)};
 }
 
+// += the wave's clamped decodes (sweep_apply_track): one atomic from the first active
+// lane, only in the (rare) waves that clamped
+__device__ __forceinline__ void count_clamps(bool clamped, uint32_t* clamps) {
+  const uint64_t b = __ballot(clamped);
+  if (b && clamps && (int)(threadIdx.x & 63) == __builtin_ctzll(__ballot(true)))
+    atomicAdd(clamps, (uint32_t)__popcll(b));
+}
+
 // sum over the 8 lanes of a player's group (every lane gets it)
 __device__ __forceinline__ float group8_sum(float x) {
   x += __shfl_xor(x, 1);
@@ -142,18 +150,21 @@ __device__ __forceinline__ void lane_delta(const TrackLane& L, const float2* __r
 __device__ __forceinline__ void lane_apply(const TrackLane& L, const float2* __restrict__ s0, float dpi,
                                           float dtau, uint32_t lo, uint32_t hi,
                                           const float4* __restrict__ attrs, const float* vst,
-                                          float unknown_sigma, bool scaled, float4* s, float2* s2) {
+                                          float unknown_sigma, bool scaled, float4* s, float2* s2,
+                                          uint32_t* clamps) {
   const float2 c = merge_ld(s0 + L.p * kLanesPerPlayer + L.t);
   const float c0mu = __shfl(c.x, L.gbase), c0sg = __shfl(c.y, L.gbase);
   bool seeded;
   float seed_mu, seed_sig;
   lane_seed(attrs, L.p, vst, unknown_sigma, seeded, seed_mu, seed_sig);
   float mu = c.x, sg = c.y;  // granule 7: the spare floats of the base row
+  bool clamped = false;
   if (L.t < kTracks) {
     const uint32_t touched = L.t < 4 ? (lo >> (4 * L.t)) & 15u : (hi >> (4 * (L.t - 4))) & 15u;
     sweep_apply_track(L.t, c.x, c.y, c0mu, c0sg, dpi, dtau, touched, seeded, seed_mu, seed_sig, scaled,
-                      mu, sg);
+                      mu, sg, clamped);
   }
+  count_clamps(clamped, clamps);
   s[L.p * kLanesPerPlayer + L.t] = make_float4(mu, 0.f, sg, 0.f);
   if (s2) merge_st(s2 + L.p * kLanesPerPlayer + L.t, make_float2(mu, sg));
 }
@@ -178,12 +189,12 @@ sweep_delta_kernel(const float2* __restrict__ s0, const float2* a0, const float4
 __global__ void __launch_bounds__(256)
 sweep_apply_kernel(const float2* __restrict__ s0, const float2* __restrict__ buf,
                    const float4* __restrict__ attrs, float4* s, float2* s2, const float* __restrict__ vst,
-                   float unknown_sigma, int scaled, int64_t P) {
+                   float unknown_sigma, int scaled, int64_t P, uint32_t* clamps) {
   const TrackLane L = track_lane();
   if (L.p >= P) return;
   const float2 d = buf[L.p * kLanesPerPlayer + L.t];
   const uint32_t lo = (uint32_t)__shfl(d.x, L.gbase + kTracks), hi = (uint32_t)__shfl(d.y, L.gbase + kTracks);
-  lane_apply(L, s0, d.x, d.y, lo, hi, attrs, vst, unknown_sigma, scaled != 0, s, s2);
+  lane_apply(L, s0, d.x, d.y, lo, hi, attrs, vst, unknown_sigma, scaled != 0, s, s2, clamps);
 }
 
 // ------------------------------------------------- compressed (fp16 / bf16) messages
@@ -230,88 +241,14 @@ template <typename H>
 __global__ void __launch_bounds__(256)
 sweep_apply_packed_kernel(const float2* __restrict__ s0, const uint32_t* __restrict__ msg,
                           const int2* __restrict__ cnt, const float4* __restrict__ attrs, float4* s,
-                          float2* s2, const float* __restrict__ vst, float unknown_sigma, int64_t P) {
+                          float2* s2, const float* __restrict__ vst, float unknown_sigma, int64_t P,
+                          uint32_t* clamps) {
   const TrackLane L = track_lane();
   if (L.p >= P) return;
   const uint32_t w = L.t < kTracks ? merge_ld(msg + L.p * kTracks + L.t) : 0u;
   const int2 c = merge_ld(cnt + L.p);  // broadcast within the group
   lane_apply(L, s0, from_half_bits<H>(w & 0xffffu), from_half_bits<H>(w >> 16), (uint32_t)c.x,
-             (uint32_t)c.y, attrs, vst, unknown_sigma, true, s, s2);
-}
-
-// ------------------------------------------------------------ lagged merge
-// One pass per boundary of the one-window-late merge (sweep_core.h
-// sweep_lag_player has the algebra): C (common roster, base rows) += the summed
-// messages that arrived, this rank's message m = nat(X) - nat(Y) against it, and
-// Y = X = C + m for the next window.  The summed messages are read from the same
-// operands the message is written to: one buffer carries the previous boundary's
-// all-reduce result in and this boundary's all-reduce input out.
-__device__ __forceinline__ void lane_lag(const TrackLane& L, float2* C, float2* Y, float4* X,
-                                         const float4* __restrict__ attrs, const float* vst, float unknown_sigma,
-                                         bool scaled, bool has_sum, float sdp, float sdt, uint32_t slo,
-                                         uint32_t shi, float& dp, float& dt, float& lo, float& hi) {
-  const int64_t i = L.p * kLanesPerPlayer + L.t;
-  const float2 c = C[i], y = Y[i];
-  const float4 x = X[i];
-  bool seeded;
-  float seed_mu, seed_sig;
-  lane_seed(attrs, L.p, vst, unknown_sigma, seeded, seed_mu, seed_sig);
-  const float c0mu = __shfl(c.x, L.gbase), c0sg = __shfl(c.y, L.gbase);
-  float cm = c.x, cs = c.y;
-  if (has_sum && L.t < kTracks) {
-    const uint32_t touched = L.t < 4 ? (slo >> (4 * L.t)) & 15u : (shi >> (4 * (L.t - 4))) & 15u;
-    sweep_apply_track(L.t, c.x, c.y, c0mu, c0sg, sdp, sdt, touched, seeded, seed_mu, seed_sig, scaled, cm, cs);
-  }
-  const float n0mu = __shfl(cm, L.gbase), n0sg = __shfl(cs, L.gbase);
-  const float y0mu = __shfl(y.x, L.gbase), y0sg = __shfl(y.y, L.gbase);
-  bool touched = false;
-  dp = dt = 0.f;
-  if (L.t < kTracks)
-    sweep_lag_delta_track(L.t, cm, cs, n0mu, n0sg, y.x, y.y, y0mu, y0sg, x.x, x.z, seeded, seed_mu, seed_sig,
-                          scaled, dp, dt, touched);
-  const float field = touched ? (float)(1 << (4 * (L.t & 3))) : 0.f;
-  lo = group8_sum(L.t < 4 ? field : 0.f);
-  hi = group8_sum(L.t >= 4 ? field : 0.f);
-  float mu = cm, sg = cs;
-  if (L.t < kTracks) {
-    const uint32_t own = L.t < 4 ? ((uint32_t)lo >> (4 * L.t)) & 15u : ((uint32_t)hi >> (4 * (L.t - 4))) & 15u;
-    sweep_apply_track(L.t, cm, cs, n0mu, n0sg, dp, dt, own, seeded, seed_mu, seed_sig, scaled, mu, sg);
-  }
-  C[i] = make_float2(cm, cs);
-  Y[i] = make_float2(mu, sg);
-  X[i] = make_float4(mu, 0.f, sg, 0.f);
-}
-
-// fp32 operands: buf [P][16] (float2 per lane; lane 7 the touch fields)
-__global__ void __launch_bounds__(256)
-sweep_lag_kernel(float2* C, float2* buf, float2* Y, float4* X, const float4* __restrict__ attrs,
-                 const float* __restrict__ vst, float unknown_sigma, int scaled, int has_sum, int64_t P) {
-  const TrackLane L = track_lane();
-  if (L.p >= P) return;
-  const int64_t i = L.p * kLanesPerPlayer + L.t;
-  const float2 d = has_sum ? buf[i] : make_float2(0.f, 0.f);
-  const uint32_t slo = (uint32_t)__shfl(d.x, L.gbase + kTracks), shi = (uint32_t)__shfl(d.y, L.gbase + kTracks);
-  float dp, dt, lo, hi;
-  lane_lag(L, C, Y, X, attrs, vst, unknown_sigma, scaled != 0, has_sum != 0, d.x, d.y, slo, shi, dp, dt, lo, hi);
-  buf[i] = L.t < kTracks ? make_float2(dp, dt) : make_float2(lo, hi);
-}
-
-// bf16 / fp16 operands: msg [P][14] halves + cnt [P][2] int32 (as sweep_*_packed)
-template <typename H>
-__global__ void __launch_bounds__(256)
-sweep_lag_packed_kernel(float2* C, uint32_t* msg, int2* cnt, float2* Y, float4* X, const float4* __restrict__ attrs,
-                        const float* __restrict__ vst, float unknown_sigma, int has_sum, int64_t P) {
-  const TrackLane L = track_lane();
-  if (L.p >= P) return;
-  const uint32_t w = has_sum && L.t < kTracks ? msg[L.p * kTracks + L.t] : 0u;
-  const int2 c = has_sum ? cnt[L.p] : make_int2(0, 0);  // broadcast within the group
-  float dp, dt, lo, hi;
-  lane_lag(L, C, Y, X, attrs, vst, unknown_sigma, true, has_sum != 0, from_half_bits<H>(w & 0xffffu),
-           from_half_bits<H>(w >> 16), (uint32_t)c.x, (uint32_t)c.y, dp, dt, lo, hi);
-  if (L.t < kTracks)
-    msg[L.p * kTracks + L.t] = (uint32_t)to_half_bits<H>(dp) | ((uint32_t)to_half_bits<H>(dt) << 16);
-  else
-    cnt[L.p] = make_int2((int)lo, (int)hi);
+             (uint32_t)c.y, attrs, vst, unknown_sigma, true, s, s2, clamps);
 }
 
 static dim3 track_grid(int64_t P) {
@@ -335,39 +272,16 @@ int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, c
 
 int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
                               const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
-                              int64_t P, hipStream_t st) {
+                              int64_t P, uint32_t* clamps, hipStream_t st) {
   if (P <= 0) return 0;
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
                        reinterpret_cast<const uint32_t*>(msg), reinterpret_cast<const int2*>(cnt),
                        reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
-                       reinterpret_cast<float2*>(s2), vst, unknown_sigma, P);
+                       reinterpret_cast<float2*>(s2), vst, unknown_sigma, P, clamps);
   };
   if (bf16) args(sweep_apply_packed_kernel<__bf16>);
   else args(sweep_apply_packed_kernel<_Float16>);
-  return (int)hipGetLastError();
-}
-
-int launch_sweep_lag(float* c, float* buf, float* y, float* x, const float* attrs, const float* vst,
-                     float unknown_sigma, int scaled, int has_sum, int64_t P, hipStream_t st) {
-  if (P <= 0) return 0;
-  hipLaunchKernelGGL(sweep_lag_kernel, track_grid(P), dim3(256), 0, st, reinterpret_cast<float2*>(c),
-                     reinterpret_cast<float2*>(buf), reinterpret_cast<float2*>(y), reinterpret_cast<float4*>(x),
-                     reinterpret_cast<const float4*>(attrs), vst, unknown_sigma, scaled, has_sum, P);
-  return (int)hipGetLastError();
-}
-
-int launch_sweep_lag_packed(float* c, void* msg, int32_t* cnt, int bf16, float* y, float* x, const float* attrs,
-                            const float* vst, float unknown_sigma, int has_sum, int64_t P, hipStream_t st) {
-  if (P <= 0) return 0;
-  auto args = [&](auto kern) {
-    hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<float2*>(c),
-                       reinterpret_cast<uint32_t*>(msg), reinterpret_cast<int2*>(cnt), reinterpret_cast<float2*>(y),
-                       reinterpret_cast<float4*>(x), reinterpret_cast<const float4*>(attrs), vst, unknown_sigma,
-                       has_sum, P);
-  };
-  if (bf16) args(sweep_lag_packed_kernel<__bf16>);
-  else args(sweep_lag_packed_kernel<_Float16>);
   return (int)hipGetLastError();
 }
 
@@ -383,12 +297,13 @@ int launch_sweep_delta(const float* s0, const float* a, const float* s, const fl
 }
 
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
-                       const float* vst, float unknown_sigma, int scaled, int64_t P, hipStream_t st) {
+                       const float* vst, float unknown_sigma, int scaled, int64_t P, uint32_t* clamps,
+                       hipStream_t st) {
   if (P <= 0) return 0;
   hipLaunchKernelGGL(sweep_apply_kernel, track_grid(P), dim3(256), 0, st,
                      reinterpret_cast<const float2*>(s0), reinterpret_cast<const float2*>(buf),
                      reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
-                     reinterpret_cast<float2*>(s2), vst, unknown_sigma, scaled, P);
+                     reinterpret_cast<float2*>(s2), vst, unknown_sigma, scaled, P, clamps);
   return (int)hipGetLastError();
 }
 

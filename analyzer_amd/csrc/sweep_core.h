@@ -91,11 +91,25 @@ ANA_HD void sweep_delta_track(int t, float cmu, float csg, float c0mu, float c0s
 // One track t of the decode: (amu, asg) the common window-start value of the track,
 // (a0mu, a0sg) the start's shared value, (dpi, dtau) the summed messages, touched the
 // summed touch count of the track.  Returns the decoded (mu, sigma).
+//
+// clamped: the merged precision came out at or below zero (or not finite) and was
+// held at the floor -- a sigma x1000 / a meaningless mean that must never be written
+// silently.  The kernels count these into a sticky word the merger raises on
+// (parallel/sweep.py SweepMerger.check).  Where it comes from (root-caused in round
+// 5 on the host mirror, profiles/r5/lag_bf16_root_cause.log): the one-window-late
+// merge (rounds 4-5, removed) measured a rank's message against its own start Y,
+// which lacks the other ranks' evidence of the previous window -- their tau^2
+// dynamics included -- so Y's precision sat above the common roster C it was added
+// to.  The precision a match's dynamics removes grows with pi^2 tau^2, so eight ranks'
+// dynamics losses measured at Y's precision overshoot C's: 1 + sum r_pi -> 0 (-0.99
+// of C in one window for a player near sigma 100) and below.  The merge measures
+// every rank against the common start and keeps a wide margin (min 0.46-0.88).
 ANA_HD void sweep_apply_track(int t, float amu, float asg, float a0mu, float a0sg, float dpi, float dtau,
                               unsigned touched, bool seeded, float seed_mu, float seed_sig, bool scaled,
-                              float& mu, float& sg) {
+                              float& mu, float& sg, bool& clamped) {
   mu = amu;
   sg = asg;
+  clamped = false;
   const bool live = amu == amu ? (dpi != 0.f || dtau != 0.f) : touched != 0u;
   if (!live) return;
   float bm, bs;
@@ -103,7 +117,8 @@ ANA_HD void sweep_apply_track(int t, float amu, float asg, float a0mu, float a0s
   if (!based) return;
   if (scaled) {  // pi = pi_b (1 + sum r_pi), mu = mu_b + sum r_tau / (1 + sum r_pi)
     float ratio = 1.f + dpi;
-    ratio = ratio > 1e-6f ? ratio : 1e-6f;
+    clamped = !(ratio > 1e-6f);
+    ratio = clamped ? 1e-6f : ratio;
     mu = bm + dtau / ratio;
     sg = bs / sqrtf(ratio);
   } else {
@@ -111,103 +126,10 @@ ANA_HD void sweep_apply_track(int t, float amu, float asg, float a0mu, float a0s
     nat_params(bm, bs, pb, tb);
     float pi = pb + dpi;
     const float tau = tb + dtau;
-    pi = pi > 1e-12f ? pi : 1e-12f;  // merged precision never below "no information"
+    clamped = !(pi > 1e-12f);
+    pi = clamped ? 1e-12f : pi;  // merged precision never below "no information"
     mu = tau / pi;
     sg = 1.f / sqrtf(pi);
-  }
-}
-
-// ---------------------------------------------------------------- lagged merge
-// The one-window-late merge (parallel/sweep.py, ``lag``): rank r rates window b from
-// Y_b = C_{b-1} + m_{b-1}^r, where C_b = start + every rank's messages of windows
-// < b is the COMMON roster and m_w^r = nat(X_w) - nat(Y_w) rank r's own evidence of
-// window w; the all-reduce of m_b runs while window b+1 rates.  At the boundary
-// after window b one pass per player does
-//   C_b     = C_{b-1} + sum_q m_{b-1}^q       (sweep_apply_track, the arrived sum)
-//   m_b^r   = nat(X_b) - nat(Y_b)             (this function; base B from C_b)
-//   Y_{b+1} = C_b + m_b^r                      (sweep_apply_track, own message only)
-// so Y_{b+1} = X_b + the other ranks' evidence of window b-1.
-//
-// One track of m_b^r.  (cmu, csg) / (c0mu, c0sg): the track / the shared track of
-// C_b -- they set the base B (track_base) the message is scaled against and
-// decoded onto; (amu, asg) / (a0mu, a0sg): the track / shared track of Y_b; (bmu,
-// bsg): the track of X_b.  Unlike sweep_delta_track, a track NULL in Y_b is
-// measured from the prior THIS rank rated it from (Y_b's shared value or the seed,
-// rater.py:115-136) rather than from B: another rank may have created the track
-// in C_b already, and measuring from B would cancel that rank's evidence.  When Y
-// is C (the first window, or a non-lagged merge) the two forms agree.
-ANA_HD void sweep_lag_delta_track(int t, float cmu, float csg, float c0mu, float c0sg, float amu, float asg,
-                                  float a0mu, float a0sg, float bmu, float bsg, bool seeded, float seed_mu,
-                                  float seed_sig, bool scaled, float& dp, float& dt, bool& touched) {
-  dp = 0.f;
-  dt = 0.f;
-  const bool had = amu == amu;
-  const bool changed = had ? (bmu != amu || bsg != asg) : bmu == bmu;
-  touched = !had && bmu == bmu;
-  float bm, bs, pm = amu, ps = asg;
-  const bool based = track_base(t, cmu, csg, c0mu, c0sg, seeded, seed_mu, seed_sig, bm, bs);
-  const bool prior = had || track_base(t, NAN, NAN, a0mu, a0sg, seeded, seed_mu, seed_sig, pm, ps);
-  if (!(changed && based && prior)) return;
-  if (scaled) {  // (pi - pi_0) / pi_B, (tau - mu_B pi - (tau_0 - mu_B pi_0)) / pi_B
-    const float r1 = bs / bsg, r0 = bs / ps;
-    dp = r1 * r1 - r0 * r0;
-    dt = r1 * r1 * (bmu - bm) - r0 * r0 * (pm - bm);
-  } else {
-    float p1, t1, p0, t0;
-    nat_params(bmu, bsg, p1, t1);
-    nat_params(pm, ps, p0, t0);
-    dp = p1 - p0;
-    dt = t1 - t0;
-  }
-}
-
-// Host mirror of the lagged boundary for one player.  c: base row of C_{b-1} (in)
-// -> C_b (out, in place); d: the summed messages of the previous boundary ([16],
-// touch fields in 14/15; nullptr = none yet); y: base row of Y_b -> Y_{b+1} (in
-// place); x: roster row X_b -> Y_{b+1} (tags 0, in place); o: this rank's message
-// m_b ([16], touch fields in 14/15).
-ANA_HD void sweep_lag_player(float* c, const float* d, float* y, float* x, const float* attr, const float* vst,
-                             float unknown_sigma, bool scaled, float* o) {
-  float seed_mu = NAN, seed_sig = NAN;
-  const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
-  float cn[2 * kGranules];
-  const unsigned slo = d ? (unsigned)d[14] : 0u, shi = d ? (unsigned)d[15] : 0u;
-  for (int g = 0; g < kGranules; ++g) {
-    cn[2 * g] = c[2 * g];
-    cn[2 * g + 1] = c[2 * g + 1];
-    if (g < kTracks && d) {
-      const unsigned touched = g < 4 ? (slo >> (4 * g)) & 15u : (shi >> (4 * (g - 4))) & 15u;
-      sweep_apply_track(g, c[2 * g], c[2 * g + 1], c[0], c[1], d[2 * g], d[2 * g + 1], touched, seeded, seed_mu,
-                        seed_sig, scaled, cn[2 * g], cn[2 * g + 1]);
-    }
-  }
-  float lo = 0.f, hi = 0.f;
-  for (int t = 0; t < kTracks; ++t) {
-    bool touched;
-    sweep_lag_delta_track(t, cn[2 * t], cn[2 * t + 1], cn[0], cn[1], y[2 * t], y[2 * t + 1], y[0], y[1], x[4 * t],
-                          x[4 * t + 2], seeded, seed_mu, seed_sig, scaled, o[2 * t], o[2 * t + 1], touched);
-    if (touched) {
-      if (t < 4) lo += (float)(1 << (4 * t));
-      else hi += (float)(1 << (4 * (t - 4)));
-    }
-  }
-  o[14] = lo;
-  o[15] = hi;
-  for (int g = 0; g < kGranules; ++g) {
-    float mu = cn[2 * g], sg = cn[2 * g + 1];
-    if (g < kTracks) {
-      const unsigned touched = g < 4 ? ((unsigned)lo >> (4 * g)) & 15u : ((unsigned)hi >> (4 * (g - 4))) & 15u;
-      sweep_apply_track(g, cn[2 * g], cn[2 * g + 1], cn[0], cn[1], o[2 * g], o[2 * g + 1], touched, seeded,
-                        seed_mu, seed_sig, scaled, mu, sg);
-    }
-    c[2 * g] = cn[2 * g];
-    c[2 * g + 1] = cn[2 * g + 1];
-    y[2 * g] = mu;
-    y[2 * g + 1] = sg;
-    x[4 * g] = mu;
-    x[4 * g + 1] = 0.f;
-    x[4 * g + 2] = sg;
-    x[4 * g + 3] = 0.f;
   }
 }
 
@@ -235,7 +157,9 @@ ANA_HD void sweep_delta_player(const float* s, const float* a, const float* b, c
 // merged window; ranks < r: rank r's prior for a causal re-sweep); o: the decoded
 // roster row (tags 0; granule 7 from the base row), ob: the same as a base row.
 ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr,
-                               const float* vst, float unknown_sigma, bool scaled, float* o, float* ob) {
+                               const float* vst, float unknown_sigma, bool scaled, float* o, float* ob,
+                               uint32_t* clamps) {
+  bool cl = false;
   float seed_mu = NAN, seed_sig = NAN;
   const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
   const unsigned lo = (unsigned)d[14], hi = (unsigned)d[15];
@@ -244,7 +168,8 @@ ANA_HD void sweep_apply_player(const float* a, const float* d, const float* attr
     if (g < kTracks) {
       const unsigned touched = g < 4 ? (lo >> (4 * g)) & 15u : (hi >> (4 * (g - 4))) & 15u;
       sweep_apply_track(g, a[2 * g], a[2 * g + 1], a[0], a[1], d[2 * g], d[2 * g + 1], touched, seeded,
-                        seed_mu, seed_sig, scaled, mu, sg);
+                        seed_mu, seed_sig, scaled, mu, sg, cl);
+      if (cl && clamps) ++*clamps;
     }
     o[4 * g] = mu;
     o[4 * g + 1] = 0.f;

@@ -87,47 +87,12 @@ def simulate_sweep_dp(rater: BatchRater, roster: Roster, shards: Sequence[torch.
                 m.decode(ro, into=m.start)
     roster.state.copy_(rosters[0].state)
     roster.epoch = rosters[0].epoch
+    global CLAMPS
+    CLAMPS += max(m.clamp_hits() for m in mergers)  # (the final decode is the same sum on every rank)
     return outs
 
 
-def simulate_lagged_dp(rater: BatchRater, roster: Roster, shard_sets: Sequence[Sequence[torch.Tensor]], K: int,
-                       comm_dtype: str = "fp32") -> List[RateResult]:
-    """The one-window-late merge (parallel/sweep.py ``lag``) of N ranks over
-    consecutive windows, in one process: after each window every rank runs its
-    boundary pass (which consumes the previous window's sum), then the sum of this
-    boundary's messages -- in the comm dtype, as the all-reduce carries them --
-    becomes every rank's operand for the next one; ``flush`` at the end.  Returns
-    the per-rank outputs of the last window; ``roster`` ends as the common roster."""
-    N = len(shard_sets[0])
-    mergers = [SweepMerger(roster.num_players, roster.device, rater.cfg, comm_dtype=comm_dtype,
-                           world_size=N, lag=True) for _ in range(N)]
-    rosters = [roster.clone() for _ in range(N)]
-    outs = [RateResult.allocate(int(s.shape[0]), K, roster.device) for s in shard_sets[-1]]
-    for m, ro in zip(mergers, rosters):
-        m.begin(ro)
-    for shards in shard_sets:
-        for r in range(N):
-            mergers[r].begin(rosters[r])
-            rater.rate(rosters[r], shards[r], K, out=outs[r])
-            mergers[r].rated()
-        for m, ro in zip(mergers, rosters):
-            m.lag_boundary(ro)
-            m._has_sum = True
-        if comm_dtype == "fp32":
-            total = torch.stack([m.buf for m in mergers]).sum(0)
-            for m in mergers:
-                m.buf.copy_(total)
-        else:  # each rank's 16-bit operand, summed in fp32 and rounded once
-            msg = torch.stack([m.msg.float() for m in mergers]).sum(0).to(mergers[0].msg.dtype)
-            cnt = torch.stack([m.cnt for m in mergers]).sum(0)
-            for m in mergers:
-                m.msg.copy_(msg)
-                m.cnt.copy_(cnt)
-    for m, ro in zip(mergers, rosters):
-        m.flush(ro)
-    roster.state.copy_(rosters[0].state)
-    roster.epoch = rosters[0].epoch
-    return outs
+CLAMPS = 0  # decodes held at the precision floor in the simulations since the last run()
 
 
 def _spearman(a: torch.Tensor, b: torch.Tensor) -> float:
@@ -185,11 +150,11 @@ def compare(approx: Roster, exact: Roster, out_a: Optional[List[RateResult]] = N
 
 def run(ranks: int, players: int, matches_per_rank: int, windows: int, sweeps: Sequence[int],
         device="cpu", team_size: int = 3, seed: int = 11, comm_dtype: str = "fp32",
-        p_rated: float = 0.3, warm_windows: int = 0, lag: bool = False) -> Dict[str, object]:
-    """Accuracy table: exact sequential vs sweep DP at each sweep count
-    (``lag``: the one-window-late merge, one sweep).
+        p_rated: float = 0.3, warm_windows: int = 0) -> Dict[str, object]:
+    """Accuracy table: exact sequential vs sweep DP at each sweep count.
     ``warm_windows``: exact windows rated first (shared by both), so the
     comparison starts from a settled roster rather than fresh priors."""
+    global CLAMPS
     dev = torch.device(device)
     K = team_size
     rater = BatchRater()
@@ -214,26 +179,18 @@ def run(ranks: int, players: int, matches_per_rank: int, windows: int, sweeps: S
         torch.cuda.synchronize(dev)
     table = {"ranks": ranks, "players": players, "matches_per_rank": M, "windows": windows,
              "warm_windows": warm_windows, "team_size": K, "comm_dtype": comm_dtype,
-             "device": str(dev), "exact_s": time.perf_counter() - t0, "sweeps": {}, "lag": bool(lag)}
-    if lag:
-        t0 = time.perf_counter()
-        approx = base.clone()
-        outs = simulate_lagged_dp(rater, approx, shard_sets, K, comm_dtype=comm_dtype)
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-        stats = compare(approx, exact, outs, out_e)
-        stats["elapsed_s"] = time.perf_counter() - t0
-        table["sweeps"]["1"] = stats
-        return table
+             "device": str(dev), "exact_s": time.perf_counter() - t0, "sweeps": {}}
     for S in sweeps:
         t0 = time.perf_counter()
         approx = base.clone()
         outs = None
+        CLAMPS = 0
         for shards in shard_sets:
             outs = simulate_sweep_dp(rater, approx, shards, K, sweeps=S, comm_dtype=comm_dtype)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         stats = compare(approx, exact, outs, out_e)
+        stats["clamp_hits"] = CLAMPS  # decodes held at the precision floor (0 = none)
         stats["elapsed_s"] = time.perf_counter() - t0
         table["sweeps"][str(S)] = stats
     return table
@@ -251,12 +208,11 @@ def main(argv=None) -> int:
     ap.add_argument("--comm-dtype", default="fp32", choices=sorted(COMM_DTYPES))
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--seed", type=int, default=11)
-    ap.add_argument("--lag", action="store_true", help="one-window-late merge (one sweep)")
     args = ap.parse_args(argv)
     sweeps = [int(x) for x in args.sweeps.split(",") if x]
     table = run(args.ranks, int(args.players), int(args.matches_per_rank), args.windows, sweeps,
                 device=args.device, team_size=args.team_size, seed=args.seed,
-                comm_dtype=args.comm_dtype, warm_windows=args.warm_windows, lag=args.lag)
+                comm_dtype=args.comm_dtype, warm_windows=args.warm_windows)
     print(json.dumps(table, indent=1), flush=True)
     return 0
 

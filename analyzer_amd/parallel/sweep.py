@@ -39,21 +39,12 @@ sweep count.  This is deliberately a prefix, not the EP cavity (merged / own
 message): the cavity would feed later ranks' evidence into earlier matches,
 which converges to a smoother, not to the reference's filter.
 
-**One-window-late merge (``lag``).**  The all-reduce of window b's messages runs
-while window b+1 rates instead of in front of it.  Each rank keeps two base-row
-snapshots: C, the COMMON roster (start + every rank's messages of the windows
-before b), and Y, its own start of window b.  At the boundary after window b one
-pass per player (csrc/sweep_core.h ``sweep_lag_player``, kernel ``sweep_lag``)
-adds the summed messages of window b-1 that have arrived to C, measures this
-rank's message nat(X_b) - nat(Y_b) against it, and restarts the roster at
-Y_{b+1} = C + that message; the message's all-reduce is then launched and only
-waited for at the next boundary.  So a rank rates window b+1 with everything of
-its own and the other ranks' evidence up to window b-1: one window of extra
-staleness (``parallel/accuracy.py --lag`` measures it) against an all-reduce
-that is no longer exposed.  ``flush`` applies the last sum, after which every
-rank holds the same roster again.  The pass reads and writes 600 B per player
-against 450 B for messages + decode, so on one GPU (``--force-merge``) it costs
-a little more; it pays where the all-reduce is real (N > 1 over xGMI).
+**No one-window-late merge.**  Rounds 4-5 built and removed a lagged merge (window
+b's all-reduce under window b+1's rating): a message measured against the rank's
+own start -- which lacks the other ranks' previous window, tau^2 dynamics included
+-- overshoots the common roster's precision, and the summed messages crossed zero
+in every precision (profiles/r5/lag_bf16_root_cause.log).  Every decode now counts
+the tracks it had to clamp (``clamps``, ``check``).
 
 With one rank the merge is skipped (the exact single-GPU result stands).
 Backend: ``nccl`` (RCCL on ROCm) for device tensors, ``gloo`` for CPU tests.
@@ -74,6 +65,13 @@ from ..ops.native import native
 from .comm import all_reduce_sum, exclusive_scan, world
 
 MAX_RANKS = 15  # touch counts are base-16 fields in fp32 (see csrc/sweep_core.h)
+
+
+class MergeClampError(FloatingPointError):
+    """A decode's merged precision came out at or below zero (sweep_core.h
+    sweep_apply_track) and was held at the floor: the reference raises on numeric
+    trouble and dead-letters the batch (/root/reference/rater.py:7-8,
+    worker.py:108-120); a silently clamped sigma must never be written."""
 BASE_FLOATS = 16  # base row: (mu, sigma) per 16-B granule of a roster row
 
 
@@ -86,8 +84,7 @@ COMM_DTYPES = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloa
 class SweepMerger:
     def __init__(self, num_players: int, device, cfg: Optional[RaterConfig] = None,
                  group=None, comm_dtype: str = "fp32", bucket_rows: Optional[int] = None,
-                 sweeps: int = 1, world_size: Optional[int] = None, force: bool = False,
-                 lag: bool = False):
+                 sweeps: int = 1, world_size: Optional[int] = None, force: bool = False):
         self.P = int(num_players)
         self.device = torch.device(device)
         self.cfg = cfg or RaterConfig.from_env()
@@ -98,11 +95,6 @@ class SweepMerger:
         if comm_dtype not in COMM_DTYPES:
             raise ValueError("comm_dtype must be one of %s" % sorted(COMM_DTYPES))
         self.sweeps = max(1, int(sweeps))
-        # lag: one-window-late merge (module docstring); one sweep only -- a causal
-        # re-sweep needs the other ranks' messages of the same window at once
-        self.lag = bool(lag)
-        if self.lag and self.sweeps > 1:
-            raise ValueError("the one-window-late merge (lag) runs one sweep per window")
         # force: run the merge kernels even on one rank (the all-reduce of one rank
         # is the identity) -- bench.py --force-merge prices the merge without comm
         self.force = bool(force)
@@ -124,6 +116,9 @@ class SweepMerger:
             if comm_dtype != "fp32" else None
         self.vst = torch.tensor(vst_table(), **f)
         self._none = torch.empty(0, **f)
+        # decoded tracks whose merged precision hit the floor, summed over every decode
+        # since the last check (sticky, on the device: no sync per merge) -- check() raises
+        self.clamps = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.comm_bytes = self.P * (16 * 4 if not self.scaled else
                                     14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4)
         if bucket_rows is None:  # ANA_MERGE_BUCKET_MB of all-reduce operands per bucket
@@ -135,12 +130,6 @@ class SweepMerger:
             # per merge instead of two per 16 MB
             bucket_rows = self.P
         self.bucket_rows = max(1, min(int(bucket_rows), max(self.P, 1)))
-        # lag: this rank's start of the current window (base rows; start is then the
-        # common roster C), the in-flight all-reduces per bucket, and whether the
-        # operands hold a summed message that has not been applied yet
-        self.y = torch.empty((self.P, BASE_FLOATS), **f) if self.lag else None
-        self._pending: Dict[int, Callable[[], None]] = {}
-        self._has_sum = False
         self.windows = 0
         self._synced = False   # start == the roster as the last merge left it
         self._sweep = 0        # sweeps rated in the current window
@@ -157,11 +146,7 @@ class SweepMerger:
         (the merge decodes into both), so only the first window -- or one after
         ``invalidate()`` -- copies it."""
         if not self._synced:
-            if self._has_sum:
-                raise RuntimeError("lagged merge: flush() the pending sum before the roster is re-snapshot")
             self.start.copy_(base_rows(roster.state))
-            if self.lag:
-                self.y.copy_(self.start)
             self._synced = True
         self._sweep = 0
 
@@ -183,7 +168,7 @@ class SweepMerger:
         s2 = into[lo:hi] if into is not None else self._none
         native().sweep_apply(self.start[lo:hi], self.buf[lo:hi], roster.attrs[lo:hi],
                              roster.state[lo:hi], s2, self.vst, float(self.cfg.unknown_player_sigma),
-                             self.scaled)
+                             self.scaled, self.clamps)
         roster.epoch = roster.epoch if roster.epoch is not None else 0  # decode wrote tag 0
 
     def messages_packed(self, roster, lo: int = 0, hi: Optional[int] = None) -> None:
@@ -198,7 +183,8 @@ class SweepMerger:
         hi = self.P if hi is None else hi
         s2 = into[lo:hi] if into is not None else self._none
         native().sweep_apply_packed(self.start[lo:hi], self.msg[lo:hi], self.cnt[lo:hi], roster.attrs[lo:hi],
-                                    roster.state[lo:hi], s2, self.vst, float(self.cfg.unknown_player_sigma))
+                                    roster.state[lo:hi], s2, self.vst, float(self.cfg.unknown_player_sigma),
+                                    self.clamps)
         roster.epoch = roster.epoch if roster.epoch is not None else 0
 
     def _packed(self) -> bool:
@@ -271,56 +257,6 @@ class SweepMerger:
             e.record()
             self._events.append((name, e))
 
-    def lag_boundary(self, roster, lo: int = 0, hi: Optional[int] = None) -> None:
-        """The lagged boundary pass over rows [lo, hi) (module docstring): start (C)
-        += the summed messages in the operands (if any), this rank's message into the
-        operands, roster rows and ``y`` := C + that message."""
-        hi = self.P if hi is None else hi
-        us = float(self.cfg.unknown_player_sigma)
-        if self.msg is not None:
-            native().sweep_lag_packed(self.start[lo:hi], self.msg[lo:hi], self.cnt[lo:hi], self.y[lo:hi],
-                                      roster.state[lo:hi], roster.attrs[lo:hi], self.vst, us, self._has_sum)
-        else:
-            native().sweep_lag(self.start[lo:hi], self.buf[lo:hi], self.y[lo:hi], roster.state[lo:hi],
-                               roster.attrs[lo:hi], self.vst, us, self.scaled, self._has_sum)
-        roster.epoch = roster.epoch if roster.epoch is not None else 0  # the pass wrote tag 0
-
-    def _merge_lagged(self, roster, overlap: Optional[Callable[[], None]]) -> None:
-        """One lagged boundary: per bucket, wait for the all-reduce launched at the
-        previous boundary, run the pass, launch this boundary's all-reduce -- which
-        then runs under the next window's rating -- and return without waiting."""
-        self._ev("begin")
-        for lo, hi in self.buckets():
-            fin = self._pending.pop(lo, None)
-            if fin is not None:
-                fin()
-            self._ev("allreduce")
-            self.lag_boundary(roster, lo, hi)
-            self._ev("apply")
-            self._pending[lo] = self._launch_reduce(lo, hi, self.msg is not None)
-        self._has_sum = True
-        self._synced = True
-        self.windows += 1
-        if overlap is not None:
-            overlap()
-
-    def flush(self, roster) -> None:
-        """Lagged merge: apply the last summed messages, so the roster is the common
-        one on every rank again (the end of a run, or before anything outside the
-        merger reads or changes the roster).  No-op otherwise."""
-        if not (self.lag and self._has_sum):
-            return
-        packed = self.msg is not None
-        dec = self.decode_packed if packed else self.decode
-        for lo, hi in self.buckets():
-            fin = self._pending.pop(lo, None)
-            if fin is not None:
-                fin()
-            dec(roster, lo, hi, into=self.start)
-        self.y.copy_(self.start)
-        self._has_sum = False
-        self._synced = True
-
     def merge(self, roster, overlap: Optional[Callable[[], None]] = None) -> None:
         """Combine every rank's window into the replicated roster (in place):
         messages -> all-reduce -> decode, pipelined over row buckets; the decode
@@ -334,9 +270,6 @@ class SweepMerger:
             self.windows += 1
             if overlap is not None:
                 overlap()
-            return
-        if self.lag:
-            self._merge_lagged(roster, overlap)
             return
         packed = self._packed()
         msg = self.messages_packed if packed else self.messages
@@ -379,6 +312,21 @@ class SweepMerger:
             self._ev("apply")
         self._synced = True
         self.windows += 1
+
+    def clamp_hits(self) -> int:
+        """Decoded tracks held at the precision floor since the last ``check`` (syncs)."""
+        return int(self.clamps.item())
+
+    def check(self) -> None:
+        """Raise MergeClampError if any decode since the last check clamped (syncs);
+        the counter restarts.  bench.py and runtime/rerate.py call it at the end of a
+        run and before every checkpoint, as they check the executor's error flags."""
+        n = self.clamp_hits()
+        if n:
+            self.clamps.zero_()
+            raise MergeClampError("sweep merge: %d decoded track(s) had a merged precision at or below zero "
+                                  "and were clamped (sigma x1000): the merged roster is not trustworthy"
+                                  % n)
 
     def stage_ms(self) -> Dict[str, float]:
         """Per-stage main-stream time of the recorded merges (syncs; ``timing``):

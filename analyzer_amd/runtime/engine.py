@@ -81,7 +81,7 @@ class WindowPipeline:
         # all-reduce costs on this interconnect (probe_placement)
         self.allreduce_probe_ms: Optional[float] = None
         if dp and self.cuda and self.ecfg.prepass_serial is None and \
-                getattr(merger, "world", 1) > 1 and not getattr(merger, "lag", False):
+                getattr(merger, "world", 1) > 1:
             self.serial = self.probe_placement(merger)
         # serial prepass: nothing to overlap, no tail signal -- unless a caller wants the
         # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail)
@@ -408,11 +408,11 @@ class WindowPipeline:
         return res, Prepared(next_rec, sched, done, used, int(window))
 
     def finish(self) -> None:
-        """End of a run of windows: a lagged DP merge applies its last summed messages
-        (parallel/sweep.py ``flush``), so every rank holds the common roster."""
-        if self.merger is not None and getattr(self.merger, "lag", False):
-            with trace_range("flush", window=self.windows_rated):
-                self.merger.flush(self.roster)
+        """End of a run of windows: every DP merge is complete when its window's
+        ``rate`` returns, so only the merge decodes' clamp counter is checked (syncs;
+        parallel/sweep.py ``check`` raises on a decode held at the precision floor)."""
+        if self.merger is not None and hasattr(self.merger, "check"):
+            self.merger.check()
 
     def run(self, windows: Iterable[torch.Tensor], out: Optional[RateResult] = None,
             on_result: Optional[Callable[[int, RateResult], None]] = None) -> int:

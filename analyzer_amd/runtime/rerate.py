@@ -178,6 +178,8 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
         if ck.due(g + 1):
             if dev.type == "cuda":  # never checkpoint over a failed window
                 rater.check_errors(dev, sticky=True)
+            if merger is not None:  # ... nor over a clamped merge decode
+                merger.check()
             if rank == 0:
                 with trace_range("checkpoint", window=g + 1):
                     ck.maybe_save(g + 1, roster, {"spec": asdict(spec), "world": size,
@@ -193,6 +195,8 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
     dt = time.perf_counter() - t0
     if dev.type == "cuda":
         rater.check_errors(dev, sticky=True)
+    if merger is not None:
+        merger.check()
     c = counts.cpu()
     local = {R.STATUS_NAMES.get(i, str(i)): float(c[i]) for i in range(256) if int(c[i])}
     local["matches"] = float(rated)

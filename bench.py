@@ -101,17 +101,10 @@ def parse(argv=None):
     ap.add_argument("--step-prepass", type=int, default=-1, choices=[-1, 0, 1],
                     help="merges per step > 1: 1 = ONE schedule prepass per step over its k windows "
                          "(links cut at the window boundaries, runtime/engine.py step_windows), 0 = a "
-                         "prepass per window (rounds 2-4), -1 = auto (1 unless --merge-lag)")
+                         "prepass per window (rounds 2-4), -1 = auto (1)")
     ap.add_argument("--force-merge", action="store_true",
                     help="N = 1: run the merge kernels after every window anyway (messages + decode, "
                          "no collective) -- prices the DP merge's device work against --merges-per-step")
-    ap.add_argument("--merge-lag", type=int, default=int(os.environ.get("ANA_MERGE_LAG") or 0), choices=[0, 1],
-                    help="1: one-window-late merge (parallel/sweep.py lag) -- window b's all-reduce runs "
-                         "under window b+1's rating instead of in front of it, for one window of extra "
-                         "staleness (the accuracy block reports it); the last sum is applied inside the "
-                         "timed region; fp32 messages unless --comm-dtype says otherwise.  Off by default: "
-                         "at N = k = 8 it leaves Spearman 0.969 and records median 63 against 0.9956 / 30 "
-                         "(profiles/r4/roster_warm_and_lag.log)")
     ap.add_argument("--sweeps", type=int, default=EngineConfig.from_env().sweeps,
                     help="causal sweeps per window (N > 1): 1 = one merge (approximate); "
                          "N = exact sequential semantics (parallel/sweep.py)")
@@ -140,14 +133,10 @@ def parse(argv=None):
         ap.error("--merges-per-step must divide --matches-per-gpu")
     if args.merges_per_step > 1 and args.config == 4:
         ap.error("--merges-per-step is for the rating configs (2, 3, 5)")
-    if args.merge_lag and args.sweeps > 1:
-        ap.error("--merge-lag runs one sweep per window")
     if args.comm_dtype is None:
         one_sweep = "fp16" if args.config == 5 else "bf16"
-        # the lagged merge keeps fp32 messages: with bf16 ones the rounding of merged
-        # precisions near zero diverges at 8 ranks (profiles/r4/roster_warm_and_lag.log)
         args.comm_dtype = os.environ.get("COMM_DTYPE") or (
-            "fp32" if args.sweeps > 1 or args.merge_lag else one_sweep)
+            "fp32" if args.sweeps > 1 else one_sweep)
     return args
 
 
@@ -245,7 +234,7 @@ def main(argv=None) -> int:
     # one prepass per step over its k windows (engine.step_windows) -- the unit of the
     # timed loop is then a step, not a window
     step_prepass = sub > 1 and args.config != 4 and (
-        args.step_prepass == 1 or (args.step_prepass < 0 and not args.merge_lag))
+        args.step_prepass == 1 or args.step_prepass < 0)
     n_windows = max(1, min(args.ring, (args.steps + args.warmup) * sub))
     total_windows = (args.steps + args.warmup) * sub
     if step_prepass:  # a ring of whole steps: window w of rank r as before, k windows per step
@@ -268,8 +257,7 @@ def main(argv=None) -> int:
         tele = [make_telemetry(tspec, windows[w], K, base=(w * world + rank) * M) for w in range(n_windows)]
         stats = allocate_stats(M, K, dev)
         n_events = sum(t.num_events for t in tele) / n_windows
-    merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge,
-                          lag=bool(args.merge_lag))
+    merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge)
               if world > 1 or args.force_merge else None)
     auto_mode = args.telemetry_mode == "auto"
     tele_path = None
@@ -364,7 +352,7 @@ def main(argv=None) -> int:
     t0 = time.perf_counter()
     for i in range(args.warmup * per, total_windows):
         step(i)
-    pipe.finish()  # lagged merge: the last window's sum applied (timed: it is part of the work)
+    pipe.finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -396,6 +384,8 @@ def main(argv=None) -> int:
                     "allreduce_probe_ms": pipe.allreduce_probe_ms,
                     # one schedule prepass per step over its k windows, or one per window
                     "prepass_per": "step" if step_prepass else "window"}
+    if merger is not None:
+        merger.check()  # a clamped merge decode fails the run, as the executor's flags do
     flags = rater.sticky_flags(dev).cpu()
     if int(flags.sum()):
         raise RuntimeError("dataflow error flags set during the benchmark: %s" % flags.tolist())
@@ -421,8 +411,7 @@ def main(argv=None) -> int:
 
         t_acc = time.perf_counter()
         tab = accuracy_run(world, P, Mw, sub, [args.sweeps], device=dev, team_size=K, seed=args.seed,
-                           comm_dtype=args.comm_dtype, p_rated=RosterSpec().p_rated, warm_windows=1,
-                           lag=bool(args.merge_lag))
+                           comm_dtype=args.comm_dtype, p_rated=RosterSpec().p_rated, warm_windows=1)
         st = tab["sweeps"][str(args.sweeps)]
         sh = st["tracks"].get("shared", {})
         accuracy = {"vs": "exact sequential rating of the same %d x %d matches (one step)" % (world, M),
@@ -433,6 +422,7 @@ def main(argv=None) -> int:
                     "records_dmu_median": st.get("records_shared_mu", {}).get("dmu_median"),
                     "records_dmu_p99": st.get("records_shared_mu", {}).get("dmu_p99"),
                     "records_dmu_max": st.get("records_shared_mu", {}).get("dmu_max"),
+                    "merge_clamp_hits": st.get("clamp_hits"),
                     "seconds": round(time.perf_counter() - t_acc, 2)}
     if world > 1:
         dist.barrier()  # the other ranks wait for rank 0's untimed accuracy pass
@@ -488,7 +478,6 @@ def main(argv=None) -> int:
                 "skew": args.skew,
                 "comm_dtype": args.comm_dtype if world > 1 or args.force_merge else None,
                 "force_merge": bool(args.force_merge),
-                "merge_lag": bool(args.merge_lag) if world > 1 or args.force_merge else None,
                 "sweeps": args.sweeps if world > 1 else None,
                 **extra,
             },

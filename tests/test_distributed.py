@@ -336,69 +336,6 @@ def test_exact_dp_with_round_check(tmp_path):
     assert len(res) == 2
 
 
-# ------------------------------------------------ one-window-late merge (lag)
-def _lagged(rank, size, P, M, K, seed, windows, comm_dtype, bucket_rows):
-    from analyzer_amd.ops.rate import BatchRater
-    from analyzer_amd.parallel.sweep import SweepMerger
-    from analyzer_amd.runtime.engine import WindowPipeline
-
-    roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
-    spec = StreamSpec(team_size=K, seed=seed + 1)
-    merger = SweepMerger(P, "cpu", comm_dtype=comm_dtype, lag=True, bucket_rows=bucket_rows)
-    pipe = WindowPipeline(BatchRater(), roster, K, merger=merger)
-    recs = [make_stream(spec, M, P, K=K, base=(w * size + rank) * M) for w in range(windows)]
-    outs = []
-    pipe.run(recs, on_result=lambda i, res: outs.append(res.s_mu.clone()))
-    return {"state": roster.state, "s_mu": outs[-1], "windows": merger.windows}
-
-
-@pytest.mark.parametrize("comm_dtype,bucket_rows", [("fp32", None), ("bf16", 37)])
-def test_lagged_merge_equals_simulation(tmp_path, comm_dtype, bucket_rows):
-    """The one-window-late merge over gloo (async all-reduce waited for at the next
-    boundary, flushed at the end of the run; ragged row buckets) gives every rank
-    the same roster, equal to the one-process simulation of parallel/accuracy.py, and
-    its error against the exact sequential result stays a sweep-DP-sized one."""
-    from analyzer_amd.ops.rate import BatchRater, Roster
-    from analyzer_amd.parallel.accuracy import compare, simulate_lagged_dp
-
-    P, M, K, seed, size, windows = 300, 500, 3, 23, 2, 4
-    res = run_ranks(_lagged, size, tmp_path, P, M, K, seed, windows, comm_dtype, bucket_rows)
-    for r in res:
-        assert r["windows"] == windows
-        assert torch.equal(r["state"].nan_to_num(-7), res[0]["state"].nan_to_num(-7))
-    spec = StreamSpec(team_size=K, seed=seed + 1)
-    start = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
-    sets = [[make_stream(spec, M, P, K=K, base=(w * size + r) * M) for r in range(size)] for w in range(windows)]
-    sim = start.clone()
-    sim_out = simulate_lagged_dp(BatchRater(), sim, sets, K, comm_dtype=comm_dtype)
-    got = res[0]["state"]
-    assert torch.equal(torch.isnan(got[:, 0::4]), torch.isnan(sim.state[:, 0::4]))
-    ok = ~torch.isnan(sim.state[:, 0::4])
-    # two-rank sums are order-independent; bf16 sums of two operands may round once
-    tol = 1e-3 if comm_dtype == "fp32" else 2.0
-    assert float((got[:, 0::4][ok] - sim.state[:, 0::4][ok]).abs().max()) < tol
-    d = (res[-1]["s_mu"] - sim_out[-1].s_mu).abs()
-    assert float(d[~torch.isnan(d)].max()) < tol
-    exact = start.clone()
-    for shards in sets:
-        for sh in shards:
-            BatchRater().rate(exact, sh, K)
-    sh = compare(Roster(got, start.attrs), exact)["tracks"]["shared"]
-    assert sh["null_mismatch"] == 0 and sh["spearman_mu_minus_sigma"] > 0.97, sh
-
-
-def test_lagged_merge_one_rank_is_exact():
-    """One rank (bench --force-merge): the lagged boundary restarts every window from
-    exactly the rank's own posterior, so the run equals plain sequential rating up to
-    the natural-parameter round trip -- fresh (NULL) tracks included."""
-    from analyzer_amd.parallel.accuracy import run
-
-    t = run(ranks=1, players=800, matches_per_rank=3000, windows=4, sweeps=[1], lag=True)
-    for name, tr in t["sweeps"]["1"]["tracks"].items():
-        assert tr["null_mismatch"] == 0 and tr["dmu_max"] < 5e-3, (name, tr)
-    assert t["sweeps"]["1"]["records_shared_mu"]["dmu_max"] < 5e-3
-
-
 def _probe(rank, size):
     from analyzer_amd.parallel.comm import time_all_reduce
 
@@ -415,3 +352,61 @@ def test_all_reduce_probe_agrees_across_ranks(tmp_path):
     assert float(res[0]["ms"]) > 0.0
     for r in res[1:]:
         assert torch.equal(r["ms"], res[0]["ms"])
+
+
+# ------------------------------------------------ merge decodes fail loudly
+def test_decode_clamps_are_counted_and_raise():
+    """A summed message that drives a track's merged precision to or below zero is
+    held at the floor by the decode -- and counted, host mirror and merger alike:
+    SweepMerger.check raises MergeClampError instead of writing sigma x1000 silently
+    (the reference raises on numeric trouble and dead-letters the batch,
+    /root/reference/rater.py:7-8, worker.py:108-120)."""
+    from analyzer_amd.ops.native import native
+    from analyzer_amd.ops.synth import RosterSpec, make_roster
+    from analyzer_amd.parallel.sweep import MergeClampError, SweepMerger, base_rows
+
+    P = 64
+    ro = make_roster(RosterSpec(num_players=P, seed=3, p_rated=1.0, p_mode_rated=1.0))
+    for comm in ("fp32", "bf16"):
+        m = SweepMerger(P, "cpu", comm_dtype=comm, force=True)
+        m.begin(ro.clone())
+        if comm == "fp32":  # raw (d_pi, d_tau): a precision loss larger than the base's
+            m.buf.zero_()
+            pi = 1.0 / m.start[:5, 1] ** 2
+            m.buf[:5, 0] = -2.0 * pi
+            m.decode(ro.clone())
+        else:               # scaled: 1 + sum r_pi <= 0 on the shared track of 5 players
+            m.msg.zero_()
+            m.cnt.zero_()
+            m.msg[:5, 0] = -1.5
+            m.decode_packed(ro.clone())
+        assert m.clamp_hits() == 5
+        with pytest.raises(MergeClampError, match="5 decoded track"):
+            m.check()
+        assert m.clamp_hits() == 0  # restarted
+        m.check()
+    # the plain decode of a healthy sum clamps nothing
+    m = SweepMerger(P, "cpu", comm_dtype="bf16", force=True)
+    r2 = ro.clone()
+    m.begin(r2)
+    m.messages_packed(r2)
+    m.decode_packed(r2)
+    m.check()
+    assert torch.equal(base_rows(r2.state).nan_to_num(-7), base_rows(ro.state).nan_to_num(-7))
+
+
+def test_default_merge_keeps_its_precision_margin_at_the_lag_reproduction_density():
+    """The round-4 lagged merge diverged at 8 ranks x 125k matches per rank-window over
+    100k players (profiles/r5/lag_bf16_root_cause.log: messages measured against each
+    rank's own start overshoot the common precision, 1 + sum r_pi crosses zero).  The
+    merge that remains measures every rank against the common start: at the same
+    density (8 ranks, 7.5 appearances per player per rank-window, bf16 messages, three
+    windows from a warm roster) no decode clamps and the roster stays close."""
+    from analyzer_amd.parallel.accuracy import run
+
+    t = run(ranks=8, players=8_000, matches_per_rank=10_000, windows=3, sweeps=[1], comm_dtype="bf16",
+            warm_windows=1)
+    st = t["sweeps"]["1"]
+    assert st["clamp_hits"] == 0
+    sh = st["tracks"]["shared"]
+    assert sh["spearman_mu_minus_sigma"] > 0.99 and sh["dmu_max"] < 1000.0, sh

@@ -313,55 +313,35 @@ def test_sweep_kernels_match_host(gpu_device, scaled, resweep):
     assert torch.equal(base_rows(sh).nan_to_num(-7), sh2.nan_to_num(-7))
 
 
-def _lag_inputs(P, seed):
-    """A lagged boundary's operands: C (common base rows), Y (a rank start that moved
-    on from C, NULL tracks touched), X (the roster after a window from Y), a sum."""
-    from analyzer_amd.parallel.sweep import base_rows
+@pytest.mark.parametrize("comm", ["fp32", "bf16"])
+def test_device_decode_counts_clamps_like_host(gpu_device, comm):
+    """The merge decode kernels count every track held at the precision floor into the
+    merger's sticky word, as the host mirror does, and write the same clamped rows."""
+    from analyzer_amd.parallel.sweep import MergeClampError, SweepMerger
 
-    c = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.5))
-    y = c.clone()
-    R.BatchRater().rate(y, make_stream(StreamSpec(team_size=3, seed=seed + 1), 3 * P // 2, P), 3)
-    x = y.clone()
-    R.BatchRater().rate(x, make_stream(StreamSpec(team_size=3, seed=seed + 2), 4 * P, P), 3)
-    cb, yb = base_rows(c.state).contiguous(), base_rows(y.state).contiguous()
-    s = torch.empty((P, 16))
-    from analyzer_amd.ops.native import native
-    from analyzer_amd.models.tiers import vst_table
-
-    vst = torch.tensor(vst_table(), dtype=torch.float32)
-    native().sweep_delta(cb, cb, y.state, c.attrs, vst, 500.0, True, s)  # "the others' sum": Y - C
-    return c, cb, yb, x, s, vst
-
-
-@pytest.mark.parametrize("has_sum", [False, True])
-def test_lag_kernel_matches_host(gpu_device, has_sum):
-    """K9 lagged boundary (C += sum, message X - Y against C, Y = X = C + message):
-    device kernel == C++ host mirror (fp32 scaled operands), and the bf16 operand
-    kernel == the fp32 kernel followed by torch's conversion of the message."""
-    from analyzer_amd.ops.native import native
-
-    P = 5000
-    c, cb, yb, x, s, vst = _lag_inputs(P, 31)
-    g = lambda t: t.to(gpu_device).clone()
-    h = [cb.clone(), s.clone(), yb.clone(), x.state.clone()]
-    native().sweep_lag(h[0], h[1], h[2], h[3], c.attrs, vst, 500.0, True, has_sum)
-    d = [g(cb), g(s), g(yb), g(x.state)]
-    native().sweep_lag(d[0], d[1], d[2], d[3], g(c.attrs), g(vst), 500.0, True, has_sum)
-    for name, a, b in zip(("c", "msg", "y", "x"), h, d):
-        np.testing.assert_allclose(b.cpu().numpy(), a.numpy(), rtol=1e-3 if name == "msg" else 2e-5,
-                                   atol=1e-5 if name == "msg" else 1e-3, equal_nan=True, err_msg=name)
-    assert torch.equal(h[3].view(P, 8, 4)[..., 1::2], torch.zeros(P, 8, 2))  # tags 0
-    msg = g(s[:, :14]).to(torch.bfloat16).contiguous()
-    cnt = g(s[:, 14:]).to(torch.int32).contiguous()
-    ref = [g(cb), torch.cat([msg.float(), cnt.float()], dim=1), g(yb), g(x.state)]
-    native().sweep_lag(ref[0], ref[1], ref[2], ref[3], g(c.attrs), g(vst), 500.0, True, has_sum)
-    p = [g(cb), msg, cnt, g(yb), g(x.state)]
-    native().sweep_lag_packed(p[0], p[1], p[2], p[3], p[4], g(c.attrs), g(vst), 500.0, has_sum)
-    assert torch.equal(p[0].nan_to_num(-7), ref[0].nan_to_num(-7))
-    assert torch.equal(p[3].nan_to_num(-7), ref[2].nan_to_num(-7))
-    assert torch.equal(p[4].nan_to_num(-7), ref[3].nan_to_num(-7))
-    assert torch.equal(p[1].view(torch.int16), ref[1][:, :14].to(torch.bfloat16).view(torch.int16))
-    assert torch.equal(p[2], ref[1][:, 14:].to(torch.int32))
+    P = 3000
+    ro = make_roster(RosterSpec(num_players=P, seed=5, p_rated=1.0, p_mode_rated=1.0))
+    outs = []
+    for dev in ("cpu", gpu_device):
+        m = SweepMerger(P, dev, comm_dtype=comm, force=True)
+        r = ro.to(dev)
+        m.begin(r)
+        idx = torch.arange(0, P, 7, device=dev)
+        if comm == "fp32":
+            m.buf.zero_()
+            m.buf[idx, 0] = -2.0 / m.start[idx, 1] ** 2   # shared track: pi_b + d_pi < 0
+            m.buf[idx, 4] = -1.0e-12                      # mode track 2: a loss it can take
+            m.decode(r)
+        else:
+            m.msg.zero_()
+            m.cnt.zero_()
+            m.msg[idx, 0] = -1.25                         # 1 + r_pi < 0
+            m.decode_packed(r)
+        outs.append((m.clamp_hits(), r.state.cpu()))
+        with pytest.raises(MergeClampError):
+            m.check()
+    assert outs[0][0] == outs[1][0] == len(range(0, P, 7))
+    np.testing.assert_allclose(outs[1][1].numpy(), outs[0][1].numpy(), rtol=5e-5, atol=1e-6, equal_nan=True)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
