@@ -48,6 +48,10 @@ def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (default: WORLD_SIZE, else 1); N > 1 without torchrun spawns N ranks")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: the C++ host mirror on the CPU, ranks over gloo -- a rehearsal of this "
+                         "driver contract (spawn, rendezvous, merges, the JSON line) without a GPU, for "
+                         "tiny sizes only (tests/test_bench.py); every number it prints is a CPU number")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--players", type=int, default=1_000_000)
@@ -207,13 +211,23 @@ def main(argv=None) -> int:
     # one rank per GPU; ANA_DIST_BACKEND=gloo lets several ranks share one GPU to
     # rehearse the multi-process path on a 1-GPU box (production: nccl = RCCL)
     backend = EngineConfig.from_env().dist_backend
-    ngpu = torch.cuda.device_count()
-    local = local % ngpu if backend != "nccl" and ngpu else local
-    blocks = shared_card_blocks(world, ngpu, backend)
-    if blocks and not os.environ.get("ANA_RATE_BLOCKS"):
-        os.environ["ANA_RATE_BLOCKS"] = str(blocks)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    cpu = args.device == "cpu"
+    if cpu:
+        backend = "gloo"
+        dev = torch.device("cpu")
+    else:
+        ngpu = torch.cuda.device_count()
+        local = local % ngpu if backend != "nccl" and ngpu else local
+        blocks = shared_card_blocks(world, ngpu, backend)
+        if blocks and not os.environ.get("ANA_RATE_BLOCKS"):
+            os.environ["ANA_RATE_BLOCKS"] = str(blocks)
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+
+    def sync():
+        if not cpu:
+            torch.cuda.synchronize()
+
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -272,7 +286,7 @@ def main(argv=None) -> int:
         # telemetry_count_row_and_tail.log); needs hipStreamWaitValue64
         from analyzer_amd.ops.native import native as _native
 
-        if _native().can_wait_value(dev.index or 0):
+        if not cpu and _native().can_wait_value(dev.index or 0):
             args.telemetry_mode = "tail"
             tele_path = ("MFMA kernel on its own stream from %s of the rating's chunks (launch > "
                          "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.4"))
@@ -280,7 +294,7 @@ def main(argv=None) -> int:
         if tele is not None and args.telemetry_mode == "tail" else 0.0
     pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
-    torch.cuda.synchronize()
+    sync()
     prepared = {0: pipe.prepare(windows[0], window=Mw if step_prepass else 0)}
 
     tstream = None
@@ -343,20 +357,20 @@ def main(argv=None) -> int:
     for i in range(args.warmup * per):
         step(i)
     pipe.finish()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     if merger is not None:
         merger.timing = True  # stage events on the main stream (no syncs)
     t0 = time.perf_counter()
     for i in range(args.warmup * per, total_windows):
         step(i)
     pipe.finish()
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
     ms = elapsed * 1000.0 / args.steps
     merge = {}
@@ -461,6 +475,7 @@ def main(argv=None) -> int:
             "accuracy": accuracy,
             "rccl_world": dist.get_world_size() if world > 1 else None,
             "dist_backend": backend if world > 1 else None,
+            "device": dev.type,
             "config": {
                 "model": "TrueSkill 2-team EP (beta=1000, tau=10, draw_probability=0), "
                          "shared + per-mode tracks",

@@ -87,3 +87,37 @@ def test_shared_card_blocks():
     assert bench.shared_card_blocks(8, 1, "gloo") == 64
     assert bench.shared_card_blocks(6, 2, "gloo") == 170
     assert bench.shared_card_blocks(64, 1, "gloo") == 16
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_multi_rank_json_contract_on_cpu(tmp_path, n):
+    """The N > 1 path of the driver contract end to end on the CPU (``--device cpu``:
+    host mirror, gloo): bench.py spawns its own N ranks (127.0.0.1 rendezvous), runs
+    one-prepass-per-step DP steps with a merge after each of k = N windows, and rank 0
+    prints ONE JSON line with the N > 1 keys -- the rank count, the merge split with the
+    prepass placement, the accuracy block with the per-participant record errors and
+    the merge decodes' clamp count."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, ANA_DIST_BACKEND="gloo", OMP_NUM_THREADS="1")
+    for var in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(var, None)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--device", "cpu", "--gpus", str(n),
+                          "--players", "2000", "--matches-per-gpu", str(1000 * n), "--steps", "2", "--warmup", "1"],
+                         cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 only
+    j = json.loads(lines[0])
+    k = min(n, 8)
+    assert j["n_gpus"] == n and j["rccl_world"] == n and j["dist_backend"] == "gloo" and j["device"] == "cpu"
+    assert j["config"]["parallelism"] == "dp%d" % n and j["config"]["merges_per_step"] == k
+    assert j["value"] == pytest.approx(n * 1000 * n / (j["ms_per_step"] / 1000.0))
+    mm = j["merge_ms"]
+    assert mm["prepass_placement"] and mm["prepass_per"] == "step" and mm["buckets"] >= 1
+    acc = j["accuracy"]
+    for key in ("records_dmu_median", "records_dmu_p99", "records_dmu_max", "spearman_mu_minus_sigma"):
+        assert acc[key] is not None, key
+    assert acc["merge_clamp_hits"] == 0
