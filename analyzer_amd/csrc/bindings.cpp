@@ -797,6 +797,14 @@ void epoch_bump(Tensor e) {
   check_hip(ana::launch_epoch_bump(e.data_ptr<int32_t>(), stream_of(e)), "epoch_bump");
 }
 
+// the all-reduce stand-in of one-GPU DP pricing (kernels.hip emulate_allreduce_kernel)
+void emulate_allreduce(Tensor buf, int64_t channels, int64_t passes, double us) {
+  TORCH_CHECK(buf.is_cuda() && buf.is_contiguous(), "emulate_allreduce: a contiguous device tensor");
+  check_hip(ana::launch_emulate_allreduce(buf.data_ptr(), (int64_t)(buf.numel() * buf.element_size()), (int)channels,
+                                          (int)passes, us, stream_of(buf)),
+            "emulate_allreduce");
+}
+
 void warm_rows(Tensor state, Tensor sink) {
   const auto dev = state.device();
   check(state, "state", torch::kFloat32, dev);
@@ -879,6 +887,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stream_wait_value64", &stream_wait_value64, "hipStreamWaitValue64(stream, ptr, >= value)");
   m.def("can_wait_value", &can_wait_value, "hipDeviceAttributeCanUseStreamWaitValue");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
+  m.def("emulate_allreduce", &emulate_allreduce,
+        "DP pricing on one GPU: an all-reduce stand-in (buffer unchanged) on N CUs for >= us microseconds");
   m.def("warm_rows", &warm_rows, "read every roster row once (cache warm-up before a rating launch)");
   m.def("epoch_bump", &epoch_bump, "device launch epoch += 1 (graph replays)");
   m.attr("ROW_FLOATS") = ana::kRowFloats;

@@ -25,6 +25,9 @@ int launch_reset_tags(float* state, int64_t P, hipStream_t s);
 int launch_warm_rows(const float* state, int64_t P, uint32_t* sink, hipStream_t s);
 // e[0] += 1 on the stream (the device epoch of graph replays, RateParams::epoch_ptr)
 int launch_epoch_bump(int32_t* e, hipStream_t s);
+// DP pricing on one GPU: an all-reduce stand-in over `bytes` of `buf` (unchanged) on
+// `channels` workgroups, `passes` streams of the buffer, held at least `us` microseconds
+int launch_emulate_allreduce(void* buf, int64_t bytes, int channels, int passes, double us, hipStream_t s);
 
 size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
 

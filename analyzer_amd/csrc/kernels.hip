@@ -122,6 +122,36 @@ int launch_warm_rows(const float* state, int64_t P, uint32_t* sink, hipStream_t 
   return (int)hipGetLastError();
 }
 
+// An all-reduce stand-in for pricing DP steps on ONE GPU (parallel/sweep.py
+// ``emulate``): what an RCCL ring all-reduce of the merge operands does to this GPU
+// -- `channels` workgroups (RCCL's channel count, one CU each) stream the operand
+// buffer `passes` times (the local reads / reduce / writes of a ring: about 3x the
+// size) and hold their CUs until `ticks` of the 100-MHz s_memrealtime clock have
+// passed since the first wave started (the xGMI transfer time of the modelled link
+// bandwidth).  The buffer is rewritten unchanged (each word xor 0 with a runtime
+// zero), so the merge decodes exactly what one rank's identity all-reduce leaves.
+__global__ void __launch_bounds__(256) emulate_allreduce_kernel(uint4* buf, int64_t n, int passes, uint32_t zero,
+                                                               uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int q = 0; q < passes; ++q)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+      uint4 v = buf[i];
+      v.x ^= zero;
+      buf[i] = v;
+    }
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+int launch_emulate_allreduce(void* buf, int64_t bytes, int channels, int passes, double us, hipStream_t s) {
+  const int64_t n = bytes / 16;
+  if (n <= 0 || channels < 1) return 0;
+  const uint64_t ticks = (uint64_t)(us > 0 ? us * 100.0 : 0.0);  // s_memrealtime: 100 MHz
+  hipLaunchKernelGGL(emulate_allreduce_kernel, dim3((unsigned)channels), dim3(256), 0, s,
+                     reinterpret_cast<uint4*>(buf), n, passes, 0u, ticks);
+  return (int)hipGetLastError();
+}
+
 // Device-side launch epoch of a captured graph: one bump per replay, before the
 // rate launch that reads it (the host resets the tags and the counter before 255).
 __global__ void epoch_bump_kernel(int32_t* e) { e[0] += 1; }

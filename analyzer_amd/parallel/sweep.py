@@ -84,7 +84,8 @@ COMM_DTYPES = {"fp32": torch.float32, "fp16": torch.float16, "bf16": torch.bfloa
 class SweepMerger:
     def __init__(self, num_players: int, device, cfg: Optional[RaterConfig] = None,
                  group=None, comm_dtype: str = "fp32", bucket_rows: Optional[int] = None,
-                 sweeps: int = 1, world_size: Optional[int] = None, force: bool = False):
+                 sweeps: int = 1, world_size: Optional[int] = None, force: bool = False,
+                 emulate: Optional[str] = None):
         self.P = int(num_players)
         self.device = torch.device(device)
         self.cfg = cfg or RaterConfig.from_env()
@@ -98,6 +99,20 @@ class SweepMerger:
         # force: run the merge kernels even on one rank (the all-reduce of one rank
         # is the identity) -- bench.py --force-merge prices the merge without comm
         self.force = bool(force)
+        # emulate = "N:GBps[:us]" (one rank, force): every all-reduce is replaced by a stand-in
+        # on a stream of its own that takes what an N-rank ring all-reduce of the operands would
+        # over links of GBps bus bandwidth (+ us latency) and streams the buffer like RCCL's
+        # channels do (csrc/kernels.hip emulate_allreduce_kernel) -- one GPU then prices the
+        # N-GPU step, the merge's exposed collective included (bench.py --emulate-allreduce)
+        self.emulate = None
+        if emulate:
+            parts = [float(x) for x in str(emulate).split(":")]
+            ranks, bw = int(parts[0]), parts[1]
+            lat = parts[2] if len(parts) > 2 else 25.0
+            if ranks < 2 or bw <= 0:
+                raise ValueError("emulate must be N:GBps[:latency_us] with N >= 2")
+            self.emulate = (ranks, bw, lat)
+        self._comm = None  # stream of the emulated collective
         # fp16/bf16: messages use the base-relative encoding (sweep_core.h) and
         # travel compressed; the touch counters travel separately as int32
         self.comm_dtype = comm_dtype
@@ -216,11 +231,38 @@ class SweepMerger:
         parts = [self.msg[lo:hi], self.cnt[lo:hi]] if packed else self._split(buf)
         # one rank (force): the sum over ranks is the message itself
         works = [all_reduce_sum(t, group=self.group, async_op=True) for t in parts] if self.world > 1 else []
+        if self.world <= 1 and self.emulate is not None and self.device.type == "cuda":
+            return self._emulated_reduce(parts, buf, packed)
 
         def finish():
             for w in works:
                 if w is not None:
                     w.wait()
+            if not packed:
+                self._join(buf, parts)
+        return finish
+
+    def emulated_us(self, nbytes: int) -> float:
+        """Modelled time of an N-rank ring all-reduce of nbytes (``emulate``)."""
+        n, bw, lat = self.emulate
+        return lat + 2.0 * (n - 1) / n * nbytes / (bw * 1e3)
+
+    def _emulated_reduce(self, parts, buf, packed):
+        """The all-reduce stand-in (``emulate``), on its own stream after the
+        messages, as RCCL runs its kernels; the finisher makes the main stream wait."""
+        main = torch.cuda.current_stream(self.device)
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(self.device)
+        self._comm.wait_stream(main)
+        nbytes = sum(t.numel() * t.element_size() for t in parts)
+        with torch.cuda.stream(self._comm):
+            for i, t in enumerate(parts):  # the time is modelled on the whole operand set
+                native().emulate_allreduce(t, 16, 3, self.emulated_us(nbytes) if i == 0 else 0.0)
+        done = torch.cuda.Event()
+        done.record(self._comm)
+
+        def finish():
+            main.wait_event(done)
             if not packed:
                 self._join(buf, parts)
         return finish

@@ -81,7 +81,7 @@ class WindowPipeline:
         # all-reduce costs on this interconnect (probe_placement)
         self.allreduce_probe_ms: Optional[float] = None
         if dp and self.cuda and self.ecfg.prepass_serial is None and \
-                getattr(merger, "world", 1) > 1:
+                (getattr(merger, "world", 1) > 1 or getattr(merger, "emulate", None) is not None):
             self.serial = self.probe_placement(merger)
         # serial prepass: nothing to overlap, no tail signal -- unless a caller wants the
         # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail)
@@ -142,9 +142,12 @@ class WindowPipeline:
         and go serial when it exceeds ANA_DP_SERIAL_AR_US (default 40 us)."""
         from ..parallel.comm import time_all_reduce
 
-        buf = torch.zeros(max(1, int(merger.comm_bytes) // 2), dtype=torch.bfloat16, device=self.device)
-        ms = time_all_reduce(buf, getattr(merger, "group", None))
-        del buf
+        if getattr(merger, "world", 1) <= 1 and getattr(merger, "emulate", None) is not None:
+            ms = merger.emulated_us(int(merger.comm_bytes)) / 1000.0  # the modelled collective
+        else:
+            buf = torch.zeros(max(1, int(merger.comm_bytes) // 2), dtype=torch.bfloat16, device=self.device)
+            ms = time_all_reduce(buf, getattr(merger, "group", None))
+            del buf
         self.allreduce_probe_ms = ms
         thr = float(os.environ.get("ANA_DP_SERIAL_AR_US") or 40.0) / 1000.0
         return ms > thr

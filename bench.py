@@ -102,6 +102,12 @@ def parse(argv=None):
                     help="N > 1: after timing, rank 0 measures the sweep-DP error of this run's "
                          "configuration against the exact sequential rating (parallel/accuracy.py, "
                          "N ranks simulated on its GPU) and reports it in the JSON line (0 = skip)")
+    ap.add_argument("--emulate-allreduce", default=None, metavar="N:GBps[:us]",
+                    help="with --force-merge on one GPU: replace the (identity) all-reduce of every merge "
+                         "by a stand-in that takes the modelled time of an N-rank ring all-reduce of the "
+                         "operands at GBps bus bandwidth (+ us latency, default 25) and streams the buffer "
+                         "on 16 CUs as RCCL's channels do -- a one-GPU projection of the N-GPU step "
+                         "(parallel/sweep.py emulate); the prepass placement follows the modelled time")
     ap.add_argument("--step-prepass", type=int, default=-1, choices=[-1, 0, 1],
                     help="merges per step > 1: 1 = ONE schedule prepass per step over its k windows "
                          "(links cut at the window boundaries, runtime/engine.py step_windows), 0 = a "
@@ -271,7 +277,10 @@ def main(argv=None) -> int:
         tele = [make_telemetry(tspec, windows[w], K, base=(w * world + rank) * M) for w in range(n_windows)]
         stats = allocate_stats(M, K, dev)
         n_events = sum(t.num_events for t in tele) / n_windows
-    merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge)
+    if args.emulate_allreduce and (world > 1 or not args.force_merge or cpu):
+        raise SystemExit("bench: --emulate-allreduce prices N ranks on ONE GPU (needs --force-merge, N = 1)")
+    merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge,
+                          emulate=args.emulate_allreduce)
               if world > 1 or args.force_merge else None)
     auto_mode = args.telemetry_mode == "auto"
     tele_path = None
@@ -493,6 +502,7 @@ def main(argv=None) -> int:
                 "skew": args.skew,
                 "comm_dtype": args.comm_dtype if world > 1 or args.force_merge else None,
                 "force_merge": bool(args.force_merge),
+                "emulated_allreduce": args.emulate_allreduce,
                 "sweeps": args.sweeps if world > 1 else None,
                 **extra,
             },

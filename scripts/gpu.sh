@@ -283,6 +283,10 @@ EOF
           ANA_PREPASS_SERIAL=1 run dpstep/k${k}_step_serial_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge \
               --merges-per-step $k
         done
+        for k in ${DPEMU_K:-8 16}; do  # N = 8 projected: the all-reduce stand-in (8 ranks, 300 GB/s bus bandwidth)
+          run dpstep/k${k}_emu8_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step $k \
+              --emulate-allreduce 8:300
+        done
         run dpstep/k8_window_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step 8 --step-prepass 0
         ANA_PREPASS_PIECES=0 run dpstep/k8_whole_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge \
             --merges-per-step 8
