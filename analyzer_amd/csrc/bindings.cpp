@@ -609,6 +609,42 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
                         s.data_ptr<float>(), p2, true, vst.data_ptr<float>(), (float)unknown_sigma, P, cl);
 }
 
+// causal record correction of a window's records (parallel/sweep.py): rows = RateResult
+// packed [M, row]; start = window-start base rows [P, 16]; prefix = the exclusive prefix of
+// the merge messages over ranks: fp32 [P, 16] raw, or bf16 / fp16 [P, 14] scaled
+void correct_records(Tensor rec, int64_t K, Tensor rows, Tensor start, Tensor prefix, Tensor attrs, Tensor vst,
+                     double unknown_sigma) {
+  const auto dev = rows.device();
+  check(rec, "rec", torch::kInt32, dev);
+  TORCH_CHECK(K >= 1 && K <= 5 && rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
+  const int64_t M = rec.size(0);
+  TORCH_CHECK(rows.dim() == 2 && rows.size(0) == M && rows.scalar_type() == torch::kFloat32 && rows.stride(1) == 1 &&
+                  rows.size(1) >= 5 * 2 * K + 2,
+              "rows must be RateResult.packed [M, row] fp32");
+  const int64_t P = start.size(0);
+  check_rows(start, "start (base rows)", P, ana::kBaseFloats, dev);
+  check_rows(attrs, "attrs", P, 4, dev);
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
+  const bool raw = prefix.scalar_type() == torch::kFloat32;
+  TORCH_CHECK(prefix.device() == dev && prefix.is_contiguous() && prefix.dim() == 2 && prefix.size(0) == P &&
+                  prefix.size(1) == (raw ? 16 : 14) &&
+                  (raw || prefix.scalar_type() == torch::kBFloat16 || prefix.scalar_type() == torch::kHalf),
+              "prefix must be fp32 [P, 16] or bf16 / fp16 [P, 14]");
+  if (dev.is_cuda()) {
+    const int kind = raw ? 0 : prefix.scalar_type() == torch::kBFloat16 ? 1 : 2;
+    check_hip(ana::launch_correct_records((int)K, rec.data_ptr<int32_t>(), M, rows.data_ptr<float>(), rows.stride(0),
+                                          start.data_ptr<float>(), prefix.data_ptr(), kind, attrs.data_ptr<float>(),
+                                          vst.data_ptr<float>(), (float)unknown_sigma, P, stream_of(rows)),
+              "correct_records");
+    return;
+  }
+  Tensor pf = raw ? prefix : prefix.to(torch::kFloat32).contiguous();
+  ana::host_correct_records((int)K, rec.data_ptr<int32_t>(), M, rows.data_ptr<float>(), rows.stride(0),
+                            start.data_ptr<float>(), pf.data_ptr<float>(), raw, attrs.data_ptr<float>(),
+                            vst.data_ptr<float>(), (float)unknown_sigma, P);
+}
+
 // ------------------------------------------------------------- C2 exchange
 // rec: the rank's slice of one round [m, 2K+2]; status: its per-match status
 // (any row stride); out: [cap, 33] float entries, cap >= m * 2K
@@ -866,6 +902,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sweep_apply_packed", &sweep_apply_packed, "K9: decode bf16/fp16 + int32 summed messages (-> s, s2)",
         py::arg("s0"), py::arg("msg"), py::arg("cnt"), py::arg("attrs"), py::arg("s"), py::arg("s2"), py::arg("vst"),
         py::arg("unknown_sigma"), py::arg("clamps") = py::none());
+  m.def("correct_records", &correct_records,
+        "K9: causal correction of a window's records by the exclusive prefix of the merge messages");
   m.def("pack_rows", &pack_rows, "C2: changed rows of a round slice -> fixed-capacity [cap, 33] entries");
   m.def("check_round", &check_round, "C2 race detector: one round's matches share no player (flag |= 1)");
   m.def("unpack_rows", &unpack_rows, "C2: write gathered entries (id >= 0) into the roster, tags zeroed");

@@ -35,4 +35,9 @@ void host_sweep_delta(const float* s0, const float* a, const float* s, const flo
 // clamps (nullable): += decoded tracks whose merged precision hit the floor (sweep_core.h)
 void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                       bool scaled, const float* vst, float unknown_sigma, int64_t P, uint32_t* clamps = nullptr);
+// causal record correction (sweep_core.h correct_record_slot); prefix: raw fp32 [P][16]
+// (raw) or the scaled messages as fp32 [P][14]
+void host_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* start,
+                          const float* prefix, bool raw, const float* attrs, const float* vst, float unknown_sigma,
+                          int64_t P);
 }  // namespace ana

@@ -251,6 +251,87 @@ sweep_apply_packed_kernel(const float2* __restrict__ s0, const uint32_t* __restr
              (uint32_t)c.y, attrs, vst, unknown_sigma, true, s, s2, clamps);
 }
 
+// ------------------------------------------------- causal record correction
+// One thread per slot of the window's records (sweep_core.h correct_record_slot):
+// rows: RateResult's packed rows [M][orow] ([s_mu | s_sig | delta | m_mu | m_sig][S],
+// quality, status byte); start: the window-start base rows; the prefix message of
+// each player, scaled H [P][14] (bf16 / fp16 merges) or raw fp32 [P][16] (RAW).
+template <int K, typename H, bool RAW>
+__global__ void __launch_bounds__(256)
+correct_records_kernel(const int32_t* __restrict__ rec, int64_t M, float* rows, int64_t orow,
+                       const float2* __restrict__ start, const void* __restrict__ prefix,
+                       const float4* __restrict__ attrs, const float* __restrict__ vst, float unknown_sigma,
+                       int64_t P) {
+  constexpr int S = 2 * K;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= M * S) return;
+  const int64_t m = e / S;
+  const int j = (int)(e - m * S);
+  float* row = rows + m * orow;
+  if (reinterpret_cast<const uint8_t*>(row + 5 * S + 1)[0] != kRated) return;
+  const int32_t* r = rec + m * (S + 2);
+  const uint32_t m0 = (uint32_t)r[S];
+  if ((j < K ? j : j - K) >= (j < K ? meta_n0(m0) : meta_n1(m0))) return;
+  const int32_t p = r[j];
+  if (p < 0 || p >= P) return;
+  const int t = 1 + meta_mode(m0);
+  float c[kBaseFloats];
+#pragma unroll
+  for (int g = 0; g < kGranules; ++g) {
+    const float2 v = start[(int64_t)p * kGranules + g];
+    c[2 * g] = v.x;
+    c[2 * g + 1] = v.y;
+  }
+  const float4 a4 = attrs[p];
+  const float attr[4] = {a4.x, a4.y, a4.z, a4.w};
+  float spi, stau, mpi, mtau;
+  if constexpr (RAW) {
+    const float* d = reinterpret_cast<const float*>(prefix) + (int64_t)p * 16;
+    float seed_mu = NAN, seed_sig = NAN;
+    const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
+    raw_to_scaled(0, c, seeded, seed_mu, seed_sig, d[0], d[1], spi, stau);
+    raw_to_scaled(t, c, seeded, seed_mu, seed_sig, d[2 * t], d[2 * t + 1], mpi, mtau);
+  } else {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(prefix) + (int64_t)p * kTracks;
+    const uint32_t w0 = w[0], wt = w[t];
+    spi = from_half_bits<H>(w0 & 0xffffu);
+    stau = from_half_bits<H>(w0 >> 16);
+    mpi = from_half_bits<H>(wt & 0xffffu);
+    mtau = from_half_bits<H>(wt >> 16);
+  }
+  float smu = row[j], ssg = row[S + j], mmu = row[3 * S + j], msg = row[4 * S + j];
+  correct_record_slot(c, t, attr, vst, unknown_sigma, spi, stau, mpi, mtau, &smu, &ssg, &mmu, &msg);
+  row[j] = smu;
+  row[S + j] = ssg;
+  row[3 * S + j] = mmu;
+  row[4 * S + j] = msg;
+}
+
+int launch_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* start,
+                           const void* prefix, int kind, const float* attrs, const float* vst,
+                           float unknown_sigma, int64_t P, hipStream_t st) {
+  const int64_t n = M * 2 * K;
+  if (n <= 0) return 0;
+  const dim3 grid((unsigned)((n + 255) / 256));
+#define ANA_CORR(k, H, RAW)                                                                                    \
+  hipLaunchKernelGGL((correct_records_kernel<k, H, RAW>), grid, dim3(256), 0, st, rec, M, rows, orow,          \
+                     reinterpret_cast<const float2*>(start), prefix, reinterpret_cast<const float4*>(attrs), vst, \
+                     unknown_sigma, P)
+#define ANA_CORR_K(k)                        \
+  case k:                                    \
+    if (kind == 0) ANA_CORR(k, float, true); \
+    else if (kind == 1) ANA_CORR(k, __bf16, false); \
+    else ANA_CORR(k, _Float16, false);       \
+    break;
+  switch (K) {
+    ANA_CORR_K(1) ANA_CORR_K(2) ANA_CORR_K(3) ANA_CORR_K(4) ANA_CORR_K(5)
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef ANA_CORR_K
+#undef ANA_CORR
+  return (int)hipGetLastError();
+}
+
 static dim3 track_grid(int64_t P) {
   return dim3((unsigned)((P * kLanesPerPlayer + 255) / 256));
 }

@@ -33,6 +33,7 @@ import torch
 from ..config import MODES
 from ..ops.rate import BatchRater, RateResult, Roster
 from ..ops.synth import RosterSpec, StreamSpec, make_roster, make_stream
+from ..ops.native import native
 from .sweep import COMM_DTYPES, SweepMerger
 
 TRACKS = ["shared"] + list(MODES)
@@ -49,10 +50,12 @@ def _quantize(buf: torch.Tensor, comm_dtype: str) -> torch.Tensor:
 
 def simulate_sweep_dp(rater: BatchRater, roster: Roster, shards: Sequence[torch.Tensor], K: int,
                       sweeps: int = 1, comm_dtype: str = "fp32",
-                      outs: Optional[List[RateResult]] = None) -> List[RateResult]:
+                      outs: Optional[List[RateResult]] = None, correct: bool = True) -> List[RateResult]:
     """Rate one window split into ``len(shards)`` time slices the way N ranks of
     sweep DP would, updating ``roster`` to the merged result.  Returns the
-    per-rank outputs of the last sweep."""
+    per-rank outputs of the last sweep; with ``correct`` (one sweep) each rank's
+    records carry the causal record correction (the prefix of the earlier ranks'
+    messages, in the wire dtype, summed in rank order)."""
     N = len(shards)
     mergers = [SweepMerger(roster.num_players, roster.device, rater.cfg, comm_dtype=comm_dtype,
                            sweeps=sweeps, world_size=N) for _ in range(N)]
@@ -80,8 +83,16 @@ def simulate_sweep_dp(rater: BatchRater, roster: Roster, shards: Sequence[torch.
                 acc = acc + msgs[r]
         else:  # final merge: every rank decodes start + all messages
             total = torch.zeros_like(msgs[0])
-            for x in msgs:
+            for r, x in enumerate(msgs):
+                if correct and sweeps == 1:
+                    # the causal record correction of rank r's records by the messages of
+                    # the ranks before it, against the window start (parallel/sweep.py)
+                    m = mergers[r]
+                    prefix = total if comm_dtype == "fp32" else total[:, :14].to(COMM_DTYPES[comm_dtype])
+                    native().correct_records(shards[r], K, outs[r].packed, m.start, prefix.contiguous(),
+                                             rosters[r].attrs, m.vst, float(rater.cfg.unknown_player_sigma))
                 total = total + x
+            total = _quantize(total, comm_dtype)  # what the collective delivers: summed, rounded once
             for m, ro in zip(mergers, rosters):
                 m.buf.copy_(total)
                 m.decode(ro, into=m.start)
@@ -150,7 +161,7 @@ def compare(approx: Roster, exact: Roster, out_a: Optional[List[RateResult]] = N
 
 def run(ranks: int, players: int, matches_per_rank: int, windows: int, sweeps: Sequence[int],
         device="cpu", team_size: int = 3, seed: int = 11, comm_dtype: str = "fp32",
-        p_rated: float = 0.3, warm_windows: int = 0) -> Dict[str, object]:
+        p_rated: float = 0.3, warm_windows: int = 0, correct: bool = True) -> Dict[str, object]:
     """Accuracy table: exact sequential vs sweep DP at each sweep count.
     ``warm_windows``: exact windows rated first (shared by both), so the
     comparison starts from a settled roster rather than fresh priors."""
@@ -179,14 +190,15 @@ def run(ranks: int, players: int, matches_per_rank: int, windows: int, sweeps: S
         torch.cuda.synchronize(dev)
     table = {"ranks": ranks, "players": players, "matches_per_rank": M, "windows": windows,
              "warm_windows": warm_windows, "team_size": K, "comm_dtype": comm_dtype,
-             "device": str(dev), "exact_s": time.perf_counter() - t0, "sweeps": {}}
+             "device": str(dev), "exact_s": time.perf_counter() - t0, "sweeps": {},
+             "records_corrected": bool(correct)}
     for S in sweeps:
         t0 = time.perf_counter()
         approx = base.clone()
         outs = None
         CLAMPS = 0
         for shards in shard_sets:
-            outs = simulate_sweep_dp(rater, approx, shards, K, sweeps=S, comm_dtype=comm_dtype)
+            outs = simulate_sweep_dp(rater, approx, shards, K, sweeps=S, comm_dtype=comm_dtype, correct=correct)
         if dev.type == "cuda":
             torch.cuda.synchronize(dev)
         stats = compare(approx, exact, outs, out_e)
@@ -208,11 +220,13 @@ def main(argv=None) -> int:
     ap.add_argument("--comm-dtype", default="fp32", choices=sorted(COMM_DTYPES))
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--seed", type=int, default=11)
+    ap.add_argument("--no-correct", action="store_true",
+                    help="records without the causal record correction (parallel/sweep.py)")
     args = ap.parse_args(argv)
     sweeps = [int(x) for x in args.sweeps.split(",") if x]
     table = run(args.ranks, int(args.players), int(args.matches_per_rank), args.windows, sweeps,
                 device=args.device, team_size=args.team_size, seed=args.seed,
-                comm_dtype=args.comm_dtype, warm_windows=args.warm_windows)
+                comm_dtype=args.comm_dtype, warm_windows=args.warm_windows, correct=not args.no_correct)
     print(json.dumps(table, indent=1), flush=True)
     return 0
 

@@ -11,6 +11,10 @@ messages through RabbitMQ (/root/reference/worker.py:44-46,85-92).
 * ``shard`` -- contiguous block partition of a range (time-axis sharding, P1/P4).
 * ``exclusive_scan`` (C1') -- per-row prefix sum over ranks (causal re-sweeps of
   parallel/sweep.py) as two all-to-alls.
+* ``scan_and_sum`` (C1 + C1') -- the merge's collective when records are corrected:
+  the sum over ranks AND each rank's exclusive prefix from one exchange (two
+  all-to-alls + an all-gather of the block sums: 3 (N-1)/N of the buffer per rank,
+  against 2 (N-1)/N for the all-reduce alone and 4 (N-1)/N for both separately).
 """
 from __future__ import annotations
 
@@ -69,6 +73,44 @@ def exclusive_scan(t: torch.Tensor, group=None) -> torch.Tensor:
     back = torch.empty_like(send)
     all_to_all_rows(back, ex.view(size * blk, C), group)  # block b = my prefix of block b
     return back[:P].view_as(t)
+
+
+def all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """``all_gather_into_tensor`` of equal row blocks (gloo + device: staged)."""
+    if _staged(inp, group):
+        o = torch.empty_like(out, device="cpu")
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def scan_and_sum(t: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(exclusive prefix over ranks, sum over ranks) of ``t``, row-wise.  Rank b
+    owns row block b: one all-to-all brings it block b of every rank, which it
+    prefix-sums and sums in rank order (floating types in fp32, rounded once to the
+    wire type); a second all-to-all returns each rank its prefix, an all-gather the
+    block sums.  One rank: (zeros, t)."""
+    _, size = world(group)
+    if size <= 1:
+        return torch.zeros_like(t), t
+    P = t.shape[0]
+    C = t[0].numel() if P else 1
+    blk = -(-P // size)
+    send = t.new_zeros((size * blk, C))
+    send[:P] = t.reshape(P, C)
+    recv = torch.empty_like(send)
+    all_to_all_rows(recv, send, group)  # recv block q = rank q's rows of my block
+    r3 = recv.view(size, blk, C)
+    acc = r3.float() if t.is_floating_point() else r3
+    cs = torch.cumsum(acc, 0)
+    ex = torch.zeros_like(cs)
+    ex[1:] = cs[:-1]
+    back = torch.empty_like(send)
+    all_to_all_rows(back, ex.to(t.dtype).view(size * blk, C), group)  # block b = my prefix of block b
+    total = torch.empty_like(send)
+    all_gather_rows(total, cs[-1].to(t.dtype).contiguous(), group)
+    return back[:P].view_as(t), total[:P].view_as(t)
 
 
 def all_reduce_sum(t: torch.Tensor, group=None, async_op: bool = False):

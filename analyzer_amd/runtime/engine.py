@@ -278,7 +278,12 @@ class WindowPipeline:
             self._rated = done
         if self.merger is not None:
             with trace_range("merge", window=self.windows_rated):
-                self.merger.merge(self.roster, overlap=overlap)
+                if getattr(self.merger, "correct", False) and res is not None and res.packed is not None and \
+                        (self.merger.world > 1 or self.merger.force):
+                    # the window's records corrected by the earlier ranks' evidence (parallel/sweep.py)
+                    self.merger.merge_corrected(self.roster, prep.rec, res, overlap=overlap)
+                else:
+                    self.merger.merge(self.roster, overlap=overlap)
         elif overlap is not None:
             overlap()
         self.windows_rated += 1

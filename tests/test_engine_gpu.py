@@ -313,6 +313,37 @@ def test_sweep_kernels_match_host(gpu_device, scaled, resweep):
     assert torch.equal(base_rows(sh).nan_to_num(-7), sh2.nan_to_num(-7))
 
 
+@pytest.mark.parametrize("comm", ["fp32", "bf16", "fp16"])
+def test_record_correction_kernel_matches_host(gpu_device, comm):
+    """K9 causal record correction (one thread per slot): device == host mirror on a
+    rated window's records, NULL tracks, seeds, AFK / invalid matches and a prefix of
+    real messages (another slice's evidence) in every wire format."""
+    from analyzer_amd.ops.native import native
+    from analyzer_amd.parallel.sweep import COMM_DTYPES, SweepMerger
+
+    P, M, K = 5000, 20000, 3
+    rs = RosterSpec(num_players=P, seed=41, p_rated=0.4)
+    start = make_roster(rs)
+    other = start.clone()
+    R.BatchRater().rate(other, make_stream(StreamSpec(team_size=K, seed=42), M, P, K=K), K)
+    m = SweepMerger(P, "cpu", comm_dtype=comm, force=True)
+    m.begin(start)
+    m.messages(other)  # an earlier slice's messages against the start: the prefix
+    prefix = m.buf.clone() if comm == "fp32" else m.buf[:, :14].to(COMM_DTYPES[comm]).contiguous()
+    rec = make_stream(StreamSpec(team_size=K, seed=43, p_afk=0.05, p_uneven=0.05), M, P, K=K)
+    ro = start.clone()
+    out = R.BatchRater().rate(ro, rec, K)
+    host = out.packed.clone()
+    native().correct_records(rec, K, host, m.start, prefix, start.attrs, m.vst, 500.0)
+    dev = out.packed.to(gpu_device)
+    g = lambda t: t.to(gpu_device)
+    native().correct_records(g(rec), K, dev, g(m.start), g(prefix), g(start.attrs), g(m.vst), 500.0)
+    torch.cuda.synchronize()
+    changed = (host != out.packed) & ~torch.isnan(host)
+    assert int(changed.sum()) > 10000  # the prefix moved most rated records
+    np.testing.assert_allclose(dev.cpu().numpy(), host.numpy(), rtol=2e-6, atol=2e-3, equal_nan=True)
+
+
 @pytest.mark.parametrize("comm", ["fp32", "bf16"])
 def test_device_decode_counts_clamps_like_host(gpu_device, comm):
     """The merge decode kernels count every track held at the precision floor into the
