@@ -575,8 +575,11 @@ void sweep_delta_packed(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor 
   cnt.copy_(buf.slice(1, 14, 16));
 }
 
+void prefix_delta(Tensor s0, Tensor prefix, Tensor attrs, Tensor vst, double unknown_sigma, Tensor delta);
+
 void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor s, Tensor s2, Tensor vst,
-                        double unknown_sigma, const c10::optional<Tensor>& clamps) {
+                        double unknown_sigma, const c10::optional<Tensor>& clamps,
+                        const c10::optional<Tensor>& prefix, const c10::optional<Tensor>& delta) {
   const auto dev = s.device();
   uint32_t* cl = clamp_ptr(clamps, dev);
   const int64_t P = s.size(0);
@@ -594,14 +597,26 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
   }
   check(vst, "vst", torch::kFloat32, dev);
   TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
+  const bool with_prefix = prefix.has_value() && prefix->defined() && prefix->numel() > 0;
+  if (with_prefix) {
+    TORCH_CHECK(delta.has_value() && delta->defined(), "a prefix needs a delta table");
+    TORCH_CHECK(prefix->scalar_type() == msg.scalar_type() && prefix->is_contiguous() && prefix->device() == dev &&
+                    prefix->sizes() == msg.sizes(),
+                "prefix must be like msg");
+    check_rows(*delta, "delta", P, 16, dev);
+  }
   if (dev.is_cuda()) {
     check_hip(ana::launch_sweep_apply_packed(s0.data_ptr<float>(), msg.data_ptr(), cnt.data_ptr<int32_t>(),
                                              msg.scalar_type() == torch::kBFloat16 ? 1 : 0,
                                              attrs.data_ptr<float>(), s.data_ptr<float>(), p2,
-                                             vst.data_ptr<float>(), (float)unknown_sigma, P, cl, stream_of(s)),
+                                             vst.data_ptr<float>(), (float)unknown_sigma, P, cl,
+                                             with_prefix ? prefix->data_ptr() : nullptr,
+                                             with_prefix ? delta->data_ptr<float>() : nullptr, stream_of(s)),
               "sweep_apply_packed");
     return;
   }
+  if (with_prefix)  // (before the host decode: it overwrites the window start through s2)
+    prefix_delta(s0, *prefix, attrs, vst, unknown_sigma, *delta);
   Tensor buf = torch::empty({P, 16}, s.options());
   buf.slice(1, 0, 14).copy_(msg);
   buf.slice(1, 14, 16).copy_(cnt);
@@ -610,10 +625,8 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
 }
 
 // causal record correction of a window's records (parallel/sweep.py): rows = RateResult
-// packed [M, row]; start = window-start base rows [P, 16]; prefix = the exclusive prefix of
-// the merge messages over ranks: fp32 [P, 16] raw, or bf16 / fp16 [P, 14] scaled
-void correct_records(Tensor rec, int64_t K, Tensor rows, Tensor start, Tensor prefix, Tensor attrs, Tensor vst,
-                     double unknown_sigma) {
+// packed [M, row] += delta [P, 16] fp32 (raw natural-parameter increments per track)
+void correct_records(Tensor rec, int64_t K, Tensor rows, Tensor delta) {
   const auto dev = rows.device();
   check(rec, "rec", torch::kInt32, dev);
   TORCH_CHECK(K >= 1 && K <= 5 && rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
@@ -621,28 +634,42 @@ void correct_records(Tensor rec, int64_t K, Tensor rows, Tensor start, Tensor pr
   TORCH_CHECK(rows.dim() == 2 && rows.size(0) == M && rows.scalar_type() == torch::kFloat32 && rows.stride(1) == 1 &&
                   rows.size(1) >= 5 * 2 * K + 2,
               "rows must be RateResult.packed [M, row] fp32");
-  const int64_t P = start.size(0);
-  check_rows(start, "start (base rows)", P, ana::kBaseFloats, dev);
-  check_rows(attrs, "attrs", P, 4, dev);
-  check(vst, "vst", torch::kFloat32, dev);
-  TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
-  const bool raw = prefix.scalar_type() == torch::kFloat32;
-  TORCH_CHECK(prefix.device() == dev && prefix.is_contiguous() && prefix.dim() == 2 && prefix.size(0) == P &&
-                  prefix.size(1) == (raw ? 16 : 14) &&
-                  (raw || prefix.scalar_type() == torch::kBFloat16 || prefix.scalar_type() == torch::kHalf),
-              "prefix must be fp32 [P, 16] or bf16 / fp16 [P, 14]");
+  const int64_t P = delta.size(0);
+  check_rows(delta, "delta", P, 16, dev);
   if (dev.is_cuda()) {
-    const int kind = raw ? 0 : prefix.scalar_type() == torch::kBFloat16 ? 1 : 2;
     check_hip(ana::launch_correct_records((int)K, rec.data_ptr<int32_t>(), M, rows.data_ptr<float>(), rows.stride(0),
-                                          start.data_ptr<float>(), prefix.data_ptr(), kind, attrs.data_ptr<float>(),
-                                          vst.data_ptr<float>(), (float)unknown_sigma, P, stream_of(rows)),
+                                          delta.data_ptr<float>(), P, stream_of(rows)),
               "correct_records");
     return;
   }
-  Tensor pf = raw ? prefix : prefix.to(torch::kFloat32).contiguous();
   ana::host_correct_records((int)K, rec.data_ptr<int32_t>(), M, rows.data_ptr<float>(), rows.stride(0),
-                            start.data_ptr<float>(), pf.data_ptr<float>(), raw, attrs.data_ptr<float>(),
-                            vst.data_ptr<float>(), (float)unknown_sigma, P);
+                            delta.data_ptr<float>(), P);
+}
+
+// the record correction's delta table [P, 16] of a scaled (bf16 / fp16) prefix [P, 14]
+// against the window start s0 [P, 16] (the fused decode computes it in production)
+void prefix_delta(Tensor s0, Tensor prefix, Tensor attrs, Tensor vst, double unknown_sigma, Tensor delta) {
+  const auto dev = s0.device();
+  const int64_t P = s0.size(0);
+  check_rows(s0, "s0 (base rows)", P, ana::kBaseFloats, dev);
+  check_rows(attrs, "attrs", P, 4, dev);
+  check_rows(delta, "delta", P, 16, dev);
+  check(vst, "vst", torch::kFloat32, dev);
+  TORCH_CHECK(prefix.device() == dev && prefix.is_contiguous() && prefix.dim() == 2 && prefix.size(0) == P &&
+                  prefix.size(1) == 14 &&
+                  (prefix.scalar_type() == torch::kBFloat16 || prefix.scalar_type() == torch::kHalf),
+              "prefix must be a contiguous bf16 / fp16 [P, 14]");
+  if (dev.is_cuda()) {
+    check_hip(ana::launch_prefix_delta(s0.data_ptr<float>(), prefix.data_ptr(),
+                                       prefix.scalar_type() == torch::kBFloat16 ? 1 : 0, attrs.data_ptr<float>(),
+                                       vst.data_ptr<float>(), (float)unknown_sigma, delta.data_ptr<float>(), P,
+                                       stream_of(s0)),
+              "prefix_delta");
+    return;
+  }
+  Tensor pf = prefix.to(torch::kFloat32).contiguous();
+  ana::host_prefix_delta(s0.data_ptr<float>(), pf.data_ptr<float>(), attrs.data_ptr<float>(), vst.data_ptr<float>(),
+                         (float)unknown_sigma, delta.data_ptr<float>(), P);
 }
 
 // ------------------------------------------------------------- C2 exchange
@@ -899,11 +926,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("s0"), py::arg("buf"), py::arg("attrs"), py::arg("s"), py::arg("s2"), py::arg("vst"),
         py::arg("unknown_sigma"), py::arg("scaled"), py::arg("clamps") = py::none());
   m.def("sweep_delta_packed", &sweep_delta_packed, "K9: messages straight into bf16/fp16 + int32 all-reduce operands");
-  m.def("sweep_apply_packed", &sweep_apply_packed, "K9: decode bf16/fp16 + int32 summed messages (-> s, s2)",
+  m.def("sweep_apply_packed", &sweep_apply_packed,
+        "K9: decode bf16/fp16 + int32 summed messages (-> s, s2); with a prefix also the record-correction delta table",
         py::arg("s0"), py::arg("msg"), py::arg("cnt"), py::arg("attrs"), py::arg("s"), py::arg("s2"), py::arg("vst"),
-        py::arg("unknown_sigma"), py::arg("clamps") = py::none());
+        py::arg("unknown_sigma"), py::arg("clamps") = py::none(), py::arg("prefix") = py::none(),
+        py::arg("delta") = py::none());
   m.def("correct_records", &correct_records,
-        "K9: causal correction of a window's records by the exclusive prefix of the merge messages");
+        "K9: causal correction of a window's records: += the delta table of the earlier ranks' messages");
+  m.def("prefix_delta", &prefix_delta, "K9: the record correction's delta table of a scaled message prefix");
   m.def("pack_rows", &pack_rows, "C2: changed rows of a round slice -> fixed-capacity [cap, 33] entries");
   m.def("check_round", &check_round, "C2 race detector: one round's matches share no player (flag |= 1)");
   m.def("unpack_rows", &unpack_rows, "C2: write gathered entries (id >= 0) into the roster, tags zeroed");

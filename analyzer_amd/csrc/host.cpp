@@ -265,11 +265,9 @@ void host_sweep_apply(const float* s0, const float* buf, const float* attrs, flo
   }
 }
 
-void host_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* start,
-                          const float* prefix, bool raw, const float* attrs, const float* vst, float unknown_sigma,
+void host_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* delta,
                           int64_t P) {
   const int S = 2 * K;
-  const int pw = raw ? 16 : kTracks * 2;  // floats per prefix row
   for (int64_t m = 0; m < M; ++m) {
     float* row = rows + m * orow;
     if (reinterpret_cast<const uint8_t*>(row + 5 * S + 1)[0] != kRated) continue;
@@ -280,20 +278,17 @@ void host_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int
       if ((j < K ? j : j - K) >= (j < K ? meta_n0(m0) : meta_n1(m0))) continue;
       const int32_t p = r[j];
       if (p < 0 || p >= P) continue;
-      const float* c = start + (int64_t)p * kBaseFloats;
-      const float* d = prefix + (int64_t)p * pw;
-      const float* attr = attrs + (int64_t)p * 4;
-      float spi = d[0], stau = d[1], mpi = d[2 * t], mtau = d[2 * t + 1];
-      if (raw) {
-        float seed_mu = NAN, seed_sig = NAN;
-        const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
-        raw_to_scaled(0, c, seeded, seed_mu, seed_sig, d[0], d[1], spi, stau);
-        raw_to_scaled(t, c, seeded, seed_mu, seed_sig, d[2 * t], d[2 * t + 1], mpi, mtau);
-      }
-      correct_record_slot(c, t, attr, vst, unknown_sigma, spi, stau, mpi, mtau, row + j, row + S + j,
-                          row + 3 * S + j, row + 4 * S + j);
+      const float* d = delta + (int64_t)p * 16;
+      correct_record_track(d[0], d[1], row[j], row[S + j]);
+      correct_record_track(d[2 * t], d[2 * t + 1], row[3 * S + j], row[4 * S + j]);
     }
   }
+}
+
+void host_prefix_delta(const float* s0, const float* prefix, const float* attrs, const float* vst,
+                       float unknown_sigma, float* delta, int64_t P) {
+  for (int64_t p = 0; p < P; ++p)
+    prefix_delta_player(s0 + p * kBaseFloats, prefix + p * 14, attrs + p * 4, vst, unknown_sigma, delta + p * 16);
 }
 
 }  // namespace ana

@@ -35,9 +35,11 @@ void host_sweep_delta(const float* s0, const float* a, const float* s, const flo
 // clamps (nullable): += decoded tracks whose merged precision hit the floor (sweep_core.h)
 void host_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                       bool scaled, const float* vst, float unknown_sigma, int64_t P, uint32_t* clamps = nullptr);
-// causal record correction (sweep_core.h correct_record_slot); prefix: raw fp32 [P][16]
-// (raw) or the scaled messages as fp32 [P][14]
-void host_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* start,
-                          const float* prefix, bool raw, const float* attrs, const float* vst, float unknown_sigma,
+// causal record correction: rows [M][orow] += delta [P][16] (raw natural-parameter
+// increments per track) of each slot's player; the delta table of a scaled prefix
+// [P][14] (fp32) against the window start s0 [P][16]
+void host_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* delta,
                           int64_t P);
+void host_prefix_delta(const float* s0, const float* prefix, const float* attrs, const float* vst,
+                       float unknown_sigma, float* delta, int64_t P);
 }  // namespace ana

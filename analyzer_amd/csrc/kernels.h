@@ -129,15 +129,17 @@ int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, fl
 int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, const float* attrs,
                               const float* vst, float unknown_sigma, int bf16, void* msg, int32_t* cnt,
                               int64_t P, hipStream_t st);
+// prefix (nullable): the scaled exclusive prefix of the messages (same type as msg) ->
+// delta [P][16] fp32, the record correction's increments (sweep_core.h prefix_delta_track)
 int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
                               const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
-                              int64_t P, uint32_t* clamps, hipStream_t st);
-// causal record correction (sweep_core.h correct_record_slot): rows = RateResult's packed
-// rows [M][orow], start = window-start base rows [P][16], prefix = the exclusive prefix of
-// the merge messages: kind 0 raw fp32 [P][16], 1 bf16 / 2 fp16 scaled [P][14]
-int launch_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* start,
-                           const void* prefix, int kind, const float* attrs, const float* vst,
-                           float unknown_sigma, int64_t P, hipStream_t st);
+                              int64_t P, uint32_t* clamps, const void* prefix, float* delta, hipStream_t st);
+int launch_prefix_delta(const float* s0, const void* prefix, int bf16, const float* attrs, const float* vst,
+                        float unknown_sigma, float* delta, int64_t P, hipStream_t st);
+// causal record correction: rows = RateResult's packed rows [M][orow] += delta [P][16]
+// fp32 (raw natural-parameter increments per track) of each slot's player
+int launch_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* delta,
+                           int64_t P, hipStream_t st);
 // C2 exact-DP exchange (sweep.hip): fixed-capacity [cap][33] entries of changed rows
 int launch_pack_rows(const int32_t* rec, int K, int64_t m, const uint8_t* status, int64_t sstride,
                      const float* state, float* out, int64_t cap, hipStream_t st);

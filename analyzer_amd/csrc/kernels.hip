@@ -134,11 +134,21 @@ __global__ void __launch_bounds__(256) emulate_allreduce_kernel(uint4* buf, int6
                                                                uint64_t ticks) {
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  constexpr int U = 8;  // loads in flight per lane (a dependent load per iteration would be latency-bound)
   for (int q = 0; q < passes; ++q)
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-      uint4 v = buf[i];
-      v.x ^= zero;
-      buf[i] = v;
+    for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += U * stride) {
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + u * stride;
+        v[u] = i < n ? buf[i] : uint4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + u * stride;
+        v[u].x ^= zero;
+        if (i < n) buf[i] = v[u];
+      }
     }
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }

@@ -237,31 +237,68 @@ sweep_delta_packed_kernel(const float2* __restrict__ s0, const float2* a0, const
     merge_st(cnt + L.p, make_int2((int)lo, (int)hi));
 }
 
+// prefix (nullable, the scaled exclusive prefix of the messages, H [P][14]) -> delta
+// [P][8] float2: the raw natural-parameter increments of the causal record correction
+// (sweep_core.h prefix_delta_track), computed from the window start before the decode
+// overwrites it
 template <typename H>
 __global__ void __launch_bounds__(256)
 sweep_apply_packed_kernel(const float2* __restrict__ s0, const uint32_t* __restrict__ msg,
                           const int2* __restrict__ cnt, const float4* __restrict__ attrs, float4* s,
                           float2* s2, const float* __restrict__ vst, float unknown_sigma, int64_t P,
-                          uint32_t* clamps) {
+                          uint32_t* clamps, const uint32_t* __restrict__ pref, float2* __restrict__ delta) {
   const TrackLane L = track_lane();
   if (L.p >= P) return;
   const uint32_t w = L.t < kTracks ? merge_ld(msg + L.p * kTracks + L.t) : 0u;
   const int2 c = merge_ld(cnt + L.p);  // broadcast within the group
+  if (pref) {  // (before lane_apply: it may overwrite the window start through s2)
+    const float2 cs = merge_ld(s0 + L.p * kLanesPerPlayer + L.t);
+    const float c0mu = __shfl(cs.x, L.gbase), c0sg = __shfl(cs.y, L.gbase);
+    float dpi = 0.f, dtau = 0.f;
+    const uint32_t pw = L.t < kTracks ? merge_ld(pref + L.p * kTracks + L.t) : 0u;
+    const float rpi = from_half_bits<H>(pw & 0xffffu), rtau = from_half_bits<H>(pw >> 16);
+    if (L.t < kTracks && (rpi != 0.f || rtau != 0.f)) {
+      bool seeded = false;
+      float seed_mu = NAN, seed_sig = NAN;
+      if (!(cs.x == cs.x) || !(c0mu == c0mu)) lane_seed(attrs, L.p, vst, unknown_sigma, seeded, seed_mu, seed_sig);
+      prefix_delta_track(L.t, cs.x, cs.y, c0mu, c0sg, seeded, seed_mu, seed_sig, rpi, rtau, dpi, dtau);
+    }
+    delta[L.p * kLanesPerPlayer + L.t] = make_float2(dpi, dtau);
+  }
   lane_apply(L, s0, from_half_bits<H>(w & 0xffffu), from_half_bits<H>(w >> 16), (uint32_t)c.x,
              (uint32_t)c.y, attrs, vst, unknown_sigma, true, s, s2, clamps);
 }
 
+// the same delta table on its own (simulations, tests): one lane per track
+template <typename H>
+__global__ void __launch_bounds__(256)
+prefix_delta_kernel(const float2* __restrict__ s0, const uint32_t* __restrict__ pref, const float4* __restrict__ attrs,
+                    const float* __restrict__ vst, float unknown_sigma, float2* __restrict__ delta, int64_t P) {
+  const TrackLane L = track_lane();
+  if (L.p >= P) return;
+  const float2 cs = s0[L.p * kLanesPerPlayer + L.t];
+  const float c0mu = __shfl(cs.x, L.gbase), c0sg = __shfl(cs.y, L.gbase);
+  float dpi = 0.f, dtau = 0.f;
+  if (L.t < kTracks) {
+    const uint32_t pw = pref[L.p * kTracks + L.t];
+    bool seeded;
+    float seed_mu, seed_sig;
+    lane_seed(attrs, L.p, vst, unknown_sigma, seeded, seed_mu, seed_sig);
+    prefix_delta_track(L.t, cs.x, cs.y, c0mu, c0sg, seeded, seed_mu, seed_sig, from_half_bits<H>(pw & 0xffffu),
+                       from_half_bits<H>(pw >> 16), dpi, dtau);
+  }
+  delta[L.p * kLanesPerPlayer + L.t] = make_float2(dpi, dtau);
+}
+
 // ------------------------------------------------- causal record correction
-// One thread per slot of the window's records (sweep_core.h correct_record_slot):
-// rows: RateResult's packed rows [M][orow] ([s_mu | s_sig | delta | m_mu | m_sig][S],
-// quality, status byte); start: the window-start base rows; the prefix message of
-// each player, scaled H [P][14] (bf16 / fp16 merges) or raw fp32 [P][16] (RAW).
-template <int K, typename H, bool RAW>
+// One thread per slot of the window's records: rows = RateResult's packed rows [M][orow]
+// ([s_mu | s_sig | delta | m_mu | m_sig][S], quality, status byte); delta = [P][8]
+// float2 natural-parameter increments per track (sweep_core.h prefix_delta_track) --
+// one 16-B gather of the player's shared and mode increments per slot.
+template <int K>
 __global__ void __launch_bounds__(256)
 correct_records_kernel(const int32_t* __restrict__ rec, int64_t M, float* rows, int64_t orow,
-                       const float2* __restrict__ start, const void* __restrict__ prefix,
-                       const float4* __restrict__ attrs, const float* __restrict__ vst, float unknown_sigma,
-                       int64_t P) {
+                       const float2* __restrict__ delta, int64_t P) {
   constexpr int S = 2 * K;
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= M * S) return;
@@ -274,61 +311,30 @@ correct_records_kernel(const int32_t* __restrict__ rec, int64_t M, float* rows, 
   if ((j < K ? j : j - K) >= (j < K ? meta_n0(m0) : meta_n1(m0))) return;
   const int32_t p = r[j];
   if (p < 0 || p >= P) return;
-  const int t = 1 + meta_mode(m0);
-  float c[kBaseFloats];
-#pragma unroll
-  for (int g = 0; g < kGranules; ++g) {
-    const float2 v = start[(int64_t)p * kGranules + g];
-    c[2 * g] = v.x;
-    c[2 * g + 1] = v.y;
-  }
-  const float4 a4 = attrs[p];
-  const float attr[4] = {a4.x, a4.y, a4.z, a4.w};
-  float spi, stau, mpi, mtau;
-  if constexpr (RAW) {
-    const float* d = reinterpret_cast<const float*>(prefix) + (int64_t)p * 16;
-    float seed_mu = NAN, seed_sig = NAN;
-    const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
-    raw_to_scaled(0, c, seeded, seed_mu, seed_sig, d[0], d[1], spi, stau);
-    raw_to_scaled(t, c, seeded, seed_mu, seed_sig, d[2 * t], d[2 * t + 1], mpi, mtau);
-  } else {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(prefix) + (int64_t)p * kTracks;
-    const uint32_t w0 = w[0], wt = w[t];
-    spi = from_half_bits<H>(w0 & 0xffffu);
-    stau = from_half_bits<H>(w0 >> 16);
-    mpi = from_half_bits<H>(wt & 0xffffu);
-    mtau = from_half_bits<H>(wt >> 16);
-  }
+  const float2 ds = delta[(int64_t)p * kGranules], dm = delta[(int64_t)p * kGranules + 1 + meta_mode(m0)];
   float smu = row[j], ssg = row[S + j], mmu = row[3 * S + j], msg = row[4 * S + j];
-  correct_record_slot(c, t, attr, vst, unknown_sigma, spi, stau, mpi, mtau, &smu, &ssg, &mmu, &msg);
+  correct_record_track(ds.x, ds.y, smu, ssg);
+  correct_record_track(dm.x, dm.y, mmu, msg);
   row[j] = smu;
   row[S + j] = ssg;
   row[3 * S + j] = mmu;
   row[4 * S + j] = msg;
 }
 
-int launch_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* start,
-                           const void* prefix, int kind, const float* attrs, const float* vst,
-                           float unknown_sigma, int64_t P, hipStream_t st) {
+int launch_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* delta,
+                           int64_t P, hipStream_t st) {
   const int64_t n = M * 2 * K;
   if (n <= 0) return 0;
   const dim3 grid((unsigned)((n + 255) / 256));
-#define ANA_CORR(k, H, RAW)                                                                                    \
-  hipLaunchKernelGGL((correct_records_kernel<k, H, RAW>), grid, dim3(256), 0, st, rec, M, rows, orow,          \
-                     reinterpret_cast<const float2*>(start), prefix, reinterpret_cast<const float4*>(attrs), vst, \
-                     unknown_sigma, P)
-#define ANA_CORR_K(k)                        \
-  case k:                                    \
-    if (kind == 0) ANA_CORR(k, float, true); \
-    else if (kind == 1) ANA_CORR(k, __bf16, false); \
-    else ANA_CORR(k, _Float16, false);       \
-    break;
+  const float2* d = reinterpret_cast<const float2*>(delta);
   switch (K) {
-    ANA_CORR_K(1) ANA_CORR_K(2) ANA_CORR_K(3) ANA_CORR_K(4) ANA_CORR_K(5)
+    case 1: hipLaunchKernelGGL(correct_records_kernel<1>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
+    case 2: hipLaunchKernelGGL(correct_records_kernel<2>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
+    case 3: hipLaunchKernelGGL(correct_records_kernel<3>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
+    case 4: hipLaunchKernelGGL(correct_records_kernel<4>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
+    case 5: hipLaunchKernelGGL(correct_records_kernel<5>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
     default: return (int)hipErrorInvalidValue;
   }
-#undef ANA_CORR_K
-#undef ANA_CORR
   return (int)hipGetLastError();
 }
 
@@ -353,16 +359,30 @@ int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, c
 
 int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
                               const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
-                              int64_t P, uint32_t* clamps, hipStream_t st) {
+                              int64_t P, uint32_t* clamps, const void* prefix, float* delta, hipStream_t st) {
   if (P <= 0) return 0;
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
                        reinterpret_cast<const uint32_t*>(msg), reinterpret_cast<const int2*>(cnt),
                        reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
-                       reinterpret_cast<float2*>(s2), vst, unknown_sigma, P, clamps);
+                       reinterpret_cast<float2*>(s2), vst, unknown_sigma, P, clamps,
+                       reinterpret_cast<const uint32_t*>(prefix), reinterpret_cast<float2*>(delta));
   };
   if (bf16) args(sweep_apply_packed_kernel<__bf16>);
   else args(sweep_apply_packed_kernel<_Float16>);
+  return (int)hipGetLastError();
+}
+
+int launch_prefix_delta(const float* s0, const void* prefix, int bf16, const float* attrs, const float* vst,
+                        float unknown_sigma, float* delta, int64_t P, hipStream_t st) {
+  if (P <= 0) return 0;
+  auto args = [&](auto kern) {
+    hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
+                       reinterpret_cast<const uint32_t*>(prefix), reinterpret_cast<const float4*>(attrs), vst,
+                       unknown_sigma, reinterpret_cast<float2*>(delta), P);
+  };
+  if (bf16) args(prefix_delta_kernel<__bf16>);
+  else args(prefix_delta_kernel<_Float16>);
   return (int)hipGetLastError();
 }
 

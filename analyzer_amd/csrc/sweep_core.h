@@ -141,51 +141,49 @@ ANA_HD void sweep_apply_track(int t, float amu, float asg, float a0mu, float a0s
 // prefix of the messages, sum_{q<r} m_q (parallel/comm.py scan_and_sum), and a record
 // (mu, sigma) of player p on track t is corrected by adding that evidence in natural
 // parameters -- the same additive approximation the merged roster makes for the whole
-// window:  nat(rec') = nat(rec) + (pi_B r_pi, pi_B (r_tau + mu_B r_pi)),  with (r_pi,
-// r_tau) the scaled prefix message and B the track's base (track_base: the window-start
-// value, else the seed / start shared value it was measured against).  At 8 ranks x
-// 1.25M-match windows over 100k players (the k = 8 density of the bench) the shared
-// records' median |d mu| against exact sequential rating falls from 29.7 to 8.0, p99
-// 156 -> 40 (profiles/r5/record_correction.log).  Rank 0's prefix is zero: its records
-// are the sequential ones already.
-ANA_HD void correct_record_track(int t, float cmu, float csg, float c0mu, float c0sg, bool seeded, float seed_mu,
-                                 float seed_sig, float rpi, float rtau, float& mu, float& sg) {
-  if (!(mu == mu) || (rpi == 0.f && rtau == 0.f)) return;
+// window:  nat(rec') = nat(rec) + delta(p, t).  At 8 ranks x 1.25M-match windows over
+// 100k players (the k = 8 density of the bench) the shared records' median |d mu|
+// against exact sequential rating falls from 29.7 to 8.0, p99 156 -> 40
+// (profiles/r5/record_correction.log).  Rank 0's prefix is zero: its records are the
+// sequential ones already.
+//
+// delta(p, t) in raw natural parameters (d_pi, d_tau): a raw fp32 prefix is that
+// already; a scaled (bf16 / fp16) prefix (r_pi, r_tau) is relative to the track's base
+// B (track_base: the window-start value, else the seed / start shared value it was
+// measured against):  (pi_B r_pi, pi_B (r_tau + mu_B r_pi)).  The merge's decode pass
+// computes it while it still holds the window start (sweep.hip), so the per-slot pass
+// over the records gathers one 64-B row per player and does no base logic.
+ANA_HD void prefix_delta_track(int t, float cmu, float csg, float c0mu, float c0sg, bool seeded, float seed_mu,
+                               float seed_sig, float rpi, float rtau, float& dpi, float& dtau) {
+  dpi = dtau = 0.f;
+  if (rpi == 0.f && rtau == 0.f) return;
   float bm, bs;
   if (!track_base(t, cmu, csg, c0mu, c0sg, seeded, seed_mu, seed_sig, bm, bs)) return;
   const float pb = 1.f / (bs * bs);
-  const float pi = 1.f / (sg * sg) + pb * rpi;
-  const float tau = mu / (sg * sg) + pb * (rtau + bm * rpi);
+  dpi = pb * rpi;
+  dtau = pb * (rtau + bm * rpi);
+}
+
+// one record (mu, sigma) += delta in natural parameters (NULL / untouched: unchanged)
+ANA_HD void correct_record_track(float dpi, float dtau, float& mu, float& sg) {
+  if (!(mu == mu) || (dpi == 0.f && dtau == 0.f)) return;
+  const float p0 = 1.f / (sg * sg);
+  const float pi = p0 + dpi;
   if (!(pi > 0.f)) return;  // (a prefix that would void the record's precision: keep the record)
-  mu = tau / pi;
+  mu = (mu * p0 + dtau) / pi;
   sg = 1.f / sqrtf(pi);
 }
 
-// The records of one slot (m, j) of a rated window: s (shared) and md (mode track t)
-// (mu, sigma) pairs in place; c: the player's window-start base row, attr / vst /
-// unknown_sigma: its seed; (spi, stau) / (mpi, mtau): the prefix message of the shared
-// / mode track, already in the base-relative form (scaled), or raw natural parameters
-// converted by the caller (raw: pass r_pi = d_pi / pi_B, r_tau = (d_tau - mu_B d_pi) /
-// pi_B -- correct_record_raw does that).
-ANA_HD void correct_record_slot(const float* c, int t, const float* attr, const float* vst, float unknown_sigma,
-                                float spi, float stau, float mpi, float mtau, float* s_mu, float* s_sig,
-                                float* m_mu, float* m_sig) {
+// host mirror of the delta table of one player: c = its window-start base row, pref =
+// the scaled prefix [14] (r_pi, r_tau per track), out = [16] (d_pi, d_tau per granule)
+ANA_HD void prefix_delta_player(const float* c, const float* pref, const float* attr, const float* vst,
+                                float unknown_sigma, float* out) {
   float seed_mu = NAN, seed_sig = NAN;
-  const bool need_seed = !(c[0] == c[0]) || !(c[2 * t] == c[2 * t]);
-  const bool seeded = need_seed && seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
-  correct_record_track(0, c[0], c[1], c[0], c[1], seeded, seed_mu, seed_sig, spi, stau, *s_mu, *s_sig);
-  correct_record_track(t, c[2 * t], c[2 * t + 1], c[0], c[1], seeded, seed_mu, seed_sig, mpi, mtau, *m_mu, *m_sig);
-}
-
-// raw natural-parameter messages (fp32 merges) -> the base-relative form of one track
-ANA_HD void raw_to_scaled(int t, const float* c, bool seeded, float seed_mu, float seed_sig, float dpi, float dtau,
-                          float& rpi, float& rtau) {
-  float bm, bs;
-  rpi = rtau = 0.f;
-  if (!track_base(t, c[2 * t], c[2 * t + 1], c[0], c[1], seeded, seed_mu, seed_sig, bm, bs)) return;
-  const float vb = bs * bs;  // 1 / pi_B
-  rpi = dpi * vb;
-  rtau = (dtau - bm * dpi) * vb;
+  const bool seeded = seed_prior<float>(attr, unknown_sigma, vst, seed_mu, seed_sig);
+  for (int t = 0; t < kTracks; ++t)
+    prefix_delta_track(t, c[2 * t], c[2 * t + 1], c[0], c[1], seeded, seed_mu, seed_sig, pref[2 * t],
+                       pref[2 * t + 1], out[2 * t], out[2 * t + 1]);
+  out[14] = out[15] = 0.f;
 }
 
 // Whole-player forms over base rows (host mirror): s, a: base rows [16] (start,

@@ -88,9 +88,13 @@ def simulate_sweep_dp(rater: BatchRater, roster: Roster, shards: Sequence[torch.
                     # the causal record correction of rank r's records by the messages of
                     # the ranks before it, against the window start (parallel/sweep.py)
                     m = mergers[r]
-                    prefix = total if comm_dtype == "fp32" else total[:, :14].to(COMM_DTYPES[comm_dtype])
-                    native().correct_records(shards[r], K, outs[r].packed, m.start, prefix.contiguous(),
-                                             rosters[r].attrs, m.vst, float(rater.cfg.unknown_player_sigma))
+                    if comm_dtype == "fp32":  # raw messages: the prefix is the increment table
+                        delta = total
+                    else:
+                        delta = torch.empty((m.P, 16), dtype=torch.float32, device=roster.device)
+                        native().prefix_delta(m.start, total[:, :14].to(COMM_DTYPES[comm_dtype]).contiguous(),
+                                              rosters[r].attrs, m.vst, float(rater.cfg.unknown_player_sigma), delta)
+                    native().correct_records(shards[r], K, outs[r].packed, delta.contiguous())
                 total = total + x
             total = _quantize(total, comm_dtype)  # what the collective delivers: summed, rounded once
             for m, ro in zip(mergers, rosters):

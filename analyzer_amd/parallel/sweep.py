@@ -115,10 +115,12 @@ class SweepMerger:
             correct_records = os.environ.get("ANA_DP_CORRECT_RECORDS", "1") not in ("", "0", "false")
         self.correct = bool(correct_records) and self.sweeps <= 1
         self._zero_prefix = None  # one rank: its prefix is zero (the pass still runs: it is priced)
+        self.delta = None         # [P, 16] fp32 increments of the record correction (decode_packed)
         # emulate = "N:GBps[:us]" (one rank, force): every all-reduce is replaced by a stand-in
         # on a stream of its own that takes what an N-rank ring all-reduce of the operands would
-        # over links of GBps bus bandwidth (+ us latency) and streams the buffer like RCCL's
-        # channels do (csrc/kernels.hip emulate_allreduce_kernel) -- one GPU then prices the
+        # over links of GBps bus bandwidth (+ us latency) and streams the buffer three times on
+        # 32 CUs, as RCCL's channels do (csrc/kernels.hip emulate_allreduce_kernel) -- one GPU
+        # then prices the
         # N-GPU step, the merge's exposed collective included (bench.py --emulate-allreduce)
         self.emulate = None
         if emulate:
@@ -209,13 +211,17 @@ class SweepMerger:
                                     roster.attrs[lo:hi], self.vst, float(self.cfg.unknown_player_sigma),
                                     self.msg[lo:hi], self.cnt[lo:hi])
 
-    def decode_packed(self, roster, lo: int = 0, hi: Optional[int] = None, into=None) -> None:
-        """``decode`` of the compressed summed messages."""
+    def decode_packed(self, roster, lo: int = 0, hi: Optional[int] = None, into=None,
+                      prefix: Optional[torch.Tensor] = None, delta: Optional[torch.Tensor] = None) -> None:
+        """``decode`` of the compressed summed messages; with ``prefix`` (this rank's
+        exclusive prefix, same layout as ``msg``) it also writes the record
+        correction's ``delta`` table from the window start before overwriting it."""
         hi = self.P if hi is None else hi
         s2 = into[lo:hi] if into is not None else self._none
         native().sweep_apply_packed(self.start[lo:hi], self.msg[lo:hi], self.cnt[lo:hi], roster.attrs[lo:hi],
                                     roster.state[lo:hi], s2, self.vst, float(self.cfg.unknown_player_sigma),
-                                    self.clamps)
+                                    self.clamps, None if prefix is None else prefix[lo:hi],
+                                    None if delta is None else delta[lo:hi])
         roster.epoch = roster.epoch if roster.epoch is not None else 0
 
     def _packed(self) -> bool:
@@ -273,7 +279,7 @@ class SweepMerger:
         nbytes = sum(t.numel() * t.element_size() for t in parts)
         with torch.cuda.stream(self._comm):
             for i, t in enumerate(parts):  # the time is modelled on the whole operand set
-                native().emulate_allreduce(t, 16, 3, self.emulated_us(nbytes) if i == 0 else 0.0)
+                native().emulate_allreduce(t, 32, 3, self.emulated_us(nbytes) if i == 0 else 0.0)
         done = torch.cuda.Event()
         done.record(self._comm)
 
@@ -327,7 +333,6 @@ class SweepMerger:
         the prefix against the window start -> the decode.  Not bucketed: the records
         name any player, so the whole prefix is needed before the pass."""
         K = (int(rec.shape[1]) - 2) // 2
-        us = float(self.cfg.unknown_player_sigma)
         self._ev("begin")
         if self.msg is not None:
             self.messages_packed(roster)
@@ -352,13 +357,17 @@ class SweepMerger:
         if overlap is not None:
             overlap()
         self._ev("overlap")
-        native().correct_records(rec, K, out.packed, self.start, prefix, roster.attrs, self.vst, us)
-        self._ev("correct")
-        if self.msg is not None:
-            self.decode_packed(roster, into=self.start)
-        else:
+        if self.msg is not None:  # the decode also turns the scaled prefix into raw increments
+            if self.delta is None:
+                self.delta = torch.empty((self.P, 16), dtype=torch.float32, device=self.device)
+            self.decode_packed(roster, into=self.start, prefix=prefix, delta=self.delta)
+            delta = self.delta
+        else:                     # raw fp32 messages: the prefix IS the increment table
             self.decode(roster, into=self.start)
+            delta = prefix
         self._ev("apply")
+        native().correct_records(rec, K, out.packed, delta)
+        self._ev("correct")
         self._synced = True
         self.windows += 1
 

@@ -386,7 +386,7 @@ def main(argv=None) -> int:
     if merger is not None:
         merger.timing = False
         merge = {k: v / args.steps for k, v in merger.stage_ms().items()}
-    vals = [ms] + [merge.get(k, 0.0) for k in ("messages", "allreduce", "apply", "overlap")]
+    vals = [ms] + [merge.get(k, 0.0) for k in ("messages", "allreduce", "apply", "overlap", "correct")]
     t = torch.tensor(vals, dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -399,7 +399,9 @@ def main(argv=None) -> int:
         # prepass_overlap: the next window's prepass, enqueued while the all-reduces
         # are in flight (serial placement); "allreduce" is what stays exposed after it
         merge_ms = {"snapshot": 0.0, "messages": mm[0], "allreduce": mm[1], "apply": mm[2],
-                    "total": sum(mm[:3]), "prepass_overlap": mm[3], "bytes_per_rank": merger.comm_bytes,
+                    # the causal record correction's pass over the window's records
+                    "correct_records": mm[4] if merger.correct else None,
+                    "total": sum(mm[:3]) + mm[4], "prepass_overlap": mm[3], "bytes_per_rank": merger.comm_bytes,
                     "buckets": len(merger.buckets()),
                     # where the next window's prepass ran: beside the merge (serial) or in
                     # the rating's tail; chosen from a timed all-reduce for N > 1

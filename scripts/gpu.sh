@@ -274,22 +274,20 @@ EOF
       done
       for f in gpurun_out/dpcost/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
       ;;
-    dpstep)  # one-GPU DP step price with ONE prepass per step (engine.step_windows) vs one per window,
-             # tail and serial placements, k = 8 / 16 / 32 (interleaved rounds)
+    dpstep)  # one-GPU DP step price: plain vs forced merges (DPSTEP_K), one prepass per step in pieces (default),
+             # whole, or per window; record correction on (default) / off; serial placement; N = 8 projected with
+             # the all-reduce stand-in (8 ranks, 300 GB/s bus bandwidth); interleaved rounds
       for r in 1 2; do
         run dpstep/plain_$r 300 $PY bench.py --steps 10 --warmup 2
-        for k in ${DPSTEP_K:-8 16 32}; do
-          run dpstep/k${k}_step_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step $k
-          ANA_PREPASS_SERIAL=1 run dpstep/k${k}_step_serial_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge \
-              --merges-per-step $k
+        for k in ${DPSTEP_K:-8 16}; do
+          A="--steps 10 --warmup 2 --force-merge --merges-per-step $k"
+          run dpstep/k${k}_pieces_$r 300 $PY bench.py $A
+          ANA_DP_CORRECT_RECORDS=0 run dpstep/k${k}_pieces_nocorr_$r 300 $PY bench.py $A
+          ANA_PREPASS_PIECES=0 run dpstep/k${k}_whole_$r 300 $PY bench.py $A
+          run dpstep/k${k}_window_$r 300 $PY bench.py $A --step-prepass 0
+          ANA_PREPASS_SERIAL=1 run dpstep/k${k}_pieces_serial_$r 300 $PY bench.py $A
+          run dpstep/k${k}_emu8_$r 300 $PY bench.py $A --emulate-allreduce 8:300
         done
-        for k in ${DPEMU_K:-8 16}; do  # N = 8 projected: the all-reduce stand-in (8 ranks, 300 GB/s bus bandwidth)
-          run dpstep/k${k}_emu8_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step $k \
-              --emulate-allreduce 8:300
-        done
-        run dpstep/k8_window_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step 8 --step-prepass 0
-        ANA_PREPASS_PIECES=0 run dpstep/k8_whole_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge \
-            --merges-per-step 8
       done
       for f in gpurun_out/dpstep/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
       ;;

@@ -329,15 +329,31 @@ def test_record_correction_kernel_matches_host(gpu_device, comm):
     m = SweepMerger(P, "cpu", comm_dtype=comm, force=True)
     m.begin(start)
     m.messages(other)  # an earlier slice's messages against the start: the prefix
-    prefix = m.buf.clone() if comm == "fp32" else m.buf[:, :14].to(COMM_DTYPES[comm]).contiguous()
+    g = lambda t: t.to(gpu_device)
+    if comm == "fp32":  # raw: the prefix is the increment table
+        dh = m.buf.clone()
+        dd = g(dh)
+    else:  # scaled: the delta table from the window start, host and device (standalone + fused decode)
+        prefix = m.buf[:, :14].to(COMM_DTYPES[comm]).contiguous()
+        dh = torch.empty(P, 16)
+        native().prefix_delta(m.start, prefix, start.attrs, m.vst, 500.0, dh)
+        dd = torch.empty((P, 16), device=gpu_device)
+        native().prefix_delta(g(m.start), g(prefix), g(start.attrs), g(m.vst), 500.0, dd)
+        fused = torch.empty((P, 16), device=gpu_device)
+        msg = torch.zeros((P, 14), dtype=prefix.dtype, device=gpu_device)
+        cnt = torch.zeros((P, 2), dtype=torch.int32, device=gpu_device)
+        native().sweep_apply_packed(g(m.start), msg, cnt, g(start.attrs), g(start.state).clone(),
+                                    g(m.start).clone(), g(m.vst), 500.0, None, g(prefix), fused)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(dd.cpu().numpy(), dh.numpy(), rtol=1e-5, atol=1e-12)
+        assert torch.equal(fused.cpu(), dd.cpu())
     rec = make_stream(StreamSpec(team_size=K, seed=43, p_afk=0.05, p_uneven=0.05), M, P, K=K)
     ro = start.clone()
     out = R.BatchRater().rate(ro, rec, K)
     host = out.packed.clone()
-    native().correct_records(rec, K, host, m.start, prefix, start.attrs, m.vst, 500.0)
+    native().correct_records(rec, K, host, dh)
     dev = out.packed.to(gpu_device)
-    g = lambda t: t.to(gpu_device)
-    native().correct_records(g(rec), K, dev, g(m.start), g(prefix), g(start.attrs), g(m.vst), 500.0)
+    native().correct_records(g(rec), K, dev, dd)
     torch.cuda.synchronize()
     changed = (host != out.packed) & ~torch.isnan(host)
     assert int(changed.sum()) > 10000  # the prefix moved most rated records
@@ -355,7 +371,7 @@ def test_device_decode_counts_clamps_like_host(gpu_device, comm):
     outs = []
     for dev in ("cpu", gpu_device):
         m = SweepMerger(P, dev, comm_dtype=comm, force=True)
-        r = ro.to(dev)
+        r = ro.clone().to(dev)  # (Roster.to of the same device aliases the tensors)
         m.begin(r)
         idx = torch.arange(0, P, 7, device=dev)
         if comm == "fp32":
