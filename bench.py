@@ -110,8 +110,10 @@ def parse(argv=None):
                          "(parallel/sweep.py emulate); the prepass placement follows the modelled time")
     ap.add_argument("--step-prepass", type=int, default=-1, choices=[-1, 0, 1],
                     help="merges per step > 1: 1 = ONE schedule prepass per step over its k windows "
-                         "(links cut at the window boundaries, runtime/engine.py step_windows), 0 = a "
-                         "prepass per window (rounds 2-4), -1 = auto (1)")
+                         "(links cut at the window boundaries, runtime/engine.py step_windows; whole or in "
+                         "pieces between the windows, ANA_PREPASS_PIECES), 0 = a prepass per window in the "
+                         "rating's tail; -1 = auto = 0: the per-window tail prepass measured fastest, k = 8 "
+                         "forced merges 11.5 vs 11.8 (whole) / 12.9 ms (pieces; profiles/r5/dp_step_price.log)")
     ap.add_argument("--force-merge", action="store_true",
                     help="N = 1: run the merge kernels after every window anyway (messages + decode, "
                          "no collective) -- prices the DP merge's device work against --merges-per-step")
@@ -254,7 +256,7 @@ def main(argv=None) -> int:
     # one prepass per step over its k windows (engine.step_windows) -- the unit of the
     # timed loop is then a step, not a window
     step_prepass = sub > 1 and args.config != 4 and (
-        args.step_prepass == 1 or args.step_prepass < 0)
+        args.step_prepass == 1)
     n_windows = max(1, min(args.ring, (args.steps + args.warmup) * sub))
     total_windows = (args.steps + args.warmup) * sub
     if step_prepass:  # a ring of whole steps: window w of rank r as before, k windows per step

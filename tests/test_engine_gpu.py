@@ -345,7 +345,8 @@ def test_record_correction_kernel_matches_host(gpu_device, comm):
         native().sweep_apply_packed(g(m.start), msg, cnt, g(start.attrs), g(start.state).clone(),
                                     g(m.start).clone(), g(m.vst), 500.0, None, g(prefix), fused)
         torch.cuda.synchronize()
-        np.testing.assert_allclose(dd.cpu().numpy(), dh.numpy(), rtol=1e-5, atol=1e-12)
+        # (d_tau = pi_B (r_tau + mu_B r_pi) cancels: device fma vs host rounding)
+        np.testing.assert_allclose(dd.cpu().numpy(), dh.numpy(), rtol=1e-4, atol=1e-9)
         assert torch.equal(fused.cpu(), dd.cpu())
     rec = make_stream(StreamSpec(team_size=K, seed=43, p_afk=0.05, p_uneven=0.05), M, P, K=K)
     ro = start.clone()
