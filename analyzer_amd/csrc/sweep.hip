@@ -291,67 +291,87 @@ prefix_delta_kernel(const float2* __restrict__ s0, const uint32_t* __restrict__ 
 }
 
 // ------------------------------------------------- causal record correction
-// ONE THREAD PER MATCH: the thread reads its match's record (ids, meta) and its whole
-// 128-B output row as full-line vector loads, gathers the 2 x 2K increments of its
-// players from the delta table ([P][8] float2: one 16-B shared + mode pair per slot,
-// all independent, so 2K gathers are in flight per lane) and writes the row back whole
-// (non-temporal: the records are a write-once stream, as the executor writes them).
-// One thread per slot was 3x slower: a dependent rec -> delta chain per thread and four
-// 4-B partial-line stores per slot (0.23 ms per 1.25M-match window).
+// A block corrects a tile of kCorrTile consecutive matches.  Their output rows are one
+// contiguous span (tile * orow floats): it is copied into LDS with fully coalesced
+// 16-B loads (a wave covers 1 KB per instruction), each thread then corrects its own
+// match's row in LDS -- status check, 2K independent 16-B delta-table reads of its
+// players ([P][8] float2: the shared and the mode pair of a slot share one 64-B line),
+// the 4K fields rewritten -- and the span goes back with coalesced 16-B stores.  LDS
+// rows are padded to orow + 1 words so the per-thread field accesses (stride orow + 1)
+// hit distinct banks.  One thread per match reading its own 128-B row (8 16-B loads at
+// a 128-B lane stride) ran at 1.6 TB/s, 0.29 ms per 1.25M-match window
+// (profiles/r5/correct_micro.log); one thread per slot 0.23 ms in the step.
+constexpr int kCorrTile = 256;
+
 template <int K>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(kCorrTile)
 correct_records_kernel(const int32_t* __restrict__ rec, int64_t M, float* rows, int64_t orow,
                        const float2* __restrict__ delta, int64_t P) {
   constexpr int S = 2 * K;
-  constexpr int RQ = (5 * S + 2 + 3) / 4;  // 16-B quads of the row's fields (quality, status included)
   typedef float v4f __attribute__((ext_vector_type(4)));
-  const int64_t m = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (m >= M) return;
-  v4f* rq = reinterpret_cast<v4f*>(rows + m * orow);
-  float f[4 * RQ];
-#pragma unroll
-  for (int q = 0; q < RQ; ++q) {
-    const v4f v = __builtin_nontemporal_load(rq + q);
-    f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+  extern __shared__ float tile[];  // [blockDim.x][orow + 1]
+  const int T = (int)blockDim.x;    // matches per tile (kCorrTile, or half of it for wide rows)
+  const int ld = (int)orow + 1;
+  const int64_t m0 = (int64_t)blockIdx.x * T;
+  const int n = (int)(M - m0 < T ? M - m0 : T);
+  const int rq = (int)(orow >> 2);  // 16-B quads per row
+  const int nq = n * rq;
+  const v4f* src = reinterpret_cast<const v4f*>(rows + m0 * orow);
+  for (int q = threadIdx.x; q < nq; q += T) {
+    const v4f v = __builtin_nontemporal_load(src + q);
+    float* d = tile + (q / rq) * ld + (q % rq) * 4;
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
   }
-  if ((__float_as_uint(f[5 * S + 1]) & 0xffu) != kRated) return;
-  const int32_t* r = rec + m * (S + 2);
-  int32_t ids[S];
+  __syncthreads();
+  const int i = threadIdx.x;
+  float* f = tile + i * ld;
+  if (i < n && (__float_as_uint(f[5 * S + 1]) & 0xffu) == kRated) {
+    const int32_t* r = rec + (m0 + i) * (S + 2);
+    int32_t ids[S];
 #pragma unroll
-  for (int j = 0; j < S; ++j) ids[j] = r[j];
-  const uint32_t m0 = (uint32_t)r[S];
-  const int t = 1 + meta_mode(m0);
-  const int n0 = meta_n0(m0), n1 = meta_n1(m0);
-  float2 ds[S], dm[S];
+    for (int j = 0; j < S; ++j) ids[j] = r[j];
+    const uint32_t mm = (uint32_t)r[S];
+    const int t = 1 + meta_mode(mm);
+    const int n0 = meta_n0(mm), n1 = meta_n1(mm);
+    float2 ds[S], dm[S];
 #pragma unroll
-  for (int j = 0; j < S; ++j) {
-    const bool in = (j < K ? j : j - K) < (j < K ? n0 : n1) && ids[j] >= 0 && ids[j] < P;
-    const int64_t base = (int64_t)(in ? ids[j] : 0) * kGranules;
-    ds[j] = in ? delta[base] : make_float2(0.f, 0.f);
-    dm[j] = in ? delta[base + t] : make_float2(0.f, 0.f);
+    for (int j = 0; j < S; ++j) {
+      const bool in = (j < K ? j : j - K) < (j < K ? n0 : n1) && ids[j] >= 0 && ids[j] < P;
+      const int64_t base = (int64_t)(in ? ids[j] : 0) * kGranules;
+      ds[j] = in ? delta[base] : make_float2(0.f, 0.f);
+      dm[j] = in ? delta[base + t] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < S; ++j) {
+      correct_record_track(ds[j].x, ds[j].y, f[j], f[S + j]);
+      correct_record_track(dm[j].x, dm[j].y, f[3 * S + j], f[4 * S + j]);
+    }
   }
-#pragma unroll
-  for (int j = 0; j < S; ++j) {
-    correct_record_track(ds[j].x, ds[j].y, f[j], f[S + j]);
-    correct_record_track(dm[j].x, dm[j].y, f[3 * S + j], f[4 * S + j]);
+  __syncthreads();
+  v4f* dst = reinterpret_cast<v4f*>(rows + m0 * orow);
+  for (int q = threadIdx.x; q < nq; q += T) {
+    const float* d = tile + (q / rq) * ld + (q % rq) * 4;
+    __builtin_nontemporal_store(v4f{d[0], d[1], d[2], d[3]}, dst + q);
   }
-#pragma unroll
-  for (int q = 0; q < RQ; ++q)
-    __builtin_nontemporal_store(v4f{f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]}, rq + q);
 }
 
 int launch_correct_records(int K, const int32_t* rec, int64_t M, float* rows, int64_t orow, const float* delta,
                            int64_t P, hipStream_t st) {
   if (M <= 0) return 0;
-  if (orow % 4 != 0) return (int)hipErrorInvalidValue;  // 16-B aligned rows (RateResult.allocate)
-  const dim3 grid((unsigned)((M + 255) / 256));
+  if (orow % 4 != 0 || orow < 5 * 2 * K + 2) return (int)hipErrorInvalidValue;  // RateResult.allocate rows
+  int T = kCorrTile;
+  while (T > 64 && (size_t)T * (size_t)(orow + 1) * sizeof(float) > 64 * 1024) T /= 2;
+  const size_t lds = (size_t)T * (size_t)(orow + 1) * sizeof(float);
+  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
+  const dim3 grid((unsigned)((M + T - 1) / T));
   const float2* d = reinterpret_cast<const float2*>(delta);
+  const dim3 blk(T);
   switch (K) {
-    case 1: hipLaunchKernelGGL(correct_records_kernel<1>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
-    case 2: hipLaunchKernelGGL(correct_records_kernel<2>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
-    case 3: hipLaunchKernelGGL(correct_records_kernel<3>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
-    case 4: hipLaunchKernelGGL(correct_records_kernel<4>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
-    case 5: hipLaunchKernelGGL(correct_records_kernel<5>, grid, dim3(256), 0, st, rec, M, rows, orow, d, P); break;
+    case 1: hipLaunchKernelGGL(correct_records_kernel<1>, grid, blk, lds, st, rec, M, rows, orow, d, P); break;
+    case 2: hipLaunchKernelGGL(correct_records_kernel<2>, grid, blk, lds, st, rec, M, rows, orow, d, P); break;
+    case 3: hipLaunchKernelGGL(correct_records_kernel<3>, grid, blk, lds, st, rec, M, rows, orow, d, P); break;
+    case 4: hipLaunchKernelGGL(correct_records_kernel<4>, grid, blk, lds, st, rec, M, rows, orow, d, P); break;
+    case 5: hipLaunchKernelGGL(correct_records_kernel<5>, grid, blk, lds, st, rec, M, rows, orow, d, P); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();

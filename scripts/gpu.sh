@@ -38,6 +38,7 @@
 #   dpacc      sweep-DP accuracy table (ranks x merges per step) incl. per-participant records
 #   dpcost     one-GPU DP step price: plain vs forced merges at k = 8 / 16
 #   dpstep     the same with one prepass per step (tail / serial placement, k = 8 / 16 / 32)
+#   corrmicro  the record correction kernel alone + a kernel trace of the k = 8 DP step
 #   gtest      a subset of the GPU tests (GTEST_K = pytest -k expression)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -281,15 +282,24 @@ EOF
         run dpstep/plain_$r 300 $PY bench.py --steps 10 --warmup 2
         for k in ${DPSTEP_K:-8 16}; do
           A="--steps 10 --warmup 2 --force-merge --merges-per-step $k"
-          run dpstep/k${k}_pieces_$r 300 $PY bench.py $A
-          ANA_DP_CORRECT_RECORDS=0 run dpstep/k${k}_pieces_nocorr_$r 300 $PY bench.py $A
-          ANA_PREPASS_PIECES=0 run dpstep/k${k}_whole_$r 300 $PY bench.py $A
-          run dpstep/k${k}_window_$r 300 $PY bench.py $A --step-prepass 0
-          ANA_PREPASS_SERIAL=1 run dpstep/k${k}_pieces_serial_$r 300 $PY bench.py $A
+          run dpstep/k${k}_window_$r 300 $PY bench.py $A
+          ANA_DP_CORRECT_RECORDS=0 run dpstep/k${k}_window_nocorr_$r 300 $PY bench.py $A
+          ANA_PREPASS_SERIAL=1 run dpstep/k${k}_window_serial_$r 300 $PY bench.py $A
           run dpstep/k${k}_emu8_$r 300 $PY bench.py $A --emulate-allreduce 8:300
+          if [ -n "${DPSTEP_ALL:-}" ]; then
+            run dpstep/k${k}_pieces_$r 300 $PY bench.py $A --step-prepass 1
+            ANA_PREPASS_PIECES=0 run dpstep/k${k}_whole_$r 300 $PY bench.py $A --step-prepass 1
+          fi
         done
       done
       for f in gpurun_out/dpstep/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
+      ;;
+    corrmicro)  # the record correction alone (scripts/correct_micro.py) + kernel trace of the forced k = 8 step
+      run corrmicro/micro 300 $PY scripts/correct_micro.py
+      run corrmicro/micro_10M 300 $PY scripts/correct_micro.py --matches 10e6
+      run corrmicro/trace 300 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/corrmicro/prof" -o run \
+          -- $PY bench.py --steps 4 --warmup 1 --force-merge --merges-per-step 8
+      find gpurun_out/corrmicro/prof -name '*kernel_stats.csv' -exec head -25 {} \;
       ;;
     workersql)  # the streaming worker on the reflected SQLAlchemy store (sqlite file), native engine
       rm -f /tmp/wsa*.db*
