@@ -140,6 +140,10 @@ def parse(argv=None):
             k *= 2
         if args.team_size == 5 and n >= 4:
             k *= 2      # 5v5: 10 appearances a match, twice the merges for the same error
+        # k = 8 at N = 8 is the smallest k that meets both fidelity bars with the causal
+        # record correction (simulated N = 8: records median 8.0 <= 15, roster Spearman
+        # 0.9956 >= 0.995; k = 4 gives records 14.1 but roster Spearman 0.983 --
+        # profiles/r5/record_correction.log)
         args.merges_per_step = k if n > 1 and args.config != 4 and args.sweeps <= 1 else 1
     if args.merges_per_step < 1 or args.matches_per_gpu % args.merges_per_step:
         ap.error("--merges-per-step must divide --matches-per-gpu")
