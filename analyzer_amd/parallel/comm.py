@@ -113,6 +113,40 @@ def scan_and_sum(t: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tenso
     return back[:P].view_as(t), total[:P].view_as(t)
 
 
+def scan_and_sum_start(t: torch.Tensor, group=None, stream=None, extra: Optional[torch.Tensor] = None):
+    """``scan_and_sum`` in flight: returns ``finish() -> (prefix, total)``.  With RCCL
+    and a side ``stream`` the two all-to-alls, the block scan between them, the
+    all-gather and the SUM all-reduce of ``extra`` (in place) all run on that stream,
+    which first waits for the current one; ``finish`` makes the current stream wait
+    for it -- the caller's stream stays free for other work in between (the DP merge
+    corrects the previous window's records there).  gloo / one rank / no stream:
+    done at once, ``finish`` only returns it."""
+    _, size = world(group)
+    side = stream is not None and t.is_cuda and size > 1 and not _staged(t, group)
+    if not side:
+        res = scan_and_sum(t, group)
+        if extra is not None and size > 1:
+            all_reduce_sum(extra, group)
+        return lambda: res
+    cur = torch.cuda.current_stream(t.device)
+    stream.wait_stream(cur)
+    with torch.cuda.stream(stream):
+        res = scan_and_sum(t, group)
+        if extra is not None:
+            all_reduce_sum(extra, group)
+    done = torch.cuda.Event()
+    done.record(stream)
+
+    def finish():
+        now = torch.cuda.current_stream(t.device)
+        now.wait_event(done)
+        for x in res:
+            if x is not t:  # allocated on the side stream, read on this one
+                x.record_stream(now)
+        return res
+    return finish
+
+
 def all_reduce_sum(t: torch.Tensor, group=None, async_op: bool = False):
     """SUM all-reduce in place; gloo + device tensor goes through the host.
     Returns a work handle (``async_op``) or None."""

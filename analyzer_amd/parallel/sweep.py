@@ -72,7 +72,7 @@ import torch.distributed as dist
 from ..config import EngineConfig, RaterConfig
 from ..models.tiers import vst_table
 from ..ops.native import native
-from .comm import all_reduce_sum, exclusive_scan, scan_and_sum, world
+from .comm import all_reduce_sum, exclusive_scan, scan_and_sum, scan_and_sum_start, world
 
 MAX_RANKS = 15  # touch counts are base-16 fields in fp32 (see csrc/sweep_core.h)
 
@@ -115,6 +115,13 @@ class SweepMerger:
             correct_records = os.environ.get("ANA_DP_CORRECT_RECORDS", "1") not in ("", "0", "false")
         self.correct = bool(correct_records) and self.sweeps <= 1
         self._zero_prefix = None  # one rank: its prefix is zero (the pass still runs: it is priced)
+        # the correction of window w's records runs in merge w+1, while window w+1's
+        # collective is in flight (its only input, the increment table, is ready once
+        # decode w ran): ANA_DP_CORRECT_DEFER=0 runs it in line after decode w.  A rating
+        # into the rows it still has to correct, finish() and results_ready() run it first
+        self.defer = os.environ.get("ANA_DP_CORRECT_DEFER", "1") not in ("", "0", "false")
+        self._pending = None      # (rec, K, rows, delta) of the deferred correction
+        self._coll = None         # side stream of the merge's collectives (RCCL)
         self.delta = None         # [P, 16] fp32 increments of the record correction (decode_packed)
         # emulate = "N:GBps[:us]" (one rank, force): every all-reduce is replaced by a stand-in
         # on a stream of its own that takes what an N-rank ring all-reduce of the operands would
@@ -329,9 +336,14 @@ class SweepMerger:
     def merge_corrected(self, roster, rec: torch.Tensor, out, overlap: Optional[Callable[[], None]] = None) -> None:
         """``merge`` with the causal record correction of this window's records
         (``rec``, RateResult ``out``): messages -> ONE collective giving the sum and
-        this rank's exclusive prefix (comm.scan_and_sum) -> the records corrected by
-        the prefix against the window start -> the decode.  Not bucketed: the records
-        name any player, so the whole prefix is needed before the pass."""
+        this rank's exclusive prefix (comm.scan_and_sum) -> the decode, which also turns
+        the prefix into the increment table -> the records pass.  Not bucketed: the
+        records name any player, so the whole prefix is needed before the pass.
+
+        Deferred (``defer``, default): the records pass of this window is enqueued by
+        the NEXT merge right after its collective is launched, so it runs while the
+        collective is in flight (RCCL on its own stream; the emulated stand-in on 32 CUs)
+        instead of on the critical path; ``flush_correction`` runs a pending pass."""
         K = (int(rec.shape[1]) - 2) // 2
         self._ev("begin")
         if self.msg is not None:
@@ -342,17 +354,24 @@ class SweepMerger:
             operand = self.buf
         self._ev("messages")
         if self.world > 1:
-            prefix, total = scan_and_sum(operand, group=self.group)
-            operand.copy_(total)
-            if self.msg is not None:
-                all_reduce_sum(self.cnt, group=self.group)
+            if self._coll is None and self.device.type == "cuda":
+                self._coll = torch.cuda.Stream(self.device)
+            fin = scan_and_sum_start(operand, group=self.group, stream=self._coll,
+                                     extra=self.cnt if self.msg is not None else None)
         else:
-            prefix = self._prefix_zero(operand)
+            prefix0 = self._prefix_zero(operand)
+            fin = lambda: (prefix0, operand)  # noqa: E731
             if self.emulate is not None and self.device.type == "cuda":  # 1.5x the all-reduce's volume
                 n, bw, lat = self.emulate
                 self.emulate = (n, bw / 1.5, lat)
-                self._launch_reduce(0, self.P, self.msg is not None)()
+                efin = self._launch_reduce(0, self.P, self.msg is not None)
                 self.emulate = (n, bw, lat)
+                fin = lambda: (efin(), (prefix0, operand))[1]  # noqa: E731
+        self.flush_correction()  # the previous window's records, beside the collective
+        self._ev("correct")
+        prefix, total = fin()
+        if total is not operand:
+            operand.copy_(total)
         self._ev("allreduce")
         if overlap is not None:
             overlap()
@@ -366,10 +385,27 @@ class SweepMerger:
             self.decode(roster, into=self.start)
             delta = prefix
         self._ev("apply")
-        native().correct_records(rec, K, out.packed, delta)
-        self._ev("correct")
+        self._pending = (rec, K, out.packed, delta)
+        if not self.defer:
+            self.flush_correction()
+            self._ev("correct")
         self._synced = True
         self.windows += 1
+
+    def flush_correction(self) -> None:
+        """Run the deferred record correction now (stream-ordered), if one is pending."""
+        if self._pending is not None:
+            rec, K, rows, delta = self._pending
+            self._pending = None
+            native().correct_records(rec, K, rows, delta)
+
+    def pending_rows(self, out) -> bool:
+        """Whether the deferred correction still has to write rows of RateResult ``out``."""
+        if self._pending is None or out is None or getattr(out, "packed", None) is None:
+            return False
+        a, b = self._pending[2], out.packed
+        a0, b0 = a.data_ptr(), b.data_ptr()
+        return a0 < b0 + b.numel() * b.element_size() and b0 < a0 + a.numel() * a.element_size()
 
     def merge(self, roster, overlap: Optional[Callable[[], None]] = None) -> None:
         """Combine every rank's window into the replicated roster (in place):

@@ -239,6 +239,8 @@ class WindowPipeline:
             main.wait_event(prep.ready)
         if self.merger is not None:
             self.merger.begin(self.roster)
+            if hasattr(self.merger, "pending_rows") and self.merger.pending_rows(out):
+                self.merger.flush_correction()  # a deferred record correction of these rows
         progress = None
         if self._signal:
             self._seq += 1
@@ -415,10 +417,19 @@ class WindowPipeline:
         self._plans = plan  # keep the plan's launches alive until the next step
         return res, Prepared(next_rec, sched, done, used, int(window))
 
+    def results_ready(self, res: Optional[RateResult]) -> None:
+        """Make ``res``'s records final before a consumer reads them: the DP merge
+        defers each window's record correction into the next merge (parallel/sweep.py
+        ``defer``), so a pending one for these rows runs now (stream-ordered)."""
+        if self.merger is not None and hasattr(self.merger, "pending_rows") and self.merger.pending_rows(res):
+            self.merger.flush_correction()
+
     def finish(self) -> None:
-        """End of a run of windows: every DP merge is complete when its window's
-        ``rate`` returns, so only the merge decodes' clamp counter is checked (syncs;
-        parallel/sweep.py ``check`` raises on a decode held at the precision floor)."""
+        """End of a run of windows: the last window's deferred record correction runs
+        (parallel/sweep.py) and the merge decodes' clamp counter is checked (syncs;
+        ``check`` raises on a decode held at the precision floor)."""
+        if self.merger is not None and hasattr(self.merger, "flush_correction"):
+            self.merger.flush_correction()
         if self.merger is not None and hasattr(self.merger, "check"):
             self.merger.check()
 
@@ -439,6 +450,7 @@ class WindowPipeline:
                 following = None
             res, nxt = self.step(cur, following, out=out)
             if on_result is not None:
+                self.results_ready(res)
                 on_result(n, res)
             n += 1
         self.finish()

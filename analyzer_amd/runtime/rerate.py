@@ -167,6 +167,7 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
             torch.cuda.current_stream(dev).wait_event(sink.copied(outs[b]))
         # window g+1 is generated before rate(g) is enqueued; its prepass waits for the tail
         res, nxt = pipe.step(cur, window_rec(g + 1) if g + 1 < total else None, out=outs[b])
+        pipe.results_ready(res)  # the DP merge's deferred record correction of these rows
         counts += torch.bincount(res.status.to(torch.int64), minlength=256)
         if records == "digest":
             digests[g] = window_digest(res)

@@ -308,6 +308,11 @@ def main(argv=None) -> int:
     tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.4 if auto_mode else 0.9)) \
         if tele is not None and args.telemetry_mode == "tail" else 0.0
     pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
+    # the DP merge corrects window i's records during window i+1's collective
+    # (parallel/sweep.py defer): records double-buffered, so window i+1's rating
+    # writes the other buffer (a consumer streams the records out of the idle one)
+    outs = [out, RateResult.allocate(Mw, K, dev)] if merger is not None and merger.correct and \
+        merger.defer and not step_prepass else [out]
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     sync()
     prepared = {0: pipe.prepare(windows[0], window=Mw if step_prepass else 0)}
@@ -330,6 +335,7 @@ def main(argv=None) -> int:
             tstream = torch.cuda.Stream(dev)
 
     def step(i):
+        out = outs[i % len(outs)]
         # rate window i, then the prepass of window i+1 on the side stream behind
         # its tail (every timed step carries exactly one prepass and one rating)
         nxt = windows[(i + 1) % n_windows]
@@ -421,6 +427,7 @@ def main(argv=None) -> int:
     if int(flags.sum()):
         raise RuntimeError("dataflow error flags set during the benchmark: %s" % flags.tolist())
     if args.check:
+        out = outs[(total_windows - 1) % len(outs)]
         counts = out.status_counts()
         assert NOT_PROCESSED not in out.status.unique().tolist(), counts
         if rank == 0:

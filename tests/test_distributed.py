@@ -453,6 +453,44 @@ def _corrected(rank, size, P, M, K, seed, windows, comm_dtype):
     return {"state": roster.state, "last": outs[-1]}
 
 
+def _corrected_ring(rank, size, P, M, K, seed, windows, defer):
+    """bench.py's use: windows rated into two alternating record buffers, nothing
+    consumed until finish() (the deferred corrections run inside later merges)."""
+    import os
+
+    from analyzer_amd.ops.rate import BatchRater, RateResult
+    from analyzer_amd.parallel.sweep import SweepMerger
+    from analyzer_amd.runtime.engine import WindowPipeline
+
+    os.environ["ANA_DP_CORRECT_DEFER"] = "1" if defer else "0"
+    roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
+    spec = StreamSpec(team_size=K, seed=seed + 1)
+    recs = [make_stream(spec, M, P, K=K, base=(w * size + rank) * M) for w in range(windows)]
+    merger = SweepMerger(P, "cpu", comm_dtype="bf16")
+    assert merger.defer == defer
+    pipe = WindowPipeline(BatchRater(), roster, K, merger=merger)
+    outs = [RateResult.allocate(M, K, "cpu") for _ in range(2)]
+    prep = pipe.prepare(recs[0])
+    for w in range(windows):
+        _, prep = pipe.step(prep, recs[w + 1] if w + 1 < windows else None, out=outs[w % 2])
+    pending = merger._pending is not None
+    pipe.finish()
+    return {"rows": [o.packed.clone() for o in outs], "pending": pending, "state": roster.state}
+
+
+def test_deferred_record_correction_matches_inline(tmp_path):
+    """The record correction deferred into the next merge (beside its collective)
+    writes exactly the records the in-line pass writes, once finish() has run."""
+    P, M, K, seed, size, windows = 300, 700, 3, 41, 2, 3
+    a = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, True)
+    b = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, False)
+    for r in range(size):
+        assert a[r]["pending"] and not b[r]["pending"]
+        assert torch.equal(a[r]["state"].view(torch.int32), b[r]["state"].view(torch.int32))
+        for x, y in zip(a[r]["rows"], b[r]["rows"]):
+            assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+
+
 @pytest.mark.parametrize("comm_dtype", ["fp32", "bf16"])
 def test_record_correction_over_ranks_equals_simulation(tmp_path, comm_dtype):
     """The corrected merge over gloo (scan_and_sum, the records pass before the
