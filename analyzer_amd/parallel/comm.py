@@ -113,27 +113,76 @@ def scan_and_sum(t: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tenso
     return back[:P].view_as(t), total[:P].view_as(t)
 
 
+def _row_bytes(x: torch.Tensor, P: int) -> torch.Tensor:
+    return x.reshape(P, -1).contiguous().view(torch.uint8)
+
+
+def scan_and_sum_rows(t: torch.Tensor, extra: torch.Tensor, group=None):
+    """``scan_and_sum`` of ``t`` whose exchanges also carry ``extra`` (rows summed,
+    not scanned) in the same payload: (prefix of t, total of t, total of extra) from
+    one all-to-all, one all-to-all back and one all-gather -- the DP merge's messages
+    and touch counts without a separate all-reduce (a collective launch per merge).
+    The rows travel as bytes and are read back through typed views."""
+    _, size = world(group)
+    if size <= 1:
+        return torch.zeros_like(t), t, extra
+    P = t.shape[0]
+    bt, be = _row_bytes(t, P), _row_bytes(extra, P)
+    ct, C = bt.shape[1], bt.shape[1] + be.shape[1]
+    if C % t.element_size() or C % extra.element_size() or ct % extra.element_size():
+        p, s = scan_and_sum(t, group)  # rows that do not view back: two exchanges
+        all_reduce_sum(extra, group)
+        return p, s, extra
+    blk = -(-P // size)
+    send = torch.zeros((size * blk, C), dtype=torch.uint8, device=t.device)
+    send[:P, :ct] = bt
+    send[:P, ct:] = be
+    recv = torch.empty_like(send)
+    all_to_all_rows(recv, send, group)  # recv block q = rank q's rows of my block
+    r3 = recv.view(size, blk, C)
+    tv = r3[..., :ct].view(t.dtype)
+    ev = r3[..., ct:].view(extra.dtype)
+    cs = torch.cumsum(tv.float() if t.is_floating_point() else tv, 0)
+    ex = torch.zeros_like(cs)
+    ex[1:] = cs[:-1]
+    back = torch.empty((size * blk, ct), dtype=torch.uint8, device=t.device)
+    all_to_all_rows(back, ex.to(t.dtype).reshape(size * blk, -1).view(torch.uint8), group)
+    tot = torch.empty((blk, C), dtype=torch.uint8, device=t.device)
+    tot[:, :ct] = cs[-1].to(t.dtype).contiguous().view(torch.uint8)
+    tot[:, ct:] = ev.sum(0).to(extra.dtype).contiguous().view(torch.uint8)
+    total = torch.empty((size * blk, C), dtype=torch.uint8, device=t.device)
+    all_gather_rows(total, tot, group)
+    prefix = back[:P].view(t.dtype).view_as(t)
+    return (prefix, total[:P, :ct].contiguous().view(t.dtype).view_as(t),
+            total[:P, ct:].contiguous().view(extra.dtype).view_as(extra))
+
+
 def scan_and_sum_start(t: torch.Tensor, group=None, stream=None, extra: Optional[torch.Tensor] = None):
     """``scan_and_sum`` in flight: returns ``finish() -> (prefix, total)``.  With RCCL
     and a side ``stream`` the two all-to-alls, the block scan between them, the
-    all-gather and the SUM all-reduce of ``extra`` (in place) all run on that stream,
+    all-gather -- which also carry ``extra``, summed in place (scan_and_sum_rows) --
+    all run on that stream,
     which first waits for the current one; ``finish`` makes the current stream wait
     for it -- the caller's stream stays free for other work in between (the DP merge
     corrects the previous window's records there).  gloo / one rank / no stream:
     done at once, ``finish`` only returns it."""
     _, size = world(group)
+
+    def run():
+        if extra is None:
+            return scan_and_sum(t, group)
+        p, s, e = scan_and_sum_rows(t, extra, group)
+        if e is not extra:
+            extra.copy_(e)
+        return p, s
     side = stream is not None and t.is_cuda and size > 1 and not _staged(t, group)
     if not side:
-        res = scan_and_sum(t, group)
-        if extra is not None and size > 1:
-            all_reduce_sum(extra, group)
+        res = run()
         return lambda: res
     cur = torch.cuda.current_stream(t.device)
     stream.wait_stream(cur)
     with torch.cuda.stream(stream):
-        res = scan_and_sum(t, group)
-        if extra is not None:
-            all_reduce_sum(extra, group)
+        res = run()
     done = torch.cuda.Event()
     done.record(stream)
 

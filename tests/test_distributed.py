@@ -420,7 +420,10 @@ def _scan_sum(rank, size):
     c = torch.full((22, 2), rank + 1, dtype=torch.int32)
     p, s = scan_and_sum(t)
     pc, sc = scan_and_sum(c)
-    return {"p": p.float(), "s": s.float(), "pc": pc, "sc": sc}
+    from analyzer_amd.parallel.comm import scan_and_sum_rows
+
+    p2, s2, e2 = scan_and_sum_rows(t, c.clone())  # one payload: bf16 rows + int32 rows
+    return {"p": p.float(), "s": s.float(), "pc": pc, "sc": sc, "p2": p2.float(), "s2": s2.float(), "e2": e2}
 
 
 def test_scan_and_sum_over_ranks(tmp_path):
@@ -436,6 +439,8 @@ def test_scan_and_sum_over_ranks(tmp_path):
         assert torch.equal(out["s"], sum(ts).to(torch.bfloat16).float())
         assert torch.equal(out["pc"], torch.full((22, 2), sum(range(1, r + 1)), dtype=torch.int32))
         assert torch.equal(out["sc"], torch.full((22, 2), 6, dtype=torch.int32))
+        assert torch.equal(out["p2"], out["p"]) and torch.equal(out["s2"], out["s"])
+        assert torch.equal(out["e2"], out["sc"])
 
 
 def _corrected(rank, size, P, M, K, seed, windows, comm_dtype):
