@@ -59,8 +59,9 @@ ANA_HD bool track_base(int t, float cmu, float csg, float c0mu, float c0sg, bool
 // measured against a's value where a has one and against B where the track is NULL
 // in a: prefix sums then telescope, so the start + the messages of ranks 0..r-1 is
 // exactly rank r-1's posterior once every earlier rank rated from its exact prior.
-// touched: the track is NULL in a and rated now (base-16 touch counters,
-// exact in fp32 for <= 15 ranks, make it non-NULL on every rank).
+// touched: this rank moved the track -- NULL in a and rated now, or changed (base-16
+// touch counters, exact in fp32 for <= 15 ranks): their sum m makes a NULL track
+// non-NULL on every rank and tells the decode how many ranks a net loss came from.
 ANA_HD void sweep_delta_track(int t, float cmu, float csg, float c0mu, float c0sg, float amu, float asg,
                               float bmu, float bsg, bool seeded, float seed_mu, float seed_sig,
                               bool scaled, float& dp, float& dt, bool& touched) {
@@ -85,7 +86,35 @@ ANA_HD void sweep_delta_track(int t, float cmu, float csg, float c0mu, float c0s
       dt = t1 - t0;
     }
   }
-  touched = !had && bmu == bmu;
+  touched = had ? changed : bmu == bmu;
+}
+
+// Decoded precision ratio pi / pi_B and mean-shift divisor of summed messages whose
+// precision ratios x_r = pi_r / pi_B sum to 1 + S over m contributing ranks.  Net
+// gain (S >= 0) or one rank: the natural-parameter sum, 1 + S -- exact for evidence.
+// Net loss over m >= 2 ranks: the tau^2 dynamics every match adds, which ADD in
+// variance, not in precision -- eight ranks that each lost 20 % of a low-sigma
+// player's precision sum to 1 + S = -0.6, where the sequential result keeps 0.38 of it
+// (the 1M-player 8-rank bench hit this on 28 tracks).  So the loss is combined in
+// variance space, as if every rank lost the mean x = 1 + S / m:
+//     pi / pi_B = 1 / (1 + m (1 / x - 1)) = x / (x + m (1 - x))   in (0, 1)
+// (x > 0 because every x_r > 0), which agrees with 1 + S to first order and is
+// exact for equal losses; the mean shift sum_r x_r dmu_r is divided by x (each rank's
+// shift counted once).  Never zero or negative, so a merge clamps only on inputs no
+// set of ranks can produce (the clamp count stays the safety net).
+// Returns true on the variance-space branch.
+ANA_HD bool merged_ratio(float S, unsigned m, float& ratio, float& mdiv) {
+  ratio = 1.f + S;
+  mdiv = ratio;
+  if (S < 0.f && m >= 2u) {
+    const float x = 1.f + S / (float)m;
+    if (x > 0.f) {
+      ratio = x / (x + (float)m * (1.f - x));
+      mdiv = x;
+      return true;
+    }
+  }
+  return false;
 }
 
 // One track t of the decode: (amu, asg) the common window-start value of the track,
@@ -115,21 +144,30 @@ ANA_HD void sweep_apply_track(int t, float amu, float asg, float a0mu, float a0s
   float bm, bs;
   const bool based = track_base(t, amu, asg, a0mu, a0sg, seeded, seed_mu, seed_sig, bm, bs);
   if (!based) return;
-  if (scaled) {  // pi = pi_b (1 + sum r_pi), mu = mu_b + sum r_tau / (1 + sum r_pi)
-    float ratio = 1.f + dpi;
+  if (scaled) {  // pi = pi_b (1 + sum r_pi), mu = mu_b + sum r_tau / (1 + sum r_pi) (merged_ratio)
+    float ratio, mdiv;
+    merged_ratio(dpi, touched, ratio, mdiv);
     clamped = !(ratio > 1e-6f);
     ratio = clamped ? 1e-6f : ratio;
-    mu = bm + dtau / ratio;
+    mdiv = clamped ? 1e-6f : mdiv;
+    mu = bm + dtau / mdiv;
     sg = bs / sqrtf(ratio);
-  } else {
+  } else {       // raw: S = d_pi / pi_b, sum_r x_r dmu_r = d_tau / pi_b - S mu_b
     float pb, tb;
     nat_params(bm, bs, pb, tb);
-    float pi = pb + dpi;
-    const float tau = tb + dtau;
-    clamped = !(pi > 1e-12f);
-    pi = clamped ? 1e-12f : pi;  // merged precision never below "no information"
-    mu = tau / pi;
-    sg = 1.f / sqrtf(pi);
+    const float S = dpi / pb;
+    float ratio, mdiv;
+    if (merged_ratio(S, touched, ratio, mdiv)) {
+      mu = bm + (dtau / pb - S * bm) / mdiv;
+      sg = bs / sqrtf(ratio);
+    } else {  // the natural-parameter sum
+      float pi = pb + dpi;
+      const float tau = tb + dtau;
+      clamped = !(pi > 1e-12f);
+      pi = clamped ? 1e-12f : pi;  // merged precision never below "no information"
+      mu = tau / pi;
+      sg = 1.f / sqrtf(pi);
+    }
   }
 }
 

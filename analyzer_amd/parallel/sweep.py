@@ -206,6 +206,14 @@ class SweepMerger:
         """roster.state[lo:hi] (and ``into``[lo:hi]) := start + summed messages in buf."""
         hi = self.P if hi is None else hi
         s2 = into[lo:hi] if into is not None else self._none
+        if self.sweeps > 1:
+            # causal re-sweeps: the messages telescope (each measured from its rank's exact
+            # causal prior), so their natural-parameter sum is exact -- every touch field
+            # held at <= 1 keeps the decode off the variance-space branch for net losses
+            # (sweep_core.h merged_ratio), which is for independent slices only
+            t = self.buf[lo:hi, 14:16]
+            x = t.to(torch.int32)
+            t.copy_(((x | (x >> 1) | (x >> 2) | (x >> 3)) & 0x11111111).to(t.dtype))
         native().sweep_apply(self.start[lo:hi], self.buf[lo:hi], roster.attrs[lo:hi],
                              roster.state[lo:hi], s2, self.vst, float(self.cfg.unknown_player_sigma),
                              self.scaled, self.clamps)

@@ -14,7 +14,7 @@
 #   bench      bench.py config 2, 20 steps, --verify      gpurun_out/bench/
 #   configs    bench.py configs 3, 4 (fused + separate), 5
 #   skew       bench.py --skew 2 and 3
-#   dp         bench.py --gpus 2 and 4 on this one GPU (gloo rehearsal of the spawn path)
+#   dp         bench.py --gpus 2, 4 and 8 on this one GPU (gloo rehearsal of the spawn path)
 #   accuracy   sweep-DP accuracy, 8 ranks x 10M matches over 1M players, sweeps 1,2,4,8
 #   graph      micro-batches (eager vs HIP graph, scripts/bench_graph.py) + prepass alone
 #   hop        quick executor A/B (serial chain + 10M window, local hand-off, timing build)
@@ -87,6 +87,7 @@ for task in "$@"; do
     dp)
       run dp/gloo2 600 env ANA_DIST_BACKEND=gloo $PY bench.py --gpus 2 --steps 5 --warmup 2
       run dp/gloo4 900 env ANA_DIST_BACKEND=gloo $PY bench.py --gpus 4 --steps 3 --warmup 1
+      run dp/gloo8 900 env ANA_DIST_BACKEND=gloo $PY bench.py --gpus 8 --steps 2 --warmup 1
       run dp/gloo2_sweeps2 600 env ANA_DIST_BACKEND=gloo $PY bench.py --gpus 2 --steps 3 --warmup 1 --sweeps 2
       ;;
     accuracy)

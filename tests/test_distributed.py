@@ -147,21 +147,38 @@ def test_sweep_merge_disjoint_equals_union(tmp_path):
     assert torch.equal(res[0]["merged"].nan_to_num(-7), res[1]["merged"].nan_to_num(-7))
 
 
+def _merged_ratio(S, m):
+    """sweep_core.h merged_ratio, re-derived: (pi / pi_B, mean-shift divisor)."""
+    var = (S < 0) & (m >= 2)
+    x = 1 + S / m.clamp(min=1)
+    return torch.where(var, x / (x + m * (1 - x)), 1 + S), torch.where(var, x, 1 + S), var
+
+
 def test_sweep_merge_overlapping_sums_messages(tmp_path):
     """Overlapping players: merged natural parameters = start + sum of every
-    rank's (posterior - start) message (EP product of the rank posteriors)."""
+    rank's (posterior - start) message (EP product of the rank posteriors) where the
+    ranks net-gained precision; a net loss (tau^2 dynamics) over m >= 2 ranks is
+    combined in variance space (sweep_core.h merged_ratio)."""
     P, M, K, seed, size = 30, 150, 3, 6, 3
     res = run_ranks(_sweep, size, tmp_path, P, M, K, seed, False)
     total = sum(r["msg"] for r in res)
     start = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.5)).state
     merged = res[0]["merged"]
+    lo, hi = total[:, 14].long(), total[:, 15].long()
+    n_var = 0
     for t in range(7):
+        m = (lo >> (4 * t)) & 15 if t < 4 else (hi >> (4 * (t - 4))) & 15
         mu0, sg0 = start[:, 4 * t], start[:, 4 * t + 2]
         have = ~torch.isnan(mu0) & ((total[:, 2 * t] != 0) | (total[:, 2 * t + 1] != 0))
-        pi = 1 / sg0[have].double() ** 2 + total[have, 2 * t].double()
-        tau = mu0[have].double() / sg0[have].double() ** 2 + total[have, 2 * t + 1].double()
-        assert torch.allclose(merged[have, 4 * t].double(), tau / pi, rtol=1e-5, atol=1e-2)
-        assert torch.allclose(merged[have, 4 * t + 2].double(), pi.rsqrt(), rtol=1e-4)
+        pb = 1 / sg0[have].double() ** 2
+        mb = mu0[have].double()
+        dpi, dtau = total[have, 2 * t].double(), total[have, 2 * t + 1].double()
+        ratio, mdiv, var = _merged_ratio(dpi / pb, m[have].double())
+        mu = torch.where(var, mb + (dtau / pb - dpi / pb * mb) / mdiv, (mb * pb + dtau) / (pb + dpi))
+        assert torch.allclose(merged[have, 4 * t].double(), mu, rtol=1e-5, atol=1e-2)
+        assert torch.allclose(merged[have, 4 * t + 2].double(), (pb * ratio).rsqrt(), rtol=1e-4)
+        n_var += int(var.sum())
+    assert n_var > 0  # both branches exercised
     for r in res[1:]:
         assert torch.equal(r["merged"].nan_to_num(-7), merged.nan_to_num(-7))
 
@@ -393,6 +410,42 @@ def test_decode_clamps_are_counted_and_raise():
     m.decode_packed(r2)
     m.check()
     assert torch.equal(base_rows(r2.state).nan_to_num(-7), base_rows(ro.state).nan_to_num(-7))
+
+
+def test_net_precision_loss_over_ranks_decodes_in_variance_space():
+    """Eight ranks that each lost 20 % of a track's precision to tau^2 dynamics (a
+    low-sigma player in every slice -- the 1M-player 8-rank bench hit 28 such tracks):
+    the natural-parameter sum is 1 - 1.6 < 0, the decode combines the losses in
+    variance space instead -- 1 / (1 + 8 (1 / 0.8 - 1)) = 1/3 of the precision, what
+    sequential dynamics give -- and clamps nothing; one rank's loss stays exact."""
+    from analyzer_amd.ops.synth import RosterSpec, make_roster
+    from analyzer_amd.parallel.sweep import SweepMerger
+
+    P = 16
+    ro = make_roster(RosterSpec(num_players=P, seed=3, p_rated=1.0, p_mode_rated=1.0))
+    for comm in ("bf16", "fp32"):
+        for m_ranks, S, want in ((8, -1.6, 1.0 / 3.0), (1, -0.7, 0.3)):
+            mg = SweepMerger(P, "cpu", comm_dtype=comm, force=True)
+            r = ro.clone()
+            mg.begin(r)
+            sg0 = mg.start[:, 1].double()
+            if comm == "bf16":
+                mg.msg.zero_()
+                mg.cnt.zero_()
+                mg.msg[:, 0] = S
+                mg.cnt[:, 0] = m_ranks  # shared track: touch field 0
+                mg.decode_packed(r)
+            else:
+                mg.buf.zero_()
+                mg.buf[:, 0] = (S / sg0 ** 2).float()
+                mg.buf[:, 1] = mg.buf[:, 0] * mg.start[:, 0]  # d_tau of an unmoved mean: mu_B d_pi
+                mg.buf[:, 14] = float(m_ranks)
+                mg.decode(r)
+            assert mg.clamp_hits() == 0
+            got = (sg0 / r.state[:, 2].double()) ** 2  # pi / pi_B
+            assert torch.allclose(got, torch.full_like(got, want), rtol=2e-2), (comm, m_ranks, got[:3])
+            mu_shift = (r.state[:, 0].double() - mg.start[:, 0].double()).abs()
+            assert float(mu_shift.max()) < 1e-2  # no mean message: the mean stays
 
 
 def test_default_merge_keeps_its_precision_margin_at_the_lag_reproduction_density():
