@@ -285,8 +285,15 @@ def main(argv=None) -> int:
         n_events = sum(t.num_events for t in tele) / n_windows
     if args.emulate_allreduce and (world > 1 or not args.force_merge or cpu):
         raise SystemExit("bench: --emulate-allreduce prices N ranks on ONE GPU (needs --force-merge, N = 1)")
+    # the causal record correction where the uncorrected records miss the fidelity bar
+    # (records median |d mu| <= 15 against exact sequential rating): 12.6 at N = 2, 27.3 at
+    # N = 4, 29.6 at N = 8 uncorrected (k = N, profiles/r4/dp_accuracy_records.log), 7.85
+    # corrected at N = 8 (profiles/r5/dp_gloo_rehearsals.log) -- so N >= 4, or the emulated
+    # N of a one-GPU projection; ANA_DP_CORRECT_RECORDS overrides
+    n_eff = world if world > 1 else (int(args.emulate_allreduce.split(":")[0]) if args.emulate_allreduce else 0)
+    correct = None if os.environ.get("ANA_DP_CORRECT_RECORDS") is not None or not n_eff else n_eff >= 4
     merger = (SweepMerger(P, dev, comm_dtype=args.comm_dtype, sweeps=args.sweeps, force=args.force_merge,
-                          emulate=args.emulate_allreduce)
+                          emulate=args.emulate_allreduce, correct_records=correct)
               if world > 1 or args.force_merge else None)
     auto_mode = args.telemetry_mode == "auto"
     tele_path = None

@@ -38,6 +38,7 @@
 #   dpacc      sweep-DP accuracy table (ranks x merges per step) incl. per-participant records
 #   dpcost     one-GPU DP step price: plain vs forced merges at k = 8 / 16
 #   dpstep     the same with one prepass per step (tail / serial placement, k = 8 / 16 / 32)
+#   project    one-GPU projection of the N = 2 / 4 / 8 DP step (emulated all-reduce, bus bandwidth sweep)
 #   corrmicro  the record correction kernel alone + a kernel trace of the k = 8 DP step
 #   gtest      a subset of the GPU tests (GTEST_K = pytest -k expression)
 set -o pipefail
@@ -294,6 +295,18 @@ EOF
         done
       done
       for f in gpurun_out/dpstep/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
+      ;;
+    project)  # N-GPU step projection on one GPU: k = N forced merges with the all-reduce stand-in
+              # (N ranks, BW GB/s bus bandwidth), N = 2 / 4 / 8 at 300 GB/s, N = 8 at 150 / 600 GB/s
+      for r in 1 2; do
+        run project/plain_$r 300 $PY bench.py --steps 10 --warmup 2
+        for nb in 2:300 4:300 8:300 8:150 8:600; do
+          n=${nb%%:*}
+          run project/emu${nb/:/_}_$r 300 $PY bench.py --steps 10 --warmup 2 --force-merge --merges-per-step $n \
+              --emulate-allreduce $nb
+        done
+      done
+      for f in gpurun_out/project/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
       ;;
     corrmicro)  # the record correction alone (scripts/correct_micro.py) + kernel trace of the forced k = 8 step
       run corrmicro/micro 300 $PY scripts/correct_micro.py
