@@ -38,6 +38,7 @@
 #   dpacc      sweep-DP accuracy table (ranks x merges per step) incl. per-participant records
 #   dpcost     one-GPU DP step price: plain vs forced merges at k = 8 / 16
 #   dpstep     the same with one prepass per step (tail / serial placement, k = 8 / 16 / 32)
+#   dpconf     gloo rehearsals of config 3 (N = 4) and config 5 (N = 2)
 #   project    one-GPU projection of the N = 2 / 4 / 8 DP step (emulated all-reduce, bus bandwidth sweep)
 #   corrmicro  the record correction kernel alone + a kernel trace of the k = 8 DP step
 #   gtest      a subset of the GPU tests (GTEST_K = pytest -k expression)
@@ -295,6 +296,10 @@ EOF
         done
       done
       for f in gpurun_out/dpstep/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
+      ;;
+    dpconf)  # gloo rehearsals of the other DP configs: 5v5 (config 3, k = 2N) and the 10M-player re-rate (config 5)
+      run dpconf/c3_gloo4 900 env ANA_DIST_BACKEND=gloo $PY bench.py --config 3 --gpus 4 --steps 1 --warmup 1
+      run dpconf/c5_gloo2 900 env ANA_DIST_BACKEND=gloo $PY bench.py --config 5 --gpus 2 --steps 1 --warmup 1
       ;;
     project)  # N-GPU step projection on one GPU: k = N forced merges with the all-reduce stand-in
               # (N ranks, BW GB/s bus bandwidth), N = 2 / 4 / 8 at 300 GB/s, N = 8 at 150 / 600 GB/s
