@@ -164,9 +164,6 @@ class EngineConfig:
                                       its rows come from the Infinity Cache (runtime/engine.py); auto =
                                       on between DP merges (short windows: k = 8 forced merges 9.30 vs
                                       9.53 ms), off for whole windows (8.02 either way)
-    ANA_PREPASS_PIECES      1         DP steps (one prepass per step of k windows): the next step's prepass
-                                      runs in k pieces, one in each window's tail / merge gap; 0 = whole,
-                                      after the last window (runtime/engine.py step_windows)
     ANA_MERGE_BUCKET_MB     16        sweep-merge bucket size (parallel/sweep.py)
     ANA_DP_SERIAL_AR_US     40        DP with N > 1 ranks: the next prepass runs beside the merge when one
                                       merge-sized all-reduce (timed when the pipeline is built, max over
@@ -204,7 +201,6 @@ class EngineConfig:
     prepass_exclusive: bool = False  # with prepass_cus: the executor gets the other CUs
     prepass_serial: Optional[bool] = None  # None = auto (WindowPipeline.serial_prepass)
     roster_warm: Optional[bool] = None  # None = auto (WindowPipeline)
-    prepass_pieces: bool = True  # DP steps: the next step's prepass in k pieces (engine.step_windows)
     merge_bucket_mb: float = 16.0
     comm_dtype: str = "fp32"
     sweeps: int = 1
@@ -245,7 +241,6 @@ class EngineConfig:
             prepass_exclusive=env.get("ANA_PREPASS_EXCLUSIVE", "0") not in ("", "0", "false"),
             prepass_serial=_tristate(env.get("ANA_PREPASS_SERIAL")),
             roster_warm=_tristate(env.get("ANA_ROSTER_WARM")),
-            prepass_pieces=env.get("ANA_PREPASS_PIECES", "1") not in ("", "0", "false"),
             merge_bucket_mb=float(_env(env, "ANA_MERGE_BUCKET_MB") or 16),
             comm_dtype=_env(env, "COMM_DTYPE") or "fp32",
             sweeps=int(_env(env, "SWEEPS") or 1),

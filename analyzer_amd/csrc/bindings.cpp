@@ -195,8 +195,7 @@ std::tuple<Tensor, int64_t> levels_device(Tensor rec, int64_t K, int64_t num_pla
 }
 
 void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
-              Tensor workspace, Tensor ctrl, bool zero_ctrl, int64_t epoch_bump_ptr, int64_t sort_nt,
-              int64_t window) {
+              Tensor workspace, Tensor ctrl, bool zero_ctrl, int64_t epoch_bump_ptr, int64_t sort_nt) {
   const auto dev = rec.device();
   check(rec, "rec", torch::kInt32, dev);
   check(link, "link", torch::kInt32, dev);
@@ -208,7 +207,6 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
   TORCH_CHECK(deps.numel() == M, "deps must have M entries");
   TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
   TORCH_CHECK(M * 2 * K <= ana::kMaxSlots, "more than 2^28 slots in one window (split the stream)");
-  TORCH_CHECK(window >= 0, "window must be >= 0 (0: one window)");
   if (dev.is_cuda()) {
     check(workspace, "workspace", torch::kUInt8, dev);
     check(ctrl, "ctrl", torch::kInt32, dev);
@@ -221,59 +219,14 @@ void schedule(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor de
                                    (size_t)workspace.numel(),
                                    reinterpret_cast<uint32_t*>(ctrl.data_ptr<int32_t>()),
                                    stream_of(rec), zero_ctrl,
-                                   reinterpret_cast<int32_t*>((intptr_t)epoch_bump_ptr), (int)sort_nt,
-                                   window),
+                                   reinterpret_cast<int32_t*>((intptr_t)epoch_bump_ptr), (int)sort_nt),
               "schedule");
   } else {
     TORCH_CHECK(ana::host_schedule((int)K, rec.data_ptr<int32_t>(), M, num_players,
                                    reinterpret_cast<uint32_t*>(link.data_ptr<int32_t>()),
-                                   deps.data_ptr<int32_t>(), window) == 0,
+                                   deps.data_ptr<int32_t>()) == 0,
                 "bad K");
   }
-}
-
-// The device schedule prepass as a plan of launches (kernels.h SchedPlan) that a DP
-// step runs in pieces between its windows (runtime/engine.py).  Holds its tensors.
-struct SchedPlanHandle {
-  ana::SchedPlan plan;
-  std::vector<Tensor> keep;
-  int64_t size() const { return plan.size(); }
-  std::vector<double> costs() const { return plan.cost; }
-  // ops [lo, hi) on the given HIP stream (0: the current torch stream of the plan's device)
-  void run(int64_t lo, int64_t hi, int64_t stream) {
-    const hipStream_t s = stream ? reinterpret_cast<hipStream_t>((intptr_t)stream) : stream_of(keep[0]);
-    plan.run(lo, hi, s);
-    check_hip((int)hipGetLastError(), "schedule plan");
-  }
-};
-
-std::shared_ptr<SchedPlanHandle> schedule_plan(Tensor rec, int64_t K, int64_t num_players, Tensor link, Tensor deps,
-                                               Tensor workspace, int64_t sort_nt, int64_t window, int64_t split) {
-  const auto dev = rec.device();
-  TORCH_CHECK(dev.is_cuda(), "schedule_plan: device tensors only");
-  check(rec, "rec", torch::kInt32, dev);
-  check(link, "link", torch::kInt32, dev);
-  check(deps, "deps", torch::kInt32, dev);
-  check(workspace, "workspace", torch::kUInt8, dev);
-  TORCH_CHECK(K >= 1 && K <= 5, "K must be 1..5");
-  TORCH_CHECK(rec.dim() == 2 && rec.size(1) == 2 * K + 2, "rec must be [M, 2K+2]");
-  const int64_t M = rec.size(0);
-  TORCH_CHECK(M >= 1, "empty stream");
-  TORCH_CHECK(link.dim() == 2 && link.size(0) == M && link.size(1) == 2 * K, "link must be [M, 2K]");
-  TORCH_CHECK(deps.numel() == M, "deps must have M entries");
-  TORCH_CHECK(num_players >= 1 && num_players < 0x7fffffffLL, "num_players out of range");
-  TORCH_CHECK(M * 2 * K <= ana::kMaxSlots, "more than 2^28 slots in one window (split the stream)");
-  TORCH_CHECK(window >= 0 && split >= 1, "window >= 0, split >= 1");
-  const size_t need = ana::schedule_workspace_bytes(M * 2 * K, num_players);
-  TORCH_CHECK((size_t)workspace.numel() >= need, "workspace too small: need ", need, " bytes");
-  auto h = std::make_shared<SchedPlanHandle>();
-  h->keep = {rec, link, deps, workspace};
-  check_hip(ana::schedule_plan(h->plan, (int)K, rec.data_ptr<int32_t>(), M, num_players,
-                               reinterpret_cast<uint32_t*>(link.data_ptr<int32_t>()), deps.data_ptr<int32_t>(),
-                               workspace.data_ptr<uint8_t>(), (size_t)workspace.numel(), (int)sort_nt, window,
-                               (int)split),
-            "schedule_plan");
-  return h;
 }
 
 // knobs (EngineConfig, config.py): [rate_idle, rate_local, rate_diag, rate_tight,
@@ -909,13 +862,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sort_pairs", &sort_pairs, "stable LSD radix sort of int32 (key, value) pairs (device)");
   m.def("levels", &levels, "K5 host levelizer: per-match conflict-free round (0 = stateless)");
   m.def("schedule", &schedule, "K5: per-slot occurrence index (chronological order per player)");
-  py::class_<SchedPlanHandle, std::shared_ptr<SchedPlanHandle>>(m, "SchedPlan")
-      .def_property_readonly("size", &SchedPlanHandle::size)
-      .def_property_readonly("costs", &SchedPlanHandle::costs, "estimated ms per op")
-      .def("run", &SchedPlanHandle::run, py::arg("lo"), py::arg("hi"), py::arg("stream") = 0,
-           "enqueue ops [lo, hi) on a HIP stream handle (0: the current stream)");
-  m.def("schedule_plan", &schedule_plan,
-        "K5: the device schedule prepass as a plan of launches, per-tile kernels split in `split` pieces");
   m.def("rate", &rate, "K1-K4/K6: exact dataflow rating of a stream");
   m.def("gen_event_counts", &gen_event_counts, "K8/K7: synthetic telemetry events per match");
   m.def("gen_events", &gen_events, "K8/K7: synthetic telemetry events (CSR by match)");

@@ -139,25 +139,15 @@ int64_t host_levels(int K, const int32_t* rec, int64_t M, int64_t P, int32_t* le
   }
 }
 
-int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps,
-                  int64_t win) {
-  if (K < 1 || K > 5) return -1;
-  if (win <= 0 || win > M) win = M;
-  const int64_t S = 2 * K;
-  for (int64_t a = 0; a < M; a += win) {  // each window on its own: local successor indices
-    const int64_t m = M - a < win ? M - a : win;
-    const int32_t* r = rec + a * (S + 2);
-    uint32_t* l = link + a * S;
-    int32_t* d = deps + a;
-    switch (K) {
-      case 1: schedule_k<1>(r, m, P, l, d); break;
-      case 2: schedule_k<2>(r, m, P, l, d); break;
-      case 3: schedule_k<3>(r, m, P, l, d); break;
-      case 4: schedule_k<4>(r, m, P, l, d); break;
-      case 5: schedule_k<5>(r, m, P, l, d); break;
-    }
+int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps) {
+  switch (K) {
+    case 1: schedule_k<1>(rec, M, P, link, deps); return 0;
+    case 2: schedule_k<2>(rec, M, P, link, deps); return 0;
+    case 3: schedule_k<3>(rec, M, P, link, deps); return 0;
+    case 4: schedule_k<4>(rec, M, P, link, deps); return 0;
+    case 5: schedule_k<5>(rec, M, P, link, deps); return 0;
+    default: return -1;
   }
-  return 0;
 }
 
 template <typename T, int K>

@@ -11,9 +11,7 @@ namespace ana {
 
 void host_gen_roster(const GenRosterParams& g, float* state, float* attrs);
 int host_gen_stream(int K, const GenStreamParams& g, int32_t* rec, int64_t M);
-// win > 0: consecutive windows of win matches, each scheduled on its own (launch_schedule)
-int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps,
-                  int64_t win = 0);
+int host_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps);
 // K5 levelizer: level[m] = 1 + max level of the previous matches of m's players
 // (1 for a player's first match), 0 for matches that touch no state.  Returns
 // the number of levels (conflict-free rounds).

@@ -4,10 +4,6 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#include <functional>
-#include <utility>
-#include <vector>
-
 #include <hip/hip_runtime_api.h>
 
 #include "common.h"
@@ -46,30 +42,7 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
                       uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
                       hipStream_t s, int32_t* deps = nullptr, uint32_t* ctrl = nullptr, int nz = 0,
-                      int32_t* epoch_bump = nullptr, int sort_nt = -1, uint32_t win = 0);
-// The schedule prepass as a plan: its dependent launches in stream order, each with a
-// cost estimate (ms), every per-tile kernel split into `split` tile-range launches
-// (radix_sort.hip build_sched_plan).  run(lo, hi) enqueues ops [lo, hi) -- a DP step
-// runs the next step's plan in pieces between its windows (runtime/engine.py).
-struct SchedPlan {
-  std::vector<std::function<void(hipStream_t)>> ops;
-  std::vector<double> cost;
-  void clear() {
-    ops.clear();
-    cost.clear();
-  }
-  void add(double c, std::function<void(hipStream_t)> f) {
-    cost.push_back(c);
-    ops.push_back(std::move(f));
-  }
-  int64_t size() const { return (int64_t)ops.size(); }
-  void run(int64_t lo, int64_t hi, hipStream_t s) const {
-    for (int64_t i = lo < 0 ? 0 : lo; i < hi && i < size(); ++i) ops[(size_t)i](s);
-  }
-};
-int build_sched_plan(SchedPlan& plan, int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
-                     uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link, int32_t* deps,
-                     uint32_t* ctrl, int nz, int32_t* epoch_bump, int sort_nt, uint32_t win, int split);
+                      int32_t* epoch_bump = nullptr, int sort_nt = -1);
 // Device levelizer (levels.hip): level[m] = 0 for a match without state, else
 // 1 + the largest level of its players' previous matches -- the exact-DP rounds --
 // as a dataflow over a fresh schedule (link, deps zeroed; deps are consumed).
@@ -82,17 +55,9 @@ int launch_levels(int K, const int32_t* rec, const uint32_t* link, int32_t* deps
 //       match is ready when its counter reaches the number of its players with
 //       kLinkHasPred, which the executor reads from the links)
 // overflow: zeroed (reserved for schedule error reporting)
-// win > 0 (< M): the stream is consecutive windows of win matches, each scheduled on
-//       its own (links cut at window boundaries, successors as indices inside their
-//       window) -- one prepass for the k windows of a DP step
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s,
-                    bool zero_ctrl = false, int32_t* epoch_bump = nullptr, int sort_nt = -1,
-                    int64_t win = 0);
-// The radix-path prepass of launch_schedule as a plan (SchedPlan) of dependent launches,
-// per-tile kernels split into `split` pieces; no control words, no epoch bump
-int schedule_plan(SchedPlan& plan, int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps,
-                  void* ws, size_t ws_bytes, int sort_nt, int64_t win, int split);
+                    bool zero_ctrl = false, int32_t* epoch_bump = nullptr, int sort_nt = -1);
 
 // out must be the packed layout (one row per match: [s_mu | s_sig | delta |
 // m_mu | m_sig][2K], quality, status byte), else hipErrorInvalidValue.

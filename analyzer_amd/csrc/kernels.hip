@@ -359,15 +359,12 @@ sched_hash_kernel(const int32_t* __restrict__ rec, int64_t M, uint32_t kend, uin
 
 int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link,
                     int32_t* deps, void* ws, size_t ws_bytes, uint32_t* overflow, hipStream_t s,
-                    bool zero_ctrl, int32_t* epoch_bump, int sort_nt, int64_t win) {
+                    bool zero_ctrl, int32_t* epoch_bump, int sort_nt) {
   // zero_ctrl: also zero the executor's control words (overflow = ctrl[0], ctrl[1..15]) for
   // a rate launch that follows on this stream and then skips its own zeroing dispatch
   const int nz = zero_ctrl ? 16 : 1;
   const int64_t n = M * 2 * K;
-  if (win >= M) win = 0;  // one window
-  if (win < 0) return (int)hipErrorInvalidValue;
-  // (sub-window cuts run on the radix path: DP steps are far above the micro-batch size)
-  if (n > 0 && n <= kSmallSched && win == 0 && P < 0x7fffffffLL && K >= 1 && K <= 5) {
+  if (n > 0 && n <= kSmallSched && P < 0x7fffffffLL && K >= 1 && K <= 5) {
     const int e = n <= 2048 ? 2 : n <= 4096 ? 4 : 8;  // elements per thread
     const char* small_e = getenv("ANA_SCHED_SMALL");  // per schedule (A/B in one process)
     const bool bitonic = small_e && small_e[0] == 'b';
@@ -409,24 +406,7 @@ int launch_schedule(int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* l
   uint32_t* keys_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   uint32_t* vals_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
   return launch_sched_sort(K, rec, M, (uint32_t)P, keys_a, vals_a, keys_b, vals_b, p, link, s, deps,
-                           overflow, nz, epoch_bump, sort_nt, (uint32_t)win);
-}
-
-int schedule_plan(SchedPlan& plan, int K, const int32_t* rec, int64_t M, int64_t P, uint32_t* link, int32_t* deps,
-                  void* ws, size_t ws_bytes, int sort_nt, int64_t win, int split) {
-  plan.clear();
-  const int64_t n = M * 2 * K;
-  if (win >= M) win = 0;
-  if (win < 0 || n <= 0 || n > kMaxSlots || P >= 0x7fffffffLL || K < 1 || K > 5) return (int)hipErrorInvalidValue;
-  if (ws_bytes < schedule_workspace_bytes(n, P)) return (int)hipErrorInvalidValue;
-  char* p = static_cast<char*>(ws);
-  uint32_t* keys_a = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
-  uint32_t* vals_a = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
-  uint32_t* keys_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
-  uint32_t* vals_b = reinterpret_cast<uint32_t*>(p); p += align_up(n * 4);
-  // (no control words: a plan runs beside other launches, never right before its own)
-  return build_sched_plan(plan, K, rec, M, (uint32_t)P, keys_a, vals_a, keys_b, vals_b, p, link, deps, nullptr, 0,
-                          nullptr, sort_nt, (uint32_t)win, split);
+                           overflow, nz, epoch_bump, sort_nt);
 }
 
 }  // namespace ana

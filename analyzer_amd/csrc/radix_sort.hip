@@ -70,19 +70,6 @@ __device__ __forceinline__ void st32(uint32_t* p, uint32_t v) {
   else *p = v;
 }
 
-// Sub-window cuts (DP steps, runtime/engine.py): one schedule over a step of k
-// windows of ``win`` matches each links only within a window -- a successor in a
-// later window is no successor, a predecessor in an earlier one no predecessor --
-// and names successors by their index inside the window, so window w's rating
-// launches over rows [w win, (w + 1) win) of rec / link / deps as if each window
-// had its own prepass.  win = 0: no cut (one window).
-__device__ __forceinline__ bool same_window(uint32_t a, uint32_t b, uint32_t win) {
-  return win == 0u || a / win == b / win;
-}
-__device__ __forceinline__ uint32_t in_window(uint32_t m, uint32_t win) {
-  return win == 0u ? m : m % win;
-}
-
 // exclusive scan of one value per thread over a 256-thread block
 __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t x, uint32_t* wsum,
                                                          uint32_t* total) {
@@ -157,15 +144,13 @@ struct SchedInit {
 template <int KS, int RB = 8, int NT = 0>
 __global__ void __launch_bounds__(kThreads)
 radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec, uint32_t kend,
-              int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles, SchedInit init = {},
-              int64_t t0 = 0, int64_t nt = -1) {
+              int64_t n, int shift, uint32_t* __restrict__ counts, int64_t tiles, SchedInit init = {}) {
   constexpr int kR = 1 << RB;
   __shared__ uint32_t hist[kWaves][kR];
   __shared__ uint32_t lkeys[KS > 0 ? kTile : 1];
   const int tid = threadIdx.x, wv = tid >> 6;
   for (int i = tid; i < kWaves * kR; i += kThreads) (&hist[0][0])[i] = 0u;
-  // tiles [t0, t0 + nt) of this launch (a prepass split into pieces, SchedPlan)
-  const int64_t tile = t0 + xcd_tile(nt < 0 ? tiles : nt);
+  const int64_t tile = xcd_tile(tiles);
   const int64_t base = tile * kTile;
   if constexpr (KS > 0) {
     if (init.deps) {  // the matches whose slots start in this tile (every match has its first slot in one)
@@ -173,7 +158,7 @@ radix_upsweep(const uint32_t* __restrict__ keys, const int32_t* __restrict__ rec
       const int64_t hi = base + kTile < n ? base + kTile : n;
       for (int64_t m = (base + S - 1) / S + tid; m < (hi + S - 1) / S; m += kThreads) init.deps[m] = 0;
     }
-    if (tile == 0) {
+    if (blockIdx.x == 0) {
       if (tid < init.nz) init.ctrl[tid] = 0u;
       if (tid == 0 && init.epoch_bump) init.epoch_bump[0] += 1;
     }
@@ -267,8 +252,7 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
                 const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
                 int64_t tiles, int slots_per_match, uint32_t* __restrict__ link,
                 uint32_t vlo = 0u, uint32_t vhi = 0xffffffffu, int bounds = 1,
-                RunEnds* __restrict__ bnd = nullptr, int nd = 0, uint32_t win = 0u,
-                int64_t t0 = 0, int64_t nt = -1) {
+                RunEnds* __restrict__ bnd = nullptr, int nd = 0) {
   constexpr int kR = 1 << RB;
   constexpr int DPT = kR >= kThreads ? kR / kThreads : 1;  // digits per thread in the scans
   static_assert(kR % kThreads == 0 || kThreads % kR == 0, "radix and block must divide");
@@ -279,7 +263,7 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
   __shared__ uint32_t gstart[kR];
   __shared__ uint32_t wsum[kWaves];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t tile = t0 + xcd_tile(nt < 0 ? tiles : nt);
+  const int64_t tile = xcd_tile(tiles);
   const int64_t base = tile * kTile;
   for (int i = tid; i < kWaves * kR; i += kThreads) (&wcnt[0][0])[i] = 0u;
   const bool local_ends = LINK && bnd != nullptr;  // uniform: no global digit offsets needed
@@ -389,14 +373,9 @@ radix_downsweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ v
           }
         }
         if (kk < kend && v >= vlo && v < vhi) {  // this part's slot range (link_parts)
-          const uint32_t m = v / (uint32_t)slots_per_match;
-          uint32_t w = kNoMatch;
-          if (!last && skey[i + 1] == kk) {
-            const uint32_t m2 = sval[i + 1] / (uint32_t)slots_per_match;
-            if (same_window(m, m2, win)) w = in_window(m2, win);
-          }
-          if (!first && skey[i - 1] == kk && same_window(sval[i - 1] / (uint32_t)slots_per_match, m, win))
-            w |= kLinkHasPred;
+          uint32_t w = (!last && skey[i + 1] == kk) ? sval[i + 1] / (uint32_t)slots_per_match
+                                                     : kNoMatch;
+          if (!first && skey[i - 1] == kk) w |= kLinkHasPred;
           // (non-temporal link stores alone measured 3.6 vs 1.6 ms per prepass: L2 write
           // combining of these random 4-B stores matters, profiles/r3/ab_link_nt.log)
           st32<NT>(link + v, w);
@@ -440,7 +419,7 @@ template <int RB = 8>
 __global__ void __launch_bounds__(kThreads)
 sched_fixup(const uint32_t* __restrict__ kout, const uint32_t* __restrict__ vout, int64_t n,
             uint32_t kend, const uint32_t* __restrict__ counts, const uint32_t* __restrict__ totals,
-            int64_t tiles, int slots_per_match, uint32_t* __restrict__ link, uint32_t win) {
+            int64_t tiles, int slots_per_match, uint32_t* __restrict__ link) {
   constexpr int kR = 1 << RB;
   __shared__ uint32_t wsum[kWaves];
   const int d = blockIdx.y;
@@ -461,12 +440,9 @@ sched_fixup(const uint32_t* __restrict__ kout, const uint32_t* __restrict__ vout
   if (c1 == c0) return;
   const int64_t of = (int64_t)dstart + c0, ol = (int64_t)dstart + c1 - 1;
   const uint32_t kf = kout[of], kl = kout[ol];
-  const uint32_t spm = (uint32_t)slots_per_match;
-  const bool pred = kf < kend && of > 0 && kout[of - 1] == kf &&
-                    same_window(vout[of - 1] / spm, vout[of] / spm, win);
-  const bool succ = kl < kend && ol + 1 < n && kout[ol + 1] == kl &&
-                    same_window(vout[ol] / spm, vout[ol + 1] / spm, win);
-  const uint32_t nxt = succ ? in_window(vout[ol + 1] / spm, win) : kNoMatch;
+  const bool pred = kf < kend && of > 0 && kout[of - 1] == kf;
+  const bool succ = kl < kend && ol + 1 < n && kout[ol + 1] == kl;
+  const uint32_t nxt = succ ? vout[ol + 1] / (uint32_t)slots_per_match : kNoMatch;
   if (of == ol) {
     if (kf < kend) link[vout[of]] = nxt | (pred ? kLinkHasPred : 0u);
     return;
@@ -509,7 +485,7 @@ sched_runs_last(const RunEnds* __restrict__ bnd, int64_t tiles, int nd, int32_t*
 
 __global__ void __launch_bounds__(kThreads)
 sched_runs_fixup(const RunEnds* __restrict__ bnd, int64_t tiles, int nd, const int32_t* __restrict__ seglast,
-                 uint32_t kend, int slots_per_match, uint32_t* __restrict__ link, uint32_t win) {
+                 uint32_t kend, int slots_per_match, uint32_t* __restrict__ link) {
   __shared__ int32_t wmax[kWaves];
   __shared__ int32_t carry_s;
   const int d = blockIdx.y, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -543,12 +519,10 @@ sched_runs_fixup(const RunEnds* __restrict__ bnd, int64_t tiles, int nd, const i
   if (!full || pred < 0 || me.kf >= kend) return;
   const RunEnds pr = bnd[(int64_t)pred * nd + d];
   if (pr.kl != me.kf) return;  // the key starts here: no earlier occurrence
-  const uint32_t spm = (uint32_t)slots_per_match;
-  if (!same_window(pr.vl / spm, me.vf / spm, win)) return;  // cut at a sub-window boundary
   // the two boundary links: each word gets its bits from one thread each (atomics on
   // disjoint fields, so a one-pair run that is both a first and a last is safe)
   atomicOr(&link[me.vf], kLinkHasPred);
-  atomicAnd(&link[pr.vl], ~kMatchMask | in_window(me.vf / spm, win));
+  atomicAnd(&link[pr.vl], ~kMatchMask | (me.vf / (uint32_t)slots_per_match));
 }
 
 }  // namespace
@@ -584,36 +558,14 @@ int launch_radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, 
 // both ends -- the first pass reads the records (no key array is written), the
 // last pass writes links instead of sorted pairs, then sched_fixup.  RB-bit
 // digits (8; 10 as an experiment).
-//
-// Built as a PLAN: the dependent launches in stream order, every per-tile kernel
-// (upsweeps, downsweeps, the link pass) split into ``split`` launches over tile
-// ranges, each op with a cost estimate (ms on MI355X, per 8192-slot tile, from the
-// config 2 kernel trace: profiles/r4/prof_config2_kernel_stats.txt).  split = 1 is
-// the one-shot prepass; a DP step runs its next step's plan in pieces, one in each
-// window's tail / merge gap (runtime/engine.py), so no window waits for a whole sort.
-namespace cost {
-constexpr double kUpFirst = 1.0e-5, kUp = 1.3e-5, kDownFirst = 4.0e-5, kDown = 3.1e-5, kLink = 1.15e-4;
-constexpr double kRowscan = 0.009, kRuns = 0.009, kFixup = 0.02;
-}  // namespace cost
-
 template <int K, int RB, int NT>
-static void sched_sort_k(SchedPlan& plan, const int32_t* rec, int64_t n, uint32_t kend, int bits, uint32_t* ka,
+static void sched_sort_k(const int32_t* rec, int64_t n, uint32_t kend, int bits, uint32_t* ka,
                          uint32_t* va, uint32_t* kb, uint32_t* vb, uint32_t* counts,
-                         int64_t tiles, uint32_t* link, const SchedInit& init, uint32_t win, int split) {
+                         int64_t tiles, uint32_t* link, const SchedInit& init, hipStream_t s) {
   constexpr int S = 2 * K;
   constexpr int kR = 1 << RB;
   uint32_t* totals = counts + tiles * kR;
-  const dim3 block(kThreads);
-  const int64_t chunks = split < 1 ? 1 : split > tiles ? tiles : split;
-  // one per-tile kernel as `chunks` launches over consecutive tile ranges
-  auto tiled = [&](double per_tile, auto launch) {
-    for (int64_t c = 0; c < chunks; ++c) {
-      const int64_t t0 = tiles * c / chunks, t1 = tiles * (c + 1) / chunks;
-      if (t1 <= t0) continue;
-      plan.add(per_tile * (double)(t1 - t0), [=](hipStream_t s) { launch(s, t0, t1 - t0); });
-    }
-  };
-  const SchedInit in = init;
+  const dim3 grid((unsigned)tiles), block(kThreads);
   const uint32_t *ki = nullptr, *vi = nullptr;
   uint32_t *ko = kb, *vo = vb;
   for (int shift = 0; shift < bits; shift += RB) {
@@ -626,72 +578,41 @@ static void sched_sort_k(SchedPlan& plan, const int32_t* rec, int64_t n, uint32_
       const int64_t nseg = (tiles + kThreads - 1) / kThreads;
       int32_t* seglast = reinterpret_cast<int32_t*>(bnd + tiles * nd);
       const int parts = link_parts(n);
-      for (int q = 0; q < parts; ++q) {
-        const uint32_t vlo = (uint32_t)(n * q / parts), vhi = (uint32_t)(n * (q + 1) / parts);
-        tiled(cost::kLink / parts, [=](hipStream_t s, int64_t t0, int64_t nt) {
-          hipLaunchKernelGGL((radix_downsweep<0, true, RB, NT>), dim3((unsigned)nt), block, 0, s, ki, vi, nullptr,
-                             kend, ko, vo, n, shift, counts, totals, tiles, S, link, vlo, vhi, q == 0 ? 1 : 0, bnd,
-                             nd, win, t0, nt);
-        });
-      }
+      for (int q = 0; q < parts; ++q)
+        hipLaunchKernelGGL((radix_downsweep<0, true, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo,
+                           n, shift, counts, totals, tiles, S, link, (uint32_t)(n * q / parts),
+                           (uint32_t)(n * (q + 1) / parts), q == 0 ? 1 : 0, bnd, nd);
       const dim3 sgrid((unsigned)nseg, (unsigned)nd);
-      plan.add(cost::kRuns, [=](hipStream_t s) {
-        hipLaunchKernelGGL(sched_runs_last, sgrid, block, 0, s, bnd, tiles, nd, seglast);
-      });
-      plan.add(cost::kRuns, [=](hipStream_t s) {
-        hipLaunchKernelGGL(sched_runs_fixup, sgrid, block, 0, s, bnd, tiles, nd, seglast, kend, S, link, win);
-      });
+      hipLaunchKernelGGL(sched_runs_last, sgrid, block, 0, s, bnd, tiles, nd, seglast);
+      hipLaunchKernelGGL(sched_runs_fixup, sgrid, block, 0, s, bnd, tiles, nd, seglast, kend, S, link);
       break;
     }
     if (first)
-      tiled(cost::kUpFirst, [=](hipStream_t s, int64_t t0, int64_t nt) {
-        hipLaunchKernelGGL((radix_upsweep<K, RB, NT>), dim3((unsigned)nt), block, 0, s, nullptr, rec, kend, n, shift,
-                           counts, tiles, in, t0, nt);
-      });
+      hipLaunchKernelGGL((radix_upsweep<K, RB, NT>), grid, block, 0, s, nullptr, rec, kend, n, shift, counts, tiles,
+                         init);
     else
-      tiled(cost::kUp, [=](hipStream_t s, int64_t t0, int64_t nt) {
-        hipLaunchKernelGGL((radix_upsweep<0, RB, NT>), dim3((unsigned)nt), block, 0, s, ki, nullptr, kend, n, shift,
-                           counts, tiles, SchedInit{}, t0, nt);
-      });
-    plan.add(cost::kRowscan, [=](hipStream_t s) {
-      hipLaunchKernelGGL(radix_rowscan, dim3(kR), block, 0, s, counts, tiles, totals);
-    });
+      hipLaunchKernelGGL((radix_upsweep<0, RB, NT>), grid, block, 0, s, ki, nullptr, kend, n, shift, counts, tiles);
+    hipLaunchKernelGGL(radix_rowscan, dim3(kR), block, 0, s, counts, tiles, totals);
     const int parts = last ? link_parts(n) : 1;
-    for (int q = 0; q < parts; ++q) {
-      const uint32_t vlo = (uint32_t)(n * q / parts), vhi = (uint32_t)(n * (q + 1) / parts);
-      const int bounds = q == 0 ? 1 : 0;
-      if (first && last)
-        tiled(cost::kLink / parts, [=](hipStream_t s, int64_t t0, int64_t nt) {
-          hipLaunchKernelGGL((radix_downsweep<K, true, RB, NT>), dim3((unsigned)nt), block, 0, s, nullptr, nullptr,
-                             rec, kend, ko, vo, n, shift, counts, totals, tiles, S, link, vlo, vhi, bounds, nullptr, 0,
-                             win, t0, nt);
-        });
-      else if (first)
-        tiled(cost::kDownFirst, [=](hipStream_t s, int64_t t0, int64_t nt) {
-          hipLaunchKernelGGL((radix_downsweep<K, false, RB, NT>), dim3((unsigned)nt), block, 0, s, nullptr, nullptr,
-                             rec, kend, ko, vo, n, shift, counts, totals, tiles, S, nullptr, 0u, 0xffffffffu, 1,
-                             nullptr, 0, 0u, t0, nt);
-        });
-      else if (last)
-        tiled(cost::kLink / parts, [=](hipStream_t s, int64_t t0, int64_t nt) {
-          hipLaunchKernelGGL((radix_downsweep<0, true, RB, NT>), dim3((unsigned)nt), block, 0, s, ki, vi, nullptr,
-                             kend, ko, vo, n, shift, counts, totals, tiles, S, link, vlo, vhi, bounds, nullptr, 0,
-                             win, t0, nt);
-        });
-      else
-        tiled(cost::kDown, [=](hipStream_t s, int64_t t0, int64_t nt) {
-          hipLaunchKernelGGL((radix_downsweep<0, false, RB, NT>), dim3((unsigned)nt), block, 0, s, ki, vi, nullptr,
-                             kend, ko, vo, n, shift, counts, totals, tiles, S, nullptr, 0u, 0xffffffffu, 1, nullptr,
-                             0, 0u, t0, nt);
-        });
-    }
-    if (last) {
-      const dim3 fgrid((unsigned)((tiles + kThreads - 1) / kThreads), kR);
-      plan.add(cost::kFixup, [=](hipStream_t s) {
-        hipLaunchKernelGGL((sched_fixup<RB>), fgrid, block, 0, s, ko, vo, n, kend, counts, totals, tiles, S, link,
-                           win);
-      });
-    }
+    if (first && last)
+      for (int q = 0; q < parts; ++q)
+        hipLaunchKernelGGL((radix_downsweep<K, true, RB, NT>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
+                           vo, n, shift, counts, totals, tiles, S, link, (uint32_t)(n * q / parts),
+                           (uint32_t)(n * (q + 1) / parts), q == 0 ? 1 : 0);
+    else if (first)
+      hipLaunchKernelGGL((radix_downsweep<K, false, RB, NT>), grid, block, 0, s, nullptr, nullptr, rec, kend, ko,
+                         vo, n, shift, counts, totals, tiles, S, nullptr);
+    else if (last)
+      for (int q = 0; q < parts; ++q)
+        hipLaunchKernelGGL((radix_downsweep<0, true, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo,
+                           n, shift, counts, totals, tiles, S, link, (uint32_t)(n * q / parts),
+                           (uint32_t)(n * (q + 1) / parts), q == 0 ? 1 : 0);
+    else
+      hipLaunchKernelGGL((radix_downsweep<0, false, RB, NT>), grid, block, 0, s, ki, vi, nullptr, kend, ko, vo, n,
+                         shift, counts, totals, tiles, S, nullptr);
+    if (last)
+      hipLaunchKernelGGL((sched_fixup<RB>), dim3((unsigned)((tiles + kThreads - 1) / kThreads), kR), block,
+                         0, s, ko, vo, n, kend, counts, totals, tiles, S, link);
     ki = ko;
     vi = vo;
     ko = ko == kb ? ka : kb;
@@ -699,10 +620,10 @@ static void sched_sort_k(SchedPlan& plan, const int32_t* rec, int64_t n, uint32_
   }
 }
 
-int build_sched_plan(SchedPlan& plan, int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
-                     uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link, int32_t* deps,
-                     uint32_t* ctrl, int nz, int32_t* epoch_bump, int sort_nt, uint32_t win, int split) {
-  plan.clear();
+int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
+                      uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
+                      hipStream_t s, int32_t* deps, uint32_t* ctrl, int nz, int32_t* epoch_bump,
+                      int sort_nt) {
   const int64_t n = M * 2 * K;
   if (n <= 0) return 0;
   if (n > kMaxSlots) return (int)hipErrorInvalidValue;
@@ -727,29 +648,17 @@ int build_sched_plan(SchedPlan& plan, int K, const int32_t* rec, int64_t M, uint
   const int nt = nt_e ? atoi(nt_e) : sort_nt >= 0 ? sort_nt : 0;
   const bool wide = bits <= 20 && rb_env == 10;
   switch (K) {
-#define ANA_SORT_CASE(k)                                                                                        \
-  case k:                                                                                                       \
-    if (wide) sched_sort_k<k, 10, 0>(plan, rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, win, split); \
-    else if (nt == 1) sched_sort_k<k, 8, 1>(plan, rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, win, split); \
-    else if (nt == 2) sched_sort_k<k, 8, 2>(plan, rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, win, split); \
-    else sched_sort_k<k, 8, 0>(plan, rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, win, split); \
+#define ANA_SORT_CASE(k)                                                                         \
+  case k:                                                                                        \
+    if (wide) sched_sort_k<k, 10, 0>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    else if (nt == 1) sched_sort_k<k, 8, 1>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    else if (nt == 2) sched_sort_k<k, 8, 2>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
+    else sched_sort_k<k, 8, 0>(rec, n, num_players, bits, ka, va, kb, vb, counts, tiles, link, init, s); \
     break;
     ANA_SORT_CASE(1) ANA_SORT_CASE(2) ANA_SORT_CASE(3) ANA_SORT_CASE(4) ANA_SORT_CASE(5)
 #undef ANA_SORT_CASE
     default: return (int)hipErrorInvalidValue;
   }
-  return 0;
-}
-
-int launch_sched_sort(int K, const int32_t* rec, int64_t M, uint32_t num_players, uint32_t* ka,
-                      uint32_t* va, uint32_t* kb, uint32_t* vb, void* ws, uint32_t* link,
-                      hipStream_t s, int32_t* deps, uint32_t* ctrl, int nz, int32_t* epoch_bump,
-                      int sort_nt, uint32_t win) {
-  SchedPlan plan;
-  const int rc = build_sched_plan(plan, K, rec, M, num_players, ka, va, kb, vb, ws, link, deps, ctrl, nz, epoch_bump,
-                                  sort_nt, win, 1);
-  if (rc) return rc;
-  plan.run(0, plan.size(), s);
   return (int)hipGetLastError();
 }
 

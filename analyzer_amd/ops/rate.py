@@ -260,8 +260,7 @@ class BatchRater:
     # ------------------------------------------------------------- schedule
     def schedule(self, rec: torch.Tensor, K: int, num_players: int,
                  tag: str = "", zero_ctrl: bool = False,
-                 epoch_bump: Optional[torch.Tensor] = None, sort_nt: int = -1,
-                 window: int = 0) -> Schedule:
+                 epoch_bump: Optional[torch.Tensor] = None, sort_nt: int = -1) -> Schedule:
         """Dependency structure of a window (K5): per slot the match of its
         player's next occurrence and whether it occurred earlier (``link``), and
         per match the completion counter ``deps`` (see ``Schedule``).  The device
@@ -273,11 +272,7 @@ class BatchRater:
         launch may be using them.  ``epoch_bump``: a device int32 launch epoch
         (graph replays) the schedule increments, saving the bump its own dispatch.
         ``sort_nt``: non-temporal accesses of the radix sort (0 none, 1 all, 2 loads
-        only; -1: ANA_SORT_NT or none) -- ANA_SORT_NT, when set, wins.
-        ``window`` > 0: ``rec`` is consecutive windows of that many matches, each
-        scheduled on its own -- links cut at window boundaries, successors as indices
-        inside their window -- so ``window_schedule(s, w, window)`` is window w's own
-        schedule: one prepass for the k windows of a DP step (runtime/engine.py)."""
+        only; -1: ANA_SORT_NT or none) -- ANA_SORT_NT, when set, wins."""
         M = rec.shape[0]
         dev = rec.device
         link = self._buffer(dev, "link" + tag, M * 2 * K, torch.int32).view(M, 2 * K)
@@ -291,30 +286,8 @@ class BatchRater:
             ctrl = torch.empty(0, dtype=torch.int32)
         bump = epoch_bump.data_ptr() if epoch_bump is not None and rec.is_cuda else 0
         native().schedule(rec, K, num_players, link, deps, ws, ctrl, bool(zero_ctrl and rec.is_cuda),
-                          bump, int(sort_nt), int(window))
+                          bump, int(sort_nt))
         return Schedule(link, deps)
-
-    def schedule_plan(self, rec: torch.Tensor, K: int, num_players: int, tag: str = "",
-                      window: int = 0, split: int = 1, sort_nt: int = -1):
-        """The device prepass of ``schedule(rec, ..., window=window)`` as a plan of
-        launches (csrc/kernels.h SchedPlan: ``size``, ``costs`` in estimated ms,
-        ``run(lo, hi, stream)``), its per-tile kernels split into ``split`` tile
-        ranges, so a DP step can run its next step's prepass in pieces between its
-        windows (runtime/engine.py).  Nothing is enqueued here.  Returns (plan,
-        Schedule of the buffers the plan fills)."""
-        M = rec.shape[0]
-        dev = rec.device
-        link = self._buffer(dev, "link" + tag, M * 2 * K, torch.int32).view(M, 2 * K)
-        deps = self._buffer(dev, "deps" + tag, M, torch.int32)
-        ws = self._buffer(dev, "sched_ws", native().schedule_workspace_bytes(M * 2 * K, num_players), torch.uint8)
-        plan = native().schedule_plan(rec, K, num_players, link, deps, ws, int(sort_nt), int(window), int(split))
-        return plan, Schedule(link, deps)
-
-    @staticmethod
-    def window_schedule(schedule: Schedule, w: int, window: int) -> Schedule:
-        """Window w of a schedule made with ``window``: its rows of link / deps."""
-        lo, hi = w * window, min((w + 1) * window, schedule.deps.shape[0])
-        return Schedule(schedule.link[lo:hi], schedule.deps[lo:hi])
 
     # ----------------------------------------------------------------- rate
     def rate(self, roster: Roster, rec: torch.Tensor, K: Optional[int] = None,

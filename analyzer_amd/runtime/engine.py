@@ -57,7 +57,6 @@ class Prepared:
     schedule: Optional[Schedule]
     ready: Optional[torch.cuda.Event]
     buffer_set: int = 0
-    window: int = 0  # > 0: rec is consecutive windows of this many matches (one prepass, step_windows)
 
 
 class WindowPipeline:
@@ -198,15 +197,13 @@ class WindowPipeline:
         native().warm_rows(self.roster.state, self._warm_sink)
 
     def prepare(self, rec: torch.Tensor,
-                produced: Optional[torch.cuda.Event] = None, stream=None, window: int = 0) -> Prepared:
+                produced: Optional[torch.cuda.Event] = None, stream=None) -> Prepared:
         """Enqueue the schedule prepass of ``rec`` on the side stream (or ``stream``),
         after the tail of the last enqueued rate launch (tail overlap) and after
         ``produced`` (default: everything enqueued on the main stream so far,
-        which is where ``rec`` was made).  ``window`` > 0: ``rec`` holds consecutive
-        windows of that many matches, scheduled by ONE prepass with links cut at the
-        window boundaries (BatchRater.schedule) -- ``step_windows`` rates them."""
+        which is where ``rec`` was made)."""
         if not self.cuda:
-            return Prepared(rec, None, None, window=int(window))
+            return Prepared(rec, None, None)
         tag = "_set%d" % self._set
         main = torch.cuda.current_stream(self.device)
         side = self.side if stream is None else stream
@@ -221,13 +218,12 @@ class WindowPipeline:
                 native().stream_wait_value64(side.cuda_stream, self._signal, self._seq)
             if self._free[self._set] is not None:  # previous user of this buffer set is done
                 side.wait_event(self._free[self._set])
-            sched = self.rater.schedule(rec, self.K, self.roster.num_players, tag=tag, sort_nt=self.sort_nt,
-                                        window=int(window))
+            sched = self.rater.schedule(rec, self.K, self.roster.num_players, tag=tag, sort_nt=self.sort_nt)
             ready = torch.cuda.Event()
             ready.record(side)
         used = self._set
         self._set ^= 1
-        return Prepared(rec, sched, ready, used, int(window))
+        return Prepared(rec, sched, ready, used)
 
     def rate(self, prep: Prepared, out: Optional[RateResult] = None, check: bool = False,
              telemetry=None, overlap: Optional[Callable[[], None]] = None) -> RateResult:
@@ -310,112 +306,6 @@ class WindowPipeline:
         res = self.rate(prep, **rate_kwargs)
         nxt = self.prepare(next_rec, produced=produced) if next_rec is not None else None
         return res, nxt
-
-    def windows_of(self, prep: Prepared):
-        """The windows of a multi-window ``Prepared`` (``prepare(window=...)``), each
-        with its rows of the one schedule; the first carries the prepass's event."""
-        M = int(prep.rec.shape[0])
-        W = prep.window if prep.window > 0 else M
-        out = []
-        for w, lo in enumerate(range(0, M, W)):
-            hi = min(lo + W, M)
-            sched = BatchRater.window_schedule(prep.schedule, w, W) if prep.schedule is not None else None
-            out.append(Prepared(prep.rec[lo:hi], sched, prep.ready if w == 0 else None, prep.buffer_set))
-        return out
-
-    @staticmethod
-    def pieces(costs, k: int):
-        """Split a plan's ops (in order) into k consecutive ranges of about equal
-        estimated cost: [(lo, hi)] * k (empty ranges allowed)."""
-        cum = [0.0]
-        for c in costs:
-            cum.append(cum[-1] + float(c))
-        total = cum[-1]
-        out, lo = [], 0
-        for j in range(k):
-            if j == k - 1:
-                hi = len(costs)
-            else:  # the cut closest to the j-th share boundary (cum is monotone)
-                target = total * (j + 1) / k
-                hi = lo
-                while hi < len(costs) and cum[hi + 1] <= target:
-                    hi += 1
-                if hi < len(costs) and target - cum[hi] > cum[hi + 1] - target:
-                    hi += 1
-            out.append((lo, hi))
-            lo = hi
-        return out
-
-    def step_windows(self, prep: Prepared, next_rec: Optional[torch.Tensor], pieces: Optional[bool] = None,
-                     **rate_kwargs):
-        """Rate every window of a multi-window ``prep`` in order (with the DP merge
-        after each) and prepare ``next_rec`` (same window size) with ONE prepass: a
-        DP step of k windows pays one 10M-slot sort instead of k short ones.
-
-        ``pieces`` (default: the device, ``ANA_PREPASS_PIECES`` != 0): the next step's
-        prepass is a plan of launches (BatchRater.schedule_plan) cut into k pieces of
-        about equal cost, and piece w runs on the side stream from the tail of window
-        w's rating (tail placement: the rating's progress signal) or from its end
-        (serial placement), beside window w's merge; window w+1's rating waits for
-        it.  So the sort fills the executors' drains and the merge gaps instead of
-        standing between two windows.  Otherwise the whole prepass runs where ``step``
-        would put it: beside the last window's merge (serial) or from its rating's
-        tail.  Returns (last result, prepared next step or None)."""
-        subs = self.windows_of(prep)
-        produced = None
-        if self.cuda and next_rec is not None:
-            produced = torch.cuda.Event()
-            produced.record(torch.cuda.current_stream(self.device))
-        if pieces is None:
-            pieces = self.ecfg.prepass_pieces
-        if pieces and self.cuda and next_rec is not None and len(subs) > 1:
-            return self._step_pieces(subs, prep.window, next_rec, produced, **rate_kwargs)
-        res = None
-        for w, sub in enumerate(subs):
-            last = w == len(subs) - 1
-            if last and self.serial and self.merger is not None and self.cuda and next_rec is not None:
-                held: List[Prepared] = []
-                res = self.rate(sub, overlap=lambda: held.append(
-                    self.prepare(next_rec, produced=self._rated, stream=self.merge_side,
-                                 window=prep.window)), **rate_kwargs)
-                return res, held[0]
-            res = self.rate(sub, **rate_kwargs)
-        nxt = self.prepare(next_rec, produced=produced, window=prep.window) if next_rec is not None else None
-        return res, nxt
-
-    def _step_pieces(self, subs, window: int, next_rec: torch.Tensor, produced, **rate_kwargs):
-        """step_windows with the next step's prepass in k pieces (see there)."""
-        main = torch.cuda.current_stream(self.device)
-        side = self.merge_side if self.serial and self.merge_side is not None else self.side
-        tag = "_set%d" % self._set
-        used = self._set
-        self._set ^= 1
-        side.wait_event(produced)
-        if self._free[used] is not None:  # the previous user of this buffer set is done
-            side.wait_event(self._free[used])
-        # per-tile kernels in 4k tile ranges (at most 32: launches cost host time),
-        # so a piece lands within ~1/4 of a kernel's share of its target
-        plan, sched = self.rater.schedule_plan(next_rec, self.K, self.roster.num_players, tag=tag,
-                                               window=window, split=min(4 * len(subs), 32),
-                                               sort_nt=self.sort_nt)
-        ranges = self.pieces(plan.costs, len(subs))
-        res, done = None, None
-        from ..ops.native import native
-
-        for w, sub in enumerate(subs):
-            res = self.rate(sub, **rate_kwargs)
-            lo, hi = ranges[w]
-            with trace_range("schedule_piece", window=self.windows_rated, ops=hi - lo):
-                if self._signal and self._seq > 0:  # from the tail of this window's rating
-                    native().stream_wait_value64(side.cuda_stream, self._signal, self._seq)
-                else:                               # from its end (serial placement)
-                    side.wait_event(self._rated)
-                plan.run(lo, hi, side.cuda_stream)
-                done = torch.cuda.Event()
-                done.record(side)
-            main.wait_event(done)  # the next window's rating never co-runs with a piece
-        self._plans = plan  # keep the plan's launches alive until the next step
-        return res, Prepared(next_rec, sched, done, used, int(window))
 
     def results_ready(self, res: Optional[RateResult]) -> None:
         """Make ``res``'s records final before a consumer reads them: the DP merge

@@ -108,12 +108,6 @@ def parse(argv=None):
                          "operands at GBps bus bandwidth (+ us latency, default 25) and streams the buffer "
                          "on 16 CUs as RCCL's channels do -- a one-GPU projection of the N-GPU step "
                          "(parallel/sweep.py emulate); the prepass placement follows the modelled time")
-    ap.add_argument("--step-prepass", type=int, default=-1, choices=[-1, 0, 1],
-                    help="merges per step > 1: 1 = ONE schedule prepass per step over its k windows "
-                         "(links cut at the window boundaries, runtime/engine.py step_windows; whole or in "
-                         "pieces between the windows, ANA_PREPASS_PIECES), 0 = a prepass per window in the "
-                         "rating's tail; -1 = auto = 0: the per-window tail prepass measured fastest, k = 8 "
-                         "forced merges 11.5 vs 11.8 (whole) / 12.9 ms (pieces; profiles/r5/dp_step_price.log)")
     ap.add_argument("--force-merge", action="store_true",
                     help="N = 1: run the merge kernels after every window anyway (messages + decode, "
                          "no collective) -- prices the DP merge's device work against --merges-per-step")
@@ -257,20 +251,10 @@ def main(argv=None) -> int:
     Mw = M // sub                        # matches per window and GPU
     roster = make_roster(RosterSpec(num_players=P, seed=args.seed), device=dev)
     spec = StreamSpec(team_size=K, seed=args.seed + 1, skew=args.skew)
-    # one prepass per step over its k windows (engine.step_windows) -- the unit of the
-    # timed loop is then a step, not a window
-    step_prepass = sub > 1 and args.config != 4 and (
-        args.step_prepass == 1)
     n_windows = max(1, min(args.ring, (args.steps + args.warmup) * sub))
     total_windows = (args.steps + args.warmup) * sub
-    if step_prepass:  # a ring of whole steps: window w of rank r as before, k windows per step
-        n_windows = max(1, min(args.ring, args.steps + args.warmup))
-        total_windows = args.steps + args.warmup
-        windows = [torch.cat([make_stream(spec, Mw, P, K=K, base=((s * sub + i) * world + rank) * Mw,
-                                          device=dev) for i in range(sub)]) for s in range(n_windows)]
-    else:
-        windows = [make_stream(spec, Mw, P, K=K, base=(w * world + rank) * Mw, device=dev)
-                   for w in range(n_windows)]
+    windows = [make_stream(spec, Mw, P, K=K, base=(w * world + rank) * Mw, device=dev)
+               for w in range(n_windows)]
     rater = BatchRater()
     if args.telemetry_mode == "fused":
         rater.tele_fuse_max = 1 << 62  # inline at any launch size
@@ -319,10 +303,10 @@ def main(argv=None) -> int:
     # (parallel/sweep.py defer): records double-buffered, so window i+1's rating
     # writes the other buffer (a consumer streams the records out of the idle one)
     outs = [out, RateResult.allocate(Mw, K, dev)] if merger is not None and merger.correct and \
-        merger.defer and not step_prepass else [out]
+        merger.defer else [out]
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     sync()
-    prepared = {0: pipe.prepare(windows[0], window=Mw if step_prepass else 0)}
+    prepared = {0: pipe.prepare(windows[0])}
 
     tstream = None
     ttail = None
@@ -346,9 +330,6 @@ def main(argv=None) -> int:
         # rate window i, then the prepass of window i+1 on the side stream behind
         # its tail (every timed step carries exactly one prepass and one rating)
         nxt = windows[(i + 1) % n_windows]
-        if step_prepass:  # step i: its k windows with a merge after each, then step i+1's prepass
-            _, prepared[i + 1] = pipe.step_windows(prepared.pop(i), nxt, out=out)
-            return
         if ttail is not None:
             # the telemetry of window i beside the tail of its rating and the next
             # prepass; rating i + 1 waits for it (no co-run with a full executor)
@@ -381,7 +362,7 @@ def main(argv=None) -> int:
             _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out,
                                            telemetry=(t.evoff, t.events, stats))
 
-    per = 1 if step_prepass else sub  # loop units per step
+    per = sub  # loop units (windows) per step
     for i in range(args.warmup * per):
         step(i)
     pipe.finish()
@@ -425,9 +406,7 @@ def main(argv=None) -> int:
                     # where the next window's prepass ran: beside the merge (serial) or in
                     # the rating's tail; chosen from a timed all-reduce for N > 1
                     "prepass_placement": "beside the merge" if pipe.serial else "rating tail %.2f" % pipe.tail,
-                    "allreduce_probe_ms": pipe.allreduce_probe_ms,
-                    # one schedule prepass per step over its k windows, or one per window
-                    "prepass_per": "step" if step_prepass else "window"}
+                    "allreduce_probe_ms": pipe.allreduce_probe_ms}
     if merger is not None:
         merger.check()  # a clamped merge decode fails the run, as the executor's flags do
     flags = rater.sticky_flags(dev).cpu()

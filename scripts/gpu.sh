@@ -37,7 +37,7 @@
 #   workersql  the worker on the reflected SQLAlchemy store (columnar batch path), sqlite file
 #   dpacc      sweep-DP accuracy table (ranks x merges per step) incl. per-participant records
 #   dpcost     one-GPU DP step price: plain vs forced merges at k = 8 / 16
-#   dpstep     the same with one prepass per step (tail / serial placement, k = 8 / 16 / 32)
+#   dpstep     forced-merge step price: record correction on / off, tail / serial placement, emulated N = 8
 #   dpconf     gloo rehearsals of config 3 (N = 4) and config 5 (N = 2)
 #   project    one-GPU projection of the N = 2 / 4 / 8 DP step (emulated all-reduce, bus bandwidth sweep)
 #   corrmicro  the record correction kernel alone + a kernel trace of the k = 8 DP step
@@ -278,9 +278,8 @@ EOF
       done
       for f in gpurun_out/dpcost/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
       ;;
-    dpstep)  # one-GPU DP step price: plain vs forced merges (DPSTEP_K), one prepass per step in pieces (default),
-             # whole, or per window; record correction on (default) / off; serial placement; N = 8 projected with
-             # the all-reduce stand-in (8 ranks, 300 GB/s bus bandwidth); interleaved rounds
+    dpstep)  # one-GPU DP step price: plain vs forced merges (DPSTEP_K); record correction on (default) / off;
+             # serial placement; N = 8 projected with the all-reduce stand-in (8 ranks, 300 GB/s); interleaved rounds
       for r in 1 2; do
         run dpstep/plain_$r 300 $PY bench.py --steps 10 --warmup 2
         for k in ${DPSTEP_K:-8 16}; do
@@ -289,10 +288,6 @@ EOF
           ANA_DP_CORRECT_RECORDS=0 run dpstep/k${k}_window_nocorr_$r 300 $PY bench.py $A
           ANA_PREPASS_SERIAL=1 run dpstep/k${k}_window_serial_$r 300 $PY bench.py $A
           run dpstep/k${k}_emu8_$r 300 $PY bench.py $A --emulate-allreduce 8:300
-          if [ -n "${DPSTEP_ALL:-}" ]; then
-            run dpstep/k${k}_pieces_$r 300 $PY bench.py $A --step-prepass 1
-            ANA_PREPASS_PIECES=0 run dpstep/k${k}_whole_$r 300 $PY bench.py $A --step-prepass 1
-          fi
         done
       done
       for f in gpurun_out/dpstep/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done

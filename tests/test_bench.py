@@ -116,7 +116,7 @@ def test_multi_rank_json_contract_on_cpu(tmp_path, n):
     assert j["config"]["parallelism"] == "dp%d" % n and j["config"]["merges_per_step"] == k
     assert j["value"] == pytest.approx(n * 1000 * n / (j["ms_per_step"] / 1000.0))
     mm = j["merge_ms"]
-    assert mm["prepass_placement"] and mm["prepass_per"] in ("step", "window") and mm["buckets"] >= 1
+    assert mm["prepass_placement"] and mm["buckets"] >= 1
     acc = j["accuracy"]
     for key in ("records_dmu_median", "records_dmu_p99", "records_dmu_max", "spearman_mu_minus_sigma"):
         assert acc[key] is not None, key

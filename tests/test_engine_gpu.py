@@ -99,66 +99,6 @@ def test_schedule_run_table_matches_host(gpu_device, P, M, K, skew, runs, rb, mo
     assert int(deps_d.abs().sum()) == 0
 
 
-@pytest.mark.parametrize("P,M,K,W,skew,runs", [(20, 3000, 3, 700, 1, "1"), (100_000, 1_000_000, 3, 125_000, 1, "1"),
-                                               (100_000, 1_000_000, 3, 125_000, 1, "0"),
-                                               (50_000, 600_000, 5, 37_500, 3, "1"), (200, 20_000, 1, 3_001, 1, "1")])
-def test_window_cut_schedule_matches_per_window_host(gpu_device, P, M, K, W, skew, runs, monkeypatch):
-    """One prepass over k windows (``window``: links cut at the window boundaries,
-    successors as indices inside their window; both last-pass paths) gives every
-    window exactly the schedule of its own prepass: device vs the host mirror run per
-    window, including a ragged last window and hot players whose runs cross windows."""
-    monkeypatch.setenv("ANA_SCHED_RUNS", runs)
-    rec = make_stream(StreamSpec(team_size=K, seed=P + W, skew=skew, p_afk=0.05), M, P, K=K)
-    br = R.BatchRater()
-    link_d, deps_d = br.schedule(rec.to(gpu_device), K, P, window=W)
-    link_d, deps_d = link_d.cpu().numpy(), deps_d.cpu()
-    assert int(deps_d.abs().sum()) == 0
-    slots, first = _stateful_slots(rec.numpy(), K, P)
-    for lo in range(0, M, W):
-        hi = min(lo + W, M)
-        link_h, deps_h = br.schedule(rec[lo:hi], K, P)
-        s = slots[lo:hi]
-        np.testing.assert_array_equal(link_d[lo:hi][s], link_h.numpy()[s])
-        need = (first[lo:hi] & ((link_d[lo:hi] & R.Schedule.HAS_PRED) != 0)).sum(1)
-        rated = s.any(1)
-        np.testing.assert_array_equal(need[rated], deps_h.numpy()[rated])
-
-
-@pytest.mark.parametrize("mode", ["pieces", "whole", "pieces_serial"])
-def test_step_windows_rate_like_separate_windows(gpu_device, monkeypatch, mode):
-    """WindowPipeline.step_windows (one prepass per step of k windows; the next
-    step's prepass whole or in k pieces in the windows' tails / merge gaps, tail or
-    serial placement) rates exactly what windows with a prepass each rate: roster and
-    the last window's records bit for bit over two steps, DP merges between the
-    windows included (forced, one rank)."""
-    from analyzer_amd.parallel.sweep import SweepMerger
-    from analyzer_amd.runtime.engine import WindowPipeline
-
-    monkeypatch.setenv("ANA_PREPASS_PIECES", "0" if mode == "whole" else "1")
-    if mode == "pieces_serial":
-        monkeypatch.setenv("ANA_PREPASS_SERIAL", "1")
-    P, K, k, Mw = 40_000, 3, 4, 60_000
-    rec = make_stream(StreamSpec(team_size=K, seed=91), 2 * k * Mw, P, K=K, device=gpu_device)
-    steps = [rec[:k * Mw], rec[k * Mw:]]
-    outs = []
-    for step_mode in (False, True):
-        ro = make_roster(RosterSpec(num_players=P, seed=92), device=gpu_device)
-        merger = SweepMerger(P, gpu_device, comm_dtype="bf16", force=True)
-        pipe = WindowPipeline(R.BatchRater(), ro, K, merger=merger)
-        out = R.RateResult.allocate(Mw, K, gpu_device)
-        if step_mode:
-            _, nxt = pipe.step_windows(pipe.prepare(steps[0], window=Mw), steps[1], out=out)
-            pipe.step_windows(nxt, None, out=out)
-        else:
-            pipe.run([rec[w * Mw:(w + 1) * Mw] for w in range(2 * k)], out=out)
-        torch.cuda.synchronize()
-        outs.append((ro.state.view(torch.int32).cpu()[:, 0::2],
-                     [getattr(out, f).cpu() for f in R.RateResult.FIELDS]))
-    assert torch.equal(outs[0][0], outs[1][0])
-    for a, b in zip(outs[0][1], outs[1][1]):
-        assert torch.equal(a.contiguous().view(torch.uint8), b.contiguous().view(torch.uint8))
-
-
 @pytest.mark.parametrize("P,M,K", [(20, 3000, 3), (70_000, 400_000, 3), (17_000_000, 300_000, 5)])
 def test_schedule_link_parts_match_host(gpu_device, P, M, K, monkeypatch):
     """The link pass split into slot-range parts (ANA_LINK_PARTS; automatic above

@@ -179,47 +179,3 @@ def test_warm_rows_host_is_a_no_op():
     with pytest.raises(RuntimeError):
         native().warm_rows(roster.state, torch.zeros(8, dtype=torch.int32))
 
-
-def test_window_cut_schedule_host():
-    """``schedule(window=W)``: every window of W matches gets its own schedule --
-    links cut at the boundaries, successors as indices inside the window -- which is
-    what the device's one-prepass-per-DP-step schedule must reproduce
-    (tests/test_engine_gpu.py::test_window_cut_schedule_matches_per_window_host)."""
-    K, P, M, W = 3, 50, 900, 250
-    rec = make_stream(StreamSpec(team_size=K, seed=8, p_afk=0.05), M, P, K=K)
-    br = R.BatchRater()
-    link, deps = (t.clone() for t in br.schedule(rec, K, P, window=W))
-    br._ws.clear()  # (the per-window schedules below must not reuse those buffers)
-    slots, _ = _stateful_slots(rec.numpy(), K, P)
-    for w, lo in enumerate(range(0, M, W)):
-        hi = min(lo + W, M)
-        l1, d1 = br.schedule(rec[lo:hi], K, P)
-        sub = R.BatchRater.window_schedule(R.Schedule(link, deps), w, W)
-        s = slots[lo:hi]  # (the slots of matches that rate nothing stay unwritten)
-        np.testing.assert_array_equal(sub.link.numpy()[s], l1.numpy()[s])
-        assert torch.equal(sub.deps, d1)
-
-
-def test_step_windows_host_equals_run():
-    """WindowPipeline.step_windows on the host mirror: the k windows of a step, a
-    forced DP merge after each, give what ``run`` gives over the same windows."""
-    from analyzer_amd.parallel.sweep import SweepMerger
-    from analyzer_amd.runtime.engine import WindowPipeline
-
-    K, P, k, Mw = 3, 300, 3, 400
-    rec = make_stream(StreamSpec(team_size=K, seed=12), k * Mw, P, K=K)
-    outs = []
-    for step in (False, True):
-        ro = make_roster(RosterSpec(num_players=P, seed=13))
-        pipe = WindowPipeline(R.BatchRater(), ro, K, merger=SweepMerger(P, "cpu", force=True))
-        out = R.RateResult.allocate(Mw, K, "cpu")
-        if step:
-            res, nxt = pipe.step_windows(pipe.prepare(rec, window=Mw), None, out=out)
-            assert nxt is None and pipe.windows_rated == k
-        else:
-            pipe.run([rec[w * Mw:(w + 1) * Mw] for w in range(k)], out=out)
-        outs.append((ro.state.clone(), [getattr(out, f).clone() for f in R.RateResult.FIELDS]))
-    assert torch.equal(outs[0][0].nan_to_num(-1), outs[1][0].nan_to_num(-1))
-    for a, b in zip(outs[0][1], outs[1][1]):
-        assert torch.equal(a.nan_to_num(-1) if a.is_floating_point() else a,
-                           b.nan_to_num(-1) if b.is_floating_point() else b)
