@@ -111,6 +111,10 @@ class WorkerConfig:
     # new: fault injection -- these match api ids fail to rate as if their
     # numerics broke: quarantined (QUARANTINE=true) or failing their batch (false)
     fault_poison: frozenset = frozenset()
+    # new: fault injection -- the process dies (exit 17) when a batch arrives after this
+    # many processed batches, holding its unacknowledged deliveries (replica death:
+    # the broker redelivers them to the other replicas, runtime/replicas.py)
+    fault_exit_after: int = 0
 
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "WorkerConfig":
@@ -137,6 +141,7 @@ class WorkerConfig:
             skip_rated=env.get("SKIP_RATED") == "true",
             pipeline=env.get("PIPELINE") == "true",
             fault_poison=frozenset(x for x in (env.get("FAULT_POISON") or "").split(",") if x),
+            fault_exit_after=int(env.get("FAULT_EXIT_AFTER") or 0),
         )
 
     @property

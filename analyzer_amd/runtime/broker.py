@@ -484,9 +484,14 @@ class PikaBroker:
 
 def connect(uri: str, clock: Optional[Callable[[], float]] = None):
     """Broker for a ``RABBITMQ_URI``.  ``memory://`` (or empty) -> in-process
-    broker; ``amqp://`` / ``amqps://`` -> ``PikaBroker`` (needs pika)."""
+    broker; ``tcp://host:port`` -> a ``BrokerServer`` that worker replicas share
+    (runtime/broker_net.py); ``amqp://`` / ``amqps://`` -> ``PikaBroker`` (needs pika)."""
     if not uri or uri.startswith("memory:"):
         return MemoryBroker(clock)
+    if uri.startswith("tcp://"):  # a BrokerServer shared by worker replicas (runtime/broker_net.py)
+        from .broker_net import connect_tcp
+
+        return connect_tcp(uri, clock)
     if uri.startswith("amqp"):
         try:
             import pika

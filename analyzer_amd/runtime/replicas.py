@@ -1,0 +1,110 @@
+"""Horizontal scale-out of the streaming worker: N worker processes on one queue
+(SURVEY P1 "replica scale-out"; /root/reference/worker.py:91).
+
+The reference scales by starting more ``worker.py`` processes against one RabbitMQ
+queue (prefetch ``BATCHSIZE`` each) and one MySQL database.  ``run_replicas`` does
+the same on one node: a ``BrokerServer`` (runtime/broker_net.py, ``tcp://``) stands
+in for RabbitMQ, the store is a shared file (``DATABASE_URI=sqlite:///path`` or any
+SQLAlchemy URL), and each replica is a child ``worker.py`` process pinned to one GPU
+(``HIP_VISIBLE_DEVICES``; on the host mirror they share the CPU).  With a real
+RabbitMQ, start the replicas the same way with ``RABBITMQ_URI=amqp://...``.
+
+Semantics are the reference's: each message is delivered to one replica at a time and
+redelivered if that replica dies before acking it (at-least-once), and replicas that
+rate matches sharing a player race on that player's row -- read, rate, write back,
+no locking -- exactly as the reference's replicas do on MySQL (worker.py:174-194).
+The launcher prints one JSON line: per-replica and total matches, acks and rate, and
+the broker's final counts.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+from typing import Dict, List, Optional
+
+
+def _gpus() -> int:
+    """Devices visible to the children (counting does not initialise the GPU here)."""
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())
+    except Exception:  # pragma: no cover - torch always present in this image
+        return 0
+
+
+def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 3, seed: int = 1,
+                 database_uri: Optional[str] = None, queue: Optional[str] = None,
+                 env: Optional[Dict[str, str]] = None, timeout: float = 600.0,
+                 worker_py: Optional[str] = None,
+                 replica_env: Optional[Dict[int, Dict[str, str]]] = None) -> Dict[str, object]:
+    """Start a broker and ``n`` worker replicas, optionally populating and enqueueing
+    ``synthetic`` matches first; wait until every replica drained the queue and exited.
+    ``replica_env``: extra environment per replica index (fault injection in tests)."""
+    from ..config import WorkerConfig
+    from .broker_net import BrokerServer
+    from .source import populate
+    from .store import open_store
+
+    base = dict(os.environ if env is None else env)
+    queue = queue or WorkerConfig.from_env(base).queue
+    tmpdir = None
+    if not database_uri:
+        database_uri = base.get("DATABASE_URI") or ""
+    if not database_uri or database_uri.startswith(("memory:", "columnar:")) or database_uri == "sqlite://":
+        # replicas need one store they all see: a SQLite file
+        tmpdir = tempfile.mkdtemp(prefix="ana_replicas_")
+        database_uri = "sqlite:///" + os.path.join(tmpdir, "store.db")
+    server = BrokerServer().start()
+    ids: List[str] = []
+    if synthetic:
+        store = open_store(database_uri)
+        matches = populate(store, synthetic, players or 2 * synthetic, team_size=team_size, seed=seed)
+        ids = [m.api_id for m in matches]
+        del store
+        server.publish(queue, [i.encode() for i in ids])
+    worker_py = worker_py or os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+        os.path.abspath(__file__)))), "worker.py")
+    gpus = _gpus()
+    procs = []
+    t0 = time.perf_counter()
+    for r in range(n):
+        e = dict(base)
+        e.update(RABBITMQ_URI=server.uri, DATABASE_URI=database_uri, QUEUE=queue, REPLICA=str(r))
+        e.update((replica_env or {}).get(r, {}))
+        if gpus > 0:  # one replica per GPU (round-robin when there are more replicas)
+            e["HIP_VISIBLE_DEVICES"] = str(r % gpus)
+        # output to files: a replica blocked on a full pipe would hold its deliveries
+        fo, fe = tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")
+        procs.append((subprocess.Popen([sys.executable, worker_py], env=e, stdout=fo, stderr=fe), fo, fe))
+    results, codes = [], []
+    deadline = time.monotonic() + timeout
+    for p, fo, fe in procs:
+        try:
+            p.wait(timeout=max(1.0, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+        codes.append(p.returncode)
+        fo.seek(0)
+        fe.seek(0)
+        out, err = fo.read(), fe.read()
+        fo.close()
+        fe.close()
+        line = [ln for ln in out.splitlines() if ln.startswith("{")]
+        results.append(json.loads(line[-1]) if line else {"error": err[-2000:]})
+    dt = time.perf_counter() - t0
+    stats = server.stats()
+    server.close()
+    total = sum(int(r.get("matches", 0)) for r in results)
+    return {"replicas": n, "gpus": gpus, "matches": total, "enqueued": len(ids),
+            "acked": sum(int(r.get("acked", 0)) for r in results),
+            "nacked": sum(int(r.get("nacked", 0)) for r in results),
+            "seconds": dt, "matches_per_s": total / dt if dt > 0 else None,
+            "per_replica": [{"matches": r.get("matches"), "acked": r.get("acked"),
+                             "matches_per_s": r.get("matches_per_s"), "error": r.get("error")} for r in results],
+            "exit_codes": codes, "broker": stats, "database_uri": database_uri}

@@ -514,7 +514,8 @@ class SqliteStore:
 
     def __init__(self, path: str = ":memory:"):
         self.path = path
-        self.conn = sqlite3.connect(path)
+        # worker replicas share the file (runtime/replicas.py): a writer waits for the lock
+        self.conn = sqlite3.connect(path, timeout=120.0)
         if path != ":memory:":
             # write-ahead log: a commit appends to the log instead of rewriting pages +
             # journal; NORMAL sync keeps every committed batch across a process crash

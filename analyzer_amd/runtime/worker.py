@@ -52,6 +52,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 import time
 from operator import attrgetter
 
@@ -175,6 +176,10 @@ class Worker:
             self.rabbit.remove_timeout(self.timer)
             self.timer = None
         batch, self.queue = self.queue, Deliveries()
+        if batch and self.cfg.fault_exit_after and self.stats.batches >= self.cfg.fault_exit_after:
+            logger.error("injected fault (FAULT_EXIT_AFTER=%d): exiting with %d deliveries unacked",
+                         self.cfg.fault_exit_after, len(batch))
+            os._exit(17)
         if self._pipe:
             self._pipeline_step(batch)
             return

@@ -11,6 +11,7 @@ Same environment variables and defaults as the reference (``RABBITMQ_URI``,
 
     python3 worker.py                      # consume QUEUE until idle
     python3 worker.py --synthetic 1000     # config 1: populate + consume 1k 3v3 matches
+    python3 worker.py --synthetic 100000 --replicas 8   # 8 worker processes on one queue
 
 Without pika / a MySQL driver in this image, ``RABBITMQ_URI`` defaults to the
 in-process broker (``memory://``) and ``DATABASE_URI`` to the in-process store;
@@ -72,7 +73,17 @@ def main(argv=None) -> int:
     ap.add_argument("--players", type=int, default=0, help="synthetic roster size (default 2*N)")
     ap.add_argument("--team-size", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--replicas", type=int, default=1,
+                    help="N > 1: a shared broker (tcp://) and N worker processes on QUEUE, one per GPU, "
+                         "over one store file (analyzer_amd/runtime/replicas.py)")
     args = ap.parse_args(argv)
+    if args.replicas > 1:
+        from analyzer_amd.runtime.replicas import run_replicas
+
+        res = run_replicas(args.replicas, synthetic=args.synthetic, players=args.players,
+                           team_size=args.team_size, seed=args.seed)
+        print(json.dumps(res), flush=True)
+        return 0 if all(c == 0 for c in res["exit_codes"]) else 1
     connect()
     if args.synthetic:
         from analyzer_amd.runtime.source import populate, publish
