@@ -38,6 +38,7 @@
 #   dpacc      sweep-DP accuracy table (ranks x merges per step) incl. per-participant records
 #   dpcost     one-GPU DP step price: plain vs forced merges at k = 8 / 16
 #   dpstep     forced-merge step price: record correction on / off, tail / serial placement, emulated N = 8
+#   replicas   worker.py --replicas 1 / 2 / 4 on the box (shared broker + SQLite store)
 #   dpconf     gloo rehearsals of config 3 (N = 4) and config 5 (N = 2)
 #   project    one-GPU projection of the N = 2 / 4 / 8 DP step (emulated all-reduce, bus bandwidth sweep)
 #   corrmicro  the record correction kernel alone + a kernel trace of the k = 8 DP step
@@ -291,6 +292,15 @@ EOF
         done
       done
       for f in gpurun_out/dpstep/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
+      ;;
+    replicas)  # worker scale-out on the box: 1 / 2 / 4 worker processes on one queue (tcp:// broker) over one
+               # SQLite store file, ENGINE=native, 40k synthetic matches
+      for n in 1 2 4; do
+        rm -f /tmp/rep$n.db*
+        ENGINE=native DATABASE_URI=sqlite:////tmp/rep$n.db run replicas/n$n 600 $PY worker.py --synthetic 40000 \
+            --replicas $n
+      done
+      grep -h -o '"matches_per_s": [0-9.]*' gpurun_out/replicas/*.log
       ;;
     dpconf)  # gloo rehearsals of the other DP configs: 5v5 (config 3, k = 2N) and the 10M-player re-rate (config 5)
       run dpconf/c3_gloo4 900 env ANA_DIST_BACKEND=gloo $PY bench.py --config 3 --gpus 4 --steps 1 --warmup 1

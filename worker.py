@@ -73,11 +73,11 @@ def main(argv=None) -> int:
     ap.add_argument("--players", type=int, default=0, help="synthetic roster size (default 2*N)")
     ap.add_argument("--team-size", type=int, default=3)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--replicas", type=int, default=1,
-                    help="N > 1: a shared broker (tcp://) and N worker processes on QUEUE, one per GPU, "
-                         "over one store file (analyzer_amd/runtime/replicas.py)")
+    ap.add_argument("--replicas", type=int, default=0,
+                    help="N >= 1: a shared broker (tcp://) and N worker processes on QUEUE, one per GPU, "
+                         "over one store file (analyzer_amd/runtime/replicas.py); 0: this process alone")
     args = ap.parse_args(argv)
-    if args.replicas > 1:
+    if args.replicas >= 1:
         from analyzer_amd.runtime.replicas import run_replicas
 
         res = run_replicas(args.replicas, synthetic=args.synthetic, players=args.players,
