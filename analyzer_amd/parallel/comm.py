@@ -85,14 +85,15 @@ def all_gather_rows(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
         dist.all_gather_into_tensor(out, inp, group=group)
 
 
-def scan_and_sum(t: torch.Tensor, group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+def scan_and_sum(t: torch.Tensor, group=None, force: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """(exclusive prefix over ranks, sum over ranks) of ``t``, row-wise.  Rank b
     owns row block b: one all-to-all brings it block b of every rank, which it
     prefix-sums and sums in rank order (floating types in fp32, rounded once to the
     wire type); a second all-to-all returns each rank its prefix, an all-gather the
-    block sums.  One rank: (zeros, t)."""
+    block sums.  One rank: (zeros, t) -- through the exchanges anyway with ``force`` (tests
+    of the collective path on a one-rank communicator)."""
     _, size = world(group)
-    if size <= 1:
+    if size <= 1 and not force:
         return torch.zeros_like(t), t
     P = t.shape[0]
     C = t[0].numel() if P else 1
@@ -117,20 +118,21 @@ def _row_bytes(x: torch.Tensor, P: int) -> torch.Tensor:
     return x.reshape(P, -1).contiguous().view(torch.uint8)
 
 
-def scan_and_sum_rows(t: torch.Tensor, extra: torch.Tensor, group=None):
+def scan_and_sum_rows(t: torch.Tensor, extra: torch.Tensor, group=None, force: bool = False):
     """``scan_and_sum`` of ``t`` whose exchanges also carry ``extra`` (rows summed,
     not scanned) in the same payload: (prefix of t, total of t, total of extra) from
     one all-to-all, one all-to-all back and one all-gather -- the DP merge's messages
     and touch counts without a separate all-reduce (a collective launch per merge).
-    The rows travel as bytes and are read back through typed views."""
+    The rows travel as bytes and are read back through typed views.  ``force``: as
+    scan_and_sum."""
     _, size = world(group)
-    if size <= 1:
+    if size <= 1 and not force:
         return torch.zeros_like(t), t, extra
     P = t.shape[0]
     bt, be = _row_bytes(t, P), _row_bytes(extra, P)
     ct, C = bt.shape[1], bt.shape[1] + be.shape[1]
     if C % t.element_size() or C % extra.element_size() or ct % extra.element_size():
-        p, s = scan_and_sum(t, group)  # rows that do not view back: two exchanges
+        p, s = scan_and_sum(t, group, force)  # rows that do not view back: two exchanges
         all_reduce_sum(extra, group)
         return p, s, extra
     blk = -(-P // size)
@@ -157,7 +159,8 @@ def scan_and_sum_rows(t: torch.Tensor, extra: torch.Tensor, group=None):
             total[:P, ct:].contiguous().view(extra.dtype).view_as(extra))
 
 
-def scan_and_sum_start(t: torch.Tensor, group=None, stream=None, extra: Optional[torch.Tensor] = None):
+def scan_and_sum_start(t: torch.Tensor, group=None, stream=None, extra: Optional[torch.Tensor] = None,
+                       force: bool = False):
     """``scan_and_sum`` in flight: returns ``finish() -> (prefix, total)``.  With RCCL
     and a side ``stream`` the two all-to-alls, the block scan between them, the
     all-gather -- which also carry ``extra``, summed in place (scan_and_sum_rows) --
@@ -170,12 +173,12 @@ def scan_and_sum_start(t: torch.Tensor, group=None, stream=None, extra: Optional
 
     def run():
         if extra is None:
-            return scan_and_sum(t, group)
-        p, s, e = scan_and_sum_rows(t, extra, group)
+            return scan_and_sum(t, group, force)
+        p, s, e = scan_and_sum_rows(t, extra, group, force)
         if e is not extra:
             extra.copy_(e)
         return p, s
-    side = stream is not None and t.is_cuda and size > 1 and not _staged(t, group)
+    side = stream is not None and t.is_cuda and (size > 1 or force) and not _staged(t, group)
     if not side:
         res = run()
         return lambda: res

@@ -364,8 +364,11 @@ class SweepMerger:
         if self.world > 1:
             if self._coll is None and self.device.type == "cuda":
                 self._coll = torch.cuda.Stream(self.device)
+            # (force: a world_size override above the group's real size runs the exchanges
+            # anyway -- the one-rank RCCL test of this path)
             fin = scan_and_sum_start(operand, group=self.group, stream=self._coll,
-                                     extra=self.cnt if self.msg is not None else None)
+                                     extra=self.cnt if self.msg is not None else None,
+                                     force=world(self.group)[1] < self.world)
         else:
             prefix0 = self._prefix_zero(operand)
             fin = lambda: (prefix0, operand)  # noqa: E731

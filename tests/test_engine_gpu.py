@@ -688,15 +688,30 @@ def _rccl_single_rank(rank, size, P, M, K, seed):
         mh._synced = True
         mh.begin(rh)
         half[cd] = (rh, mh)
+    # the corrected merge (bench N >= 4): the scan collective (byte rows: bf16 messages +
+    # int32 touch fields) on a side stream, the records pass deferred into the next merge
+    rc = roster.clone()
+    mc = SweepMerger(P, dev, world_size=2, comm_dtype="bf16", correct_records=True)
+    mc.start.copy_(merger.start)
+    mc._synced = True
+    mc.begin(rc)
+    out = R.RateResult.allocate(M, K, dev)
+    out.packed.copy_(torch.randn_like(out.packed))
+    rows0 = out.packed.clone()
     merger.merge(roster)
     ran = []
     for cd, (rh, mh) in half.items():
         mh.merge(rh, overlap=lambda: ran.append(torch.ones(4, device=dev).sum()))
+    mc.merge_corrected(rc, rec, out, overlap=lambda: ran.append(torch.ones(4, device=dev).sum()))
+    assert mc._pending is not None  # deferred
+    mc.flush_correction()
+    mc.check()
     torch.cuda.synchronize()
-    assert len(ran) == 2
+    assert len(ran) == 3
     return {"x": x.cpu(), "z": z.float().cpu(), "y": y.float().cpu(), "g": g[:1000].cpu(),
             "posterior": posterior.cpu(), "merged": roster.state.cpu(),
-            "merged_bf16": half["bf16"][0].state.cpu(), "merged_fp16": half["fp16"][0].state.cpu()}
+            "merged_bf16": half["bf16"][0].state.cpu(), "merged_fp16": half["fp16"][0].state.cpu(),
+            "merged_corrected": rc.state.cpu(), "rows_changed": int((out.packed != rows0).sum())}
 
 
 def test_rccl_single_rank_collectives_and_merge(gpu_device, tmp_path, monkeypatch):
@@ -718,6 +733,10 @@ def test_rccl_single_rank_collectives_and_merge(gpu_device, tmp_path, monkeypatc
     got = r["merged"].view(P, 8, 4)[..., 0::2]
     np.testing.assert_allclose(got[..., 0].numpy(), post[..., 0].numpy(), rtol=0, atol=2e-3, equal_nan=True)
     np.testing.assert_allclose(got[..., 1].numpy(), post[..., 1].numpy(), rtol=1e-4, atol=0, equal_nan=True)
+    # one rank's exclusive prefix is zero: the corrected merge leaves the records alone and
+    # decodes like the plain bf16 merge
+    assert r["rows_changed"] == 0
+    assert torch.equal(r["merged_corrected"].view(torch.int32), r["merged_bf16"].view(torch.int32))
     for cd, tol_mu, tol_sig in (("fp16", 1.0, 2e-3), ("bf16", 8.0, 1e-2)):  # as test_distributed
         gh = r["merged_" + cd].view(P, 8, 4)[..., 0::2]
         np.testing.assert_allclose(gh[..., 0].numpy(), post[..., 0].numpy(), rtol=0, atol=tol_mu, equal_nan=True)
