@@ -41,10 +41,13 @@ def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 
                  database_uri: Optional[str] = None, queue: Optional[str] = None,
                  env: Optional[Dict[str, str]] = None, timeout: float = 600.0,
                  worker_py: Optional[str] = None,
-                 replica_env: Optional[Dict[int, Dict[str, str]]] = None) -> Dict[str, object]:
+                 replica_env: Optional[Dict[int, Dict[str, str]]] = None,
+                 first_alone_until_acked: int = 0) -> Dict[str, object]:
     """Start a broker and ``n`` worker replicas, optionally populating and enqueueing
     ``synthetic`` matches first; wait until every replica drained the queue and exited.
-    ``replica_env``: extra environment per replica index (fault injection in tests)."""
+    ``replica_env``: extra environment per replica index (fault injection in tests);
+    ``first_alone_until_acked``: start replica 0 alone and the others once the broker
+    counted that many acks (a deterministic first consumer for tests)."""
     from ..config import WorkerConfig
     from .broker_net import BrokerServer
     from .source import populate
@@ -81,6 +84,11 @@ def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 
         # output to files: a replica blocked on a full pipe would hold its deliveries
         fo, fe = tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")
         procs.append((subprocess.Popen([sys.executable, worker_py], env=e, stdout=fo, stderr=fe), fo, fe))
+        if r == 0 and first_alone_until_acked:
+            wait_until = time.monotonic() + timeout / 2
+            while (server.stats()["acked"] < first_alone_until_acked and procs[0][0].poll() is None
+                   and time.monotonic() < wait_until):
+                time.sleep(0.05)
     results, codes = [], []
     deadline = time.monotonic() + timeout
     for p, fo, fe in procs:
