@@ -313,23 +313,24 @@ class SqliteSession(_SessionBase):
         """Stored (ratings [n,14], attributes [n,3]) of integer player keys."""
         import numpy as np
 
-        names = [self.store.player_names[int(k)] for k in keys]
+        pn = self.store.player_names
+        names = [pn[k] for k in np.asarray(keys).tolist()]
         cols = ("api_id", "rowid", "rank_points_ranked", "rank_points_blitz", "skill_tier") + PLAYER_RATING_COLS
-        got = {}
+        rows: list = []
         for chunk in _chunks(names, 500):
-            for row in self.conn.execute("SELECT %s FROM player WHERE api_id IN (%s)"
-                                         % (", ".join(_q(c) for c in cols), ", ".join("?" * len(chunk))),
-                                         chunk):
-                got[row[0]] = row[2:]
-                self.store.player_rowid[row[0]] = row[1]
-        nan = float("nan")
-        att = np.full((len(names), 3), nan)
-        rat = np.full((len(names), 14), nan)
-        for i, a in enumerate(names):
-            row = got.get(a)
-            if row is not None:
-                att[i] = [nan if v is None else float(v) for v in row[:3]]
-                rat[i] = [nan if v is None else float(v) for v in row[3:]]
+            rows += self.conn.execute("SELECT %s FROM player WHERE api_id IN (%s)"
+                                      % (", ".join(_q(c) for c in cols), ", ".join("?" * len(chunk))),
+                                      chunk).fetchall()
+        att = np.full((len(names), 3), np.nan)
+        rat = np.full((len(names), 14), np.nan)
+        if rows:
+            # one numpy conversion (None -> NaN) instead of a Python float() per column
+            where = {a: i for i, a in enumerate(names)}
+            pos = np.fromiter((where[r[0]] for r in rows), dtype=np.int64, count=len(rows))
+            vals = np.array([r[2:] for r in rows], dtype=np.float64)
+            att[pos] = vals[:, :3]
+            rat[pos] = vals[:, 3:]
+            self.store.player_rowid.update((r[0], r[1]) for r in rows)
         return rat, att
 
     def _write_batch(self, b) -> None:
@@ -381,16 +382,20 @@ class SqliteSession(_SessionBase):
                           [[names[p], names[p]] + v for p, v in zip(b.part[ss].tolist(), st8)])
         if b.final_keys is not None and len(b.final_keys):
             pn, prow_of = self.store.player_names, self.store.player_rowid
-            f = b.final
-            groups: Dict[tuple, list] = {}  # one UPDATE per set of touched tracks
-            for u, k in enumerate(b.final_keys.tolist()):
-                tracks = tuple(np.nonzero(b.final_tracks[u])[0].tolist())
-                vals = []
-                for t in tracks:
-                    vals += [None if f[u, 2 * t] != f[u, 2 * t] else float(f[u, 2 * t]),
-                             None if f[u, 2 * t + 1] != f[u, 2 * t + 1] else float(f[u, 2 * t + 1])]
-                groups.setdefault(tracks, []).append(vals + [prow_of[pn[int(k)]]])
-            for tracks, rows in groups.items():
+            f = np.asarray(b.final, dtype=np.float64)
+            touched = np.asarray(b.final_tracks, dtype=bool)
+            rowids = np.array([prow_of[pn[k]] for k in b.final_keys.tolist()], dtype=np.int64)
+            # one UPDATE per set of touched tracks: players grouped by their track bitmask
+            masks = (touched.astype(np.int64) << np.arange(touched.shape[1], dtype=np.int64)).sum(1)
+            for m in np.unique(masks).tolist():
+                if m == 0:
+                    continue
+                sel = masks == m
+                tracks = [t for t in range(touched.shape[1]) if (m >> t) & 1]
+                cols = np.array([[2 * t, 2 * t + 1] for t in tracks]).reshape(-1)
+                vals = f[np.ix_(sel, cols)].astype(object)
+                vals[np.isnan(f[np.ix_(sel, cols)])] = None  # NaN -> NULL
+                rows = np.concatenate([vals, rowids[sel, None].astype(object)], axis=1).tolist()
                 sets = ", ".join("%s=?, %s=?" % (_q(TRACK_COLUMNS[t] + "_mu"), _q(TRACK_COLUMNS[t] + "_sigma"))
                                  for t in tracks)
                 c.executemany("UPDATE player SET %s WHERE rowid=?" % sets, rows)
