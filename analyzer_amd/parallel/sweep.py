@@ -165,9 +165,9 @@ class SweepMerger:
             mb = EngineConfig.from_env().merge_bucket_mb
             row_bytes = 16 * 4 if not self.scaled else 14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4
             bucket_rows = int(mb * (1 << 20)) // row_bytes if mb > 0 else self.P
-        if self.world <= 1 and self.emulate is None:
+        if self.world <= 1:
             # one rank (force): no collective to overlap, so one bucket -- two launches
-            # per merge instead of two per 16 MB (an emulated collective keeps the buckets)
+            # per merge instead of two per 16 MB
             bucket_rows = self.P
         self.bucket_rows = max(1, min(int(bucket_rows), max(self.P, 1)))
         self.windows = 0
@@ -233,11 +233,10 @@ class SweepMerger:
         correction's ``delta`` table from the window start before overwriting it."""
         hi = self.P if hi is None else hi
         s2 = into[lo:hi] if into is not None else self._none
-        if prefix is not None and prefix.shape[0] != hi - lo:
-            prefix = prefix[lo:hi]  # a whole-roster prefix (a bucket's own one is used as is)
         native().sweep_apply_packed(self.start[lo:hi], self.msg[lo:hi], self.cnt[lo:hi], roster.attrs[lo:hi],
                                     roster.state[lo:hi], s2, self.vst, float(self.cfg.unknown_player_sigma),
-                                    self.clamps, prefix, None if delta is None else delta[lo:hi])
+                                    self.clamps, None if prefix is None else prefix[lo:hi],
+                                    None if delta is None else delta[lo:hi])
         roster.epoch = roster.epoch if roster.epoch is not None else 0
 
     def _packed(self) -> bool:
@@ -346,11 +345,8 @@ class SweepMerger:
         """``merge`` with the causal record correction of this window's records
         (``rec``, RateResult ``out``): messages -> ONE collective giving the sum and
         this rank's exclusive prefix (comm.scan_and_sum) -> the decode, which also turns
-        the prefix into the increment table -> the records pass.  Compressed messages go
-        in row buckets (``buckets``): every bucket's messages and collective are launched
-        first, then each bucket decodes as its collective lands, so the collectives run
-        under the other buckets' kernels; the records pass needs the whole table, which
-        the deferral gives it (fp32 messages: one bucket).
+        the prefix into the increment table -> the records pass.  Not bucketed: the
+        records name any player, so the whole prefix is needed before the pass.
 
         Deferred (``defer``, default): the records pass of this window is enqueued by
         the NEXT merge right after its collective is launched, so it runs while the
@@ -358,66 +354,54 @@ class SweepMerger:
         instead of on the critical path; ``flush_correction`` runs a pending pass."""
         K = (int(rec.shape[1]) - 2) // 2
         self._ev("begin")
-        packed = self.msg is not None
-        buckets = self.buckets() if packed else [(0, self.P)]
-        force = world(self.group)[1] < self.world
-        if self.world > 1 and self._coll is None and self.device.type == "cuda":
-            self._coll = torch.cuda.Stream(self.device)
-        fins = []
-        for lo, hi in buckets:
-            if packed:
-                self.messages_packed(roster, lo, hi)
-                operand = self.msg[lo:hi]
-            else:
-                self.messages(roster)
-                operand = self.buf
-            if self.world > 1:
-                # (force: a world_size override above the group's real size runs the
-                # exchanges anyway -- the one-rank RCCL test of this path)
-                fin = scan_and_sum_start(operand, group=self.group, stream=self._coll,
-                                         extra=self.cnt[lo:hi] if packed else None, force=force)
-            else:
-                fin = self._zero_scan(operand, lo, hi, packed)
-            fins.append((lo, hi, operand, fin))
+        if self.msg is not None:
+            self.messages_packed(roster)
+            operand = self.msg
+        else:
+            self.messages(roster)
+            operand = self.buf
         self._ev("messages")
-        self.flush_correction()  # the previous window's records, beside the collectives
+        if self.world > 1:
+            if self._coll is None and self.device.type == "cuda":
+                self._coll = torch.cuda.Stream(self.device)
+            # (force: a world_size override above the group's real size runs the exchanges
+            # anyway -- the one-rank RCCL test of this path)
+            fin = scan_and_sum_start(operand, group=self.group, stream=self._coll,
+                                     extra=self.cnt if self.msg is not None else None,
+                                     force=world(self.group)[1] < self.world)
+        else:
+            prefix0 = self._prefix_zero(operand)
+            fin = lambda: (prefix0, operand)  # noqa: E731
+            if self.emulate is not None and self.device.type == "cuda":  # 1.5x the all-reduce's volume
+                n, bw, lat = self.emulate
+                self.emulate = (n, bw / 1.5, lat)
+                efin = self._launch_reduce(0, self.P, self.msg is not None)
+                self.emulate = (n, bw, lat)
+                fin = lambda: (efin(), (prefix0, operand))[1]  # noqa: E731
+        self.flush_correction()  # the previous window's records, beside the collective
         self._ev("correct")
+        prefix, total = fin()
+        if total is not operand:
+            operand.copy_(total)
+        self._ev("allreduce")
         if overlap is not None:
             overlap()
         self._ev("overlap")
-        if packed and self.delta is None:
-            self.delta = torch.empty((self.P, 16), dtype=torch.float32, device=self.device)
-        delta = self.delta
-        for lo, hi, operand, fin in fins:
-            prefix, total = fin()
-            if total is not operand:
-                operand.copy_(total)
-            self._ev("allreduce")
-            if packed:  # the decode also turns the scaled prefix into raw increments
-                self.decode_packed(roster, lo, hi, into=self.start, prefix=prefix, delta=self.delta)
-            else:       # raw fp32 messages: the prefix IS the increment table
-                self.decode(roster, into=self.start)
-                delta = prefix
-            self._ev("apply")
+        if self.msg is not None:  # the decode also turns the scaled prefix into raw increments
+            if self.delta is None:
+                self.delta = torch.empty((self.P, 16), dtype=torch.float32, device=self.device)
+            self.decode_packed(roster, into=self.start, prefix=prefix, delta=self.delta)
+            delta = self.delta
+        else:                     # raw fp32 messages: the prefix IS the increment table
+            self.decode(roster, into=self.start)
+            delta = prefix
+        self._ev("apply")
         self._pending = (rec, K, out.packed, delta)
         if not self.defer:
             self.flush_correction()
             self._ev("correct")
         self._synced = True
         self.windows += 1
-
-    def _zero_scan(self, operand: torch.Tensor, lo: int, hi: int, packed: bool):
-        """One rank: prefix zero, sum = the message itself -- with an emulated collective
-        (1.5x an all-reduce's volume for the scan) on its stream in between."""
-        prefix0 = self._prefix_zero(self.msg if packed else operand)[lo:hi] if packed else \
-            self._prefix_zero(operand)
-        if self.emulate is not None and self.device.type == "cuda":
-            n, bw, lat = self.emulate
-            self.emulate = (n, bw / 1.5, lat)
-            efin = self._launch_reduce(lo, hi, packed)
-            self.emulate = (n, bw, lat)
-            return lambda: (efin(), (prefix0, operand))[1]
-        return lambda: (prefix0, operand)
 
     def flush_correction(self) -> None:
         """Run the deferred record correction now (stream-ordered), if one is pending."""

@@ -496,7 +496,7 @@ def test_scan_and_sum_over_ranks(tmp_path):
         assert torch.equal(out["e2"], out["sc"])
 
 
-def _corrected(rank, size, P, M, K, seed, windows, comm_dtype, bucket_rows=None):
+def _corrected(rank, size, P, M, K, seed, windows, comm_dtype):
     from analyzer_amd.ops.rate import BatchRater
     from analyzer_amd.parallel.sweep import SweepMerger
     from analyzer_amd.runtime.engine import WindowPipeline
@@ -504,7 +504,7 @@ def _corrected(rank, size, P, M, K, seed, windows, comm_dtype, bucket_rows=None)
     roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
     spec = StreamSpec(team_size=K, seed=seed + 1)
     recs = [make_stream(spec, M, P, K=K, base=(w * size + rank) * M) for w in range(windows)]
-    merger = SweepMerger(P, "cpu", comm_dtype=comm_dtype, bucket_rows=bucket_rows)
+    merger = SweepMerger(P, "cpu", comm_dtype=comm_dtype)
     pipe = WindowPipeline(BatchRater(), roster, K, merger=merger)
     outs = []
     pipe.run(recs, on_result=lambda i, res: outs.append((res.s_mu.clone(), res.m_mu.clone())))
@@ -549,17 +549,17 @@ def test_deferred_record_correction_matches_inline(tmp_path):
             assert torch.equal(x.view(torch.int32), y.view(torch.int32))
 
 
-@pytest.mark.parametrize("comm_dtype,bucket_rows", [("fp32", None), ("bf16", None), ("bf16", 137)])
-def test_record_correction_over_ranks_equals_simulation(tmp_path, comm_dtype, bucket_rows):
+@pytest.mark.parametrize("comm_dtype", ["fp32", "bf16"])
+def test_record_correction_over_ranks_equals_simulation(tmp_path, comm_dtype):
     """The corrected merge over gloo (scan_and_sum, the records pass before the
-    decode; bf16 also in row buckets of 137 players) gives every rank's records what the one-process simulation of
+    decode) gives every rank's records what the one-process simulation of
     parallel/accuracy.py gives, and the corrected records sit much closer to exact
     sequential rating than the uncorrected ones."""
     from analyzer_amd.ops.rate import BatchRater
     from analyzer_amd.parallel.accuracy import compare, simulate_sweep_dp
 
     P, M, K, seed, size, windows = 400, 900, 3, 31, 3, 3
-    res = run_ranks(_corrected, size, tmp_path, P, M, K, seed, windows, comm_dtype, bucket_rows)
+    res = run_ranks(_corrected, size, tmp_path, P, M, K, seed, windows, comm_dtype)
     spec = StreamSpec(team_size=K, seed=seed + 1)
     sets = [[make_stream(spec, M, P, K=K, base=(w * size + r) * M) for r in range(size)] for w in range(windows)]
     start = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
