@@ -125,6 +125,7 @@ constexpr int tele_scratch_floats() {
 typedef __bf16 tele_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float tele_f32x4 __attribute__((ext_vector_type(4)));
 typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int tele_i32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void tele_lds_fence() {
   // LDS ops of one wave execute in order; this only pins the program order
@@ -158,7 +159,7 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   static_assert(SPAN >= 1 && SPAN <= kTeleMaxSpan, "span must fit the lanes");
   const int64_t m0 = tile * SPAN;
   const int nm = (int)(tp.num_matches - m0 < SPAN ? tp.num_matches - m0 : SPAN);
-  const int64_t off = lane <= nm ? tp.evoff[m0 + lane] : 0;
+  const int64_t off = lane <= nm ? __builtin_nontemporal_load(tp.evoff + m0 + lane) : 0;
   const int64_t e0 = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(off >> 32), 0) << 32) |
                                (uint32_t)__builtin_amdgcn_readlane((int)off, 0));
   const int32_t roff = (int32_t)(off - e0);  // lane j <= nm: first event of match j
@@ -200,7 +201,11 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
       const int c0 = f < 3 ? f + 1 : split ? 3 * f - 5 : 0;
       const float x0 = r[c0], x1 = r[split ? c0 + 1 : 16], x2 = r[split ? c0 + 2 : 16];
       const float v = split ? (x0 + x1) + x2 : x0;
-      if (16 * c + (o >> 3) < nrows) dst[16 * c * kStatFeatures + o] = v;
+      // non-temporal: the stats (2 GB per 10M 3v3 window) and the events (3.2 GB) stream
+      // past the Infinity Cache instead of evicting the roster the co-running executor
+      // gathers from -- config 4 step 9.66 -> 9.34 ms, the kernel alone unchanged; loads
+      // or stores alone 9.62 / 9.56 (profiles/r5/config4_nontemporal.log)
+      if (16 * c + (o >> 3) < nrows) __builtin_nontemporal_store(v, dst + 16 * c * kStatFeatures + o);
     }
     tele_lds_fence();
     // the operand tiles are kept zero between uses: clear the stage's 1088 B
@@ -227,7 +232,10 @@ __device__ __forceinline__ void telemetry_tile_mfma(const TelemetryParams& tp, i
   for (int pr = 0; pr < ne; pr += 64 * NB) {
     int2 ev[NB];
 #pragma unroll
-    for (int q = 0; q < NB; ++q) ev[q] = evs[min(pr + 64 * q + lane, elast)];
+    for (int q = 0; q < NB; ++q) {
+      const tele_i32x2 x = __builtin_nontemporal_load(reinterpret_cast<const tele_i32x2*>(evs + min(pr + 64 * q + lane, elast)));
+      ev[q] = make_int2(x.x, x.y);
+    }
 #pragma unroll
   for (int q = 0; q < NB; ++q) {
     const int pb = pr + 64 * q;

@@ -24,6 +24,7 @@
 #   slices     sweep-DP accuracy and 1-GPU step time vs slice size (fixed 80M-match history)
 #   excl       prepass on its own CUs beside the executor on the rest (ANA_PREPASS_EXCLUSIVE sweep)
 #   tele       config 4 telemetry placement (separate / fused / CU-masked overlap)
+#   teleab     config 4 A/B of builds (AB_LIBS), optional tail-point sweep (TELEAB_TAIL_AT)
 #   tail       prepass start point sweep for config 2 (ANA_PREPASS_AT, serial)
 #   ab         in-call A/B of executor builds (AB_LIBS, scripts/ab_build.sh), interleaved rounds
 #   micro      executor hop latency A/B (scripts/tune_rate.py: serial / uniform / skewed, timing build)
@@ -176,6 +177,21 @@ for task in "$@"; do
         ANA_TELE_CUS=$n run tele/overlap_cus$n 400 $PY bench.py --config 4 --steps 10 --warmup 2 --telemetry-mode overlap
       done
       for f in gpurun_out/tele/*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done
+      ;;
+    teleab)  # config 4 A/B of builds (AB_LIBS as for ab): bench step + the standalone aggregation, interleaved
+      for r in $(seq ${TELEAB_ROUNDS:-3}); do
+        for spec in ${AB_LIBS:-cur:}; do
+          name=${spec%%:*}; lib=${spec#*:}
+          ANA_NATIVE_LIB=$lib run teleab/bench_${name}_$r 300 $PY bench.py --config 4 --steps 10 --warmup 2
+          [ "${TELEAB_KERNEL:-1}" = 0 ] || \
+            ANA_NATIVE_LIB=$lib run teleab/kernel_${name}_$r 300 $PY scripts/tune_tele.py --variants impl1 --rounds 1
+          for at in ${TELEAB_TAIL_AT:-}; do
+            ANA_TELE_TAIL_AT=$at ANA_NATIVE_LIB=$lib run teleab/bench_${name}_at${at}_$r 300 $PY bench.py --config 4 \
+                --steps 10 --warmup 2
+          done
+        done
+      done
+      for f in gpurun_out/teleab/bench_*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f)"; done | sort
       ;;
     tail)  # where the next window's prepass starts (ANA_PREPASS_AT sweep, config 2; 0 = with the launch)
       for r in 1 2; do
