@@ -180,7 +180,7 @@ class EngineConfig:
     CHECKPOINT_DIR / _EVERY -- / 1    re-rate checkpoints (runtime/rerate.py)
     ANA_TRACE               0         roctx ranges + Chrome trace (utils/trace.py)
     ANA_CHECK_ROUNDS        0         exact DP race detector: rounds share no player (parallel/exact_dp.py)
-    ANA_RATE_IDLE           0         executor: max s_sleep rounds of an idle wave (0 = 8, < 0 none)
+    ANA_RATE_IDLE           0         executor: max s_sleep rounds of an idle wave (<= 0: none)
     ANA_RATE_LOCAL          1         executor: LDS hand-off of successors the producing wave holds
     ANA_RATE_DIAG           0         executor timing build: per-phase clocks in ctrl[20..47] (ops/rate.diag)
     ANA_RATE_TIGHT          -1        executor: 2K lanes per match instead of the next power of two (-1 auto)

@@ -79,7 +79,7 @@ struct RateParams {
   int32_t epoch;               // 1..255: granule tag word 1 of this launch (word 3 = match)
   const int32_t* epoch_ptr;    // device: read the epoch here instead (graph replays bump it)
   const float* vst;            // vst_points[tier + 1], kVstTiers entries (device/host memory)
-  int32_t idle_spins;          // dataflow: max s_sleep(2) rounds of an idle wave (0 = default 8, < 0 = none)
+  int32_t idle_spins;          // dataflow: max s_sleep(2) rounds of an idle wave (<= 0: none, the default)
   int32_t tight_groups;        // dataflow: 2K lanes per match instead of the next power of two
                                // (-1 auto, 0 off, 1 on)
   int32_t local_handoff;       // dataflow: a successor held by the producing wave is released

@@ -261,7 +261,12 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       tp_m = -1;
     }
   };
-  const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : prm.idle_spins < 0 ? 0u : 8u;
+  // an idle wave polls again at once by default: with most waves idle (skewed windows,
+  // where the critical path crosses waves) a sleeping holder adds its back-off to every
+  // global hand-off -- quadratic skew 193.5 -> 166.4 ms per 10M window, cubic 1528 -> 1457,
+  // configs 2 / 3 unchanged (profiles/r5/idle_backoff_skew.log); ANA_RATE_IDLE = n > 0
+  // restores a back-off of up to n s_sleep(2) rounds
+  const uint32_t max_spins = prm.idle_spins > 0 ? (uint32_t)prm.idle_spins : 0u;
   const int cl = prm.chunk_len;  // matches per ticket (<= kChunk lanes)
   // chunks in the window (hoisted: a 64-bit division is ~130 scalar instructions)
   const int64_t nchunks = (M + cl - 1) / cl;
