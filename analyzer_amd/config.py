@@ -159,7 +159,7 @@ class EngineConfig:
     ======================  ========  =============================================
     variable                default   consumer
     ======================  ========  =============================================
-    ANA_RATE_BLOCKS         512       persistent grid of a window launch (ops/rate.py)
+    ANA_RATE_BLOCKS         0         persistent grid of a window launch (0: 256 or 512 by workload, ops/rate.py)
     ANA_PREPASS_AT          0.7       tail overlap point of the next prepass (runtime/engine.py; 0.9 for
                                       1v1-4v4 windows between DP merges)
     ANA_PREPASS_CUS         0         CU-masked prepass stream, 0 = off (runtime/engine.py)
@@ -199,7 +199,7 @@ class EngineConfig:
     (read once per BatchRater, passed to csrc/bindings.cpp ``rate``).
     """
 
-    rate_blocks: int = 512
+    rate_blocks: int = 0  # 0: per launch (ops/rate.py launch_blocks)
     prepass_at: float = 0.7
     prepass_at_set: bool = False  # ANA_PREPASS_AT given explicitly (else the engine picks per mode)
     prepass_cus: int = 0
@@ -239,7 +239,7 @@ class EngineConfig:
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "EngineConfig":
         return EngineConfig(
-            rate_blocks=int(_env(env, "ANA_RATE_BLOCKS") or 512),
+            rate_blocks=int(_env(env, "ANA_RATE_BLOCKS") or 0),
             prepass_at=float(_env(env, "ANA_PREPASS_AT") or 0.7) if env.get("ANA_PREPASS_AT") != "0" else 0.0,
             prepass_at_set=bool(env.get("ANA_PREPASS_AT")),
             prepass_cus=int(_env(env, "ANA_PREPASS_CUS") or 0),

@@ -175,8 +175,10 @@ class BatchRater:
         self.cfg = cfg or RaterConfig.from_env()
         self.host_fp64 = host_fp64
         ecfg = EngineConfig.from_env()
-        # persistent-grid size of the dataflow launch (4 waves per block)
-        self.blocks = int(blocks or ecfg.rate_blocks)
+        # persistent-grid size of the dataflow launch (4 waves per block): fixed by the
+        # argument or ANA_RATE_BLOCKS, else chosen per launch (launch_blocks)
+        self.fixed_blocks = int(blocks or ecfg.rate_blocks or 0)
+        self.blocks = self.fixed_blocks or 512  # the full grid (aggregation tiles)
         self.knobs = ecfg.rate_knobs()  # executor / fused-telemetry tuning (csrc/bindings.cpp)
         # inline (fused) telemetry up to this many matches per launch, the MFMA kernel after
         # the rating above (scripts/tele_batch.py, profiles/r3/tele_fused_vs_separate_by_batch.log)
@@ -206,7 +208,18 @@ class BatchRater:
         separate), while a worker batch is launch-bound (500 matches: 44 vs 80 us)."""
         return self.has_telemetry(telemetry) and (self.knobs[5] >= 0 or M <= self.tele_fuse_max)
 
-    def chunk_len(self, M: int, telemetry: bool = False) -> int:
+    def launch_blocks(self, K: int = 3, roster_bytes: int = 0) -> int:
+        """Workgroups of a window launch: 256 (one wave per SIMD) for teams of <= 3 over a
+        roster that fits the 256-MB Infinity Cache, else 512.  Measured per workload on
+        MI355X (profiles/r5/executor_grid.log, 256 vs 512): 3v3 over 1M players 6.56 vs
+        6.65 ms per 10M window, config 2 step 7.95 vs 8.01, config 4 8.85 vs 9.35, skewed
+        windows -4.5 / -6 %; 5v5 (config 3) 20.3-20.5 vs 20.1 and 10M players (config 5,
+        1.28-GB roster: the gathers miss to HBM and need the waves) 13.05 vs 11.73."""
+        if self.fixed_blocks:
+            return self.fixed_blocks
+        return 256 if K <= 3 and roster_bytes <= (256 << 20) else 512
+
+    def chunk_len(self, M: int, telemetry: bool = False, blocks: Optional[int] = None) -> int:
         """Matches per executor ticket: 64 (one per lane) for windows, shorter
         (8-32, a power of two) when 64-match chunks would leave the full grid
         (``4 * self.blocks`` waves) short of work.  A wave rates 64/G matches per
@@ -214,22 +227,22 @@ class BatchRater:
         dependent iterations; in 8-match chunks it runs 63 waves x 1."""
         if telemetry:
             return 64
-        need = -(-M // (4 * self.blocks))  # matches per wave at the full grid
+        need = -(-M // (4 * (blocks or self.blocks)))  # matches per wave at the full grid
         cl = 8
         while cl < need and cl < 64:
             cl *= 2
         return cl
 
-    def grid_blocks(self, M: int, telemetry: bool = False) -> int:
-        """Persistent-grid size for a window of M matches: ``self.blocks`` (512,
-        measured best for 10M-match windows), but no more than one wave per
-        chunk (``chunk_len``) -- a micro-batch of 500 matches needs 63 waves, not
-        2048 (the extra workgroups only cost launch and exit time).  Fused
-        telemetry keeps the full grid (its tiles need the waves)."""
+    def grid_blocks(self, M: int, telemetry: bool = False, blocks: Optional[int] = None) -> int:
+        """Persistent-grid size for a window of M matches: ``blocks`` (launch_blocks),
+        but no more than one wave per chunk (``chunk_len``) -- a micro-batch of 500
+        matches needs 63 waves, not 2048 (the extra workgroups only cost launch and exit
+        time).  Fused telemetry tiles keep the full grid (they need the waves)."""
         if telemetry:
             return self.blocks
-        chunks = -(-M // self.chunk_len(M))
-        return max(1, min(self.blocks, -(-chunks // 4)))
+        b = blocks or self.blocks
+        chunks = -(-M // self.chunk_len(M, blocks=b))
+        return max(1, min(b, -(-chunks // 4)))
 
     # ------------------------------------------------------------- buffers
     def vst(self, device) -> torch.Tensor:
@@ -330,6 +343,7 @@ class BatchRater:
             link = deps = ctrl = torch.empty(0, dtype=torch.int32)
             epoch = 1
             ctrl_ready = False
+        blocks = self.launch_blocks(K, roster.state.numel() * roster.state.element_size())
         # aggregation tiles need the full grid and whole chunks; inline aggregation
         # (ANA_TELE_ROLE < 0: each lane group folds its own match's events) does not
         tiles = self.tiles(telemetry, M)
@@ -343,11 +357,11 @@ class BatchRater:
         native().rate(rec, K, link, deps, roster.state, roster.attrs, fp, out.quality, out.status,
                       out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
                       float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
-                      record, self.grid_blocks(M, tiles), epoch,
+                      record, self.grid_blocks(M, tiles, blocks), epoch,
                       self.host_fp64, *telemetry,
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
                       epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
-                      self.chunk_len(M, tiles), ctrl_ready, self.knobs)
+                      self.chunk_len(M, tiles, blocks), ctrl_ready, self.knobs)
         if after is not None:
             # same stream, after the rating; malformed events count into ctrl[13] as in
             # the fused launch (zeroed by this launch, read by telemetry_errors)

@@ -241,7 +241,8 @@ class WindowPipeline:
         if self._signal:
             self._seq += 1
             M = int(prep.rec.shape[0])
-            cl = self.rater.chunk_len(M, self.rater.tiles(telemetry, M))
+            blocks = self.rater.launch_blocks(self.K, self.roster.state.numel() * self.roster.state.element_size())
+            cl = self.rater.chunk_len(M, self.rater.tiles(telemetry, M), blocks)
             at = int(self.tail * ((M + cl - 1) // cl))
             progress = (self._signal, self._seq, at)
         if self.warm and self.cuda:
