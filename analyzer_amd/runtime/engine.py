@@ -13,18 +13,22 @@ Two schedule buffer sets alternate; events order "schedule(i+1) may reuse the
 set that rate(i-1) consumed" and "rate(i) needs schedule(i)".  On the CPU the
 same API runs the host mirror sequentially.
 
-Placement (``ANA_PREPASS_SERIAL``, default auto): for 1v1..4v4 the prepass runs
-on the main stream between launches; for 5v5 it overlaps the executor's tail.
-Measured on MI355X (profiles/r2/prepass_placement.log), the co-running prepass
-slows the 3v3 executor by more than it hides (config 2: 8.07 ms serial vs
-8.34-8.47 ms overlapped at 0.7-0.3), while the 5v5 executor -- 3000+ levels,
-~75% of its wave iterations idle, a 5.4 ms prepass over 125M slots -- absorbs
-it (config 3: 22.12 ms overlapped at 0.7 vs 22.9-23.2 ms serial).
+Placement (``ANA_PREPASS_SERIAL``, default auto): the prepass overlaps the executor's
+tail when the executor leaves room for it, else it runs on the main stream between
+launches.  Room means 5v5 -- 3000+ levels, ~75% of its wave iterations idle, a 5.4 ms
+prepass over 125M slots (config 3: 22.12 ms overlapped at 0.7 vs 22.9-23.2 ms serial,
+profiles/r2/prepass_placement.log) -- or, since round 5, a launch of one wave per SIMD
+(ops/rate.py launch_blocks: 1v1-3v3 over a roster the Infinity Cache holds), whose
+spare wave slots the sort fills: config 2 7.69 ms overlapped at 0.75 vs 7.95 serial,
+config 4 8.62 vs 8.85 (profiles/r5/prepass_overlap_grid256.log).  At two waves per
+SIMD the co-running prepass slows the 3v3 executor by more than it hides (round 2:
+config 2 8.07 ms serial vs 8.34-8.47 overlapped; config 5 at HEAD 11.73 vs 11.77).
 ``ANA_PREPASS_CUS=n`` confines an overlapped prepass to n CUs, and with
 ``ANA_PREPASS_EXCLUSIVE=1`` the rating launches get the other CUs; both measured
 slower than the defaults (profiles/r2/prepass_cu_mask.log, prepass_exclusive_cus.log).
 
-Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.7): the
+Tail overlap (``ANA_PREPASS_AT``, fraction of the window, default 0.7; 0.75 at one wave
+per SIMD): the
 prepass of window i+1 does not start with rate(i) -- co-running the two for the
 whole launch costs the latency-bound executor about as much as the prepass
 itself -- but when rate(i) reaches its tail: the executor stores its launch
@@ -49,6 +53,7 @@ from ..utils.trace import trace_range
 
 CHUNK = 64  # matches per executor ticket of a window (csrc/dataflow.hip kChunk; BatchRater.chunk_len)
 DP_TAIL_AT = 0.9  # tail-overlap start of the next prepass between DP merges (3v3; see tail_point)
+SPARE_TAIL_AT = 0.75  # ... of a window launch at one wave per SIMD (config 2: 0.6-0.8 swept)
 
 
 @dataclass
@@ -75,7 +80,10 @@ class WindowPipeline:
         # tail overlap: signal word + number of the last enqueued rate launch
         self.ecfg = EngineConfig.from_env()
         dp = merger is not None
-        self.serial = self.serial_prepass(self.K, self.ecfg, dp)
+        # the executor's grid for this roster (BatchRater.launch_blocks): at 256 workgroups
+        # (one wave per SIMD) the overlapped prepass has wave slots of its own
+        self.grid = rater.launch_blocks(self.K, roster.state.numel() * roster.state.element_size())
+        self.serial = self.serial_prepass(self.K, self.ecfg, dp, self.grid)
         # DP over real collectives: the placement depends on what one merge's
         # all-reduce costs on this interconnect (probe_placement)
         self.allreduce_probe_ms: Optional[float] = None
@@ -83,9 +91,10 @@ class WindowPipeline:
                 (getattr(merger, "world", 1) > 1 or getattr(merger, "emulate", None) is not None):
             self.serial = self.probe_placement(merger)
         # serial prepass: nothing to overlap, no tail signal -- unless a caller wants the
-        # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail)
-        self.tail = (float(signal_at) if signal_at > 0 else 0.0) if self.serial else \
-            self.tail_point(self.K, self.ecfg, dp)
+        # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail),
+        # which then also starts an overlapped prepass
+        self.tail = float(signal_at) if signal_at > 0 else 0.0 if self.serial else \
+            self.tail_point(self.K, self.ecfg, dp, self.grid)
         # a prepass in the rating's tail streams its sort input with non-temporal loads
         # (ANA_SORT_NT=2), so it evicts less of the roster the executor's drain reads:
         # eight 1.25M windows with forced merges 9.08-9.13 vs 9.32-9.40 ms (with the merge
@@ -121,13 +130,14 @@ class WindowPipeline:
                 self._signal = native().progress_signal(dev)
 
     @staticmethod
-    def serial_prepass(K: int, ecfg: EngineConfig, dp: bool = False) -> bool:
-        """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial
-        below 5v5 -- except under DP merges (``dp``), where the windows are short
-        (k per step) and the tail overlap pays (see the module docstring)."""
+    def serial_prepass(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512) -> bool:
+        """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial below
+        5v5 at two waves per SIMD (``grid`` 512) -- except under DP merges (``dp``), where
+        the windows are short (k per step) and the tail overlap pays (see the module
+        docstring)."""
         if ecfg.prepass_serial is not None:
             return ecfg.prepass_serial
-        return K < 5 and not dp
+        return K < 5 and not dp and grid >= 512
 
     def probe_placement(self, merger) -> bool:
         """Windows between DP merges: serial placement (the next prepass on its own
@@ -152,13 +162,16 @@ class WindowPipeline:
         return ms > thr
 
     @staticmethod
-    def tail_point(K: int, ecfg: EngineConfig, dp: bool = False) -> float:
+    def tail_point(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512) -> float:
         """Where the overlapped prepass starts: ``ANA_PREPASS_AT`` if set, else 0.7,
-        and DP_TAIL_AT for 1v1-4v4 windows between merges (measured: config 2 with 8
-        merges per step, profiles/r3/dp_prepass_placement_k8.log)."""
-        if ecfg.prepass_at_set or K >= 5 or not dp:
+        DP_TAIL_AT for 1v1-4v4 windows between merges (measured: config 2 with 8 merges
+        per step, profiles/r3/dp_prepass_placement_k8.log), SPARE_TAIL_AT for 1v1-4v4
+        windows at one wave per SIMD."""
+        if ecfg.prepass_at_set or K >= 5:
             return ecfg.prepass_at
-        return DP_TAIL_AT
+        if dp:
+            return DP_TAIL_AT
+        return SPARE_TAIL_AT if grid < 512 else ecfg.prepass_at
 
     def _side_stream(self):
         """Side stream of the prepass; ``ANA_PREPASS_CUS=n`` confines it to n CUs

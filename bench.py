@@ -286,17 +286,19 @@ def main(argv=None) -> int:
     if tele is not None and auto_mode and not rater.fuses((tele[0].evoff, tele[0].events, stats), Mw):
         tele_path = "MFMA kernel after the rating (launch > ANA_TELE_FUSE_MAX)"
         # window-sized launches: the MFMA kernel on its own stream, started once the
-        # rating has claimed 0.4 of its chunks (beside the rest of the rating, its drain
-        # and the next prepass): 9.54-9.56 ms against 9.67-9.70 from 0.8 and 9.85 for the
-        # kernel behind the rating (profiles/r4/config4_tail_point_and_c3_warm.log,
-        # telemetry_count_row_and_tail.log); needs hipStreamWaitValue64
+        # rating has claimed 0.5 of its chunks (beside the rest of the rating, its drain
+        # and the next prepass, which the same signal starts when it overlaps): 8.62 ms
+        # against 8.79 from 0.7 and 8.85 with a serial prepass (profiles/r5/
+        # prepass_overlap_grid256.log; round 4 at two waves per SIMD: 0.4 best, 9.54-9.56 vs
+        # 9.67-9.70 from 0.8 and 9.85 behind the rating, config4_tail_point_and_c3_warm.log);
+        # needs hipStreamWaitValue64
         from analyzer_amd.ops.native import native as _native
 
         if not cpu and _native().can_wait_value(dev.index or 0):
             args.telemetry_mode = "tail"
             tele_path = ("MFMA kernel on its own stream from %s of the rating's chunks (launch > "
-                         "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.4"))
-    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.4 if auto_mode else 0.9)) \
+                         "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.5"))
+    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.5 if auto_mode else 0.9)) \
         if tele is not None and args.telemetry_mode == "tail" else 0.0
     pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
     # the DP merge corrects window i's records during window i+1's collective

@@ -150,7 +150,8 @@ def test_skewed_activity_draw(skew):
 
 
 def test_prepass_placement_knob():
-    """ANA_PREPASS_SERIAL: 1/0 force the placement; unset or auto -> serial below 5v5."""
+    """ANA_PREPASS_SERIAL: 1/0 force the placement; unset or auto -> serial below 5v5 at two
+    waves per SIMD; the executor grid per launch (BatchRater.launch_blocks)."""
     from analyzer_amd.config import EngineConfig
     from analyzer_amd.runtime.engine import WindowPipeline
 
@@ -165,6 +166,14 @@ def test_prepass_placement_knob():
     assert WindowPipeline.tail_point(3, auto, dp=True) == 0.9 and WindowPipeline.tail_point(5, auto, dp=True) == 0.7
     assert WindowPipeline.tail_point(3, EngineConfig.from_env({"ANA_PREPASS_AT": "0.5"}), dp=True) == 0.5
     assert WindowPipeline.tail_point(3, auto) == 0.7
+    # one wave per SIMD (256 workgroups: <= 3v3 over a cached roster): the tail overlap from 0.75
+    assert not WindowPipeline.serial_prepass(3, auto, grid=256) and WindowPipeline.serial_prepass(3, on, grid=256)
+    assert WindowPipeline.tail_point(3, auto, grid=256) == 0.75 and WindowPipeline.tail_point(3, auto, dp=True, grid=256) == 0.9
+    from analyzer_amd.ops.rate import BatchRater
+
+    br = BatchRater()
+    assert br.launch_blocks(3, 128 << 20) == 256 and br.launch_blocks(3, 1280 << 20) == 512
+    assert br.launch_blocks(5, 128 << 20) == 512 and BatchRater(blocks=384).launch_blocks(3, 0) == 384
     assert not auto.roster_warm and EngineConfig.from_env({"ANA_ROSTER_WARM": "1"}).roster_warm
 
 
