@@ -84,8 +84,16 @@ struct Batch {
 // match it rated (TelemetryParams::role_stride < 0).  DIAG: the timing build
 // (ANA_RATE_DIAG=1) -- every wave clocks its iterations and its wait with
 // s_memrealtime and adds them to ctrl[20..27] at exit (launch_rate).
-template <int K, int G, int TELE, bool DIAG>
-__global__ void __launch_bounds__(256)
+// WPE: the waves per SIMD the kernel is compiled for.  Plain 1v1-3v3 launches of two
+// waves per SIMD (512 workgroups: config 5's 10M-player roster) take the 4-wave build
+// (<= 128 VGPRs; the 3v3 kernel 137 -> 128, no spills): a radix-sort workgroup of the
+// next window's prepass (2 waves per SIMD of 108-115 VGPRs) then still fits beside
+// them, so that prepass can overlap the rating (config 5 11.73 -> 11.19 ms from 0.1,
+// profiles/r5/executor_vgpr_cap.log).  At one wave per SIMD (256 workgroups) it fits
+// anyway and the uncapped build is 0.01-0.02 ms faster.  Telemetry, diagnostic,
+// tight-group and 4v4 / 5v5 instantiations would spill under the cap.
+template <int K, int G, int TELE, bool DIAG, int WPE = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict__ link,
                      int32_t* deps, float* state, const float* __restrict__ attrs,
                      float* __restrict__ first_prior, float* __restrict__ orows, int64_t orow,
@@ -994,9 +1002,18 @@ int launch_rate(int K, const int32_t* rec, const uint32_t* link, int32_t* deps, 
   // config 3 step 21.5 vs 21.9 ms, profiles/r2/tight_groups.log) -> auto = tight
   // for 5v5 only.
   const bool tight = prm.tight_groups > 0 || (prm.tight_groups < 0 && K == 5);
-#define ANA_RATE_LAUNCH_D(k, g, tele, diag)                                                        \
-  hipLaunchKernelGGL((rate_dataflow_kernel<k, g, tele, diag>), dim3((unsigned)blocks), dim3(256), 0, s, \
+#define ANA_RATE_LAUNCH_W(k, g, tele, diag, w)                                                     \
+  hipLaunchKernelGGL((rate_dataflow_kernel<k, g, tele, diag, w>), dim3((unsigned)blocks), dim3(256), 0, s, \
                      rec, link, deps, state, attrs, first_prior, out.s_mu, out.row, ctrl, prm, tp)
+#define ANA_RATE_LAUNCH_D(k, g, tele, diag)                                                        \
+  do {                                                                                             \
+    if constexpr (tele == 0 && !diag && k <= 3 && (g & (g - 1)) == 0) {                            \
+      if (blocks > 256) ANA_RATE_LAUNCH_W(k, g, tele, diag, 4); /* two waves per SIMD */          \
+      else ANA_RATE_LAUNCH_W(k, g, tele, diag, 1);                                                 \
+    } else {                                                                                       \
+      ANA_RATE_LAUNCH_W(k, g, tele, diag, 1);                                                      \
+    }                                                                                              \
+  } while (0)
 #define ANA_RATE_LAUNCH(k, g)                                      \
   do {                                                             \
     if (tp.evoff && tp.role_stride < 0) ANA_RATE_LAUNCH_D(k, g, 2, false); \

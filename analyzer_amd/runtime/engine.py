@@ -54,6 +54,7 @@ from ..utils.trace import trace_range
 CHUNK = 64  # matches per executor ticket of a window (csrc/dataflow.hip kChunk; BatchRater.chunk_len)
 DP_TAIL_AT = 0.9  # tail-overlap start of the next prepass between DP merges (3v3; see tail_point)
 SPARE_TAIL_AT = 0.75  # ... of a window launch at one wave per SIMD (config 2: 0.6-0.8 swept)
+FULL_TAIL_AT = 0.1  # ... of a 1v1-3v3 launch at two waves per SIMD (config 5: 0-0.7 swept)
 
 
 @dataclass
@@ -131,13 +132,15 @@ class WindowPipeline:
 
     @staticmethod
     def serial_prepass(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512) -> bool:
-        """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial below
-        5v5 at two waves per SIMD (``grid`` 512) -- except under DP merges (``dp``), where
-        the windows are short (k per step) and the tail overlap pays (see the module
+        """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial only for
+        4v4 at two waves per SIMD (``grid`` 512), where a sort workgroup does not fit beside
+        the executor's waves -- 1v1-3v3 launches are compiled to leave it room
+        (csrc/dataflow.hip ANA_EXEC_WPE), 5v5 absorbs it in its idle iterations, and under
+        DP merges (``dp``) the windows are short and the tail overlap pays (see the module
         docstring)."""
         if ecfg.prepass_serial is not None:
             return ecfg.prepass_serial
-        return K < 5 and not dp and grid >= 512
+        return K == 4 and not dp and grid >= 512
 
     def probe_placement(self, merger) -> bool:
         """Windows between DP merges: serial placement (the next prepass on its own
@@ -166,12 +169,12 @@ class WindowPipeline:
         """Where the overlapped prepass starts: ``ANA_PREPASS_AT`` if set, else 0.7,
         DP_TAIL_AT for 1v1-4v4 windows between merges (measured: config 2 with 8 merges
         per step, profiles/r3/dp_prepass_placement_k8.log), SPARE_TAIL_AT for 1v1-4v4
-        windows at one wave per SIMD."""
+        windows at one wave per SIMD, FULL_TAIL_AT for 1v1-3v3 windows at two."""
         if ecfg.prepass_at_set or K >= 5:
             return ecfg.prepass_at
         if dp:
             return DP_TAIL_AT
-        return SPARE_TAIL_AT if grid < 512 else ecfg.prepass_at
+        return SPARE_TAIL_AT if grid < 512 else FULL_TAIL_AT if K <= 3 else ecfg.prepass_at
 
     def _side_stream(self):
         """Side stream of the prepass; ``ANA_PREPASS_CUS=n`` confines it to n CUs

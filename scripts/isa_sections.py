@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Static instruction counts of the dataflow executor, per source section.
 
-    python scripts/isa_sections.py [K G TELE DIAG]   (default: 3 8 0 0, the config 2 launch)
+    python scripts/isa_sections.py [K G TELE DIAG WPE]   (default: 3 8 0 0 1, the config 2 launch;
+                                                          WPE 4 = the build for two waves per SIMD)
 
 Compiles csrc/dataflow.hip for gfx950 with line tables (the production flags of
 build_ext.py plus -gline-tables-only), takes the instantiation
@@ -63,7 +64,7 @@ def classify(op):
 
 
 def main():
-    K, G, TELE, DIAG = (sys.argv[1:5] + ["3", "8", "0", "0"][len(sys.argv[1:5]):])
+    K, G, TELE, DIAG, WPE = (sys.argv[1:6] + ["3", "8", "0", "0", "1"][len(sys.argv[1:6]):])
     diag = "true" if DIAG in ("1", "true") else "false"
     with tempfile.TemporaryDirectory() as td:
         asm = os.path.join(td, "df.s")
@@ -73,7 +74,7 @@ def main():
         subprocess.run(cmd, check=True)
         text = open(asm).read().splitlines()
     files = {}
-    want = "rate_dataflow_kernelILi%sELi%sELi%sELb%dE" % (K, G, TELE, 1 if diag == "true" else 0)
+    want = "rate_dataflow_kernelILi%sELi%sELi%sELb%dELi%sE" % (K, G, TELE, 1 if diag == "true" else 0, WPE)
     start = None
     for i, ln in enumerate(text):
         m = re.match(r'\s*\.file\s+(\d+)\s+"([^"]*)"(?:\s+"([^"]*)")?', ln)
@@ -116,8 +117,8 @@ def main():
         if vgpr and sgpr:
             break
     cols = ["VALU", "SALU", "VMEM", "LDS", "SMEM", "WAIT", "BR", "MFMA", "OTHER"]
-    print("rate_dataflow_kernel<%s, %s, %s, %s>  (VGPRs %s, SGPRs %s), static instructions per section"
-          % (K, G, TELE, diag, vgpr, sgpr))
+    print("rate_dataflow_kernel<%s, %s, %s, %s, %s>  (VGPRs %s, SGPRs %s), static instructions per section"
+          % (K, G, TELE, diag, WPE, vgpr, sgpr))
     print("%-46s" % "section" + "".join("%7s" % c for c in cols) + "  total")
     tot = collections.Counter()
     order = [n for _, n in secs] + sorted(n for n in counts if n.startswith("inlined"))

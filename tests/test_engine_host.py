@@ -150,14 +150,16 @@ def test_skewed_activity_draw(skew):
 
 
 def test_prepass_placement_knob():
-    """ANA_PREPASS_SERIAL: 1/0 force the placement; unset or auto -> serial below 5v5 at two
-    waves per SIMD; the executor grid per launch (BatchRater.launch_blocks)."""
+    """ANA_PREPASS_SERIAL: 1/0 force the placement; unset or auto -> serial only for 4v4 at
+    two waves per SIMD; the executor grid per launch (BatchRater.launch_blocks)."""
     from analyzer_amd.config import EngineConfig
     from analyzer_amd.runtime.engine import WindowPipeline
 
     auto = EngineConfig.from_env({})
     assert auto.prepass_serial is None and EngineConfig.from_env({"ANA_PREPASS_SERIAL": "auto"}).prepass_serial is None
-    assert WindowPipeline.serial_prepass(3, auto) and not WindowPipeline.serial_prepass(5, auto)
+    assert WindowPipeline.serial_prepass(4, auto) and not WindowPipeline.serial_prepass(5, auto)
+    # 1v1-3v3 launches leave a sort workgroup room at either grid (csrc/dataflow.hip ANA_EXEC_WPE)
+    assert not WindowPipeline.serial_prepass(3, auto) and WindowPipeline.tail_point(3, auto) == 0.1
     on, off = (EngineConfig.from_env({"ANA_PREPASS_SERIAL": v}) for v in ("1", "0"))
     assert WindowPipeline.serial_prepass(5, on) and not WindowPipeline.serial_prepass(3, off)
     assert auto.prepass_at == 0.7 and EngineConfig.from_env({"ANA_PREPASS_AT": "0"}).prepass_at == 0.0
@@ -165,7 +167,7 @@ def test_prepass_placement_knob():
     assert not WindowPipeline.serial_prepass(3, auto, dp=True) and WindowPipeline.serial_prepass(3, on, dp=True)
     assert WindowPipeline.tail_point(3, auto, dp=True) == 0.9 and WindowPipeline.tail_point(5, auto, dp=True) == 0.7
     assert WindowPipeline.tail_point(3, EngineConfig.from_env({"ANA_PREPASS_AT": "0.5"}), dp=True) == 0.5
-    assert WindowPipeline.tail_point(3, auto) == 0.7
+    assert WindowPipeline.tail_point(4, auto) == 0.7
     # one wave per SIMD (256 workgroups: <= 3v3 over a cached roster): the tail overlap from 0.75
     assert not WindowPipeline.serial_prepass(3, auto, grid=256) and WindowPipeline.serial_prepass(3, on, grid=256)
     assert WindowPipeline.tail_point(3, auto, grid=256) == 0.75 and WindowPipeline.tail_point(3, auto, dp=True, grid=256) == 0.9
