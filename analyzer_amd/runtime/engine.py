@@ -21,8 +21,12 @@ profiles/r2/prepass_placement.log) -- or, since round 5, a launch of one wave pe
 (ops/rate.py launch_blocks: 1v1-3v3 over a roster the Infinity Cache holds), whose
 spare wave slots the sort fills: config 2 7.69 ms overlapped at 0.75 vs 7.95 serial,
 config 4 8.62 vs 8.85 (profiles/r5/prepass_overlap_grid256.log).  At two waves per
-SIMD the co-running prepass slows the 3v3 executor by more than it hides (round 2:
-config 2 8.07 ms serial vs 8.34-8.47 overlapped; config 5 at HEAD 11.73 vs 11.77).
+SIMD (512 workgroups: config 5) the 1v1-3v3 launch takes a 128-VGPR build
+(csrc/dataflow.hip WPE) that leaves a sort workgroup room: config 5 11.19 ms overlapped
+from 0.1 vs 11.73 serial (profiles/r5/executor_vgpr_cap.log).  Without that room the
+co-running prepass waits for executor workgroups to exit, or slows the executor by more
+than it hides (round 2: config 2 8.07 ms serial vs 8.34-8.47 overlapped); 4v4 at 512
+workgroups stays serial.
 ``ANA_PREPASS_CUS=n`` confines an overlapped prepass to n CUs, and with
 ``ANA_PREPASS_EXCLUSIVE=1`` the rating launches get the other CUs; both measured
 slower than the defaults (profiles/r2/prepass_cu_mask.log, prepass_exclusive_cus.log).
