@@ -160,6 +160,33 @@ def test_device_repeat_launch_deterministic(gpu_device):
     assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32))
 
 
+@pytest.mark.parametrize("K", [2, 3])
+def test_grid_and_register_builds_bit_identical(gpu_device, K):
+    """The launch grid picks the build: at two waves per SIMD (> 256 workgroups) plain
+    1v1-3v3 launches run the kernel compiled for 4 waves per SIMD (128 VGPRs,
+    csrc/dataflow.hip WPE), at <= 256 the unconstrained one.  Grid and build change
+    only when a match runs: every combination gives the bits of the 256-workgroup run."""
+    P, M = 100000, 600000
+    rs = RosterSpec(num_players=P, seed=11)
+    rec = make_stream(StreamSpec(team_size=K, seed=12), M, P, K=K, device=gpu_device)
+    outs = {}
+    for blocks in (256, 512, 64):
+        ro = make_roster(rs, device=gpu_device)
+        rater = R.BatchRater(blocks=blocks)
+        assert rater.launch_blocks(K, ro.state.numel() * ro.state.element_size()) == blocks
+        res = rater.rate(ro, rec, K)
+        assert int(rater.error_flags(gpu_device).sum()) == 0
+        outs[blocks] = (ro.state.cpu(), res.s_mu.cpu(), res.status.cpu(), res.quality.cpu())
+    a = outs[256]
+    for blocks in (512, 64):
+        b = outs[blocks]
+        assert torch.equal(a[0][:, 0::2].contiguous().view(torch.int32),
+                           b[0][:, 0::2].contiguous().view(torch.int32)), blocks
+        assert torch.equal(a[1].view(torch.int32), b[1].view(torch.int32)), blocks
+        assert torch.equal(a[2], b[2]), blocks
+        assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32)), blocks
+
+
 @pytest.mark.parametrize("K,P,M,skew", [(3, 16, 4000, 1), (3, 100000, 1000000, 1), (5, 2000, 200000, 1),
                                         (3, 100000, 300000, 3)])
 def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K, P, M, skew):
