@@ -496,8 +496,16 @@ void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor s2, Tenso
   }
 }
 
-// compressed merge operands: msg [P, 14] bf16/fp16, cnt [P, 2] int32 (sweep.hip);
-// the CPU path goes through the fp32 host mirror and torch's conversions
+// compressed merge operands: msg [P, 14] bf16/fp16, cnt [P, 1] int32 = the two base-16 touch
+// fields packed as lo | hi << 16 (4 + 3 nibbles; sweep.hip); the CPU path goes through the
+// fp32 host mirror and torch's conversions
+static Tensor pack_touch(const Tensor& lohi) {  // [P, 2] float fields -> [P, 1] int32
+  const Tensor x = lohi.to(torch::kInt32);
+  return x.slice(1, 0, 1).bitwise_or(x.slice(1, 1, 2).bitwise_left_shift(16));
+}
+static Tensor unpack_touch(const Tensor& cnt) {  // [P, 1] int32 -> [P, 2] (lo, hi)
+  return torch::cat({cnt.bitwise_and(0xffff), cnt.bitwise_right_shift(16)}, 1);
+}
 void sweep_delta_packed(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor vst, double unknown_sigma,
                         Tensor msg, Tensor cnt) {
   const auto dev = s.device();
@@ -509,7 +517,7 @@ void sweep_delta_packed(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor 
   TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
                   msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
               "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
-  check_rows(cnt, "cnt", P, 2, dev, torch::kInt32);
+  check_rows(cnt, "cnt", P, 1, dev, torch::kInt32);
   check(vst, "vst", torch::kFloat32, dev);
   TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
   if (dev.is_cuda()) {
@@ -525,7 +533,7 @@ void sweep_delta_packed(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor 
                         attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma, true,
                         buf.data_ptr<float>(), P);
   msg.copy_(buf.slice(1, 0, 14));
-  cnt.copy_(buf.slice(1, 14, 16));
+  cnt.copy_(pack_touch(buf.slice(1, 14, 16)));
 }
 
 void prefix_delta(Tensor s0, Tensor prefix, Tensor attrs, Tensor vst, double unknown_sigma, Tensor delta);
@@ -540,7 +548,7 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
   TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
                   msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
               "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
-  check_rows(cnt, "cnt", P, 2, dev, torch::kInt32);
+  check_rows(cnt, "cnt", P, 1, dev, torch::kInt32);
   check_rows(attrs, "attrs", P, 4, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
   float* p2 = nullptr;
@@ -572,7 +580,7 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
     prefix_delta(s0, *prefix, attrs, vst, unknown_sigma, *delta);
   Tensor buf = torch::empty({P, 16}, s.options());
   buf.slice(1, 0, 14).copy_(msg);
-  buf.slice(1, 14, 16).copy_(cnt);
+  buf.slice(1, 14, 16).copy_(unpack_touch(cnt));
   ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
                         s.data_ptr<float>(), p2, true, vst.data_ptr<float>(), (float)unknown_sigma, P, cl);
 }

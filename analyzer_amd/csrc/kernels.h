@@ -90,7 +90,7 @@ int launch_sweep_delta(const float* s0, const float* a, const float* s, const fl
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                        const float* vst, float unknown_sigma, int scaled, int64_t P, uint32_t* clamps,
                        hipStream_t st);
-// compressed merges: msg [P][14] bf16 (bf16 != 0) or fp16 + cnt [P][2] int32
+// compressed merges: msg [P][14] bf16 (bf16 != 0) or fp16 + cnt [P] int32 (touch fields lo | hi << 16)
 int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, const float* attrs,
                               const float* vst, float unknown_sigma, int bf16, void* msg, int32_t* cnt,
                               int64_t P, hipStream_t st);

@@ -200,7 +200,7 @@ sweep_apply_kernel(const float2* __restrict__ s0, const float2* __restrict__ buf
 // ------------------------------------------------- compressed (fp16 / bf16) messages
 // COMM_DTYPE=bf16/fp16 merges write / read the all-reduce operands directly:
 // msg [P][14] in the 16-bit type (round to nearest even, as torch's .to()) --
-// lane t < 7 one 4-B word (its track's two halves) --, cnt [P][2] int32 (the
+// lane t < 7 one 4-B word (its track's two halves) --, cnt [P] int32 (the
 // base-16 touch fields, exact integers; lane 7).
 // The empty asm pins x as the rounded fp32 message: without it the compiler folds
 // the message's last fma into the conversion (v_fma_mixlo_f16, one rounding
@@ -226,7 +226,7 @@ template <typename H>
 __global__ void __launch_bounds__(256)
 sweep_delta_packed_kernel(const float2* __restrict__ s0, const float2* a0, const float4* __restrict__ s,
                           const float4* __restrict__ attrs, const float* __restrict__ vst,
-                          float unknown_sigma, uint32_t* __restrict__ msg, int2* __restrict__ cnt, int64_t P) {
+                          float unknown_sigma, uint32_t* __restrict__ msg, uint32_t* __restrict__ cnt, int64_t P) {
   const TrackLane L = track_lane();
   if (L.p >= P) return;
   float dp, dt, lo, hi;
@@ -234,7 +234,7 @@ sweep_delta_packed_kernel(const float2* __restrict__ s0, const float2* a0, const
   if (L.t < kTracks)  // 14 halves = 7 words (28 B per player, contiguous over the wave)
     merge_st(msg + L.p * kTracks + L.t, (uint32_t)to_half_bits<H>(dp) | ((uint32_t)to_half_bits<H>(dt) << 16));
   else
-    merge_st(cnt + L.p, make_int2((int)lo, (int)hi));
+    merge_st(cnt + L.p, (uint32_t)lo | ((uint32_t)hi << 16));  // 4 + 3 nibbles: 32 B per player on the wire
 }
 
 // prefix (nullable, the scaled exclusive prefix of the messages, H [P][14]) -> delta
@@ -244,13 +244,13 @@ sweep_delta_packed_kernel(const float2* __restrict__ s0, const float2* a0, const
 template <typename H>
 __global__ void __launch_bounds__(256)
 sweep_apply_packed_kernel(const float2* __restrict__ s0, const uint32_t* __restrict__ msg,
-                          const int2* __restrict__ cnt, const float4* __restrict__ attrs, float4* s,
+                          const uint32_t* __restrict__ cnt, const float4* __restrict__ attrs, float4* s,
                           float2* s2, const float* __restrict__ vst, float unknown_sigma, int64_t P,
                           uint32_t* clamps, const uint32_t* __restrict__ pref, float2* __restrict__ delta) {
   const TrackLane L = track_lane();
   if (L.p >= P) return;
   const uint32_t w = L.t < kTracks ? merge_ld(msg + L.p * kTracks + L.t) : 0u;
-  const int2 c = merge_ld(cnt + L.p);  // broadcast within the group
+  const uint32_t c = merge_ld(cnt + L.p);  // broadcast within the group: lo | hi << 16
   if (pref) {  // (before lane_apply: it may overwrite the window start through s2)
     const float2 cs = merge_ld(s0 + L.p * kLanesPerPlayer + L.t);
     const float c0mu = __shfl(cs.x, L.gbase), c0sg = __shfl(cs.y, L.gbase);
@@ -265,8 +265,8 @@ sweep_apply_packed_kernel(const float2* __restrict__ s0, const uint32_t* __restr
     }
     delta[L.p * kLanesPerPlayer + L.t] = make_float2(dpi, dtau);
   }
-  lane_apply(L, s0, from_half_bits<H>(w & 0xffffu), from_half_bits<H>(w >> 16), (uint32_t)c.x,
-             (uint32_t)c.y, attrs, vst, unknown_sigma, true, s, s2, clamps);
+  lane_apply(L, s0, from_half_bits<H>(w & 0xffffu), from_half_bits<H>(w >> 16), c & 0xffffu, c >> 16, attrs,
+             vst, unknown_sigma, true, s, s2, clamps);
 }
 
 // the same delta table on its own (simulations, tests): one lane per track
@@ -389,7 +389,7 @@ int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, c
     hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
                        reinterpret_cast<const float2*>(a), reinterpret_cast<const float4*>(s),
                        reinterpret_cast<const float4*>(attrs), vst, unknown_sigma,
-                       reinterpret_cast<uint32_t*>(msg), reinterpret_cast<int2*>(cnt), P);
+                       reinterpret_cast<uint32_t*>(msg), reinterpret_cast<uint32_t*>(cnt), P);
   };
   if (bf16) args(sweep_delta_packed_kernel<__bf16>);
   else args(sweep_delta_packed_kernel<_Float16>);
@@ -402,7 +402,7 @@ int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* c
   if (P <= 0) return 0;
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
-                       reinterpret_cast<const uint32_t*>(msg), reinterpret_cast<const int2*>(cnt),
+                       reinterpret_cast<const uint32_t*>(msg), reinterpret_cast<const uint32_t*>(cnt),
                        reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
                        reinterpret_cast<float2*>(s2), vst, unknown_sigma, P, clamps,
                        reinterpret_cast<const uint32_t*>(prefix), reinterpret_cast<float2*>(delta));

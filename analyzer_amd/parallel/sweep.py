@@ -149,10 +149,11 @@ class SweepMerger:
         self.prior = None                            # this rank's prior (re-sweeps only; base rows)
         self.buf = torch.empty((self.P, 16), **f)
         # fp16/bf16: merge() writes and reads the all-reduce operands directly
-        # (messages [P, 14] in the comm dtype + touch counts [P, 2] int32)
+        # (messages [P, 14] in the comm dtype + the two touch-count fields packed in one
+        # int32, lo | hi << 16: 32 B per player on the wire)
         self.msg = torch.empty((self.P, 14), dtype=COMM_DTYPES[comm_dtype], device=self.device) \
             if comm_dtype != "fp32" else None
-        self.cnt = torch.empty((self.P, 2), dtype=torch.int32, device=self.device) \
+        self.cnt = torch.empty((self.P, 1), dtype=torch.int32, device=self.device) \
             if comm_dtype != "fp32" else None
         self.vst = torch.tensor(vst_table(), **f)
         self._none = torch.empty(0, **f)
@@ -160,10 +161,10 @@ class SweepMerger:
         # since the last check (sticky, on the device: no sync per merge) -- check() raises
         self.clamps = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.comm_bytes = self.P * (16 * 4 if not self.scaled else
-                                    14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4)
+                                    14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 4)
         if bucket_rows is None:  # ANA_MERGE_BUCKET_MB of all-reduce operands per bucket
             mb = EngineConfig.from_env().merge_bucket_mb
-            row_bytes = 16 * 4 if not self.scaled else 14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 2 * 4
+            row_bytes = 16 * 4 if not self.scaled else 14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 4
             bucket_rows = int(mb * (1 << 20)) // row_bytes if mb > 0 else self.P
         if self.world <= 1:
             # one rank (force): no collective to overlap, so one bucket -- two launches

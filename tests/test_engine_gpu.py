@@ -308,7 +308,7 @@ def test_record_correction_kernel_matches_host(gpu_device, comm):
         native().prefix_delta(g(m.start), g(prefix), g(start.attrs), g(m.vst), 500.0, dd)
         fused = torch.empty((P, 16), device=gpu_device)
         msg = torch.zeros((P, 14), dtype=prefix.dtype, device=gpu_device)
-        cnt = torch.zeros((P, 2), dtype=torch.int32, device=gpu_device)
+        cnt = torch.zeros((P, 1), dtype=torch.int32, device=gpu_device)
         native().sweep_apply_packed(g(m.start), msg, cnt, g(start.attrs), g(start.state).clone(),
                                     g(m.start).clone(), g(m.vst), 500.0, None, g(prefix), fused)
         torch.cuda.synchronize()
@@ -377,12 +377,13 @@ def test_packed_sweep_kernels_match_fp32_path(gpu_device, dtype):
     buf = torch.empty((P, 16), device=gpu_device)
     native().sweep_delta(sb, sb, after.state, start.attrs, vst, 500.0, True, buf)
     msg = torch.empty((P, 14), dtype=dtype, device=gpu_device)
-    cnt = torch.empty((P, 2), dtype=torch.int32, device=gpu_device)
+    cnt = torch.empty((P, 1), dtype=torch.int32, device=gpu_device)
     native().sweep_delta_packed(sb, sb, after.state, start.attrs, vst, 500.0, msg, cnt)
     assert torch.equal(msg.view(torch.int16), buf[:, :14].to(dtype).view(torch.int16))
-    assert torch.equal(cnt, buf[:, 14:].to(torch.int32))
-    msg2, cnt2 = msg * 2, cnt * 2  # a "sum" of two ranks
-    joined = torch.cat([msg2.float(), cnt2.float()], dim=1)
+    lohi = buf[:, 14:].to(torch.int32)  # the touch fields travel packed: lo | hi << 16
+    assert torch.equal(cnt, lohi[:, :1] | (lohi[:, 1:] << 16))
+    msg2, cnt2 = msg * 2, cnt * 2  # a "sum" of two ranks (nibble fields: no carry)
+    joined = torch.cat([msg2.float(), (cnt2 & 0xffff).float(), (cnt2 >> 16).float()], dim=1)
     s_ref, s2_ref = start.state.clone(), torch.zeros_like(sb)
     native().sweep_apply(sb, joined, start.attrs, s_ref, s2_ref, vst, 500.0, True)
     s_p, s2_p = start.state.clone(), torch.zeros_like(sb)
