@@ -483,6 +483,10 @@ def main(argv=None) -> int:
             "dtype": "fp32",
             "data": "synthetic (on-device counter RNG stream, random-init %d-player roster)" % P,
             "merge_ms": merge_ms,
+            # how the step was scheduled: the executor's grid (ops/rate.py launch_blocks) and
+            # where the next window's prepass ran (runtime/engine.py placement)
+            "schedule": {"executor_workgroups": pipe.grid,
+                         "prepass": ("serial" if pipe.serial else "rating tail %.2f" % pipe.tail)},
             "verify": verify,
             "accuracy": accuracy,
             "rccl_world": dist.get_world_size() if world > 1 else None,
