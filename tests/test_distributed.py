@@ -585,3 +585,38 @@ def test_record_correction_over_ranks_equals_simulation(tmp_path, comm_dtype):
     med_c = compare(sim, exact, corrected, out_e)["records_shared_mu"]["dmu_median"]
     med_p = compare(sim, exact, plain, out_e)["records_shared_mu"]["dmu_median"]
     assert med_c < 0.6 * med_p, (med_c, med_p)
+
+
+def test_packed_touch_word_decodes_like_the_fp32_fields():
+    """The compressed merge carries the two base-16 touch fields in one int32 (lo | hi << 16:
+    tracks 0-3 in lo, 4-6 in hi).  On the host path, the packed decode of a sum with touch
+    counts on every track -- mode tracks (hi) included -- equals the fp32 decode of the same
+    fields, and the packed messages round-trip the fields exactly."""
+    from analyzer_amd.models.tiers import vst_table
+    from analyzer_amd.ops.native import native
+    from analyzer_amd.ops.rate import BatchRater
+    from analyzer_amd.parallel.sweep import base_rows
+
+    P = 3000
+    start = make_roster(RosterSpec(num_players=P, seed=5, p_rated=0.7))
+    after = start.clone()
+    BatchRater().rate(after, make_stream(StreamSpec(team_size=3, seed=6), 12000, P), 3)
+    vst = torch.tensor(vst_table(), dtype=torch.float32)
+    sb = base_rows(start.state).contiguous()
+    buf = torch.empty((P, 16))
+    native().sweep_delta(sb, sb, after.state, start.attrs, vst, 500.0, True, buf)
+    msg = torch.empty((P, 14), dtype=torch.bfloat16)
+    cnt = torch.empty((P, 1), dtype=torch.int32)
+    native().sweep_delta_packed(sb, sb, after.state, start.attrs, vst, 500.0, msg, cnt)
+    lohi = buf[:, 14:].to(torch.int32)
+    assert torch.equal(cnt, lohi[:, :1] | (lohi[:, 1:] << 16))
+    assert int((lohi[:, 1] > 0).sum()) > 0, "some mode track (hi field) must be touched"
+    # a "sum" over three ranks: every nibble x3 (no carry below 16)
+    msg3, cnt3 = (msg.float() * 3).to(torch.bfloat16), cnt * 3
+    joined = torch.cat([msg3.float(), (cnt3 & 0xffff).float(), (cnt3 >> 16).float()], dim=1)
+    s_ref, s2_ref = start.state.clone(), torch.zeros_like(sb)
+    native().sweep_apply(sb, joined, start.attrs, s_ref, s2_ref, vst, 500.0, True)
+    s_p, s2_p = start.state.clone(), torch.zeros_like(sb)
+    native().sweep_apply_packed(sb, msg3, cnt3, start.attrs, s_p, s2_p, vst, 500.0)
+    assert torch.equal(s_p.nan_to_num(-7), s_ref.nan_to_num(-7))
+    assert torch.equal(s2_p.nan_to_num(-7), s2_ref.nan_to_num(-7))
