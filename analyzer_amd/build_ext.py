@@ -27,7 +27,8 @@ BUILD = PKG.parent / "build" / "analyzer_amd"
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
-HIP_SOURCES = ["kernels.hip", "radix_sort.hip", "dataflow.hip", "sweep.hip", "telemetry.hip", "levels.hip"]
+HIP_SOURCES = ["kernels.hip", "radix_sort.hip", "dataflow.hip", "sweep.hip", "telemetry.hip", "levels.hip",
+               "digest.hip"]
 # per-file device flags.  The executor's divisions/sqrt take the 1-ulp hardware
 # paths (v_rcp_f32 instead of the ~10-instruction IEEE division expansion: -9%
 # static instructions); NaN/Inf semantics are untouched (no -ffinite-math-only),

@@ -841,6 +841,26 @@ void warm_rows(Tensor state, Tensor sink) {
             "warm_rows");
 }
 
+// runtime/rerate.py window digest of the packed output rows (digest.hip); out [3 + 10K] fp64
+void records_digest(Tensor rows, int64_t K, Tensor scratch, Tensor out) {
+  const auto dev = rows.device();
+  check(rows, "rows", torch::kFloat32, dev);
+  check(scratch, "scratch", torch::kFloat64, dev);
+  check(out, "out", torch::kFloat64, dev);
+  TORCH_CHECK(K >= 1 && K <= 5, "records_digest: K in 1..5");
+  TORCH_CHECK(rows.dim() == 2 && rows.size(1) >= 10 * K + 2 && rows.size(1) % 4 == 0,
+              "records_digest: rows must be the packed [M, W] output rows");
+  TORCH_CHECK(out.numel() == 3 + 10 * K, "records_digest: out needs 3 + 10K doubles");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(rows.data_ptr()) % 16 == 0, "records_digest: rows must be 16-B aligned");
+  TORCH_CHECK(dev.is_cuda(), "records_digest: device rows (the host path is runtime/rerate.py window_digest)");
+  TORCH_CHECK((size_t)scratch.numel() >= ana::records_digest_scratch_doubles((int)K), "records_digest: scratch too small");
+  check_hip(ana::launch_records_digest((int)K, rows.data_ptr<float>(), rows.size(0), rows.size(1),
+                                       scratch.data_ptr<double>(), out.data_ptr<double>(), stream_of(rows)),
+            "records_digest");
+}
+
+int64_t records_digest_scratch(int64_t K) { return (int64_t)ana::records_digest_scratch_doubles((int)K); }
+
 void reset_tags(Tensor state) {
   const auto dev = state.device();
   check(state, "state", torch::kFloat32, dev);
@@ -909,6 +929,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stream_wait_value64", &stream_wait_value64, "hipStreamWaitValue64(stream, ptr, >= value)");
   m.def("can_wait_value", &can_wait_value, "hipDeviceAttributeCanUseStreamWaitValue");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
+  m.def("records_digest", &records_digest, "deterministic fp64 digest of a window's packed output rows");
+  m.def("records_digest_scratch", &records_digest_scratch, "scratch doubles of records_digest");
   m.def("emulate_allreduce", &emulate_allreduce,
         "DP pricing on one GPU: an all-reduce stand-in (buffer unchanged) on N CUs for >= us microseconds");
   m.def("warm_rows", &warm_rows, "read every roster row once (cache warm-up before a rating launch)");

@@ -113,6 +113,8 @@ class _ServerConn:
             return ch.basic_consume(self._deliver, queue=f[2])
         elif op == "depth":
             return b.depth(f[2])
+        elif op == "in_flight":
+            return self.server.in_flight(f[2])
         elif op == "stats":
             return self.server.stats()
         else:
@@ -132,7 +134,7 @@ class _ServerConn:
                             res, err = self._apply(f), None
                         except Exception as e:  # reported to a request, else dropped with the connection
                             res, err = None, "%s: %s" % (type(e).__name__, e)
-                        if f[0] in ("declare", "bind", "qos", "consume", "depth", "stats"):
+                        if f[0] in ("declare", "bind", "qos", "consume", "depth", "in_flight", "stats"):
                             self.out.put(_pack(["reply", f[1], res, err]))
                         elif err is not None:
                             raise RuntimeError(err)
@@ -213,6 +215,16 @@ class BrokerServer:
             for b in bodies:
                 self.broker.publish("", queue, b if isinstance(b, bytes) else str(b).encode(), BasicProperties())
         self.pump()
+
+    def in_flight(self, queue: str) -> int:
+        """Messages of ``queue`` not yet settled anywhere: ready ones plus every open
+        consumer's unacknowledged deliveries.  A replica may only leave when this is
+        zero -- if another replica still holds a prefetch window and dies, its
+        deliveries are requeued and need a consumer (at-least-once)."""
+        with self.lock:
+            b = self.broker
+            held = sum(1 for c in b.channels if c.is_open for m in c.unacked.values() if m.queue == queue)
+            return b.depth(queue) + held
 
     def stats(self) -> Dict[str, object]:
         with self.lock:
@@ -308,8 +320,9 @@ class NetBroker:
 
     ``run`` delivers and fires timers until ``stop()`` / ``until()``; with ``idle_exit``
     (default) it also returns once nothing is in flight here, no timer is pending and
-    the server reports the consumed queue empty -- a replica drains the queue and exits,
-    as the in-process broker's loop does."""
+    the server reports nothing of the consumed queue unsettled -- neither ready nor held
+    unacknowledged by another replica (which could still die and have its window
+    requeued) -- so the last replica leaves only when the queue is truly drained."""
 
     def __init__(self, host: str, port: int, clock: Optional[Callable[[], float]] = None):
         self.clock = clock or time.monotonic
@@ -381,6 +394,10 @@ class NetBroker:
     def depth(self, queue: str) -> int:
         return int(self._request("depth", queue))
 
+    def in_flight(self, queue: str) -> int:
+        """Ready + unacknowledged-anywhere messages of ``queue`` (BrokerServer.in_flight)."""
+        return int(self._request("in_flight", queue))
+
     def stats(self) -> Dict[str, object]:
         return self._request("stats")
 
@@ -427,7 +444,7 @@ class NetBroker:
             if self._read(wait):
                 continue
             if (idle_exit and dl is None and queue is not None and not self._ch.outstanding
-                    and not self._deliveries and self.depth(queue) == 0):
+                    and not self._deliveries and self.in_flight(queue) == 0):
                 # nothing here or in the queue; a last look for deliveries sent meanwhile
                 if not self._read(0.05) and not self._deliveries:
                     return

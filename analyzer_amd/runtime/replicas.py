@@ -27,6 +27,21 @@ import time
 from typing import Dict, List, Optional
 
 
+def _visible_devices(env: Dict[str, str], n: int) -> List[str]:
+    """The HIP_VISIBLE_DEVICES values the children may use: the entries of the
+    parent's own HIP_VISIBLE_DEVICES (or CUDA_VISIBLE_DEVICES, which HIP also reads)
+    when it runs under one (e.g. '4,5'), else 0..n-1 -- replica r gets entry r mod n,
+    never a raw index outside the parent's set.  ROCR_VISIBLE_DEVICES is inherited by
+    the children and HIP indexes within it, so there 0..n-1 is already right."""
+    for key in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(key)
+        if v:
+            ids = [x.strip() for x in v.split(",") if x.strip()]
+            if ids:
+                return ids[:n] if n > 0 else ids
+    return [str(i) for i in range(n)]
+
+
 def _gpus() -> int:
     """Devices visible to the children (counting does not initialise the GPU here)."""
     try:
@@ -80,7 +95,8 @@ def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 
         e.update(RABBITMQ_URI=server.uri, DATABASE_URI=database_uri, QUEUE=queue, REPLICA=str(r))
         e.update((replica_env or {}).get(r, {}))
         if gpus > 0:  # one replica per GPU (round-robin when there are more replicas)
-            e["HIP_VISIBLE_DEVICES"] = str(r % gpus)
+            ids = _visible_devices(base, gpus)
+            e["HIP_VISIBLE_DEVICES"] = ids[r % len(ids)]
         # output to files: a replica blocked on a full pipe would hold its deliveries
         fo, fe = tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")
         procs.append((subprocess.Popen([sys.executable, worker_py], env=e, stdout=fo, stderr=fe), fo, fe))
@@ -107,6 +123,10 @@ def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 
         results.append(json.loads(line[-1]) if line else {"error": err[-2000:]})
     dt = time.perf_counter() - t0
     stats = server.stats()
+    # messages neither acked nor dead-lettered when the last replica left (ready, or
+    # held by a replica that exited without settling them): lost work -- the launcher
+    # reports it and worker.py --replicas exits non-zero
+    unsettled = server.in_flight(queue)
     server.close()
     total = sum(int(r.get("matches", 0)) for r in results)
     return {"replicas": n, "gpus": gpus, "matches": total, "enqueued": len(ids),
@@ -115,4 +135,5 @@ def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 
             "seconds": dt, "matches_per_s": total / dt if dt > 0 else None,
             "per_replica": [{"matches": r.get("matches"), "acked": r.get("acked"),
                              "matches_per_s": r.get("matches_per_s"), "error": r.get("error")} for r in results],
-            "exit_codes": codes, "broker": stats, "database_uri": database_uri}
+            "exit_codes": codes, "broker": stats, "unsettled": unsettled,
+            "ok": unsettled == 0 and all(c == 0 for c in codes), "database_uri": database_uri}

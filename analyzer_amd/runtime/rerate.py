@@ -86,10 +86,34 @@ def window_slice(spec: RerateSpec, g: int, rank: int, size: int):
     return lo, max(lo, hi)
 
 
+class _Digest:
+    """Per-window digests on the device: one deterministic streaming pass over the
+    packed output rows (csrc/digest.hip) -- 7 torch nansum passes and a bincount
+    before, 8.5 ms per 16M-match window (profiles/r6/rerate_attribution.log)."""
+
+    def __init__(self):
+        self._scratch = {}
+
+    def __call__(self, res: R.RateResult, K: int) -> torch.Tensor:
+        rows = res.packed
+        if rows is None or not rows.is_cuda:
+            return window_digest(res)
+        from ..ops.native import native
+
+        key = (rows.device, K)
+        if key not in self._scratch:
+            self._scratch[key] = torch.empty(native().records_digest_scratch(K), dtype=torch.float64,
+                                             device=rows.device)
+        out = torch.empty(3 + 10 * K, dtype=torch.float64, device=rows.device)
+        native().records_digest(rows, K, self._scratch[key], out)
+        return out
+
+
 def window_digest(res: R.RateResult) -> torch.Tensor:
-    """[2 + 5*2K + 1] fp64 on the device: matches with records (rated / AFK /
-    invalid), participant records written (non-NULL shared mu), then the column
-    sums of the five per-slot outputs and quality over written values."""
+    """[2 + 5*2K + 1] fp64: matches with records (rated / AFK / invalid),
+    participant records written (non-NULL shared mu), then the column sums of the
+    five per-slot outputs and quality over written values (the host / unpacked
+    path; on the device ``_Digest`` computes the same in one kernel)."""
     S = res.s_mu.shape[1]
     st = res.status
     wrote = (st == R.RATED) | (st == R.AFK) | (st == R.INVALID_ROSTERS)
@@ -136,6 +160,7 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
     total = n_windows(spec, size)
     counts = torch.zeros(256, dtype=torch.int64, device=dev)
     digests = {}
+    digest = _Digest()
     sspec = spec.stream_spec()
     outs = [None, None]  # double-buffered: the sink copies one while the next is rated
     host_stats = {"windows": 0, "participant_records": 0}
@@ -170,7 +195,7 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
         pipe.results_ready(res)  # the DP merge's deferred record correction of these rows
         counts += torch.bincount(res.status.to(torch.int64), minlength=256)
         if records == "digest":
-            digests[g] = window_digest(res)
+            digests[g] = digest(res, K)
         elif sink is not None:
             sink.push(window_slice(spec, g, rank, size)[0], res)
         rated += M
@@ -186,11 +211,16 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
                     ck.maybe_save(g + 1, roster, {"spec": asdict(spec), "world": size,
                                                   "next_offset": window_slice(spec, g + 1, 0, size)[0]})
         if fault_kill_after is not None and g + 1 >= fault_kill_after:
+            # the simulated crash hits once the checkpoints submitted so far are
+            # committed (asynchronous writes, runtime/checkpoint.py): a real crash
+            # loses the ones still in flight and resumes from the one before
+            ck.flush()
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             raise InjectedFault(17)
     if sink is not None:
         sink.flush()
+    ck.flush()  # the run ends when its last checkpoint is committed
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0

@@ -90,3 +90,49 @@ def test_replica_death_redelivers_to_the_others(tmp_path):
     assert res["broker"]["dead_lettered"] == 0
     n_single = _rated(res["database_uri"])
     assert n_single[1] == 600 and n_single[0] >= 550
+
+
+def test_idle_exit_waits_for_other_replicas_unacked_windows():
+    """A consumer with nothing of its own in flight must not leave while another
+    consumer still holds unacknowledged deliveries: if that one dies, its window is
+    requeued and needs a consumer (at-least-once; BrokerServer.in_flight)."""
+    srv = BrokerServer().start()
+    try:
+        srv.publish("q", [b"m%d" % i for i in range(4)])
+        a = connect(srv.uri)
+        ca = a.channel()
+        ca.basic_qos(prefetch_count=10)
+        held = []
+        ca.basic_consume(lambda ch, m, p, body: held.append(m.delivery_tag), queue="q")
+        while len(held) < 4:
+            a._read(0.05)
+            a.process_data_events()
+        assert srv.in_flight("q") == 4 and srv.stats()["depth"]["q"] == 0
+        b = connect(srv.uri)
+        cb = b.channel()
+        cb.basic_qos(prefetch_count=10)
+        got = []
+
+        def on(ch, m, p, body):
+            got.append(body)
+            ch.basic_ack(m.delivery_tag)
+        cb.basic_consume(on, queue="q")
+        t = threading.Thread(target=b.run)
+        t.start()
+        t.join(0.5)
+        assert t.is_alive()  # the queue is empty, but a's window is not settled
+        a.close()            # a dies holding 4 deliveries: they go to b
+        t.join(10.0)
+        assert not t.is_alive() and len(got) == 4
+        assert srv.in_flight("q") == 0
+        b.close()
+    finally:
+        srv.close()
+
+
+def test_visible_device_mapping_follows_the_parent():
+    from analyzer_amd.runtime.replicas import _visible_devices
+
+    assert _visible_devices({"HIP_VISIBLE_DEVICES": "4,5"}, 2) == ["4", "5"]
+    assert _visible_devices({}, 3) == ["0", "1", "2"]
+    assert _visible_devices({"ROCR_VISIBLE_DEVICES": "6,7"}, 2) == ["0", "1"]

@@ -110,3 +110,44 @@ def test_time_axis_sharded_rerate_two_ranks(tmp_path, sweeps):
         assert float(err.median()) < 25.0
     else:  # sweeps == ranks: the exact sequential result up to fp32 rounding
         assert float(err.max()) < 0.05
+
+
+def test_checkpoint_format2_and_format1_compat(tmp_path):
+    """Format 2 keeps (mu, sigma) + attrs (80 B per player, no tags); a format-1
+    directory (full [P, 32] rows) still loads, with its tags reset."""
+    from safetensors.torch import save_file
+    import json
+
+    roster = make_roster(SPEC.roster_spec())
+    roster.state.view(-1, 8, 4)[:, :, 1::2] = 3.0  # tags: never saved
+    checkpoint.save(str(tmp_path / "c2"), roster, {"x": 1})
+    from safetensors.torch import load_file
+    t = load_file(str(tmp_path / "c2" / checkpoint.TENSORS))
+    assert sorted(t) == ["attrs", "base"] and tuple(t["base"].shape) == (SPEC.players, 16)
+    r2, meta = checkpoint.load(str(tmp_path / "c2"))
+    assert meta["format"] == 2
+    base = lambda s: s.view(-1, 8, 4)[:, :, 0::2].nan_to_num(-7)  # noqa: E731
+    assert torch.equal(base(r2.state), base(roster.state))
+    assert float(r2.state.view(-1, 8, 4)[:, :, 1::2].abs().max()) == 0.0
+    d1 = tmp_path / "c1"
+    d1.mkdir()
+    save_file({"state": roster.state.contiguous(), "attrs": roster.attrs.contiguous()}, str(d1 / checkpoint.TENSORS))
+    (d1 / checkpoint.META).write_text(json.dumps({"format": 1, "windows_done": 3}))
+    r1, meta1 = checkpoint.load(str(d1))
+    assert meta1["windows_done"] == 3 and torch.equal(base(r1.state), base(roster.state))
+
+
+def test_async_checkpointer_on_host(tmp_path):
+    """The asynchronous writer's host path: two buffers, back-pressure, every
+    submitted checkpoint committed by flush, the last one wins."""
+    roster = make_roster(SPEC.roster_spec())
+    ck = checkpoint.AsyncCheckpointer("cpu", SPEC.players, buffers=2, fsync=False)
+    p = str(tmp_path / "latest")
+    for i in range(5):
+        roster.state[:, 0].add_(1.0)
+        ck.submit(p, roster, {"windows_done": i + 1})
+    ck.flush()
+    assert ck.written == 5
+    r, meta = checkpoint.load(p)
+    assert meta["windows_done"] == 5
+    assert torch.equal(r.state[:, 0].nan_to_num(-7), roster.state[:, 0].nan_to_num(-7))

@@ -83,7 +83,7 @@ def main(argv=None) -> int:
         res = run_replicas(args.replicas, synthetic=args.synthetic, players=args.players,
                            team_size=args.team_size, seed=args.seed)
         print(json.dumps(res), flush=True)
-        return 0 if all(c == 0 for c in res["exit_codes"]) else 1
+        return 0 if res["ok"] else 1
     connect()
     if args.synthetic:
         from analyzer_amd.runtime.source import populate, publish
