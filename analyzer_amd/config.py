@@ -47,6 +47,11 @@ def _tristate(v: Optional[str]) -> Optional[bool]:
 def _resident_default(env: Mapping[str, str]) -> bool:
     v = env.get("RESIDENT")
     if v:
+        # several replicas on one store (runtime/replicas.py sets REPLICA, a tcp:// broker):
+        # a resident roster would keep rating from its own cached rows and overwrite the
+        # other replicas' commits -- the device rows are re-read from the store per batch
+        if v == "true" and (env.get("REPLICA") or (env.get("RABBITMQ_URI") or "").startswith("tcp://")):
+            return False
         return v == "true"
     uri = env.get("DATABASE_URI") or ""
     return uri == "" or uri.startswith(("memory:", "columnar:"))
@@ -115,6 +120,10 @@ class WorkerConfig:
     # many processed batches, holding its unacknowledged deliveries (replica death:
     # the broker redelivers them to the other replicas, runtime/replicas.py)
     fault_exit_after: int = 0
+    # new: replicas on one SQL store (runtime/store.py versioned player rows): a batch whose
+    # compare-and-set player writes find a row another replica changed since it was read is
+    # rolled back and rated again from fresh rows, up to this many times (then it fails)
+    cas_retries: int = 50
 
     @staticmethod
     def from_env(env: Mapping[str, str] = os.environ) -> "WorkerConfig":
@@ -142,6 +151,7 @@ class WorkerConfig:
             pipeline=env.get("PIPELINE") == "true",
             fault_poison=frozenset(x for x in (env.get("FAULT_POISON") or "").split(",") if x),
             fault_exit_after=int(env.get("FAULT_EXIT_AFTER") or 0),
+            cas_retries=int(env.get("CAS_RETRIES") or 50),
         )
 
     @property

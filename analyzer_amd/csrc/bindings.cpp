@@ -499,6 +499,20 @@ void sweep_apply(Tensor s0, Tensor buf, Tensor attrs, Tensor s, Tensor s2, Tenso
 // compressed merge operands: msg [P, 14] bf16/fp16, cnt [P, 1] int32 = the two base-16 touch
 // fields packed as lo | hi << 16 (4 + 3 nibbles; sweep.hip); the CPU path goes through the
 // fp32 host mirror and torch's conversions
+// msg: [P, 14] rows with unit column stride and an even row stride (a separate [P, 14]
+// tensor, or columns 0..13 of the split collective's [P, 16] operand rows); cnt: [P, 1] int32
+// with any row stride (its own tensor, or word 7 of those rows)
+static void check_operands(const Tensor& msg, const Tensor& cnt, int64_t P, const torch::Device& dev) {
+  TORCH_CHECK(msg.device() == dev && msg.dim() == 2 && msg.size(0) == P && msg.size(1) == 14 &&
+                  msg.stride(1) == 1 && msg.stride(0) % 2 == 0 &&
+                  (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
+              "msg must be [P, 14] bf16/fp16 rows (unit column stride, even row stride) on the state's device");
+  TORCH_CHECK(cnt.device() == dev && cnt.scalar_type() == torch::kInt32 && cnt.dim() == 2 && cnt.size(0) == P &&
+                  cnt.size(1) == 1,
+              "cnt must be [P, 1] int32 on the state's device");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(msg.data_ptr()) % 4 == 0, "msg rows must be 4-B aligned");
+}
+
 static Tensor pack_touch(const Tensor& lohi) {  // [P, 2] float fields -> [P, 1] int32
   const Tensor x = lohi.to(torch::kInt32);
   return x.slice(1, 0, 1).bitwise_or(x.slice(1, 1, 2).bitwise_left_shift(16));
@@ -514,17 +528,15 @@ void sweep_delta_packed(Tensor s0, Tensor prior, Tensor s, Tensor attrs, Tensor 
   check_rows(prior, "prior (base rows)", P, ana::kBaseFloats, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
   check_rows(attrs, "attrs", P, 4, dev);
-  TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
-                  msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
-              "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
-  check_rows(cnt, "cnt", P, 1, dev, torch::kInt32);
+  check_operands(msg, cnt, P, dev);
   check(vst, "vst", torch::kFloat32, dev);
   TORCH_CHECK(vst.numel() == ana::kVstTiers, "vst must have 31 entries");
   if (dev.is_cuda()) {
     check_hip(ana::launch_sweep_delta_packed(s0.data_ptr<float>(), prior.data_ptr<float>(), s.data_ptr<float>(),
                                              attrs.data_ptr<float>(), vst.data_ptr<float>(), (float)unknown_sigma,
                                              msg.scalar_type() == torch::kBFloat16 ? 1 : 0, msg.data_ptr(),
-                                             cnt.data_ptr<int32_t>(), P, stream_of(s)),
+                                             cnt.data_ptr<int32_t>(), P, stream_of(s), msg.stride(0) / 2,
+                                             cnt.stride(0)),
               "sweep_delta_packed");
     return;
   }
@@ -545,10 +557,7 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
   uint32_t* cl = clamp_ptr(clamps, dev);
   const int64_t P = s.size(0);
   check_rows(s0, "s0 (base rows)", P, ana::kBaseFloats, dev);
-  TORCH_CHECK(msg.device() == dev && msg.is_contiguous() && msg.dim() == 2 && msg.size(0) == P &&
-                  msg.size(1) == 14 && (msg.scalar_type() == torch::kBFloat16 || msg.scalar_type() == torch::kHalf),
-              "msg must be a contiguous [P, 14] bf16/fp16 tensor on the state's device");
-  check_rows(cnt, "cnt", P, 1, dev, torch::kInt32);
+  check_operands(msg, cnt, P, dev);
   check_rows(attrs, "attrs", P, 4, dev);
   check_rows(s, "state", P, ana::kRowFloats, dev);
   float* p2 = nullptr;
@@ -563,7 +572,7 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
     TORCH_CHECK(delta.has_value() && delta->defined(), "a prefix needs a delta table");
     TORCH_CHECK(prefix->scalar_type() == msg.scalar_type() && prefix->is_contiguous() && prefix->device() == dev &&
                     prefix->sizes() == msg.sizes(),
-                "prefix must be like msg");
+                "prefix must be a contiguous [P, 14] tensor of msg's type");
     check_rows(*delta, "delta", P, 16, dev);
   }
   if (dev.is_cuda()) {
@@ -572,7 +581,8 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
                                              attrs.data_ptr<float>(), s.data_ptr<float>(), p2,
                                              vst.data_ptr<float>(), (float)unknown_sigma, P, cl,
                                              with_prefix ? prefix->data_ptr() : nullptr,
-                                             with_prefix ? delta->data_ptr<float>() : nullptr, stream_of(s)),
+                                             with_prefix ? delta->data_ptr<float>() : nullptr, stream_of(s),
+                                             msg.stride(0) / 2, cnt.stride(0)),
               "sweep_apply_packed");
     return;
   }
@@ -583,6 +593,28 @@ void sweep_apply_packed(Tensor s0, Tensor msg, Tensor cnt, Tensor attrs, Tensor 
   buf.slice(1, 14, 16).copy_(unpack_touch(cnt));
   ana::host_sweep_apply(s0.data_ptr<float>(), buf.data_ptr<float>(), attrs.data_ptr<float>(),
                         s.data_ptr<float>(), p2, true, vst.data_ptr<float>(), (float)unknown_sigma, P, cl);
+}
+
+// the split collective's owner reduce (sweep.hip): recv [N * blk, 8] int32 words of
+// bf16 / fp16 halves + the touch word -> total [blk, 8] and, when given, the exclusive
+// prefixes pref [N * blk, 7] (device tensors; the CPU path is parallel/comm.py)
+void sweep_block_reduce(Tensor recv, int64_t N, bool bf16, Tensor total, const c10::optional<Tensor>& pref) {
+  const auto dev = recv.device();
+  TORCH_CHECK(dev.is_cuda(), "sweep_block_reduce: device tensors (the host path is parallel/comm.py)");
+  check(recv, "recv", torch::kInt32, dev);
+  check(total, "total", torch::kInt32, dev);
+  TORCH_CHECK(N >= 1 && recv.dim() == 2 && recv.size(1) == 8 && recv.size(0) % N == 0, "recv must be [N * blk, 8]");
+  const int64_t blk = recv.size(0) / N;
+  TORCH_CHECK(total.dim() == 2 && total.size(0) == blk && total.size(1) == 8, "total must be [blk, 8]");
+  int32_t* pp = nullptr;
+  if (pref.has_value() && pref->defined() && pref->numel()) {
+    check(*pref, "pref", torch::kInt32, dev);
+    TORCH_CHECK(pref->dim() == 2 && pref->size(0) == N * blk && pref->size(1) == 7, "pref must be [N * blk, 7]");
+    pp = pref->data_ptr<int32_t>();
+  }
+  check_hip(ana::launch_sweep_block_reduce(recv.data_ptr<int32_t>(), (int)N, blk, bf16 ? 1 : 0,
+                                           total.data_ptr<int32_t>(), pp, stream_of(recv)),
+            "sweep_block_reduce");
 }
 
 // causal record correction of a window's records (parallel/sweep.py): rows = RateResult
@@ -789,6 +821,14 @@ void stream_wait_value64(int64_t stream, int64_t ptr, int64_t value) {
             "hipStreamWaitValue64");
 }
 
+// the host side of a tail gate: write ``value`` to the signal word in stream order (releases
+// waiters whose launch will not come, runtime/engine.py)
+void stream_write_value64(int64_t stream, int64_t ptr, int64_t value) {
+  check_hip((int)hipStreamWriteValue64(reinterpret_cast<hipStream_t>((intptr_t)stream),
+                                       reinterpret_cast<void*>((intptr_t)ptr), (uint64_t)value, 0),
+            "hipStreamWriteValue64");
+}
+
 bool can_wait_value(int64_t device) {
   int v = 0;
   return hipDeviceGetAttribute(&v, hipDeviceAttributeCanUseStreamWaitValue, (int)device) ==
@@ -907,6 +947,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("delta") = py::none());
   m.def("correct_records", &correct_records,
         "K9: causal correction of a window's records: += the delta table of the earlier ranks' messages");
+  m.def("sweep_block_reduce", &sweep_block_reduce, "K9: owner block sum (+ exclusive prefixes) of the split collective",
+        py::arg("recv"), py::arg("N"), py::arg("bf16"), py::arg("total"), py::arg("pref") = py::none());
   m.def("prefix_delta", &prefix_delta, "K9: the record correction's delta table of a scaled message prefix");
   m.def("pack_rows", &pack_rows, "C2: changed rows of a round slice -> fixed-capacity [cap, 33] entries");
   m.def("check_round", &check_round, "C2 race detector: one round's matches share no player (flag |= 1)");
@@ -927,6 +969,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("device"), py::arg("num_cus"), py::arg("invert") = false);
   m.def("progress_signal", &progress_signal, "8-B signal-memory word for the executor's tail signal");
   m.def("stream_wait_value64", &stream_wait_value64, "hipStreamWaitValue64(stream, ptr, >= value)");
+  m.def("stream_write_value64", &stream_write_value64, "hipStreamWriteValue64(stream, ptr, value)");
   m.def("can_wait_value", &can_wait_value, "hipDeviceAttributeCanUseStreamWaitValue");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
   m.def("records_digest", &records_digest, "deterministic fp64 digest of a window's packed output rows");

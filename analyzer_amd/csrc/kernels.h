@@ -98,15 +98,22 @@ int launch_sweep_delta(const float* s0, const float* a, const float* s, const fl
 int launch_sweep_apply(const float* s0, const float* buf, const float* attrs, float* s, float* s2,
                        const float* vst, float unknown_sigma, int scaled, int64_t P, uint32_t* clamps,
                        hipStream_t st);
-// compressed merges: msg [P][14] bf16 (bf16 != 0) or fp16 + cnt [P] int32 (touch fields lo | hi << 16)
+// compressed merges: msg [P][14] bf16 (bf16 != 0) or fp16 + cnt [P] int32 (touch fields lo | hi << 16);
+// mstride / cstride: row strides in 32-bit words (7 / 1 for separate tensors, 8 / 8 for the
+// split collective's [P][8]-word operand rows with the touch word last)
 int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, const float* attrs,
                               const float* vst, float unknown_sigma, int bf16, void* msg, int32_t* cnt,
-                              int64_t P, hipStream_t st);
+                              int64_t P, hipStream_t st, int64_t mstride = 7, int64_t cstride = 1);
+// split collective (parallel/comm.py): recv [N][blk][8] words -> total [blk][8] (+ the exclusive
+// prefixes pref [N][blk][7] when non-null)
+int launch_sweep_block_reduce(const int32_t* recv, int N, int64_t blk, int bf16, int32_t* total, int32_t* pref,
+                              hipStream_t st);
 // prefix (nullable): the scaled exclusive prefix of the messages (same type as msg) ->
 // delta [P][16] fp32, the record correction's increments (sweep_core.h prefix_delta_track)
 int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
                               const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
-                              int64_t P, uint32_t* clamps, const void* prefix, float* delta, hipStream_t st);
+                              int64_t P, uint32_t* clamps, const void* prefix, float* delta, hipStream_t st,
+                              int64_t mstride = 7, int64_t cstride = 1);
 int launch_prefix_delta(const float* s0, const void* prefix, int bf16, const float* attrs, const float* vst,
                         float unknown_sigma, float* delta, int64_t P, hipStream_t st);
 // causal record correction: rows = RateResult's packed rows [M][orow] += delta [P][16]

@@ -226,15 +226,16 @@ template <typename H>
 __global__ void __launch_bounds__(256)
 sweep_delta_packed_kernel(const float2* __restrict__ s0, const float2* a0, const float4* __restrict__ s,
                           const float4* __restrict__ attrs, const float* __restrict__ vst,
-                          float unknown_sigma, uint32_t* __restrict__ msg, uint32_t* __restrict__ cnt, int64_t P) {
+                          float unknown_sigma, uint32_t* __restrict__ msg, uint32_t* __restrict__ cnt, int64_t P,
+                          int64_t mstride, int64_t cstride) {
   const TrackLane L = track_lane();
   if (L.p >= P) return;
   float dp, dt, lo, hi;
   lane_delta(L, s0, a0, s, attrs, vst, unknown_sigma, true, dp, dt, lo, hi);
   if (L.t < kTracks)  // 14 halves = 7 words (28 B per player, contiguous over the wave)
-    merge_st(msg + L.p * kTracks + L.t, (uint32_t)to_half_bits<H>(dp) | ((uint32_t)to_half_bits<H>(dt) << 16));
+    merge_st(msg + L.p * mstride + L.t, (uint32_t)to_half_bits<H>(dp) | ((uint32_t)to_half_bits<H>(dt) << 16));
   else
-    merge_st(cnt + L.p, (uint32_t)lo | ((uint32_t)hi << 16));  // 4 + 3 nibbles: 32 B per player on the wire
+    merge_st(cnt + L.p * cstride, (uint32_t)lo | ((uint32_t)hi << 16));  // 4 + 3 nibbles: 32 B per player on the wire
 }
 
 // prefix (nullable, the scaled exclusive prefix of the messages, H [P][14]) -> delta
@@ -246,11 +247,12 @@ __global__ void __launch_bounds__(256)
 sweep_apply_packed_kernel(const float2* __restrict__ s0, const uint32_t* __restrict__ msg,
                           const uint32_t* __restrict__ cnt, const float4* __restrict__ attrs, float4* s,
                           float2* s2, const float* __restrict__ vst, float unknown_sigma, int64_t P,
-                          uint32_t* clamps, const uint32_t* __restrict__ pref, float2* __restrict__ delta) {
+                          uint32_t* clamps, const uint32_t* __restrict__ pref, float2* __restrict__ delta,
+                          int64_t mstride, int64_t cstride) {
   const TrackLane L = track_lane();
   if (L.p >= P) return;
-  const uint32_t w = L.t < kTracks ? merge_ld(msg + L.p * kTracks + L.t) : 0u;
-  const uint32_t c = merge_ld(cnt + L.p);  // broadcast within the group: lo | hi << 16
+  const uint32_t w = L.t < kTracks ? merge_ld(msg + L.p * mstride + L.t) : 0u;
+  const uint32_t c = merge_ld(cnt + L.p * cstride);  // broadcast within the group: lo | hi << 16
   if (pref) {  // (before lane_apply: it may overwrite the window start through s2)
     const float2 cs = merge_ld(s0 + L.p * kLanesPerPlayer + L.t);
     const float c0mu = __shfl(cs.x, L.gbase), c0sg = __shfl(cs.y, L.gbase);
@@ -288,6 +290,56 @@ prefix_delta_kernel(const float2* __restrict__ s0, const uint32_t* __restrict__ 
                        from_half_bits<H>(pw >> 16), dpi, dtau);
   }
   delta[L.p * kLanesPerPlayer + L.t] = make_float2(dpi, dtau);
+}
+
+// ------------------------------------------------- split collective: the owner's block reduce
+// The merge's exchange (parallel/comm.py split_exchange) is all-to-all -> this reduce ->
+// all-gather on the critical path, an all-reduce's volume, and -- deferred, beside the
+// next window's rating -- an all-to-all that returns each rank its exclusive prefix.
+// Rank b owns row block b of the [P][8]-word operand rows (words 0..6: a track's two
+// 16-bit message halves, word 7: the touch fields lo | hi << 16) and receives block b of
+// every rank: recv [N][blk][8].  One lane per word: the halves are summed in fp32 in rank
+// order and rounded once to the wire type (what torch's fp32 cumsum + .to() gives), the
+// touch word as an integer (nibble fields, <= 15 ranks: no carries).  pref (nullable)
+// [N][blk][7]: rank q's exclusive prefix of the halves (ranks < q; zeros for q = 0), the
+// record correction's input -- the touch word has no prefix.
+template <typename H>
+__global__ void __launch_bounds__(256)
+sweep_block_reduce_kernel(const uint32_t* __restrict__ recv, int N, int64_t blk, uint32_t* __restrict__ total,
+                          uint32_t* __restrict__ pref) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gid >> 3;
+  const int w = (int)(gid & 7);
+  if (row >= blk) return;
+  if (w == kTracks) {
+    uint32_t c = 0u;
+    for (int q = 0; q < N; ++q) c += merge_ld(recv + ((int64_t)q * blk + row) * 8 + w);
+    merge_st(total + row * 8 + w, c);
+    return;
+  }
+  float a = 0.f, b = 0.f;
+  for (int q = 0; q < N; ++q) {
+    if (pref)  // the prefix of rank q: the sum so far, rounded once
+      merge_st(pref + ((int64_t)q * blk + row) * kTracks + w,
+               (uint32_t)to_half_bits<H>(a) | ((uint32_t)to_half_bits<H>(b) << 16));
+    const uint32_t x = merge_ld(recv + ((int64_t)q * blk + row) * 8 + w);
+    a += from_half_bits<H>(x & 0xffffu);
+    b += from_half_bits<H>(x >> 16);
+  }
+  merge_st(total + row * 8 + w, (uint32_t)to_half_bits<H>(a) | ((uint32_t)to_half_bits<H>(b) << 16));
+}
+
+int launch_sweep_block_reduce(const int32_t* recv, int N, int64_t blk, int bf16, int32_t* total, int32_t* pref,
+                              hipStream_t st) {
+  if (blk <= 0 || N <= 0) return 0;
+  const dim3 grid((unsigned)((blk * 8 + 255) / 256));
+  auto args = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(256), 0, st, reinterpret_cast<const uint32_t*>(recv), N, blk,
+                       reinterpret_cast<uint32_t*>(total), reinterpret_cast<uint32_t*>(pref));
+  };
+  if (bf16) args(sweep_block_reduce_kernel<__bf16>);
+  else args(sweep_block_reduce_kernel<_Float16>);
+  return (int)hipGetLastError();
 }
 
 // ------------------------------------------------- causal record correction
@@ -383,13 +435,13 @@ static dim3 track_grid(int64_t P) {
 
 int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, const float* attrs,
                               const float* vst, float unknown_sigma, int bf16, void* msg, int32_t* cnt,
-                              int64_t P, hipStream_t st) {
+                              int64_t P, hipStream_t st, int64_t mstride, int64_t cstride) {
   if (P <= 0) return 0;
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
                        reinterpret_cast<const float2*>(a), reinterpret_cast<const float4*>(s),
                        reinterpret_cast<const float4*>(attrs), vst, unknown_sigma,
-                       reinterpret_cast<uint32_t*>(msg), reinterpret_cast<uint32_t*>(cnt), P);
+                       reinterpret_cast<uint32_t*>(msg), reinterpret_cast<uint32_t*>(cnt), P, mstride, cstride);
   };
   if (bf16) args(sweep_delta_packed_kernel<__bf16>);
   else args(sweep_delta_packed_kernel<_Float16>);
@@ -398,14 +450,15 @@ int launch_sweep_delta_packed(const float* s0, const float* a, const float* s, c
 
 int launch_sweep_apply_packed(const float* s0, const void* msg, const int32_t* cnt, int bf16,
                               const float* attrs, float* s, float* s2, const float* vst, float unknown_sigma,
-                              int64_t P, uint32_t* clamps, const void* prefix, float* delta, hipStream_t st) {
+                              int64_t P, uint32_t* clamps, const void* prefix, float* delta, hipStream_t st,
+                              int64_t mstride, int64_t cstride) {
   if (P <= 0) return 0;
   auto args = [&](auto kern) {
     hipLaunchKernelGGL(kern, track_grid(P), dim3(256), 0, st, reinterpret_cast<const float2*>(s0),
                        reinterpret_cast<const uint32_t*>(msg), reinterpret_cast<const uint32_t*>(cnt),
                        reinterpret_cast<const float4*>(attrs), reinterpret_cast<float4*>(s),
                        reinterpret_cast<float2*>(s2), vst, unknown_sigma, P, clamps,
-                       reinterpret_cast<const uint32_t*>(prefix), reinterpret_cast<float2*>(delta));
+                       reinterpret_cast<const uint32_t*>(prefix), reinterpret_cast<float2*>(delta), mstride, cstride);
   };
   if (bf16) args(sweep_apply_packed_kernel<__bf16>);
   else args(sweep_apply_packed_kernel<_Float16>);

@@ -11,7 +11,10 @@ messages through RabbitMQ (/root/reference/worker.py:44-46,85-92).
 * ``shard`` -- contiguous block partition of a range (time-axis sharding, P1/P4).
 * ``exclusive_scan`` (C1') -- per-row prefix sum over ranks (causal re-sweeps of
   parallel/sweep.py) as two all-to-alls.
-* ``scan_and_sum`` (C1 + C1') -- the merge's collective when records are corrected:
+* ``SplitExchange`` (C1 + C1') -- the merge's collective since round 6: all-to-all ->
+  owner reduce -> all-gather of the sums on the critical path (an all-reduce's volume),
+  the prefixes' return all-to-all deferred beside the next window's rating.
+* ``scan_and_sum`` (C1 + C1') -- the round-5 collective when records are corrected:
   the sum over ranks AND each rank's exclusive prefix from one exchange (two
   all-to-alls + an all-gather of the block sums: 3 (N-1)/N of the buffer per rank,
   against 2 (N-1)/N for the all-reduce alone and 4 (N-1)/N for both separately).
@@ -197,6 +200,139 @@ def scan_and_sum_start(t: torch.Tensor, group=None, stream=None, extra: Optional
                 x.record_stream(now)
         return res
     return finish
+
+
+def block_reduce_rows(recv: torch.Tensor, n: int, dtype: torch.dtype, want_prefix: bool):
+    """The owner reduce of the split exchange on the host (csrc/sweep.hip
+    sweep_block_reduce_kernel, bit for bit): recv [n * blk, 8] int32 words -- 7 words of
+    two ``dtype`` halves (the messages) and the touch word -- -> (total [blk, 8],
+    exclusive prefixes [n * blk, 7] or None).  Halves are summed in fp32 in rank order and
+    rounded once; the touch words are summed as integers."""
+    blk = recv.shape[0] // n
+    r = recv.view(n, blk, 8)
+    halves = r[..., :7].contiguous().view(dtype)  # [n, blk, 14]
+    acc = torch.zeros((blk, 14), dtype=torch.float32, device=recv.device)
+    pref = torch.empty((n, blk, 7), dtype=torch.int32, device=recv.device) if want_prefix else None
+    for q in range(n):
+        if pref is not None:
+            pref[q] = acc.to(dtype).view(torch.int32)
+        acc = acc + halves[q].float()
+    total = torch.empty((blk, 8), dtype=torch.int32, device=recv.device)
+    total[:, :7] = acc.to(dtype).view(torch.int32)
+    total[:, 7] = r[..., 7].sum(0, dtype=torch.int64).to(torch.int32)
+    return total, (pref.view(n * blk, 7) if pref is not None else None)
+
+
+class SplitExchange:
+    """The DP merge's collective, split at what the next window needs (SURVEY C1;
+    parallel/sweep.py ``merge_split``).
+
+    Every rank holds operand rows op [P, 8] int32 words (7 words of two bf16 / fp16
+    message halves + the packed touch word).  The next window's roster needs only the
+    SUM over ranks; only this window's records need each rank's exclusive PREFIX.  So:
+
+    * critical (``total``): all-to-all (rank b receives row block b of every rank) ->
+      owner reduce (csrc/sweep.hip sweep_block_reduce: the block's sum AND every rank's
+      prefix of it, one pass) -> all-gather of the block sums.  2 (N-1)/N of the buffer
+      per rank: an all-reduce's volume, where the round-5 scan moved 3 (N-1)/N before
+      the decode could start.
+    * deferred (``prefix``): the all-to-all that returns each rank its prefix of every
+      block, (N-1)/N of 7/8 of the buffer, enqueued right behind the critical part on the
+      collective stream -- it runs beside the decode and the next window's rating, and
+      only the record correction (off the critical path too) waits for it.
+
+    On xGMI's point-to-point mesh every block of an all-to-all travels its own link, so
+    the split costs about one all-reduce on the critical path.  ``stream``: the
+    collective stream (RCCL); gloo / host tensors run synchronously (the host reduce is
+    ``block_reduce_rows``, bit-identical to the kernel).  ``force``: run the exchanges on
+    a one-rank group (tests)."""
+
+    def __init__(self, op: torch.Tensor, dtype: torch.dtype, group=None, stream=None,
+                 want_prefix: bool = True, force: bool = False):
+        _, size = world(group)
+        self.P = int(op.shape[0])
+        self.size = size
+        self.dtype = dtype
+        self._prefix = None
+        self._pref = None
+        self._total = None
+        self._ev_total = self._ev_prefix = None
+        run_side = stream is not None and op.is_cuda and not _staged(op, group)
+        blk = -(-self.P // size) if size > 0 else self.P
+        if blk * size == self.P:
+            send = op
+        else:
+            send = op.new_zeros((size * blk, 8))
+            send[:self.P] = op
+        if run_side:
+            stream.wait_stream(torch.cuda.current_stream(op.device))
+            ctx = torch.cuda.stream(stream)
+        else:
+            ctx = _Null()
+        with ctx:
+            recv = torch.empty_like(send)
+            all_to_all_rows(recv, send, group)
+            if op.is_cuda:
+                from ..ops.native import native
+
+                tot = torch.empty((blk, 8), dtype=torch.int32, device=op.device)
+                pref = torch.empty((size * blk, 7), dtype=torch.int32, device=op.device) if want_prefix else None
+                native().sweep_block_reduce(recv, size, dtype == torch.bfloat16, tot, pref)
+            else:
+                tot, pref = block_reduce_rows(recv, size, dtype, want_prefix)
+            total = torch.empty((size * blk, 8), dtype=torch.int32, device=op.device)
+            all_gather_rows(total, tot, group)
+            self._total = total[:self.P]
+            if run_side:
+                self._ev_total = torch.cuda.Event()
+                self._ev_total.record(stream)
+        self._pref = pref
+        self._blk = blk
+        self._group = group
+        self._stream = stream if run_side else None
+
+    def send_prefix(self, gate=None) -> None:
+        """Enqueue the deferred all-to-all that returns every rank its prefix (on the
+        collective stream, after ``gate(stream)`` -- the DP merge passes a wait on the next
+        rating's tail, so the exchange does not compete with the rating's start)."""
+        if self._pref is None or self._prefix is not None:
+            return
+        st = self._stream
+        with (torch.cuda.stream(st) if st is not None else _Null()):
+            if st is not None and gate is not None:
+                gate(st)
+            back = torch.empty((self.size * self._blk, 7), dtype=torch.int32, device=self._pref.device)
+            all_to_all_rows(back, self._pref, self._group)
+            self._prefix = back[:self.P]
+            if st is not None:
+                self._ev_prefix = torch.cuda.Event()
+                self._ev_prefix.record(st)
+
+    def total(self) -> torch.Tensor:
+        """[P, 8] words of the summed operands; the current stream waits for them."""
+        if self._ev_total is not None:
+            cur = torch.cuda.current_stream(self._total.device)
+            cur.wait_event(self._ev_total)
+            self._total.record_stream(cur)
+        return self._total
+
+    def prefix(self) -> Optional[torch.Tensor]:
+        """[P, 7] words of this rank's exclusive prefix; the current stream waits for it
+        (``send_prefix`` first, or it is sent now, ungated)."""
+        self.send_prefix()
+        if self._prefix is not None and self._ev_prefix is not None:
+            cur = torch.cuda.current_stream(self._prefix.device)
+            cur.wait_event(self._ev_prefix)
+            self._prefix.record_stream(cur)
+        return self._prefix
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 def all_reduce_sum(t: torch.Tensor, group=None, async_op: bool = False):

@@ -72,7 +72,7 @@ import torch.distributed as dist
 from ..config import EngineConfig, RaterConfig
 from ..models.tiers import vst_table
 from ..ops.native import native
-from .comm import all_reduce_sum, exclusive_scan, scan_and_sum, scan_and_sum_start, world
+from .comm import SplitExchange, all_reduce_sum, exclusive_scan, scan_and_sum, scan_and_sum_start, world
 
 MAX_RANKS = 15  # touch counts are base-16 fields in fp32 (see csrc/sweep_core.h)
 
@@ -155,6 +155,28 @@ class SweepMerger:
             if comm_dtype != "fp32" else None
         self.cnt = torch.empty((self.P, 1), dtype=torch.int32, device=self.device) \
             if comm_dtype != "fp32" else None
+        # the split merge's operand rows (merge_split): [P, 16] halves = 8 words per player,
+        # messages in words 0..6 and the touch word last (32 B per player on the wire), and
+        # two window starts -- decode w reads one and writes the other, so window w's start
+        # stays intact for its deferred record correction while window w+1 is rated
+        self.op = torch.empty((self.P, 16), dtype=COMM_DTYPES[comm_dtype], device=self.device) \
+            if comm_dtype != "fp32" else None
+        self._starts = [self.start, None]
+        self.use_split = os.environ.get("ANA_DP_SPLIT", "1") not in ("", "0", "false")
+        # where the deferred prefix exchange + record correction start: a callable that makes
+        # a stream wait for the NEXT rating launch's tail (runtime/engine.py sets it when the
+        # launches carry a tail signal, ANA_DP_DEFER_AT); None: right behind the decode
+        self.defer_gate: Optional[Callable] = None
+        self._side = None         # stream of the deferred record correction (merge_split)
+        self._corr_done = None    # event: the last deferred correction finished
+        self._pd_done = None      # event: its delta table is written (the start it read is free)
+        self._split_pending = None  # the correction waiting for the next merge (defer_mode "next")
+        # ANA_DP_DEFER: "next" (default) -- window w's correction runs beside window w+1's
+        # collective; "tail" -- behind the decode, gated on the next rating's tail; "now" --
+        # behind the decode at once
+        self.defer_mode = os.environ.get("ANA_DP_DEFER") or "next"
+        self._corr_rows = None    # RateResult rows it writes
+        self._corr_events: List[tuple] = []  # (begin, end) timing events on the side stream
         self.vst = torch.tensor(vst_table(), **f)
         self._none = torch.empty(0, **f)
         # decoded tracks whose merged precision hit the floor, summed over every decode
@@ -220,12 +242,14 @@ class SweepMerger:
                              self.scaled, self.clamps)
         roster.epoch = roster.epoch if roster.epoch is not None else 0  # decode wrote tag 0
 
-    def messages_packed(self, roster, lo: int = 0, hi: Optional[int] = None) -> None:
-        """``messages`` straight into the compressed all-reduce operands (first sweep)."""
+    def messages_packed(self, roster, lo: int = 0, hi: Optional[int] = None, into=None) -> None:
+        """``messages`` straight into the compressed all-reduce operands (first sweep);
+        ``into`` = (msg, cnt) views (merge_split's operand rows), else ``msg`` / ``cnt``."""
         hi = self.P if hi is None else hi
+        msg, cnt = into if into is not None else (self.msg, self.cnt)
         native().sweep_delta_packed(self.start[lo:hi], self.start[lo:hi], roster.state[lo:hi],
                                     roster.attrs[lo:hi], self.vst, float(self.cfg.unknown_player_sigma),
-                                    self.msg[lo:hi], self.cnt[lo:hi])
+                                    msg[lo:hi], cnt[lo:hi])
 
     def decode_packed(self, roster, lo: int = 0, hi: Optional[int] = None, into=None,
                       prefix: Optional[torch.Tensor] = None, delta: Optional[torch.Tensor] = None) -> None:
@@ -242,6 +266,229 @@ class SweepMerger:
 
     def _packed(self) -> bool:
         return self.msg is not None and (self._sweep <= 1 or self.prior is None)
+
+    # --------------------------------------------------- the split merge (round 6)
+    def op_views(self):
+        """(msg [P, 14], cnt [P, 1] int32) views of the split merge's operand rows."""
+        return self.op[:, :14], self.op.view(torch.int32)[:, 7:8]
+
+    def split(self) -> bool:
+        """Merges of this merger go through ``merge_split`` (compressed messages, one sweep;
+        ``ANA_DP_SPLIT=0``: the round-5 merges, kept as the reference the tests compare with)."""
+        return self.op is not None and self.sweeps <= 1 and self.use_split
+
+    def _emulated(self, t: torch.Tensor, nbytes: float, passes: int, stream) -> None:
+        """The collective stand-in (``emulate``) over ``t`` on ``stream``: the modelled time
+        of ``nbytes`` per rank over the emulated links plus one latency."""
+        n, bw, lat = self.emulate
+        with torch.cuda.stream(stream):
+            native().emulate_allreduce(t, 32, passes, lat + nbytes / (bw * 1e3))
+
+    def merge_split(self, roster, rec: Optional[torch.Tensor] = None, out=None,
+                    overlap: Optional[Callable[[], None]] = None) -> None:
+        """One window's merge with the collective split at what the next window needs
+        (comm.SplitExchange): messages -> all-to-all / owner reduce / all-gather of the
+        SUM -> decode into the roster and the other window start -> the next rating may
+        start.  With the causal record correction (``correct`` and ``rec``/``out``) the
+        prefix return (an all-to-all on the collective stream) and the correction (the
+        delta table from this window's start + the prefix, then the records pass, on a
+        side stream) are enqueued behind it and run beside the next window's rating.
+
+        Round 5 ran the scan (3 (N-1)/N of the buffer) and the previous window's
+        correction in front of the decode (emulated N = 8: 11.24 ms per step,
+        docs/DP_PROJECTION.md)."""
+        if self.world <= 1 and not self.force:
+            self.windows += 1
+            if overlap is not None:
+                overlap()
+            return
+        correct = self.correct and rec is not None and out is not None and out.packed is not None
+        K = (int(rec.shape[1]) - 2) // 2 if rec is not None else 0
+        cuda = self.device.type == "cuda"
+        main = torch.cuda.current_stream(self.device) if cuda else None
+        msg, cnt = self.op_views()
+        self._ev("begin")
+        nxt = self._starts[1]
+        if nxt is None:
+            nxt = self._starts[1] = torch.empty_like(self.start)
+        self.messages_packed(roster, into=(msg, cnt))
+        self._ev("messages")
+        words = self.op.view(torch.int32)
+        n_emul = self.emulate[0] if (self.emulate is not None and self.world <= 1 and cuda) else 0
+        # the previous window's record correction goes beside this merge's collective: enqueued
+        # first on the side stream, it starts behind these messages (defer_mode "next")
+        pending_prev = self._split_pending is not None
+        if cuda and self._coll is None:
+            self._coll = torch.cuda.Stream(self.device)
+        prefix = None
+        if self.world > 1:
+            ex = SplitExchange(words, self.op.dtype, group=self.group, stream=self._coll,
+                               want_prefix=correct, force=world(self.group)[1] < self.world)
+            if pending_prev:
+                self._enqueue_split_correction()
+            if overlap is not None:
+                overlap()
+            self._ev("overlap")
+            total = ex.total()
+            get_prefix = ex.prefix
+            send_prefix = (lambda: ex.send_prefix(self.defer_gate))  # noqa: E731
+        else:
+            # one rank (force): the sum is the operand itself and the prefix zero; with
+            # ``emulate`` the stand-ins price the N-rank exchange on the collective stream --
+            # the critical part (2 (N-1)/N of the buffer + the owner reduce of N blocks) in
+            # front of the decode, the prefix return behind it beside the next rating
+            total = words
+            zero = self._prefix_zero(self.op[:, :14]).view(torch.int32) if correct else None
+            get_prefix = (lambda: zero)  # noqa: E731
+            send_prefix = None
+            if n_emul:
+                self._coll.wait_stream(main)
+                nb = float(self.P * 32)
+                self._emulated(words, 2.0 * (n_emul - 1) / n_emul * nb, 3, self._coll)
+                blk = self.P // n_emul
+                if blk > 0:
+                    if getattr(self, "_emul_scratch", None) is None:
+                        self._emul_scratch = (torch.empty((blk, 8), dtype=torch.int32, device=self.device),
+                                              torch.empty((n_emul * blk, 7), dtype=torch.int32,
+                                                          device=self.device))
+                    tot_s, pref_s = self._emul_scratch
+                    with torch.cuda.stream(self._coll):
+                        native().sweep_block_reduce(words[:n_emul * blk], n_emul, self.op.dtype == torch.bfloat16,
+                                                    tot_s, pref_s if correct else None)
+                done = torch.cuda.Event()
+                done.record(self._coll)
+                if correct and blk > 0:  # the deferred prefix return, sent behind the decode
+                    pref_ev = {}
+
+                    def send_prefix():
+                        with torch.cuda.stream(self._coll):
+                            if self.defer_gate is not None:
+                                self.defer_gate(self._coll)
+                        self._emulated(self._emul_scratch[1], (n_emul - 1) / n_emul * self.P * 28.0, 2,
+                                       self._coll)
+                        pref_ev["ev"] = torch.cuda.Event()
+                        pref_ev["ev"].record(self._coll)
+
+                    get_prefix = (lambda: (torch.cuda.current_stream(self.device).wait_event(pref_ev["ev"]),  # noqa: E731
+                                           zero)[1])
+                if pending_prev:
+                    self._enqueue_split_correction()
+                if overlap is not None:
+                    overlap()
+                self._ev("overlap")
+                main.wait_event(done)
+            else:
+                if pending_prev:
+                    self._enqueue_split_correction()
+                if overlap is not None:
+                    overlap()
+                self._ev("overlap")
+        self._ev("allreduce")
+        if cuda and self._pd_done is not None:
+            # the previous window's deferred delta table read the start this decode writes
+            main.wait_event(self._pd_done)
+        tmsg = total.view(self.op.dtype)[:, :14] if total is not words else msg
+        tcnt = total[:, 7:8] if total is not words else cnt
+        native().sweep_apply_packed(self.start, tmsg, tcnt, roster.attrs, roster.state, nxt, self.vst,
+                                    float(self.cfg.unknown_player_sigma), self.clamps, None, None)
+        roster.epoch = roster.epoch if roster.epoch is not None else 0
+        self._ev("apply")
+        cur = self.start
+        if correct and send_prefix is not None:
+            send_prefix()  # the prefix return: gated on the next rating's tail (defer_gate)
+        if correct:
+            pend = dict(cur=cur, rec=rec, K=K, rows=out.packed, get_prefix=get_prefix, attrs=roster.attrs)
+            self._corr_rows = out.packed
+            if self.defer_mode == "next" and cuda:
+                self._split_pending = pend  # beside the next merge's collective (or a flush)
+            else:
+                self._split_pending = pend
+                self._enqueue_split_correction(gate=self.defer_gate if self.defer_mode == "tail" else None)
+        self._starts = [nxt, cur]
+        self.start = nxt
+        self._synced = True
+        self.windows += 1
+
+    def _enqueue_split_correction(self, gate=None) -> None:
+        """Enqueue the pending record correction of the split merge (``merge_split``): on
+        the side stream behind everything the current stream enqueued so far (in the default
+        placement: the next window's messages, so it runs beside that merge's collective,
+        where the GPU is otherwise idle), the delta table from that window's start + the
+        prefix, then the records pass.  Host tensors: at once."""
+        pend = self._split_pending
+        if pend is None:
+            return
+        self._split_pending = None
+        cuda = self.device.type == "cuda"
+        if self.delta is None:
+            self.delta = torch.empty((self.P, 16), dtype=torch.float32, device=self.device)
+        if cuda:
+            if self._side is None:
+                self._side = torch.cuda.Stream(self.device)
+            self._side.wait_stream(torch.cuda.current_stream(self.device))
+            ctx = torch.cuda.stream(self._side)
+        else:
+            ctx = _NullCtx()
+        with ctx:
+            b = None
+            if cuda and gate is not None:
+                gate(self._side)
+            if cuda and self.timing:
+                b = torch.cuda.Event(enable_timing=True)
+                b.record()
+            pw = pend["get_prefix"]()
+            native().prefix_delta(pend["cur"], pw.view(self.op.dtype), pend["attrs"], self.vst,
+                                  float(self.cfg.unknown_player_sigma), self.delta)
+            if cuda:
+                self._pd_done = torch.cuda.Event()
+                self._pd_done.record()
+            native().correct_records(pend["rec"], pend["K"], pend["rows"], self.delta)
+            if cuda:
+                if b is not None:
+                    e = torch.cuda.Event(enable_timing=True)
+                    e.record()
+                    self._corr_events.append((b, e))
+                self._corr_done = torch.cuda.Event()
+                self._corr_done.record()
+                for t in (pend["cur"], pend["rec"], pend["rows"], pw):
+                    t.record_stream(self._side)
+
+    def flush_split(self) -> None:
+        """Enqueue a correction still waiting for the next merge (finish, a consumer)."""
+        if self._split_pending is not None:
+            self._enqueue_split_correction()
+
+    def correction_touches(self, rows) -> bool:
+        """Whether the last deferred record correction writes (part of) ``rows``."""
+        if self._corr_rows is None:
+            return False
+        a, b = self._corr_rows, rows
+        a0, b0 = a.data_ptr(), b.data_ptr()
+        return a0 < b0 + b.numel() * b.element_size() and b0 < a0 + a.numel() * a.element_size()
+
+    def wait_correction(self, rows=None) -> None:
+        """Make the current stream wait for the deferred record correction (of ``rows``,
+        when given: only if it writes them); a pending one is enqueued first."""
+        if rows is not None and not self.correction_touches(rows):
+            return
+        self.flush_split()
+        if self._corr_done is None or self.device.type != "cuda":
+            return
+        if rows is not None and self._corr_rows is not None:
+            a, b = self._corr_rows, rows
+            a0, b0 = a.data_ptr(), b.data_ptr()
+            if not (a0 < b0 + b.numel() * b.element_size() and b0 < a0 + a.numel() * a.element_size()):
+                return
+        torch.cuda.current_stream(self.device).wait_event(self._corr_done)
+
+    def correction_ms(self) -> float:
+        """Side-stream time of the deferred corrections since the last call (syncs)."""
+        if not self._corr_events:
+            return 0.0
+        torch.cuda.synchronize(self.device)
+        ms = sum(b.elapsed_time(e) for b, e in self._corr_events)
+        self._corr_events.clear()
+        return ms
 
     # legacy name: decode the all-reduced messages into the roster only
     def apply(self, roster, lo: int = 0, hi: Optional[int] = None) -> None:
@@ -504,6 +751,14 @@ class SweepMerger:
             prev = e
         self._events.clear()
         return out
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 def rate_window_dp(rater, merger: SweepMerger, roster, rec, K=None, out=None, check=True,

@@ -59,6 +59,8 @@ CHUNK = 64  # matches per executor ticket of a window (csrc/dataflow.hip kChunk;
 DP_TAIL_AT = 0.9  # tail-overlap start of the next prepass between DP merges (3v3; see tail_point)
 SPARE_TAIL_AT = 0.75  # ... of a window launch at one wave per SIMD (config 2: 0.6-0.8 swept)
 FULL_TAIL_AT = 0.1  # ... of a 1v1-3v3 launch at two waves per SIMD (config 5: 0-0.7 swept)
+DP_DEFER_AT = 0.8  # split DP merge: the deferred prefix exchange + record correction of window w
+#                    start once rating w+1 claimed this fraction of its chunks (ANA_DP_DEFER_AT)
 
 
 @dataclass
@@ -106,6 +108,16 @@ class WindowPipeline:
         # kernels' non-temporal operands), config 3 20.15-20.18 vs 20.26-20.34 ms; a serial
         # prepass gains nothing (config 2: 8.00 vs 7.98; profiles/r4/merge_nt_and_sort_nt.log)
         self.sort_nt = 2 if not self.serial else -1
+        # the split DP merge's deferred work (parallel/sweep.py merge_split) waits for the next
+        # rating's tail: started right behind the decode it co-runs with the launch's ramp
+        # and slows the rating by more than it takes (ANA_DP_DEFER_AT; <= 0: ungated)
+        self.defer_at = 0.0
+        if dp and self.cuda and getattr(merger, "split", None) is not None and merger.split() and \
+                getattr(merger, "correct", False) and (merger.world > 1 or getattr(merger, "force", False)):
+            env = os.environ.get("ANA_DP_DEFER_AT")
+            self.defer_at = float(env) if env else DP_DEFER_AT
+            if self.defer_at > 0 and self.tail == 0:
+                self.tail = self.defer_at
         self._signal = 0
         self._seq = 0
         self.side = self._side_stream() if self.cuda else None
@@ -133,6 +145,8 @@ class WindowPipeline:
             dev = self.device.index or 0
             if native().can_wait_value(dev):
                 self._signal = native().progress_signal(dev)
+        if self._signal and self.defer_at > 0:
+            merger.defer_gate = self._gate_next
 
     @staticmethod
     def serial_prepass(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512) -> bool:
@@ -192,6 +206,34 @@ class WindowPipeline:
             handle = native().cu_masked_stream(self.device.index or 0, n)
             return torch.cuda.ExternalStream(handle, device=self.device)
         return torch.cuda.Stream(self.device)
+
+    def _gate_next(self, stream) -> None:
+        """Make ``stream`` wait until the NEXT rating launch (not enqueued yet) reaches its
+        tail -- the split DP merge's deferred work (``merger.defer_gate``)."""
+        from ..ops.native import native
+
+        native().stream_wait_value64(stream.cuda_stream, self._signal, self._seq + 1)
+
+    def _release_gate(self) -> None:
+        """Open a gate set by ``_gate_next`` now (stream-ordered on the main stream): before
+        anything waits for the gated work while no further launch will release it."""
+        if self.cuda and self._signal and getattr(self.merger, "defer_gate", None) is not None:
+            from ..ops.native import native
+
+            native().stream_write_value64(torch.cuda.current_stream(self.device).cuda_stream, self._signal,
+                                          self._seq + 1)
+
+    def _settle_correction(self, rows=None) -> None:
+        """The split merge's deferred record correction of ``rows`` (all, with None) is
+        done before the current stream goes on: release its gate, then wait."""
+        m = self.merger
+        if m is None or not hasattr(m, "wait_correction") or \
+                (getattr(m, "_corr_done", None) is None and getattr(m, "_split_pending", None) is None):
+            return
+        if rows is not None and not m.correction_touches(rows):
+            return
+        self._release_gate()
+        m.wait_correction(rows)
 
     def wait_tail(self, stream) -> bool:
         """Make ``stream`` wait until the last enqueued rating launch reached its tail
@@ -257,6 +299,8 @@ class WindowPipeline:
             self.merger.begin(self.roster)
             if hasattr(self.merger, "pending_rows") and self.merger.pending_rows(out):
                 self.merger.flush_correction()  # a deferred record correction of these rows
+            if out is not None and getattr(out, "packed", None) is not None:
+                self._settle_correction(out.packed)  # ... still running on the side stream
         progress = None
         if self._signal:
             self._seq += 1
@@ -297,7 +341,11 @@ class WindowPipeline:
             self._rated = done
         if self.merger is not None:
             with trace_range("merge", window=self.windows_rated):
-                if getattr(self.merger, "correct", False) and res is not None and res.packed is not None and \
+                if hasattr(self.merger, "split") and self.merger.split():
+                    # the round-6 merge: the sum on the critical path, the prefix and the
+                    # record correction deferred beside the next rating (parallel/sweep.py)
+                    self.merger.merge_split(self.roster, prep.rec, res, overlap=overlap)
+                elif getattr(self.merger, "correct", False) and res is not None and res.packed is not None and \
                         (self.merger.world > 1 or self.merger.force):
                     # the window's records corrected by the earlier ranks' evidence (parallel/sweep.py)
                     self.merger.merge_corrected(self.roster, prep.rec, res, overlap=overlap)
@@ -334,6 +382,8 @@ class WindowPipeline:
         ``defer``), so a pending one for these rows runs now (stream-ordered)."""
         if self.merger is not None and hasattr(self.merger, "pending_rows") and self.merger.pending_rows(res):
             self.merger.flush_correction()
+        if res is not None and getattr(res, "packed", None) is not None:
+            self._settle_correction(res.packed)
 
     def finish(self) -> None:
         """End of a run of windows: the last window's deferred record correction runs
@@ -341,6 +391,7 @@ class WindowPipeline:
         ``check`` raises on a decode held at the precision floor)."""
         if self.merger is not None and hasattr(self.merger, "flush_correction"):
             self.merger.flush_correction()
+        self._settle_correction()
         if self.merger is not None and hasattr(self.merger, "check"):
             self.merger.check()
 

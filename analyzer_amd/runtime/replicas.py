@@ -9,10 +9,17 @@ SQLAlchemy URL), and each replica is a child ``worker.py`` process pinned to one
 (``HIP_VISIBLE_DEVICES``; on the host mirror they share the CPU).  With a real
 RabbitMQ, start the replicas the same way with ``RABBITMQ_URI=amqp://...``.
 
-Semantics are the reference's: each message is delivered to one replica at a time and
-redelivered if that replica dies before acking it (at-least-once), and replicas that
-rate matches sharing a player race on that player's row -- read, rate, write back,
-no locking -- exactly as the reference's replicas do on MySQL (worker.py:174-194).
+Delivery semantics are the reference's: each message is delivered to one replica at a
+time and redelivered if that replica dies before acking it (at-least-once).  Player rows
+are NOT raced on: the reference's replicas read, rate and write back with no locking,
+so two replicas rating matches that share a player overwrite each other's update
+(worker.py:174-194).  Here the store's player rows carry a version (runtime/store.py):
+every write is a compare-and-set on the version the batch read, and a batch that loses
+the race is rolled back and rated again from the fresh rows (runtime/worker.py
+``process``; counted as ``cas_retries``) -- no update is lost, and the committed
+batches are equivalent to rating them one after another in commit order
+(tests/test_replicas.py replays the commit log).  ``racy=True`` (PLAYER_CAS=0) restores
+the reference's behaviour for comparison.
 The launcher prints one JSON line: per-replica and total matches, acks and rate, and
 the broker's final counts.
 """
@@ -57,7 +64,7 @@ def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 
                  env: Optional[Dict[str, str]] = None, timeout: float = 600.0,
                  worker_py: Optional[str] = None,
                  replica_env: Optional[Dict[int, Dict[str, str]]] = None,
-                 first_alone_until_acked: int = 0) -> Dict[str, object]:
+                 first_alone_until_acked: int = 0, racy: bool = False) -> Dict[str, object]:
     """Start a broker and ``n`` worker replicas, optionally populating and enqueueing
     ``synthetic`` matches first; wait until every replica drained the queue and exited.
     ``replica_env``: extra environment per replica index (fault injection in tests);
@@ -93,6 +100,8 @@ def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 
     for r in range(n):
         e = dict(base)
         e.update(RABBITMQ_URI=server.uri, DATABASE_URI=database_uri, QUEUE=queue, REPLICA=str(r))
+        if racy:
+            e["PLAYER_CAS"] = "0"
         e.update((replica_env or {}).get(r, {}))
         if gpus > 0:  # one replica per GPU (round-robin when there are more replicas)
             ids = _visible_devices(base, gpus)
@@ -132,6 +141,7 @@ def run_replicas(n: int, synthetic: int = 0, players: int = 0, team_size: int = 
     return {"replicas": n, "gpus": gpus, "matches": total, "enqueued": len(ids),
             "acked": sum(int(r.get("acked", 0)) for r in results),
             "nacked": sum(int(r.get("nacked", 0)) for r in results),
+            "cas_retries": sum(int(r.get("cas_retries", 0) or 0) for r in results),
             "seconds": dt, "matches_per_s": total / dt if dt > 0 else None,
             "per_replica": [{"matches": r.get("matches"), "acked": r.get("acked"),
                              "matches_per_s": r.get("matches_per_s"), "error": r.get("error")} for r in results],

@@ -50,9 +50,18 @@ def _q(col: str) -> str:
     return '"%s"' % col  # 5v5_* columns start with a digit
 
 
+class WriteConflict(RuntimeError):
+    """A versioned player write found the row changed since the batch read it (another
+    replica committed in between): the batch must be rolled back and rated again from
+    fresh rows (runtime/worker.py).  The reference has no such check -- its replicas
+    overwrite each other's player rows (/root/reference/worker.py:174-194)."""
+
+
 SCHEMA = [
+    # version: bumped by every rating write; replicas write with compare-and-set on it
+    # (SqliteStore.versioned) -- a column the reference's schema does not have
     "CREATE TABLE IF NOT EXISTS player (api_id TEXT PRIMARY KEY, skill_tier INTEGER, "
-    "rank_points_ranked REAL, rank_points_blitz REAL, %s)"
+    "rank_points_ranked REAL, rank_points_blitz REAL, %s, version INTEGER NOT NULL DEFAULT 0)"
     % ", ".join("%s REAL" % _q(c) for c in PLAYER_RATING_COLS),
     "CREATE TABLE IF NOT EXISTS match (api_id TEXT PRIMARY KEY, game_mode TEXT, "
     "created_at REAL, trueskill_quality REAL)",
@@ -76,6 +85,10 @@ SCHEMA = [
     "CREATE TABLE IF NOT EXISTS asset (api_id TEXT PRIMARY KEY, match_api_id TEXT, url TEXT)",
     "CREATE INDEX IF NOT EXISTS asset_match ON asset(match_api_id)",
 ]
+# BATCH_LOG=true: every commit also records its matches in commit order (tests replay the
+# log to show that no replica's update was lost)
+BATCH_LOG_DDL = ("CREATE TABLE IF NOT EXISTS batch_log (seq INTEGER PRIMARY KEY AUTOINCREMENT, "
+                 "replica TEXT, match_ids TEXT)")
 
 
 def match_order(api_id: str, created_at) -> tuple:
@@ -229,6 +242,8 @@ class SqliteSession(_SessionBase):
         self.conn = store.conn
         self._players: Dict[str, Player] = {}  # identity map
         self._batches: List = []
+        self._versions: Dict[str, int] = {}    # api id -> version read (versioned stores)
+        self._log_ids: List[str] = []          # matches of this transaction (BATCH_LOG)
 
     # ------------------------------------------------------------- columnar batches
     def load_batch(self, ids: Iterable[str], chunksize: int = 100):
@@ -316,6 +331,8 @@ class SqliteSession(_SessionBase):
         pn = self.store.player_names
         names = [pn[k] for k in np.asarray(keys).tolist()]
         cols = ("api_id", "rowid", "rank_points_ranked", "rank_points_blitz", "skill_tier") + PLAYER_RATING_COLS
+        if self.store.versioned:
+            cols = cols + ("version",)
         rows: list = []
         for chunk in _chunks(names, 500):
             rows += self.conn.execute("SELECT %s FROM player WHERE api_id IN (%s)"
@@ -327,6 +344,9 @@ class SqliteSession(_SessionBase):
             # one numpy conversion (None -> NaN) instead of a Python float() per column
             where = {a: i for i, a in enumerate(names)}
             pos = np.fromiter((where[r[0]] for r in rows), dtype=np.int64, count=len(rows))
+            if self.store.versioned:
+                self._versions.update((r[0], r[-1]) for r in rows)
+                rows = [r[:-1] for r in rows]
             vals = np.array([r[2:] for r in rows], dtype=np.float64)
             att[pos] = vals[:, :3]
             rat[pos] = vals[:, 3:]
@@ -342,6 +362,7 @@ class SqliteSession(_SessionBase):
             return
         c = self.conn
         st = b.status
+        self._log_ids += list(b.ids)
         rated = st == RATED
         afkm = (st == AFK) | (st == INVALID)
         c.executemany("UPDATE match SET trueskill_quality=? WHERE api_id=?",
@@ -398,16 +419,31 @@ class SqliteSession(_SessionBase):
                 rows = np.concatenate([vals, rowids[sel, None].astype(object)], axis=1).tolist()
                 sets = ", ".join("%s=?, %s=?" % (_q(TRACK_COLUMNS[t] + "_mu"), _q(TRACK_COLUMNS[t] + "_sigma"))
                                  for t in tracks)
-                c.executemany("UPDATE player SET %s WHERE rowid=?" % sets, rows)
+                if self.store.versioned:
+                    # compare-and-set: only rows still at the version this batch read
+                    ver = self._versions
+                    vs = [ver.get(pn[k], 0) for k in np.asarray(b.final_keys)[sel].tolist()]
+                    rows = [r + [v] for r, v in zip(rows, vs)]
+                    cur = c.executemany("UPDATE player SET %s, version=version+1 WHERE rowid=? AND version=?"
+                                        % sets, rows)
+                    if cur.rowcount != len(rows):
+                        raise WriteConflict("%d of %d player rows changed since this batch read them"
+                                            % (len(rows) - max(cur.rowcount, 0), len(rows)))
+                else:
+                    c.executemany("UPDATE player SET %s WHERE rowid=?" % sets, rows)
 
     def _load_players(self, api_ids: Sequence[str]) -> None:
         need = [a for a in set(api_ids) if a not in self._players]
         cols = ("api_id", "skill_tier", "rank_points_ranked", "rank_points_blitz") + PLAYER_RATING_COLS
+        sel = cols + (("version",) if self.store.versioned else ())
         for chunk in _chunks(need, 500):
             rows = self.conn.execute(
-                "SELECT %s FROM player WHERE api_id IN (%s)" % (", ".join(_q(c) for c in cols),
+                "SELECT %s FROM player WHERE api_id IN (%s)" % (", ".join(_q(c) for c in sel),
                                                                 ", ".join("?" * len(chunk))), chunk)
             for row in rows:
+                if self.store.versioned:
+                    self._versions[row[0]] = row[-1]
+                    row = row[:-1]
                 kw = dict(zip(cols, row))
                 api = kw.pop("api_id")
                 tier = kw.pop("skill_tier")
@@ -492,8 +528,20 @@ class SqliteSession(_SessionBase):
                 c.execute("UPDATE participant_items SET %s WHERE participant_api_id=?"
                           % ", ".join("%s=?" % _q(col) for col in ITEM_WRITE_COLS), vals + [p.api_id])
         for pl, _ in self._player_snaps.values():
-            c.execute("UPDATE player SET %s WHERE api_id=?" % ", ".join("%s=?" % _q(col) for col in PLAYER_RATING_COLS),
-                      [getattr(pl, col) for col in PLAYER_RATING_COLS] + [pl.api_id])
+            sets = ", ".join("%s=?" % _q(col) for col in PLAYER_RATING_COLS)
+            vals = [getattr(pl, col) for col in PLAYER_RATING_COLS] + [pl.api_id]
+            if self.store.versioned:
+                cur = c.execute("UPDATE player SET %s, version=version+1 WHERE api_id=? AND version=?" % sets,
+                                vals + [self._versions.get(pl.api_id, 0)])
+                if cur.rowcount != 1:
+                    raise WriteConflict("player %s changed since this batch read it" % pl.api_id)
+            else:
+                c.execute("UPDATE player SET %s WHERE api_id=?" % sets, vals)
+        if self.store.batch_log:
+            ids = self._log_ids + [m.api_id for m, _ in self._match_snaps.values()]
+            c.execute("INSERT INTO batch_log (replica, match_ids) VALUES (?, ?)",
+                      (self.store.replica, ",".join(ids)))
+        self._log_ids = []
         c.commit()
         self.store.commits += 1
         self._match_snaps.clear()
@@ -502,6 +550,8 @@ class SqliteSession(_SessionBase):
     def rollback(self) -> None:
         super().rollback()
         self._batches.clear()
+        self._versions.clear()
+        self._log_ids = []
         self.conn.rollback()
 
     def participant_stats(self, participant_api_id: str):
@@ -528,6 +578,20 @@ class SqliteStore:
             self.conn.execute("PRAGMA synchronous=NORMAL")
         for ddl in SCHEMA:
             self.conn.execute(ddl)
+        import os
+
+        cols = {r[1] for r in self.conn.execute("PRAGMA table_info(player)")}
+        cas = os.environ.get("PLAYER_CAS", "auto")
+        if cas == "1" and "version" not in cols:  # an older file: add the column
+            self.conn.execute("ALTER TABLE player ADD COLUMN version INTEGER NOT NULL DEFAULT 0")
+            cols.add("version")
+        # versioned player writes (compare-and-set, WriteConflict): on for a player table with
+        # a version column unless PLAYER_CAS=0 (the reference's racing replicas)
+        self.versioned = "version" in cols and cas != "0"
+        self.batch_log = os.environ.get("BATCH_LOG") == "true"
+        self.replica = os.environ.get("REPLICA") or ""
+        if self.batch_log:
+            self.conn.execute(BATCH_LOG_DDL)
         self.conn.commit()
         self.commits = 0
         # integer keys of player api ids (columnar batches, resident roster rows)

@@ -53,6 +53,7 @@ from __future__ import annotations
 import json
 import logging
 import os
+import random
 import time
 from operator import attrgetter
 
@@ -81,6 +82,7 @@ class WorkerStats:
     nacked: int = 0
     published: Dict[str, int] = field(default_factory=dict)
     seconds: float = 0.0
+    cas_retries: int = 0  # batches rated again after a versioned write conflict
 
     def bump(self, key: str, n: int = 1) -> None:
         self.published[key] = self.published.get(key, 0) + n
@@ -364,6 +366,33 @@ class Worker:
         logger.info("analyzing batch %s", str(len(batch)))
         ids = batch.match_ids() if isinstance(batch, Deliveries) else list(set(_decode(b) for _, _, b in batch))
         self.stats.messages += len(batch)
+        from .store import WriteConflict
+
+        attempt = 0
+        while True:
+            try:
+                matches, quarantined, counts = self._process_once(ids)
+                break
+            except WriteConflict as e:
+                # another replica committed some of this batch's players since they were
+                # read: everything was rolled back -- rate the batch again from fresh rows
+                attempt += 1
+                self.stats.cas_retries += 1
+                if attempt > self.cfg.cas_retries:
+                    raise
+                logger.info("batch write conflict (%s): retry %d", e, attempt)
+                time.sleep(random.uniform(0.0, 0.002 * min(attempt, 10)))
+        self.stats.matches += len(matches)
+        self.stats.quarantined += len(quarantined)
+        self.failed_ids += quarantined
+        if logger.isEnabledFor(logging.INFO):
+            logger.info(json.dumps({"batch": self.stats.batches, "messages": len(batch),
+                                    "matches": len(matches), "engine": self.cfg.engine,
+                                    "quarantined": len(quarantined), **counts}))
+        return quarantined
+
+    def _process_once(self, ids):
+        """One attempt at a batch: load, rate, commit (all rolled back on an exception)."""
         session = self.store.session()
         quarantined: List[str] = []
         counts: Dict[str, int] = {}
@@ -371,7 +400,8 @@ class Worker:
             if self.cfg.engine == "native" and not self.cfg.skip_rated and hasattr(session, "load_batch"):
                 # columnar path: no per-object work (runtime/columnar.py); without
                 # RESIDENT the batch's players are all re-read from the store
-                if not self.cfg.resident:
+                if not self.cfg.resident or getattr(self.store, "versioned", False):
+                    # (versioned writes need the version of every player row read)
                     self._batched().resident.reset()
                 with trace_range("load", ids=len(ids)):
                     mb = session.load_batch(ids, self.cfg.chunksize)
@@ -403,14 +433,7 @@ class Worker:
             raise
         finally:
             session.close()
-        self.stats.matches += len(matches)
-        self.stats.quarantined += len(quarantined)
-        self.failed_ids += quarantined
-        if logger.isEnabledFor(logging.INFO):
-            logger.info(json.dumps({"batch": self.stats.batches, "messages": len(batch),
-                                    "matches": len(matches), "engine": self.cfg.engine,
-                                    "quarantined": len(quarantined), **counts}))
-        return quarantined
+        return matches, quarantined, counts
 
     def _rate_python(self, session, matches, counts) -> List[str]:
         bad = []
@@ -510,7 +533,7 @@ class Worker:
                 matches = [m for m in matches if m.api_id not in self.cfg.fault_poison]
         rater = self._batched()
         res = getattr(rater, "resident", None)
-        if res is not None and not self.cfg.resident:
+        if res is not None and (not self.cfg.resident or getattr(self.store, "versioned", False)):
             # a ResidentBatchRater on a columnar-capable store without RESIDENT (the
             # object path: SKIP_RATED, or a store without load_batch): the device rows
             # cached by api id would go stale against other replicas' commits, so the

@@ -385,10 +385,16 @@ def main(argv=None) -> int:
     elapsed = time.perf_counter() - t0
     ms = elapsed * 1000.0 / args.steps
     merge = {}
+    side_correct = None
     if merger is not None:
         merger.timing = False
         merge = {k: v / args.steps for k, v in merger.stage_ms().items()}
-    vals = [ms] + [merge.get(k, 0.0) for k in ("messages", "allreduce", "apply", "overlap", "correct")]
+        if merger.split() and merger.correct and (world > 1 or args.force_merge):
+            # the split merge corrects the records on a side stream beside the next rating:
+            # its own time, off the main stream (parallel/sweep.py merge_split)
+            side_correct = merger.correction_ms() / args.steps
+    vals = [ms] + [merge.get(k, 0.0) for k in ("messages", "allreduce", "apply", "overlap", "correct")] + \
+        [side_correct or 0.0]
     t = torch.tensor(vals, dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -400,10 +406,19 @@ def main(argv=None) -> int:
         # start in one pass, so no per-window copy of the roster is taken
         # prepass_overlap: the next window's prepass, enqueued while the all-reduces
         # are in flight (serial placement); "allreduce" is what stays exposed after it
+        split = merger.split()
         merge_ms = {"snapshot": 0.0, "messages": mm[0], "allreduce": mm[1], "apply": mm[2],
-                    # the causal record correction's pass over the window's records
-                    "correct_records": mm[4] if merger.correct else None,
-                    "total": sum(mm[:3]) + mm[4], "prepass_overlap": mm[3], "bytes_per_rank": merger.comm_bytes,
+                    # the causal record correction's pass over the window's records: on the main
+                    # stream (round-5 merges), or beside the next rating (split merge: side-stream
+                    # time, not part of "total")
+                    "correct_records": (mm[5] if split else mm[4]) if merger.correct else None,
+                    "correct_records_on": ("side stream beside the next rating" if split else "main stream")
+                    if merger.correct else None,
+                    "collective": ("split: all-to-all + owner reduce + all-gather of the sum (critical), "
+                                   "prefix all-to-all deferred" if split else "scan (3 (N-1)/N)" if merger.correct
+                                   else "bucketed all-reduce"),
+                    "total": sum(mm[:3]) + (0.0 if split else mm[4]), "prepass_overlap": mm[3],
+                    "bytes_per_rank": merger.comm_bytes,
                     "buckets": len(merger.buckets()),
                     # where the next window's prepass ran: beside the merge (serial) or in
                     # the rating's tail; chosen from a timed all-reduce for N > 1
@@ -503,8 +518,8 @@ def main(argv=None) -> int:
                 "team_size": K,
                 "parallelism": "dp%d" % world,
                 "mode": ("exact" if world == 1 else
-                         "sweep (exact per rank + RCCL posterior merge, %d causal sweep%s)"
-                         % (args.sweeps, "s" if args.sweeps > 1 else "")),
+                         "sweep (exact per rank + %s posterior merge, %d causal sweep%s)"
+                         % ("RCCL" if backend == "nccl" else backend, args.sweeps, "s" if args.sweeps > 1 else "")),
                 "bench_config": args.config,
                 "skew": args.skew,
                 "comm_dtype": args.comm_dtype if world > 1 or args.force_merge else None,

@@ -113,10 +113,13 @@ def test_multi_rank_json_contract_on_cpu(tmp_path, n):
     j = json.loads(lines[0])
     k = min(n, 8)
     assert j["n_gpus"] == n and j["rccl_world"] == n and j["dist_backend"] == "gloo" and j["device"] == "cpu"
+    # the mode names the backend that merged (a gloo rehearsal never claims RCCL)
+    assert "gloo posterior merge" in j["config"]["mode"] and "RCCL" not in j["config"]["mode"]
     assert j["config"]["parallelism"] == "dp%d" % n and j["config"]["merges_per_step"] == k
     assert j["value"] == pytest.approx(n * 1000 * n / (j["ms_per_step"] / 1000.0))
     mm = j["merge_ms"]
     assert mm["prepass_placement"] and mm["buckets"] >= 1
+    assert mm["collective"].startswith("split")  # the round-6 merge
     acc = j["accuracy"]
     for key in ("records_dmu_median", "records_dmu_p99", "records_dmu_max", "spearman_mu_minus_sigma"):
         assert acc[key] is not None, key

@@ -511,21 +511,24 @@ def _corrected(rank, size, P, M, K, seed, windows, comm_dtype):
     return {"state": roster.state, "last": outs[-1]}
 
 
-def _corrected_ring(rank, size, P, M, K, seed, windows, defer):
+def _corrected_ring(rank, size, P, M, K, seed, windows, mode):
     """bench.py's use: windows rated into two alternating record buffers, nothing
-    consumed until finish() (the deferred corrections run inside later merges)."""
+    consumed until finish().  mode: "split" (the round-6 merge: the sum on the critical
+    path, prefix + correction deferred), "defer" / "inline" (the round-5 scan merge with
+    the correction run inside the next merge / right after the decode)."""
     import os
 
     from analyzer_amd.ops.rate import BatchRater, RateResult
     from analyzer_amd.parallel.sweep import SweepMerger
     from analyzer_amd.runtime.engine import WindowPipeline
 
-    os.environ["ANA_DP_CORRECT_DEFER"] = "1" if defer else "0"
+    os.environ["ANA_DP_SPLIT"] = "1" if mode == "split" else "0"
+    os.environ["ANA_DP_CORRECT_DEFER"] = "1" if mode == "defer" else "0"
     roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
     spec = StreamSpec(team_size=K, seed=seed + 1)
     recs = [make_stream(spec, M, P, K=K, base=(w * size + rank) * M) for w in range(windows)]
-    merger = SweepMerger(P, "cpu", comm_dtype="bf16")
-    assert merger.defer == defer
+    merger = SweepMerger(P, "cpu", comm_dtype="bf16", correct_records=True)
+    assert merger.split() == (mode == "split")
     pipe = WindowPipeline(BatchRater(), roster, K, merger=merger)
     outs = [RateResult.allocate(M, K, "cpu") for _ in range(2)]
     prep = pipe.prepare(recs[0])
@@ -537,16 +540,20 @@ def _corrected_ring(rank, size, P, M, K, seed, windows, defer):
 
 
 def test_deferred_record_correction_matches_inline(tmp_path):
-    """The record correction deferred into the next merge (beside its collective)
-    writes exactly the records the in-line pass writes, once finish() has run."""
+    """The record correction deferred into the next merge (beside its collective), and
+    the round-6 split merge (all-to-all / owner reduce / all-gather of the sum, the prefix
+    returned and the records corrected after the decode), write exactly the records and
+    the roster the in-line pass writes, once finish() has run."""
     P, M, K, seed, size, windows = 300, 700, 3, 41, 2, 3
-    a = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, True)
-    b = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, False)
+    a = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, "defer")
+    b = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, "inline")
+    c = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, "split")
     for r in range(size):
         assert a[r]["pending"] and not b[r]["pending"]
-        assert torch.equal(a[r]["state"].view(torch.int32), b[r]["state"].view(torch.int32))
-        for x, y in zip(a[r]["rows"], b[r]["rows"]):
-            assert torch.equal(x.view(torch.int32), y.view(torch.int32))
+        for o in (a[r], c[r]):
+            assert torch.equal(o["state"].view(torch.int32), b[r]["state"].view(torch.int32))
+            for x, y in zip(o["rows"], b[r]["rows"]):
+                assert torch.equal(x.view(torch.int32), y.view(torch.int32))
 
 
 @pytest.mark.parametrize("comm_dtype", ["fp32", "bf16"])
@@ -620,3 +627,35 @@ def test_packed_touch_word_decodes_like_the_fp32_fields():
     native().sweep_apply_packed(sb, msg3, cnt3, start.attrs, s_p, s2_p, vst, 500.0)
     assert torch.equal(s_p.nan_to_num(-7), s_ref.nan_to_num(-7))
     assert torch.equal(s2_p.nan_to_num(-7), s2_ref.nan_to_num(-7))
+
+
+def _split_ex(rank, size):
+    from analyzer_amd.parallel.comm import SplitExchange
+
+    P = 22
+    h = (torch.arange(P * 14, dtype=torch.float32).view(P, 14) * 0.37 + 100 * rank).to(torch.bfloat16)
+    op = torch.empty((P, 8), dtype=torch.int32)
+    op[:, :7] = h.view(torch.int32)
+    op[:, 7] = rank + 1
+    ex = SplitExchange(op, torch.bfloat16, want_prefix=True)
+    return {"h": h.float(), "total": ex.total().clone(), "prefix": ex.prefix().clone()}
+
+
+def test_split_exchange_over_ranks(tmp_path):
+    """The split merge's collective (comm.SplitExchange): every rank gets the sum over
+    ranks (bf16 summed in fp32 in rank order, rounded once; the touch word as an integer)
+    and its exclusive prefix, with ragged row blocks (22 rows over 3 ranks)."""
+    size = 3
+    res = run_ranks(_split_ex, size, tmp_path)
+    hs = [r["h"] for r in res]
+    for r, out in enumerate(res):
+        acc = torch.zeros(22, 14)
+        for q in range(r):
+            acc = acc + hs[q]
+        assert torch.equal(out["prefix"].view(torch.bfloat16).float(), acc.to(torch.bfloat16).float())
+        tot = torch.zeros(22, 14)
+        for q in range(size):
+            tot = tot + hs[q]
+        assert torch.equal(out["total"][:, :7].contiguous().view(torch.bfloat16).float(),
+                           tot.to(torch.bfloat16).float())
+        assert torch.equal(out["total"][:, 7], torch.full((22,), 6, dtype=torch.int32))

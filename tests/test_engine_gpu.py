@@ -833,3 +833,29 @@ def test_make_telemetry_host_counts_match_device(gpu_device, monkeypatch):
     monkeypatch.setattr(T, "HOST_COUNTS_MAX", 0)
     b = T.make_telemetry(spec, rec, K, base=1234)
     assert torch.equal(a.evoff, b.evoff) and torch.equal(a.events, b.events)
+
+
+@pytest.mark.parametrize("dtype,N", [(torch.bfloat16, 8), (torch.float16, 8), (torch.bfloat16, 3), (torch.float16, 1)])
+def test_split_block_reduce_kernel_matches_host(gpu_device, dtype, N):
+    """csrc/sweep.hip sweep_block_reduce (the split merge's owner reduce) against the host
+    reduce parallel/comm.py block_reduce_rows, bit for bit: sums and exclusive prefixes of
+    the 16-bit halves in fp32 in rank order, rounded once; touch words as integers."""
+    from analyzer_amd.ops.native import native
+    from analyzer_amd.parallel.comm import block_reduce_rows
+
+    g = torch.Generator().manual_seed(5 + N)
+    blk = 10007
+    h = (torch.randn((N * blk, 14), generator=g) * 40).to(dtype)
+    recv = torch.empty((N * blk, 8), dtype=torch.int32)
+    recv[:, :7] = h.view(torch.int32)
+    recv[:, 7] = torch.randint(0, 1 << 20, (N * blk,), generator=g, dtype=torch.int32)
+    tot_h, pref_h = block_reduce_rows(recv, N, dtype, True)
+    rd = recv.to(gpu_device)
+    tot = torch.empty((blk, 8), dtype=torch.int32, device=gpu_device)
+    pref = torch.empty((N * blk, 7), dtype=torch.int32, device=gpu_device)
+    native().sweep_block_reduce(rd, N, dtype == torch.bfloat16, tot, pref)
+    tot2 = torch.empty_like(tot)
+    native().sweep_block_reduce(rd, N, dtype == torch.bfloat16, tot2)  # no prefix
+    torch.cuda.synchronize()
+    assert torch.equal(tot.cpu(), tot_h) and torch.equal(tot2.cpu(), tot_h)
+    assert torch.equal(pref.cpu(), pref_h)

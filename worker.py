@@ -97,7 +97,7 @@ def main(argv=None) -> int:
     st = _worker.stats
     print(json.dumps({"matches": st.matches, "messages": st.messages, "batches": st.batches,
                       "failed_batches": st.failed_batches, "quarantined": st.quarantined,
-                      "acked": st.acked, "nacked": st.nacked, "seconds": dt,
+                      "acked": st.acked, "nacked": st.nacked, "cas_retries": st.cas_retries, "seconds": dt,
                       "matches_per_s": st.matches / dt if dt > 0 else None,
                       "engine": CONFIG.engine}), flush=True)
     return 0
