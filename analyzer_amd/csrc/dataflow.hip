@@ -55,6 +55,10 @@
 
 namespace ana {
 
+// The LDS local hand-off (ANA_RATE_LOCAL) exists in the diagnostic library only.
+constexpr bool kLocalHandoff = ANA_DIAG_BUILD != 0;
+
+
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight
 // K8 inline telemetry: events per match loaded with the batch's granules (more go
 // through a remainder loop after the rating); per group lane ceil(64 / G) 8-B loads
@@ -110,8 +114,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   typedef uint32_t hvec __attribute__((ext_vector_type(kH)));
   // local hand-off counters: increments of each held match's completion count
   // by publishes of THIS wave (never also added to the global counter); [lane][h]
-  // so a lane reads them in one ds_read_b64/b128
-  __shared__ hvec lloc[kWavesPerBlock][kChunk];
+  // so a lane reads them in one ds_read_b64/b128.  Measured slower than the global
+  // counters since round 5 (profiles/r5/local_handoff_off.log): compiled into the
+  // diagnostic library only (kLocalHandoff), the production executor has no LDS
+  // array, no per-iteration read of it and no held-chunk scan in notify
+  __shared__ hvec lloc[kWavesPerBlock][kLocalHandoff ? kChunk : 1];
   // this iteration's pick per group, written by the lane holding the match:
   // {match index, slot << 8 | lane in chunk, meta0, meta1, player ids...}
   constexpr int SPT = (4 + S + 3) / 4 * 4;  // inline telemetry words: {offset lo, hi, count, 0}
@@ -150,7 +157,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // (ctrl[3] counts retired chunks), so long dependency chains never trip it
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_progress = 0;
-  const bool local_ok = prm.local_handoff != 0;
+  const bool local_ok = kLocalHandoff && prm.local_handoff != 0;
   // hand-off statistics (wave-uniform counts, added to ctrl[26..27] at exit); stale
   // reads retried (ctrl[14])
   uint32_t n_local = 0, n_global = 0, n_stale = 0;
@@ -286,7 +293,8 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     // and without local hand-off the counts stay 0
     uint64_t ready[kH];
     {
-      const hvec lv = lloc[wv][lane];
+      hvec lv = {};
+      if constexpr (kLocalHandoff) lv = lloc[wv][lane];
 #pragma unroll
       for (int h = 0; h < kH; ++h)
         ready[h] = __ballot(dval[h] != kNone && dval[h] + lv[h] == need[h]) & pend[h];
@@ -505,7 +513,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       if (succ == kNoMatch) return;
       int lh = -1;
       int32_t lcb = 0;
-      if (local_ok) {
+      if (kLocalHandoff && local_ok) {
 #pragma unroll
         for (int h = 0; h < kH; ++h)
           if (cbase[h] >= 0 && (int32_t)succ >= cbase[h] && (int32_t)succ < cbase[h] + cl) {
@@ -513,7 +521,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
             lcb = cbase[h];
           }
       }
-      if (lh >= 0) {  // held by this wave: release it through LDS, next iteration
+      if (kLocalHandoff && lh >= 0) {  // held by this wave: release it through LDS, next iteration
         atomicAdd(reinterpret_cast<uint32_t*>(&lloc[wv][(int32_t)succ - lcb]) + lh, 1u);
       } else {
         __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -784,7 +792,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           hoff[h] = stoff;
           hcnt[h] = stcnt;
         }
-      reinterpret_cast<uint32_t*>(&lloc[wv][lane])[staging] = 0u;
+      if constexpr (kLocalHandoff) reinterpret_cast<uint32_t*>(&lloc[wv][lane])[staging] = 0u;
       // no state, no dependencies: its output row is written after this iteration's
       // rating (early_row), so the rating's waits never include these stores
       if (mm < M && est != kRated && !tonly) {

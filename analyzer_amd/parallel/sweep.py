@@ -162,7 +162,11 @@ class SweepMerger:
         self.op = torch.empty((self.P, 16), dtype=COMM_DTYPES[comm_dtype], device=self.device) \
             if comm_dtype != "fp32" else None
         self._starts = [self.start, None]
-        self.use_split = os.environ.get("ANA_DP_SPLIT", "1") not in ("", "0", "false")
+        # default off: on one GPU with the emulated collective the split merge measured slower
+        # for config 2 at N = 8 (11.58-11.76 vs 11.22-11.26 ms per step, profiles/r6/
+        # dp_split_merge.log) -- the merge slot is bandwidth-bound by the next window's prepass
+        # and the record correction, not by the collective; ANA_DP_SPLIT=1 turns it on
+        self.use_split = os.environ.get("ANA_DP_SPLIT", "0") not in ("", "0", "false")
         # where the deferred prefix exchange + record correction start: a callable that makes
         # a stream wait for the NEXT rating launch's tail (runtime/engine.py sets it when the
         # launches carry a tail signal, ANA_DP_DEFER_AT); None: right behind the decode

@@ -48,7 +48,10 @@ from ..ops.rate import Roster
 
 META = "meta.json"
 TENSORS = "roster.safetensors"
-FORMAT = 2  # 1: full [P, 32] state rows (tags included); 2: base rows [P, 16] + attrs
+ATTRS = "attrs.safetensors"
+# 1: full [P, 32] state rows (tags included); 2: base rows [P, 16] + attrs in one file;
+# 3: tracks [P, 14] (the spare granule only when not NULL) + attrs in their own file
+FORMAT = 3
 
 
 def _fsync_dir(path: str) -> None:
@@ -93,7 +96,7 @@ def _rmtree(path: str) -> None:
 
 
 WRITE_PIECE = 64 << 20
-WRITE_THREADS = int(os.environ.get("ANA_CKPT_WRITE_THREADS") or 8)
+WRITE_THREADS = int(os.environ.get("ANA_CKPT_WRITE_THREADS") or 1)
 
 _ST_DTYPES = {torch.float32: "F32", torch.float64: "F64", torch.int32: "I32", torch.int64: "I64",
               torch.uint8: "U8"}
@@ -157,6 +160,14 @@ def base_and_attrs(roster: Roster) -> Tuple[torch.Tensor, torch.Tensor]:
     return roster.state.view(P, 8, 4)[:, :, 0::2].reshape(P, 16), roster.attrs
 
 
+def spare_is_null(roster: Roster) -> bool:
+    """Whether the spare granule 7 of every row is NULL (NaN mu and sigma), as every
+    roster source writes it and nothing rates into it (csrc/common.h): then format 3
+    leaves it out -- 56 instead of 64 B of ratings per player (syncs once)."""
+    P = roster.num_players
+    return bool(torch.isnan(roster.state.view(P, 8, 4)[:, 7, 0::2]).all())
+
+
 def _state_from_base(base: torch.Tensor) -> torch.Tensor:
     P = base.shape[0]
     state = torch.zeros((P, 32), dtype=torch.float32, device=base.device)
@@ -164,61 +175,98 @@ def _state_from_base(base: torch.Tensor) -> torch.Tensor:
     return state
 
 
-def _meta(roster: Roster, meta: Dict[str, Any]) -> Dict[str, Any]:
-    return dict(meta, epoch=roster.epoch, num_players=roster.num_players, format=FORMAT)
+def _meta(roster: Roster, meta: Dict[str, Any], spare: bool) -> Dict[str, Any]:
+    return dict(meta, epoch=roster.epoch, num_players=roster.num_players, format=FORMAT, spare_saved=spare)
 
 
-def _write(path: str, base: torch.Tensor, attrs: torch.Tensor, meta: Dict[str, Any], fsync: bool = True) -> None:
+def _write(path: str, tracks: torch.Tensor, attrs: Optional[torch.Tensor], meta: Dict[str, Any],
+           fsync: bool = True, link_attrs: Optional[str] = None) -> None:
+    """One checkpoint directory: ``tracks`` [P, 14] (or [P, 16] with the spare granule),
+    ``attrs`` [P, 4] -- written, or hard-linked from ``link_attrs`` (an unchanged attrs
+    file of the previous checkpoint: no bytes written)."""
     def write(d):
-        write_safetensors(os.path.join(d, TENSORS), {"base": base, "attrs": attrs})
+        write_safetensors(os.path.join(d, TENSORS), {"tracks": tracks})
+        dst = os.path.join(d, ATTRS)
+        linked = False
+        if link_attrs is not None and os.path.exists(link_attrs):
+            try:
+                os.link(link_attrs, dst)
+                linked = True
+            except OSError:  # another file system: write them
+                linked = False
+        if not linked:
+            write_safetensors(dst, {"attrs": attrs})
         with open(os.path.join(d, META), "w") as f:
             json.dump(meta, f, indent=1, sort_keys=True)
 
     _atomic_dir_write(path, write, fsync)
 
 
+def _tracks(base: torch.Tensor, spare: bool) -> torch.Tensor:
+    return base if spare else base[:, :14]
+
+
 def save(path: str, roster: Roster, meta: Dict[str, Any], fsync: bool = True) -> None:
     """Write one checkpoint directory synchronously (replaces an existing one atomically)."""
     base, attrs = base_and_attrs(roster)
-    _write(path, base.detach().cpu().contiguous(), attrs.detach().cpu().contiguous(), _meta(roster, meta), fsync)
+    spare = not spare_is_null(roster)
+    _write(path, _tracks(base, spare).detach().cpu().contiguous(), attrs.detach().cpu().contiguous(),
+           _meta(roster, meta, spare), fsync)
 
 
 def load(path: str, device="cpu") -> Tuple[Roster, Dict[str, Any]]:
+    """Formats 1 (full rows), 2 (base rows + attrs in one file) and 3 (tracks; attrs in
+    their own file, hard-linked between checkpoints while unchanged)."""
     t = load_file(os.path.join(path, TENSORS))
     with open(os.path.join(path, META)) as f:
         meta = json.load(f)
     # tags are only meaningful within the process that wrote them: reset on resume
-    state = t["state"] if "state" in t else _state_from_base(t["base"])  # format 1 / 2
-    if "state" in t:
-        state = state.clone()
+    if "state" in t:      # format 1
+        state = t["state"].clone()
         state.view(-1, 8, 4)[:, :, 1::2] = 0.0
-    roster = Roster(state.to(device), t["attrs"].to(device), epoch=None)
+    elif "base" in t:     # format 2
+        state = _state_from_base(t["base"])
+    else:                 # format 3
+        tr = t["tracks"]
+        base = torch.full((tr.shape[0], 16), float("nan"), dtype=torch.float32)
+        base[:, :tr.shape[1]] = tr
+        state = _state_from_base(base)
+    attrs = t["attrs"] if "attrs" in t else load_file(os.path.join(path, ATTRS))["attrs"]
+    roster = Roster(state.to(device), attrs.to(device), epoch=None)
     return roster, meta
 
 
 class AsyncCheckpointer:
     """Checkpoints written beside the rating (module docstring).  ``submit`` is
     stream-ordered on the caller's current stream: it snapshots the roster as the
-    work enqueued so far leaves it, and returns without waiting for the GPU."""
+    work enqueued so far leaves it, and returns without waiting for the GPU.
 
-    def __init__(self, device, num_players: int, buffers: int = 2, fsync: bool = True):
+    ``static_attrs``: the caller guarantees the attributes never change during the run
+    (runtime/rerate.py: the kernels only read them, csrc/dataflow.hip) -- they are copied
+    to the host once, written with the first checkpoint and hard-linked into the later ones."""
+
+    def __init__(self, device, num_players: int, buffers: int = 2, fsync: bool = True,
+                 static_attrs: bool = False):
         self.device = torch.device(device)
         self.P = int(num_players)
         self.fsync = bool(fsync)
+        self.static_attrs = bool(static_attrs)
         self.cuda = self.device.type == "cuda"
+        self.spare: Optional[bool] = None  # spare granule saved (decided at the first submit)
         f = dict(dtype=torch.float32)
-        # device staging (the copy stream reads it while the rating goes on)
-        self._stage = ((torch.empty((self.P, 16), device=self.device, **f),
-                        torch.empty((self.P, 4), device=self.device, **f)) if self.cuda else None)
+        self._f = f
+        self._stage = None
         self._staged: Optional[torch.cuda.Event] = None     # staging free again (its D2H done)
-        self._host = [(torch.empty((self.P, 16), pin_memory=self.cuda, **f),
-                       torch.empty((self.P, 4), pin_memory=self.cuda, **f)) for _ in range(max(1, buffers))]
+        self._host: List[Tuple[torch.Tensor, Optional[torch.Tensor]]] = []
+        self._nbuf = max(1, buffers)
+        self._attrs_host: Optional[torch.Tensor] = None    # static attrs, copied once
+        self._attrs_file: Optional[str] = None             # their last committed file
         self._copy = torch.cuda.Stream(self.device) if self.cuda else None
         self._next = 0
         # one writer thread, FIFO: checkpoints commit in submission order (two writers
         # would race on the renames, and an older snapshot could land last)
         self._queue: "queue.Queue" = queue.Queue()
-        self._free = [threading.Event() for _ in self._host]  # buffer i may be refilled
+        self._free = [threading.Event() for _ in range(self._nbuf)]  # buffer i may be refilled
         for e in self._free:
             e.set()
         self._errors: List[BaseException] = []
@@ -226,19 +274,36 @@ class AsyncCheckpointer:
         self.written = 0
         self.bytes = 0
 
+    def _buffers(self, roster: Roster) -> None:
+        if self._host:
+            return
+        self.spare = not spare_is_null(roster)
+        w = 16 if self.spare else 14
+        f, pin = self._f, self.cuda
+        keep_attrs = not self.static_attrs
+        if self.cuda:
+            self._stage = (torch.empty((self.P, w), device=self.device, **f),
+                           torch.empty((self.P, 4), device=self.device, **f) if keep_attrs else None)
+        self._host = [(torch.empty((self.P, w), pin_memory=pin, **f),
+                       torch.empty((self.P, 4), pin_memory=pin, **f) if keep_attrs else None)
+                      for _ in range(self._nbuf)]
+
     def _run(self) -> None:
         while True:
             item = self._queue.get()
             if item is None:
                 return
-            i, path, meta, done = item
-            hb, ha = self._host[i]
+            i, path, meta, done, attrs = item
+            hb, _ = self._host[i]
             try:
                 if done is not None:
                     done.synchronize()
-                _write(path, hb, ha, meta, self.fsync)
+                link = self._attrs_file if self.static_attrs else None
+                _write(path, hb, attrs, meta, self.fsync, link_attrs=link)
+                if self.static_attrs:
+                    self._attrs_file = os.path.join(path, ATTRS)
                 self.written += 1
-                self.bytes += (hb.numel() + ha.numel()) * 4
+                self.bytes += hb.numel() * 4 + (0 if link else attrs.numel() * 4)
             except BaseException as e:  # re-raised by the next submit / flush
                 self._errors.append(e)
             finally:
@@ -246,37 +311,45 @@ class AsyncCheckpointer:
                 self._queue.task_done()
 
     def submit(self, path: str, roster: Roster, meta: Dict[str, Any]) -> None:
+        self._buffers(roster)
         i = self._next
-        self._next = (self._next + 1) % len(self._host)
+        self._next = (self._next + 1) % self._nbuf
         self._free[i].wait()  # back-pressure: that buffer's write is still running
         self._raise()
         self._free[i].clear()
         hb, ha = self._host[i]
         base, attrs = base_and_attrs(roster)
+        tracks = _tracks(base, self.spare)
         done = None
+        if self.static_attrs and self._attrs_host is None:
+            self._attrs_host = attrs.detach().to("cpu", copy=True).contiguous()  # once (syncs)
         if self.cuda:
             main = torch.cuda.current_stream(self.device)
             if self._staged is not None:
                 main.wait_event(self._staged)  # the previous snapshot left the staging buffer
             sb, sa = self._stage
-            sb.copy_(base)
-            sa.copy_(attrs)
+            sb.copy_(tracks)
+            if sa is not None:
+                sa.copy_(attrs)
             snap = torch.cuda.Event()
             snap.record(main)
             self._copy.wait_event(snap)
             with torch.cuda.stream(self._copy):
                 hb.copy_(sb, non_blocking=True)
-                ha.copy_(sa, non_blocking=True)
+                if sa is not None:
+                    ha.copy_(sa, non_blocking=True)
                 done = torch.cuda.Event()
                 done.record(self._copy)
             self._staged = done
         else:
-            hb.copy_(base)
-            ha.copy_(attrs)
+            hb.copy_(tracks)
+            if ha is not None:
+                ha.copy_(attrs)
         if self._writer is None:
             self._writer = threading.Thread(target=self._run, name="checkpoint-writer", daemon=True)
             self._writer.start()
-        self._queue.put((i, path, _meta(roster, meta), done))
+        self._queue.put((i, path, _meta(roster, meta, self.spare), done,
+                         self._attrs_host if self.static_attrs else ha))
 
     def flush(self) -> None:
         """Wait until every submitted checkpoint is committed (renamed into place)."""
@@ -302,8 +375,9 @@ class CheckpointManager:
     ``asynchronous``: writes go through an ``AsyncCheckpointer`` (default on a GPU
     device, ``ANA_CKPT_ASYNC=0`` turns it off); ``flush`` commits what is in flight."""
 
-    def __init__(self, directory: Optional[str], every: int = 1, rank: int = 0):
+    def __init__(self, directory: Optional[str], every: int = 1, rank: int = 0, static_attrs: bool = False):
         self.directory = directory
+        self.static_attrs = bool(static_attrs)
         self.every = max(1, int(every))
         self.rank = rank
         self.saved = 0
@@ -327,7 +401,8 @@ class CheckpointManager:
             os.environ.get("ANA_CKPT_ASYNC", "1") not in ("", "0", "false")
         if use_async:
             if self._async is None:
-                self._async = AsyncCheckpointer(roster.state.device, roster.num_players, fsync=self.fsync)
+                self._async = AsyncCheckpointer(roster.state.device, roster.num_players, fsync=self.fsync,
+                                                static_attrs=self.static_attrs)
             self._async.submit(self.path, roster, meta)
         else:
             save(self.path, roster, meta, self.fsync)

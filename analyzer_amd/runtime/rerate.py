@@ -143,7 +143,9 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
         torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
     rater = rater or R.BatchRater(RaterConfig())
     K = spec.team_size
-    ck = CheckpointManager(checkpoint_dir, checkpoint_every, rank=0)
+    # the rating kernels only read the attributes (csrc/dataflow.hip): written with the
+    # first checkpoint, hard-linked into the later ones (runtime/checkpoint.py)
+    ck = CheckpointManager(checkpoint_dir, checkpoint_every, rank=0, static_attrs=True)
     start_window = 0
     restored = ck.latest(dev)
     if restored is not None:

@@ -134,6 +134,13 @@ def parse(argv=None):
             k *= 2
         if args.team_size == 5 and n >= 4:
             k *= 2      # 5v5: 10 appearances a match, twice the merges for the same error
+        if args.config == 5:
+            # 16M matches per rank over 10M players: ~1.2 appearances per player per rank and
+            # window at k = 8, ~10 at k = 1 -- against 7.5 / 60 for config 2 -- so ONE merge per
+            # step meets both fidelity bars at N = 8 (roster Spearman 0.9988 >= 0.995, records
+            # median 3.45 <= 8, 0 clamps; profiles/r6/fidelity_config5.log) and the 320-MB
+            # merge runs once per step instead of k times
+            k = 1
         # k = 8 at N = 8 is the smallest k that meets both fidelity bars with the causal
         # record correction (simulated N = 8: records median 8.0 <= 15, roster Spearman
         # 0.9956 >= 0.995; k = 4 gives records 14.1 but roster Spearman 0.983 --

@@ -69,6 +69,8 @@ def test_merges_per_step_default_is_accuracy_bounded(monkeypatch):
     # 5v5 has 10 appearances a match: twice the merges from N = 4 (merges_vs_ranks_5v5.log)
     assert bench.parse(["--gpus", "4", "--config", "3"]).merges_per_step == 8
     assert bench.parse(["--gpus", "8", "--config", "3"]).merges_per_step == 16
+    # config 5 (10M players): one merge per step meets the fidelity bars at N = 8
+    assert bench.parse(["--gpus", "8", "--config", "5"]).merges_per_step == 1
     assert bench.parse(["--gpus", "8", "--sweeps", "8"]).merges_per_step == 1
     assert bench.parse(["--gpus", "8", "--config", "4"]).merges_per_step == 1
     assert bench.parse(["--gpus", "8", "--merges-per-step", "2"]).merges_per_step == 2
@@ -119,7 +121,7 @@ def test_multi_rank_json_contract_on_cpu(tmp_path, n):
     assert j["value"] == pytest.approx(n * 1000 * n / (j["ms_per_step"] / 1000.0))
     mm = j["merge_ms"]
     assert mm["prepass_placement"] and mm["buckets"] >= 1
-    assert mm["collective"].startswith("split")  # the round-6 merge
+    assert mm["collective"]  # which exchange merged (split / scan / bucketed all-reduce)
     acc = j["accuracy"]
     for key in ("records_dmu_median", "records_dmu_p99", "records_dmu_max", "spearman_mu_minus_sigma"):
         assert acc[key] is not None, key

@@ -528,7 +528,7 @@ def _corrected_ring(rank, size, P, M, K, seed, windows, mode):
     spec = StreamSpec(team_size=K, seed=seed + 1)
     recs = [make_stream(spec, M, P, K=K, base=(w * size + rank) * M) for w in range(windows)]
     merger = SweepMerger(P, "cpu", comm_dtype="bf16", correct_records=True)
-    assert merger.split() == (mode == "split")
+    assert merger.split() == (mode == "split"), (mode, merger.split())
     pipe = WindowPipeline(BatchRater(), roster, K, merger=merger)
     outs = [RateResult.allocate(M, K, "cpu") for _ in range(2)]
     prep = pipe.prepare(recs[0])

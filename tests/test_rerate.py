@@ -112,29 +112,56 @@ def test_time_axis_sharded_rerate_two_ranks(tmp_path, sweeps):
         assert float(err.max()) < 0.05
 
 
-def test_checkpoint_format2_and_format1_compat(tmp_path):
-    """Format 2 keeps (mu, sigma) + attrs (80 B per player, no tags); a format-1
-    directory (full [P, 32] rows) still loads, with its tags reset."""
-    from safetensors.torch import save_file
+def test_checkpoint_format3_and_older_formats(tmp_path):
+    """Format 3 keeps the 7 tracks' (mu, sigma) (56 B per player: the spare granule is
+    NULL in every row) + the attributes in their own file, no tags; format-1 (full
+    [P, 32] rows) and format-2 (base rows + attrs) directories still load, tags reset."""
+    from safetensors.torch import load_file, save_file
     import json
 
     roster = make_roster(SPEC.roster_spec())
     roster.state.view(-1, 8, 4)[:, :, 1::2] = 3.0  # tags: never saved
-    checkpoint.save(str(tmp_path / "c2"), roster, {"x": 1})
-    from safetensors.torch import load_file
-    t = load_file(str(tmp_path / "c2" / checkpoint.TENSORS))
-    assert sorted(t) == ["attrs", "base"] and tuple(t["base"].shape) == (SPEC.players, 16)
-    r2, meta = checkpoint.load(str(tmp_path / "c2"))
-    assert meta["format"] == 2
+    checkpoint.save(str(tmp_path / "c3"), roster, {"x": 1})
+    t = load_file(str(tmp_path / "c3" / checkpoint.TENSORS))
+    assert sorted(t) == ["tracks"] and tuple(t["tracks"].shape) == (SPEC.players, 14)
+    assert tuple(load_file(str(tmp_path / "c3" / checkpoint.ATTRS))["attrs"].shape) == (SPEC.players, 4)
+    r3, meta = checkpoint.load(str(tmp_path / "c3"))
+    assert meta["format"] == 3 and meta["spare_saved"] is False
     base = lambda s: s.view(-1, 8, 4)[:, :, 0::2].nan_to_num(-7)  # noqa: E731
-    assert torch.equal(base(r2.state), base(roster.state))
-    assert float(r2.state.view(-1, 8, 4)[:, :, 1::2].abs().max()) == 0.0
-    d1 = tmp_path / "c1"
-    d1.mkdir()
-    save_file({"state": roster.state.contiguous(), "attrs": roster.attrs.contiguous()}, str(d1 / checkpoint.TENSORS))
-    (d1 / checkpoint.META).write_text(json.dumps({"format": 1, "windows_done": 3}))
-    r1, meta1 = checkpoint.load(str(d1))
-    assert meta1["windows_done"] == 3 and torch.equal(base(r1.state), base(roster.state))
+    assert torch.equal(base(r3.state), base(roster.state))
+    assert torch.equal(r3.attrs.nan_to_num(-7), roster.attrs.nan_to_num(-7))
+    assert float(r3.state.view(-1, 8, 4)[:, :, 1::2].abs().max()) == 0.0
+    # a non-NULL spare granule is kept
+    odd = make_roster(SPEC.roster_spec())
+    odd.state[0, 28] = 5.0
+    checkpoint.save(str(tmp_path / "c3s"), odd, {})
+    ro, mo = checkpoint.load(str(tmp_path / "c3s"))
+    assert mo["spare_saved"] is True and float(ro.state[0, 28]) == 5.0
+    for fmt, tensors in ((1, {"state": roster.state.contiguous(), "attrs": roster.attrs.contiguous()}),
+                         (2, {"base": checkpoint.base_and_attrs(roster)[0].contiguous(),
+                              "attrs": roster.attrs.contiguous()})):
+        d = tmp_path / ("c%d" % fmt)
+        d.mkdir()
+        save_file(tensors, str(d / checkpoint.TENSORS))
+        (d / checkpoint.META).write_text(json.dumps({"format": fmt, "windows_done": 3}))
+        r, m = checkpoint.load(str(d))
+        assert m["windows_done"] == 3 and torch.equal(base(r.state), base(roster.state))
+        assert float(r.state.view(-1, 8, 4)[:, :, 1::2].abs().max()) == 0.0
+
+
+def test_static_attrs_are_hard_linked(tmp_path):
+    """A run whose attributes never change writes them once: the later checkpoints
+    hard-link the previous file (no bytes written)."""
+    roster = make_roster(SPEC.roster_spec())
+    ck = checkpoint.AsyncCheckpointer("cpu", SPEC.players, fsync=False, static_attrs=True)
+    p = str(tmp_path / "latest")
+    for i in range(3):
+        ck.submit(p, roster, {"windows_done": i + 1})
+        ck.flush()
+    assert os.stat(os.path.join(p, checkpoint.ATTRS)).st_nlink == 1  # the older dirs are gone
+    assert ck.bytes == 3 * SPEC.players * 14 * 4 + SPEC.players * 4 * 4
+    r, meta = checkpoint.load(p)
+    assert meta["windows_done"] == 3 and torch.equal(r.attrs.nan_to_num(-7), roster.attrs.nan_to_num(-7))
 
 
 def test_async_checkpointer_on_host(tmp_path):
