@@ -187,28 +187,26 @@ def test_grid_and_register_builds_bit_identical(gpu_device, K):
         assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32)), blocks
 
 
-@pytest.mark.parametrize("K,P,M,skew", [(3, 16, 4000, 1), (3, 100000, 1000000, 1), (5, 2000, 200000, 1),
-                                        (3, 100000, 300000, 3)])
-def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K, P, M, skew):
-    """The LDS local hand-off (ANA_RATE_LOCAL) and the timing build (ANA_RATE_DIAG)
-    change only WHEN a match runs, never its result: every executor gives the same
-    bits, and hot chains (16 players, skewed activity) actually take the local path."""
+def _handoff_run(K, P, M, skew, device, expect_local):
+    """Rate one stream with every (ANA_RATE_LOCAL, ANA_RATE_DIAG) setting; the results
+    must be bit-identical, and the local hand-off must (or, in the production library,
+    where it is compiled out, must not) take hot chains."""
     rs = RosterSpec(num_players=P, seed=P + 3)
-    rec = make_stream(StreamSpec(team_size=K, seed=M + 1, skew=skew), M, P, K=K, device=gpu_device)
+    rec = make_stream(StreamSpec(team_size=K, seed=M + 1, skew=skew), M, P, K=K, device=device)
     outs = []
     for local, diag in (("0", "0"), ("1", "0"), ("1", "1"), ("0", "1")):
-        monkeypatch.setenv("ANA_RATE_LOCAL", local)
-        monkeypatch.setenv("ANA_RATE_DIAG", diag)
-        ro = make_roster(rs, device=gpu_device)
+        os.environ["ANA_RATE_LOCAL"] = local
+        os.environ["ANA_RATE_DIAG"] = diag
+        ro = make_roster(rs, device=device)
         rater = R.BatchRater()
         res = rater.rate(ro, rec, K)
-        assert int(rater.error_flags(gpu_device).sum()) == 0
-        nl, ng = rater.handoffs(gpu_device)
-        if local == "0":
-            assert nl == 0
+        assert int(rater.error_flags(device).sum()) == 0
+        nl, ng = rater.handoffs(device)
+        if local == "0" or not expect_local:
+            assert nl == 0, (local, nl)
         elif P <= 16 or skew > 1:
             assert nl > 0, (nl, ng)
-        d = rater.diag(gpu_device)
+        d = rater.diag(device)
         if diag == "1":
             assert d["worked_iterations"] > 0 and d["wait_us"] > 0.0 and d["after_us"] > 0.0, d
         outs.append((ro.state.cpu(), res.s_mu.cpu(), res.status.cpu(), res.quality.cpu()))
@@ -219,6 +217,40 @@ def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K
         assert torch.equal(a[1].view(torch.int32), b[1].view(torch.int32))
         assert torch.equal(a[2], b[2])
         assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32))
+
+
+@pytest.mark.parametrize("K,P,M,skew", [(3, 16, 4000, 1), (3, 100000, 1000000, 1), (5, 2000, 200000, 1),
+                                        (3, 100000, 300000, 3)])
+def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K, P, M, skew):
+    """The timing build (ANA_RATE_DIAG) changes only WHEN a match runs, never its result.
+    The LDS local hand-off (ANA_RATE_LOCAL) is compiled out of the production library
+    (csrc/dataflow.hip kLocalHandoff): setting it changes nothing, no hand-off goes local."""
+    monkeypatch.setenv("ANA_RATE_LOCAL", "0")
+    monkeypatch.setenv("ANA_RATE_DIAG", "0")
+    _handoff_run(K, P, M, skew, gpu_device, expect_local=False)
+
+
+def test_local_handoff_in_diagnostic_library(gpu_device):
+    """The diagnostic library (_C_diag, ANA_DIAG_BUILD) keeps the local hand-off: hot
+    chains (16 players, cubic skew) take it and every result is bit-identical (run in a
+    child process: one library per process)."""
+    import subprocess
+    import sys
+
+    from analyzer_amd.build_ext import target_path
+
+    lib = str(target_path(diag=True))
+    if not os.path.exists(lib):
+        pytest.skip("diagnostic library not built (python -m analyzer_amd.build_ext --diag)")
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "import torch, test_engine_gpu as t\n"
+            "for args in ((3, 16, 4000, 1), (3, 100000, 300000, 3)):\n"
+            "    t._handoff_run(*args, torch.device('cuda:0'), True)\n"
+            "print('ok')\n") % (os.path.dirname(os.path.abspath(__file__)),
+                                 os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env = dict(os.environ, ANA_NATIVE_LIB=lib)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "ok" in out.stdout, out.stderr[-3000:]
 
 
 @pytest.mark.parametrize("n,bits", [(1, 8), (4095, 20), (4097, 12), (1_000_003, 20), (300_000, 32)])
