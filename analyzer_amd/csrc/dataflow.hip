@@ -59,9 +59,14 @@ namespace ana {
 constexpr bool kLocalHandoff = ANA_DIAG_BUILD != 0;
 
 
-constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight
-#ifndef ANA_REC_LDS
-#define ANA_REC_LDS 1  // 4v4 / 5v5: held chunks' records in LDS (0: registers, the round-5 build)
+constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight (1v1-4v4)
+// 5v5 keeps two: config 3 19.23-19.27 ms per step against 20.08-20.15 with four (in-call A/B,
+// profiles/r6/config3_held_chunks.log) -- its 3,000+ dependency levels leave most held
+// matches waiting, so the two extra chunks only add polls and staging to every iteration
+// (and 24 registers: 166 -> 142 VGPRs); holding the records in LDS instead of registers
+// (120 VGPRs, 55.7 KB of LDS) measured no faster (20.10-20.22)
+#ifndef ANA_HELD5
+#define ANA_HELD5 2
 #endif
 // K8 inline telemetry: events per match loaded with the batch's granules (more go
 // through a remainder loop after the rating); per group lane ceil(64 / G) 8-B loads
@@ -108,7 +113,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
                      RateParams prm, TelemetryParams tp) {
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
-  constexpr int kH = kHeld;
+  constexpr int kH = K >= 5 ? ANA_HELD5 : kHeld;
   constexpr bool TILES = TELE == 1;  // K8 tiles taken by idle / dedicated waves
   constexpr bool INL = TELE == 2;    // K8 inline: each group folds its match's events
   static_assert(G >= S && G <= 64, "a group holds one match");
@@ -173,13 +178,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // per lane: the record of match cbase[h] + lane (ids, meta0, meta1), kept in
   // registers so the lane that picks a match hands the whole record to its group
   // through one LDS slot (one round trip instead of pick -> meta -> id)
-  // 4v4 / 5v5 (R = 10 / 12 words): in LDS instead ([wave][held][word][lane], each word
-  // read by a whole wave is one conflict-free run), which takes the kH x R registers off
-  // the 5v5 executor's 166 -- so a radix-sort workgroup of the next window's prepass
-  // fits beside its two waves per SIMD (round-5 verdict item 5)
-  constexpr bool RECLDS = ANA_REC_LDS != 0 && K >= 4;
-  __shared__ int32_t lrec[kWavesPerBlock][RECLDS ? kH : 1][RECLDS ? R : 1][64];
-  int32_t hrec[RECLDS ? 1 : kH][R];
+  int32_t hrec[kH][R];
   int64_t hoff[kH];    // per lane (inline telemetry): first event of match cbase + lane
   int32_t hcnt[kH];    // ... and its event count
   int32_t cbase[kH];   // wave-uniform: first match of each held chunk, -1 = free slot
@@ -192,10 +191,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     cbase[h] = -1;
     pend[h] = 0ull;
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      if constexpr (RECLDS) lrec[wv][h][k][lane] = -1;
-      else hrec[h][k] = -1;
-    }
+    for (int k = 0; k < R; ++k) hrec[h][k] = -1;
     dval[h] = kNone;
     need[h] = 0u;
     hoff[h] = 0;
@@ -352,17 +348,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           int32_t w[SP];
           w[0] = cbase[h] + lane;
           w[1] = (h << 8) | lane;
-          if constexpr (RECLDS) {
-            w[2] = lrec[wv][h][S][lane];
-            w[3] = lrec[wv][h][S + 1][lane];
+          w[2] = hrec[h][S];
+          w[3] = hrec[h][S + 1];
 #pragma unroll
-            for (int k = 0; k < SPT - 4; ++k) w[4 + k] = k < S ? lrec[wv][h][k][lane] : -1;
-          } else {
-            w[2] = hrec[h][S];
-            w[3] = hrec[h][S + 1];
-#pragma unroll
-            for (int k = 0; k < SPT - 4; ++k) w[4 + k] = k < S ? hrec[h][k] : -1;
-          }
+          for (int k = 0; k < SPT - 4; ++k) w[4 + k] = k < S ? hrec[h][k] : -1;
           if constexpr (INL) {
             w[SPT] = (int32_t)(uint32_t)hoff[h];
             w[SPT + 1] = (int32_t)(hoff[h] >> 32);
@@ -803,17 +792,11 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       // (its counter needs 0), flagged tele-only (meta1 bit 4) with its status in bits 28..31
       const bool tonly = tele_inline && mm < M && est != kRated;
       if (tonly) r[S + 1] = (int32_t)(((uint32_t)r[S + 1] & 0x0fffffffu) | 16u | ((uint32_t)est << 28));
-      if constexpr (RECLDS) {
-#pragma unroll
-        for (int k = 0; k < R; ++k) lrec[wv][staging][k][lane] = r[k];
-      }
 #pragma unroll
       for (int h = 0; h < kH; ++h)
         if (h == staging) {
-          if constexpr (!RECLDS) {
 #pragma unroll
-            for (int k = 0; k < R; ++k) hrec[h][k] = r[k];
-          }
+          for (int k = 0; k < R; ++k) hrec[h][k] = r[k];
           hoff[h] = stoff;
           hcnt[h] = stcnt;
         }

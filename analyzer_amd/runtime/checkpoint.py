@@ -38,7 +38,6 @@ import queue
 import struct
 import tempfile
 import threading
-from concurrent.futures import ThreadPoolExecutor
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
@@ -95,8 +94,8 @@ def _rmtree(path: str) -> None:
     os.rmdir(path)
 
 
-WRITE_PIECE = 64 << 20
-WRITE_THREADS = int(os.environ.get("ANA_CKPT_WRITE_THREADS") or 1)
+DIRECT_IO = os.environ.get("ANA_CKPT_DIRECT", "0") not in ("", "0", "false")
+DIRECT_BLOCK = 4096
 
 _ST_DTYPES = {torch.float32: "F32", torch.float64: "F64", torch.int32: "I32", torch.int64: "I64",
               torch.uint8: "U8"}
@@ -118,39 +117,65 @@ def write_safetensors(path: str, tensors: Dict[str, torch.Tensor], metadata: Opt
     if metadata:
         header["__metadata__"] = {str(k): str(v) for k, v in metadata.items()}
     h = json.dumps(header, separators=(",", ":")).encode()
-    h += b" " * (-len(h) % 8)  # the data starts 8-B aligned
+    # the data starts 8-B aligned; with direct I/O at a 4-KB block boundary (the JSON
+    # header may carry trailing spaces, safetensors allows it)
+    align = DIRECT_BLOCK if DIRECT_IO else 8
+    h += b" " * (-(8 + len(h)) % align)
     head = struct.pack("<Q", len(h)) + h
-    # the payload goes to the file in 64-MB pieces from WRITE_THREADS threads (pwrite at
-    # their offsets; the copies into the page cache run in parallel, the GIL is released
-    # in the syscall): one thread writes ~3.5 GB/s on the GPU box (profiles/r6/
-    # rerate_attribution.log), the checkpoint of a 10M-player roster is 800 MB
-    pieces = []
-    pos = len(head)
-    for t in tensors.values():
-        if t.numel():
-            mv = memoryview(t.view(torch.uint8).reshape(-1).numpy())
-            for a in range(0, len(mv), WRITE_PIECE):
-                pieces.append((pos + a, mv[a:a + WRITE_PIECE]))
-        pos += t.numel() * t.element_size()
-    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    bufs = [memoryview(t.view(torch.uint8).reshape(-1).numpy()) for t in tensors.values() if t.numel()]
+    if DIRECT_IO and _write_direct(path, head, bufs):
+        return len(head) + off
+    with open(path, "wb", buffering=0) as f:
+        f.write(head)
+        for mv in bufs:
+            while len(mv):
+                mv = mv[f.write(mv):]
+    return len(head) + off
+
+
+def _write_direct(path: str, head: bytes, bufs) -> bool:
+    """O_DIRECT writes (ANA_CKPT_DIRECT=1): the block-aligned body of each buffer goes
+    from its (page-aligned, pinned) memory straight to the device -- no page-cache copy
+    and no dirty-page write-back for fsync to wait on; the unaligned tails and the header
+    go through an ordinary descriptor.  False (nothing written) when the file system or
+    a buffer's alignment does not allow it."""
+    import mmap
+
+    if any(b.nbytes and (b.obj.ctypes.data if hasattr(b.obj, "ctypes") else 0) % DIRECT_BLOCK for b in bufs):
+        return False
+    try:
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC | os.O_DIRECT, 0o644)
+    except (OSError, AttributeError):
+        return False
+    tails = []
+    try:
+        pos = len(head)
+        for mv in bufs:
+            body = (len(mv) // DIRECT_BLOCK) * DIRECT_BLOCK
+            o = 0
+            while o < body:
+                n = os.pwrite(fd, mv[o:body], pos + o)
+                if n <= 0:
+                    raise OSError("short direct write")
+                o += n
+            if body < len(mv):
+                tails.append((pos + body, mv[body:]))
+            pos += len(mv)
+    except OSError:
+        os.close(fd)
+        os.remove(path)
+        return False
+    os.close(fd)
+    fd = os.open(path, os.O_WRONLY)
     try:
         os.pwrite(fd, head, 0)
-
-        def put(item):
-            o, mv = item
+        for o, mv in tails:
             while len(mv):
                 n = os.pwrite(fd, mv, o)
                 o, mv = o + n, mv[n:]
-
-        if len(pieces) > 1 and WRITE_THREADS > 1:
-            with ThreadPoolExecutor(WRITE_THREADS) as ex:
-                list(ex.map(put, pieces))
-        else:
-            for it in pieces:
-                put(it)
     finally:
         os.close(fd)
-    return len(head) + off
+    return True
 
 
 def base_and_attrs(roster: Roster) -> Tuple[torch.Tensor, torch.Tensor]:

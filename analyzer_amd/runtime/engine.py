@@ -15,9 +15,10 @@ same API runs the host mirror sequentially.
 
 Placement (``ANA_PREPASS_SERIAL``, default auto): the prepass overlaps the executor's
 tail when the executor leaves room for it, else it runs on the main stream between
-launches.  Room means 5v5 -- 3000+ levels, ~75% of its wave iterations idle, a 5.4 ms
-prepass over 125M slots (config 3: 22.12 ms overlapped at 0.7 vs 22.9-23.2 ms serial,
-profiles/r2/prepass_placement.log) -- or, since round 5, a launch of one wave per SIMD
+launches.  Room meant 5v5 until round 6 (config 3: 22.12 ms overlapped at 0.7 vs
+22.9-23.2 ms serial, profiles/r2/prepass_placement.log; since the 5v5 executor holds two
+chunks, serial is faster: 19.23-19.27 vs 19.66-19.73 ms, profiles/r6/config3_held_chunks.log),
+and, since round 5, a launch of one wave per SIMD
 (ops/rate.py launch_blocks: 1v1-3v3 over a roster the Infinity Cache holds), whose
 spare wave slots the sort fills: config 2 7.69 ms overlapped at 0.75 vs 7.95 serial,
 config 4 8.62 vs 8.85 (profiles/r5/prepass_overlap_grid256.log).  At two waves per
@@ -150,15 +151,16 @@ class WindowPipeline:
 
     @staticmethod
     def serial_prepass(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512) -> bool:
-        """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial only for
-        4v4 at two waves per SIMD (``grid`` 512), where a sort workgroup does not fit beside
+        """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial for 4v4 and
+        5v5 at two waves per SIMD (``grid`` 512), where a sort workgroup does not fit beside
         the executor's waves -- 1v1-3v3 launches are compiled to leave it room
-        (csrc/dataflow.hip ANA_EXEC_WPE), 5v5 absorbs it in its idle iterations, and under
-        DP merges (``dp``) the windows are short and the tail overlap pays (see the module
-        docstring)."""
+        (csrc/dataflow.hip ANA_EXEC_WPE); under DP merges (``dp``) the windows are short and
+        the placement follows the collective's cost (probe_placement).  5v5 was overlapped
+        from 0.7 until round 6; with the two-chunk 5v5 executor the serial prepass is
+        faster (config 3 19.23-19.27 vs 19.66-19.73 ms, profiles/r6/config3_held_chunks.log)."""
         if ecfg.prepass_serial is not None:
             return ecfg.prepass_serial
-        return K == 4 and not dp and grid >= 512
+        return K >= 4 and not dp and grid >= 512
 
     def probe_placement(self, merger) -> bool:
         """Windows between DP merges: serial placement (the next prepass on its own

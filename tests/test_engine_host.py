@@ -150,14 +150,15 @@ def test_skewed_activity_draw(skew):
 
 
 def test_prepass_placement_knob():
-    """ANA_PREPASS_SERIAL: 1/0 force the placement; unset or auto -> serial only for 4v4 at
-    two waves per SIMD; the executor grid per launch (BatchRater.launch_blocks)."""
+    """ANA_PREPASS_SERIAL: 1/0 force the placement; unset or auto -> serial for 4v4 and 5v5
+    at two waves per SIMD; the executor grid per launch (BatchRater.launch_blocks)."""
     from analyzer_amd.config import EngineConfig
     from analyzer_amd.runtime.engine import WindowPipeline
 
     auto = EngineConfig.from_env({})
     assert auto.prepass_serial is None and EngineConfig.from_env({"ANA_PREPASS_SERIAL": "auto"}).prepass_serial is None
-    assert WindowPipeline.serial_prepass(4, auto) and not WindowPipeline.serial_prepass(5, auto)
+    assert WindowPipeline.serial_prepass(4, auto) and WindowPipeline.serial_prepass(5, auto)
+    assert not WindowPipeline.serial_prepass(5, auto, dp=True)  # between DP merges: the probe decides
     # 1v1-3v3 launches leave a sort workgroup room at either grid (csrc/dataflow.hip ANA_EXEC_WPE)
     assert not WindowPipeline.serial_prepass(3, auto) and WindowPipeline.tail_point(3, auto) == 0.1
     on, off = (EngineConfig.from_env({"ANA_PREPASS_SERIAL": v}) for v in ("1", "0"))
