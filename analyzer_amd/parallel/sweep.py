@@ -457,6 +457,23 @@ class SweepMerger:
                 for t in (pend["cur"], pend["rec"], pend["rows"], pw):
                     t.record_stream(self._side)
 
+    def rec_in_use(self, rec) -> bool:
+        """Whether a deferred record correction still has to read match records in the
+        memory of ``rec`` (round-5 ``_pending`` or a pending split correction).  The records
+        of window i must stay unchanged until the merge of window i+1 has been enqueued:
+        a caller refilling window i's tensor in place for window i+1 would have the
+        correction read the wrong player ids -- runtime/engine.py refuses such a window."""
+        pend = []
+        if self._pending is not None:
+            pend.append(self._pending[0])
+        if self._split_pending is not None:
+            pend.append(self._split_pending["rec"])
+        for a in pend:
+            a0, b0 = a.data_ptr(), rec.data_ptr()
+            if a0 < b0 + rec.numel() * rec.element_size() and b0 < a0 + a.numel() * a.element_size():
+                return True
+        return False
+
     def flush_split(self) -> None:
         """Enqueue a correction still waiting for the next merge (finish, a consumer)."""
         if self._split_pending is not None:

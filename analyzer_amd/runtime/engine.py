@@ -75,7 +75,8 @@ class Prepared:
 class WindowPipeline:
     """Rate consecutive windows against one roster, prepass overlapped."""
 
-    def __init__(self, rater: BatchRater, roster: Roster, K: int, merger=None, signal_at: float = 0.0):
+    def __init__(self, rater: BatchRater, roster: Roster, K: int, merger=None, signal_at: float = 0.0,
+                 telemetry: bool = False):
         self.rater = rater
         self.roster = roster
         self.K = int(K)
@@ -101,8 +102,12 @@ class WindowPipeline:
         # serial prepass: nothing to overlap, no tail signal -- unless a caller wants the
         # launches' tail for other work (``signal_at``: bench.py --telemetry-mode tail),
         # which then also starts an overlapped prepass
-        self.tail = float(signal_at) if signal_at > 0 else 0.0 if self.serial else \
-            self.tail_point(self.K, self.ecfg, dp, self.grid)
+        # (the 0.1 start of two-waves-per-SIMD 1v1-3v3 windows assumes the 128-VGPR build,
+        # which launches without fused telemetry and outside the timing build only:
+        # ``capped``, csrc/dataflow.hip ANA_RATE_LAUNCH_D)
+        capped = not telemetry and not self.ecfg.rate_diag
+        self.tail = float(signal_at) if signal_at > 0 else (
+            0.0 if self.serial else self.tail_point(self.K, self.ecfg, dp, self.grid, capped))
         # a prepass in the rating's tail streams its sort input with non-temporal loads
         # (ANA_SORT_NT=2), so it evicts less of the roster the executor's drain reads:
         # eight 1.25M windows with forced merges 9.08-9.13 vs 9.32-9.40 ms (with the merge
@@ -185,16 +190,20 @@ class WindowPipeline:
         return ms > thr
 
     @staticmethod
-    def tail_point(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512) -> float:
+    def tail_point(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512, capped: bool = True) -> float:
         """Where the overlapped prepass starts: ``ANA_PREPASS_AT`` if set, else 0.7,
         DP_TAIL_AT for 1v1-4v4 windows between merges (measured: config 2 with 8 merges
         per step, profiles/r3/dp_prepass_placement_k8.log), SPARE_TAIL_AT for 1v1-4v4
-        windows at one wave per SIMD, FULL_TAIL_AT for 1v1-3v3 windows at two."""
+        windows at one wave per SIMD, FULL_TAIL_AT for 1v1-3v3 windows at two when the
+        launch takes the 128-VGPR build (``capped``: no fused telemetry, no timing build --
+        the uncapped build leaves a sort workgroup no room, so its prepass starts at 0.7)."""
         if ecfg.prepass_at_set or K >= 5:
             return ecfg.prepass_at
         if dp:
             return DP_TAIL_AT
-        return SPARE_TAIL_AT if grid < 512 else FULL_TAIL_AT if K <= 3 else ecfg.prepass_at
+        if grid < 512:
+            return SPARE_TAIL_AT
+        return FULL_TAIL_AT if K <= 3 and capped else ecfg.prepass_at
 
     def _side_stream(self):
         """Side stream of the prepass; ``ANA_PREPASS_CUS=n`` confines it to n CUs
@@ -298,6 +307,10 @@ class WindowPipeline:
         if prep.ready is not None:
             main.wait_event(prep.ready)
         if self.merger is not None:
+            if hasattr(self.merger, "rec_in_use") and self.merger.rec_in_use(prep.rec):
+                raise ValueError("window records reuse the memory of the previous window's records, which its "
+                                 "deferred record correction has not read yet (parallel/sweep.py rec_in_use): "
+                                 "give each window its own records tensor (a ring of two suffices)")
             self.merger.begin(self.roster)
             if hasattr(self.merger, "pending_rows") and self.merger.pending_rows(out):
                 self.merger.flush_correction()  # a deferred record correction of these rows

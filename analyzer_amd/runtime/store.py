@@ -363,6 +363,39 @@ class SqliteSession(_SessionBase):
         c = self.conn
         st = b.status
         self._log_ids += list(b.ids)
+        # the players first: with versioned rows a lost race (WriteConflict) shows before any
+        # other row of the batch was written
+        if b.final_keys is not None and len(b.final_keys):
+            pn, prow_of = self.store.player_names, self.store.player_rowid
+            f = np.asarray(b.final, dtype=np.float64)
+            touched = np.asarray(b.final_tracks, dtype=bool)
+            rowids = np.array([prow_of[pn[k]] for k in b.final_keys.tolist()], dtype=np.int64)
+            # one UPDATE per set of touched tracks: players grouped by their track bitmask
+            masks = (touched.astype(np.int64) << np.arange(touched.shape[1], dtype=np.int64)).sum(1)
+            for m in np.unique(masks).tolist():
+                if m == 0:
+                    continue
+                sel = masks == m
+                tracks = [t for t in range(touched.shape[1]) if (m >> t) & 1]
+                cols = np.array([[2 * t, 2 * t + 1] for t in tracks]).reshape(-1)
+                vals = f[np.ix_(sel, cols)].astype(object)
+                vals[np.isnan(f[np.ix_(sel, cols)])] = None  # NaN -> NULL
+                rows = np.concatenate([vals, rowids[sel, None].astype(object)], axis=1).tolist()
+                sets = ", ".join("%s=?, %s=?" % (_q(TRACK_COLUMNS[t] + "_mu"), _q(TRACK_COLUMNS[t] + "_sigma"))
+                                 for t in tracks)
+                if self.store.versioned:
+                    # compare-and-set: only rows still at the version this batch read
+                    ver = self._versions
+                    vs = [ver.get(pn[k], 0) for k in np.asarray(b.final_keys)[sel].tolist()]
+                    rows = [r + [v] for r, v in zip(rows, vs)]
+                    cur = c.executemany("UPDATE player SET %s, version=version+1 WHERE rowid=? AND version=?"
+                                        % sets, rows)
+                    if cur.rowcount != len(rows):
+                        raise WriteConflict("%d of %d player rows changed since this batch read them"
+                                            % (len(rows) - max(cur.rowcount, 0), len(rows)))
+                else:
+                    c.executemany("UPDATE player SET %s WHERE rowid=?" % sets, rows)
+
         rated = st == RATED
         afkm = (st == AFK) | (st == INVALID)
         c.executemany("UPDATE match SET trueskill_quality=? WHERE api_id=?",
@@ -401,37 +434,6 @@ class SqliteSession(_SessionBase):
             c.executemany("INSERT OR REPLACE INTO participant_stats VALUES (?, ?, %s)"
                           % ", ".join("?" * len(STAT_COLUMNS)),
                           [[names[p], names[p]] + v for p, v in zip(b.part[ss].tolist(), st8)])
-        if b.final_keys is not None and len(b.final_keys):
-            pn, prow_of = self.store.player_names, self.store.player_rowid
-            f = np.asarray(b.final, dtype=np.float64)
-            touched = np.asarray(b.final_tracks, dtype=bool)
-            rowids = np.array([prow_of[pn[k]] for k in b.final_keys.tolist()], dtype=np.int64)
-            # one UPDATE per set of touched tracks: players grouped by their track bitmask
-            masks = (touched.astype(np.int64) << np.arange(touched.shape[1], dtype=np.int64)).sum(1)
-            for m in np.unique(masks).tolist():
-                if m == 0:
-                    continue
-                sel = masks == m
-                tracks = [t for t in range(touched.shape[1]) if (m >> t) & 1]
-                cols = np.array([[2 * t, 2 * t + 1] for t in tracks]).reshape(-1)
-                vals = f[np.ix_(sel, cols)].astype(object)
-                vals[np.isnan(f[np.ix_(sel, cols)])] = None  # NaN -> NULL
-                rows = np.concatenate([vals, rowids[sel, None].astype(object)], axis=1).tolist()
-                sets = ", ".join("%s=?, %s=?" % (_q(TRACK_COLUMNS[t] + "_mu"), _q(TRACK_COLUMNS[t] + "_sigma"))
-                                 for t in tracks)
-                if self.store.versioned:
-                    # compare-and-set: only rows still at the version this batch read
-                    ver = self._versions
-                    vs = [ver.get(pn[k], 0) for k in np.asarray(b.final_keys)[sel].tolist()]
-                    rows = [r + [v] for r, v in zip(rows, vs)]
-                    cur = c.executemany("UPDATE player SET %s, version=version+1 WHERE rowid=? AND version=?"
-                                        % sets, rows)
-                    if cur.rowcount != len(rows):
-                        raise WriteConflict("%d of %d player rows changed since this batch read them"
-                                            % (len(rows) - max(cur.rowcount, 0), len(rows)))
-                else:
-                    c.executemany("UPDATE player SET %s WHERE rowid=?" % sets, rows)
-
     def _load_players(self, api_ids: Sequence[str]) -> None:
         need = [a for a in set(api_ids) if a not in self._players]
         cols = ("api_id", "skill_tier", "rank_points_ranked", "rank_points_blitz") + PLAYER_RATING_COLS
@@ -546,6 +548,13 @@ class SqliteSession(_SessionBase):
         self.store.commits += 1
         self._match_snaps.clear()
         self._player_snaps.clear()
+
+    def lock(self) -> None:
+        """Take the database's write lock now (BEGIN IMMEDIATE): a batch retried after a
+        write conflict reads its players and commits under the lock, so it cannot lose
+        again (runtime/worker.py ``process``)."""
+        if not self.conn.in_transaction:
+            self.conn.execute("BEGIN IMMEDIATE")
 
     def rollback(self) -> None:
         super().rollback()

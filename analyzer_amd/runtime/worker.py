@@ -369,9 +369,12 @@ class Worker:
         from .store import WriteConflict
 
         attempt = 0
+        lock_first = os.environ.get("CAS_LOCK") == "always"
         while True:
             try:
-                matches, quarantined, counts = self._process_once(ids)
+                # a retried batch takes the store's write lock before it reads its players
+                # (SqliteSession.lock): it cannot lose the race twice
+                matches, quarantined, counts = self._process_once(ids, locked=attempt > 0 or lock_first)
                 break
             except WriteConflict as e:
                 # another replica committed some of this batch's players since they were
@@ -391,9 +394,12 @@ class Worker:
                                     "quarantined": len(quarantined), **counts}))
         return quarantined
 
-    def _process_once(self, ids):
-        """One attempt at a batch: load, rate, commit (all rolled back on an exception)."""
+    def _process_once(self, ids, locked: bool = False):
+        """One attempt at a batch: load, rate, commit (all rolled back on an exception);
+        ``locked``: under the store's write lock from the start (stores that have one)."""
         session = self.store.session()
+        if locked and hasattr(session, "lock"):
+            session.lock()
         quarantined: List[str] = []
         counts: Dict[str, int] = {}
         try:

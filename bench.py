@@ -307,7 +307,8 @@ def main(argv=None) -> int:
                          "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.5"))
     tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.5 if auto_mode else 0.9)) \
         if tele is not None and args.telemetry_mode == "tail" else 0.0
-    pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at)
+    pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at,
+                          telemetry=tele is not None and args.telemetry_mode == "fused")
     # the DP merge corrects window i's records during window i+1's collective
     # (parallel/sweep.py defer): records double-buffered, so window i+1's rating
     # writes the other buffer (a consumer streams the records out of the idle one)

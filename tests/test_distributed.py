@@ -659,3 +659,25 @@ def test_split_exchange_over_ranks(tmp_path):
         assert torch.equal(out["total"][:, :7].contiguous().view(torch.bfloat16).float(),
                            tot.to(torch.bfloat16).float())
         assert torch.equal(out["total"][:, 7], torch.full((22,), 6, dtype=torch.int32))
+
+
+def test_reused_records_tensor_is_refused():
+    """A window whose records tensor is the previous window's (refilled in place) is
+    refused while that window's record correction is still deferred: the correction
+    would read the new window's player ids (advisor finding, round 5)."""
+    from analyzer_amd.ops.rate import BatchRater, RateResult
+    from analyzer_amd.parallel.sweep import SweepMerger
+    from analyzer_amd.runtime.engine import WindowPipeline
+
+    P, M, K = 200, 300, 3
+    roster = make_roster(RosterSpec(num_players=P, seed=3))
+    rec = make_stream(StreamSpec(team_size=K, seed=4), M, P, K=K)
+    merger = SweepMerger(P, "cpu", comm_dtype="bf16", correct_records=True, world_size=1, force=True)
+    merger.defer = True
+    pipe = WindowPipeline(BatchRater(), roster, K, merger=merger)
+    out = [RateResult.allocate(M, K, "cpu") for _ in range(2)]
+    prep = pipe.prepare(rec)
+    _, prep2 = pipe.step(prep, rec, out=out[0])  # the next window reuses the same tensor
+    assert merger.rec_in_use(rec)
+    with pytest.raises(ValueError):
+        pipe.step(prep2, None, out=out[1])

@@ -161,6 +161,8 @@ def test_prepass_placement_knob():
     assert not WindowPipeline.serial_prepass(5, auto, dp=True)  # between DP merges: the probe decides
     # 1v1-3v3 launches leave a sort workgroup room at either grid (csrc/dataflow.hip ANA_EXEC_WPE)
     assert not WindowPipeline.serial_prepass(3, auto) and WindowPipeline.tail_point(3, auto) == 0.1
+    # ... which assumes the 128-VGPR build: fused telemetry / the timing build launch uncapped
+    assert WindowPipeline.tail_point(3, auto, capped=False) == 0.7
     on, off = (EngineConfig.from_env({"ANA_PREPASS_SERIAL": v}) for v in ("1", "0"))
     assert WindowPipeline.serial_prepass(5, on) and not WindowPipeline.serial_prepass(3, off)
     assert auto.prepass_at == 0.7 and EngineConfig.from_env({"ANA_PREPASS_AT": "0"}).prepass_at == 0.0
