@@ -184,7 +184,8 @@ class EngineConfig:
                                       merge-sized all-reduce (timed when the pipeline is built, max over
                                       ranks) takes longer than this, else in the rating's tail
                                       (runtime/engine.py probe_placement)
-    COMM_DTYPE              fp32      sweep-merge message precision (bench.py, rerate)
+    COMM_DTYPE              (unset)   sweep-merge message precision (bench.py, rerate): unset = fp16 for one
+                                      sweep (BASELINE config 5: fp16 moments), fp32 for causal re-sweeps
     SWEEPS                  1         causal sweeps per window (bench.py, rerate)
     ANA_DIST_BACKEND        nccl      process group backend (gloo: N ranks on one GPU)
     CHECKPOINT_DIR / _EVERY -- / 1    re-rate checkpoints (runtime/rerate.py)
@@ -217,7 +218,7 @@ class EngineConfig:
     prepass_serial: Optional[bool] = None  # None = auto (WindowPipeline.serial_prepass)
     roster_warm: Optional[bool] = None  # None = auto (WindowPipeline)
     merge_bucket_mb: float = 16.0
-    comm_dtype: str = "fp32"
+    comm_dtype: str = ""  # "" = by sweeps (runtime/rerate.py default_comm_dtype)
     sweeps: int = 1
     dist_backend: str = "nccl"
     checkpoint_every: int = 1
@@ -261,7 +262,7 @@ class EngineConfig:
             prepass_serial=_tristate(env.get("ANA_PREPASS_SERIAL")),
             roster_warm=_tristate(env.get("ANA_ROSTER_WARM")),
             merge_bucket_mb=float(_env(env, "ANA_MERGE_BUCKET_MB") or 16),
-            comm_dtype=_env(env, "COMM_DTYPE") or "fp32",
+            comm_dtype=_env(env, "COMM_DTYPE") or "",
             sweeps=int(_env(env, "SWEEPS") or 1),
             dist_backend=_env(env, "ANA_DIST_BACKEND") or "nccl",
             checkpoint_every=int(_env(env, "CHECKPOINT_EVERY") or 1),

@@ -178,3 +178,11 @@ def test_async_checkpointer_on_host(tmp_path):
     r, meta = checkpoint.load(p)
     assert meta["windows_done"] == 5
     assert torch.equal(r.state[:, 0].nan_to_num(-7), roster.state[:, 0].nan_to_num(-7))
+
+
+def test_rerate_merge_precision_default():
+    """BASELINE config 5 names fp16 moments: one-sweep re-rates merge in fp16 by default,
+    causal re-sweeps in fp32 (their prefixes telescope)."""
+    from analyzer_amd.runtime.rerate import default_comm_dtype
+
+    assert default_comm_dtype(1) == "fp16" and default_comm_dtype(2) == "fp32"
