@@ -377,18 +377,25 @@ def time_all_reduce(t: torch.Tensor, group=None, iters: int = 3) -> float:
 
 def init_from_env(backend: Optional[str] = None) -> Tuple[int, int, torch.device]:
     """Initialise the default group from the torchrun environment (no-op for one
-    process).  Returns (rank, world_size, device)."""
+    process).  Returns (rank, world_size, device).  ``backend`` (default
+    ``ANA_DIST_BACKEND``, else nccl = RCCL on a GPU): with ``gloo`` on a GPU box the ranks
+    still rate on the device -- several may share one GPU (a rehearsal) -- and the
+    collectives stage their tensors through the host (``_staged``)."""
     rank = int(os.environ.get("RANK", "0"))
     size = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    backend = backend or os.environ.get("ANA_DIST_BACKEND") or None
+    use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        ngpu = torch.cuda.device_count()
+        local = local % ngpu if backend == "gloo" and ngpu else local
     dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(local)
     if size > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if use_gpu:
-            dist.init_process_group(backend or "nccl", device_id=dev)
+        if use_gpu and backend in (None, "nccl"):
+            dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend or "gloo")
     return rank, size, dev
@@ -406,8 +413,13 @@ def broadcast_roster(roster, src: int = 0, group=None) -> None:
     _, size = world()
     if size <= 1:
         return
-    dist.broadcast(roster.state, src=src, group=group)
-    dist.broadcast(roster.attrs, src=src, group=group)
+    for t in (roster.state, roster.attrs):
+        if _staged(t, group):
+            h = t.cpu()
+            dist.broadcast(h, src=src, group=group)
+            t.copy_(h)
+        else:
+            dist.broadcast(t, src=src, group=group)
 
 
 def reduce_counts(counts: Dict[str, float], device, group=None, op: str = "sum") -> Dict[str, float]:
@@ -421,5 +433,7 @@ def reduce_counts(counts: Dict[str, float], device, group=None, op: str = "sum")
     dist.all_gather_object(gathered, keys, group=group)
     keys = sorted(set(k for ks in gathered for k in ks))
     t = torch.tensor([float(counts.get(k, 0.0)) for k in keys], dtype=torch.float64, device=device)
+    if _staged(t, group):
+        t = t.cpu()
     dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM, group=group)
     return {k: float(v) for k, v in zip(keys, t.cpu().tolist())}

@@ -41,6 +41,7 @@
 #   dpstep     forced-merge step price: record correction on / off, tail / serial placement, emulated N = 8
 #   replicas   worker.py --replicas 1 / 2 / 4 on the box (shared broker + SQLite store)
 #   dpconf     gloo rehearsals of config 3 (N = 4) and config 5 (N = 2)
+#   rerate_dp  config-5-shaped re-rate over 2 gloo ranks on this GPU: checkpoint, kill, resume, bit-identity
 #   project    one-GPU projection of the N = 2 / 4 / 8 DP step (emulated all-reduce, bus bandwidth sweep)
 #   corrmicro  the record correction kernel alone + a kernel trace of the k = 8 DP step
 #   gtest      a subset of the GPU tests (GTEST_K = pytest -k expression)
@@ -317,6 +318,30 @@ EOF
             --replicas $n
       done
       grep -h -o '"matches_per_s": [0-9.]*' gpurun_out/replicas/*.log
+      ;;
+    rerate_dp)  # P4 time-axis sharding end to end: 2 gloo ranks sharing this GPU (10M players, 2 x 16M matches per
+                # global window, fp16 merges), checkpoint every 2 windows, kill after 5, resume, compare with a full run
+      mkdir -p gpurun_out/rerate_dp
+      rm -rf /tmp/ckdp /tmp/ckdp_full
+      RDP="$PY -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 \
+          -m analyzer_amd.runtime.rerate --matches 2.56e8 --players 1e7 --window 1.6e7 --checkpoint-every 2 --digests"
+      ANA_DIST_BACKEND=gloo ANA_RATE_BLOCKS=256 run rerate_dp/full 900 $RDP --checkpoint-dir /tmp/ckdp_full
+      echo "== rerate_dp/kill"
+      ANA_DIST_BACKEND=gloo ANA_RATE_BLOCKS=256 timeout -k 10 900 $RDP --checkpoint-dir /tmp/ckdp --fault-kill-after 5 \
+          > gpurun_out/rerate_dp/kill.log 2>&1
+      rc=$?; tail -2 gpurun_out/rerate_dp/kill.log
+      if [ $rc -eq 0 ]; then echo "!! expected a failure exit from the injected fault"; exit 1; fi
+      ANA_DIST_BACKEND=gloo ANA_RATE_BLOCKS=256 run rerate_dp/resume 900 $RDP --checkpoint-dir /tmp/ckdp
+      $PY - <<'EOF2'
+import json
+def last(p):
+    return json.loads([l for l in open(p).read().splitlines() if l.startswith("{")][-1])
+full, res = last("gpurun_out/rerate_dp/full.log"), last("gpurun_out/rerate_dp/resume.log")
+same = all(full["window_digests"][g] == d for g, d in res["window_digests"].items())
+print("2 ranks | resumed from window", int(res["resumed_from_window"]), "| roster bit-identical:",
+      full["roster_sha256"] == res["roster_sha256"], "| re-rated windows' records identical:", same,
+      "| full run %.2f s, %d windows" % (full["seconds"], full["windows"]))
+EOF2
       ;;
     dpconf)  # gloo rehearsals of the other DP configs: 5v5 (config 3, k = 2N) and the 10M-player re-rate (config 5)
       run dpconf/c3_gloo4 900 env ANA_DIST_BACKEND=gloo $PY bench.py --config 3 --gpus 4 --steps 1 --warmup 1
