@@ -49,8 +49,14 @@
 #include "rate_dev.h"
 #include "telemetry_dev.h"
 
+// Chunks a wave keeps in flight: ONE since round 6.  Re-measured at one wave per SIMD with
+// the global counters (in-call A/B of builds, profiles/r6/held_chunks.log): 4 -> 1 held
+// chunk takes config 2 7.64 -> 7.10 ms per step, config 4 8.62 -> 7.83, config 5 11.34 ->
+// 10.92, quadratic / cubic skew -13 / -8 %, the serial hop 2.14 -> 2.00 us -- a wave with
+// one chunk claims the next one sooner, closer to the dependency frontier, and polls and
+// stages a quarter of the counters every iteration.
 #ifndef ANA_HELD
-#define ANA_HELD 4
+#define ANA_HELD 1
 #endif
 
 namespace ana {
@@ -60,9 +66,9 @@ constexpr bool kLocalHandoff = ANA_DIAG_BUILD != 0;
 
 
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight (1v1-4v4)
-// 5v5 keeps two: config 3 19.23-19.27 ms per step against 20.08-20.15 with four (in-call A/B,
+// 5v5: two beat four (config 3 19.23-19.27 ms per step against 20.08-20.15, in-call A/B,
 // profiles/r6/config3_held_chunks.log) -- its 3,000+ dependency levels leave most held
-// matches waiting, so the two extra chunks only add polls and staging to every iteration
+// matches waiting, so the extra chunks only add polls and staging to every iteration
 // (and 24 registers: 166 -> 142 VGPRs); holding the records in LDS instead of registers
 // (120 VGPRs, 55.7 KB of LDS) measured no faster (20.10-20.22)
 #ifndef ANA_HELD5
@@ -118,8 +124,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   constexpr bool INL = TELE == 2;    // K8 inline: each group folds its match's events
   static_assert(G >= S && G <= 64, "a group holds one match");
   constexpr int NG = 64 / G;
-  static_assert(kH == 2 || kH == 4, "readiness reads the held chunks' local counts as one vector");
-  typedef uint32_t hvec __attribute__((ext_vector_type(kH)));
+  static_assert(kH >= 1 && kH <= 4, "held chunks");
+  // the held chunks' local hand-off counts are read as one vector (diagnostic library): 1 or 3
+  // held chunks use a 2 / 4-wide one, the upper lanes unused
+  typedef uint32_t hvec __attribute__((ext_vector_type(kH <= 2 ? 2 : 4)));
   // local hand-off counters: increments of each held match's completion count
   // by publishes of THIS wave (never also added to the global counter); [lane][h]
   // so a lane reads them in one ds_read_b64/b128.  Measured slower than the global
