@@ -66,13 +66,14 @@ constexpr bool kLocalHandoff = ANA_DIAG_BUILD != 0;
 
 
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight (1v1-4v4)
-// 5v5: two beat four (config 3 19.23-19.27 ms per step against 20.08-20.15, in-call A/B,
-// profiles/r6/config3_held_chunks.log) -- its 3,000+ dependency levels leave most held
-// matches waiting, so the extra chunks only add polls and staging to every iteration
-// (and 24 registers: 166 -> 142 VGPRs); holding the records in LDS instead of registers
-// (120 VGPRs, 55.7 KB of LDS) measured no faster (20.10-20.22)
+// 5v5 likewise: two beat four (config 3 19.23-19.27 ms per step against 20.08-20.15) and
+// one beats two (18.48-18.89 against 19.27-19.62; in-call A/Bs, profiles/r6/
+// config3_held_chunks.log) -- its 3,000+ dependency levels leave most held matches
+// waiting, so extra chunks only add polls and staging to every iteration (and 24
+// registers each: 166 -> 138 VGPRs at two); holding the records in LDS instead of
+// registers (120 VGPRs, 55.7 KB of LDS) measured no faster (20.10-20.22)
 #ifndef ANA_HELD5
-#define ANA_HELD5 2
+#define ANA_HELD5 1
 #endif
 // K8 inline telemetry: events per match loaded with the batch's granules (more go
 // through a remainder loop after the rating); per group lane ceil(64 / G) 8-B loads
