@@ -58,7 +58,8 @@ from ..utils.trace import trace_range
 
 CHUNK = 64  # matches per executor ticket of a window (csrc/dataflow.hip kChunk; BatchRater.chunk_len)
 DP_TAIL_AT = 0.9  # tail-overlap start of the next prepass between DP merges (3v3; see tail_point)
-SPARE_TAIL_AT = 0.75  # ... of a window launch at one wave per SIMD (config 2: 0.6-0.8 swept)
+SPARE_TAIL_AT = 0.55  # ... of a window launch at one wave per SIMD (config 2, one held chunk: 0.45-0.65
+#                       6.87-6.90 ms vs 7.10 at 0.75, profiles/r6/tail_points.log; 0.75 with four held chunks)
 FULL_TAIL_AT = 0.1  # ... of a 1v1-3v3 launch at two waves per SIMD (config 5: 0-0.7 swept)
 DP_DEFER_AT = 0.8  # split DP merge: the deferred prefix exchange + record correction of window w
 #                    start once rating w+1 claimed this fraction of its chunks (ANA_DP_DEFER_AT)

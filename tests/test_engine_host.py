@@ -171,9 +171,9 @@ def test_prepass_placement_knob():
     assert WindowPipeline.tail_point(3, auto, dp=True) == 0.9 and WindowPipeline.tail_point(5, auto, dp=True) == 0.7
     assert WindowPipeline.tail_point(3, EngineConfig.from_env({"ANA_PREPASS_AT": "0.5"}), dp=True) == 0.5
     assert WindowPipeline.tail_point(4, auto) == 0.7
-    # one wave per SIMD (256 workgroups: <= 3v3 over a cached roster): the tail overlap from 0.75
+    # one wave per SIMD (256 workgroups: <= 3v3 over a cached roster): the tail overlap from 0.55
     assert not WindowPipeline.serial_prepass(3, auto, grid=256) and WindowPipeline.serial_prepass(3, on, grid=256)
-    assert WindowPipeline.tail_point(3, auto, grid=256) == 0.75 and WindowPipeline.tail_point(3, auto, dp=True, grid=256) == 0.9
+    assert WindowPipeline.tail_point(3, auto, grid=256) == 0.55 and WindowPipeline.tail_point(3, auto, dp=True, grid=256) == 0.9
     from analyzer_amd.ops.rate import BatchRater
 
     br = BatchRater()
