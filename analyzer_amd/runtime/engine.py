@@ -170,14 +170,15 @@ class WindowPipeline:
 
     def probe_placement(self, merger) -> bool:
         """Windows between DP merges: serial placement (the next prepass on its own
-        stream beside the merge's all-reduces) or the tail overlap (5v5 too: between
-        merges its windows are short, k = 16 at N = 8, and so is their prepass).  On one GPU
-        (forced merges, no collective) the tail wins by ~0.04 ms per window
-        (profiles/r3/dp_prepass_placement_k8.log: 9.54 vs 9.87 ms per 8 windows), but
-        there the all-reduce takes no time; with N ranks it is exposed in the tail
-        placement and runs under the 0.2-ms prepass in the serial one.  So time one
-        merge's all-reduce on this group (the max over ranks, identical everywhere)
-        and go serial when it exceeds ANA_DP_SERIAL_AR_US (default 40 us)."""
+        stream beside the merge's collective) or the tail overlap.  Rounds 3-5 went serial
+        once one merge's all-reduce cost more than 40 us (profiles/r3/
+        dp_prepass_placement_k8.log: the collective exposed in the tail placement ran under
+        the prepass in the serial one).  With the one-held-chunk executor (round 6) the tail
+        wins even beside an emulated N = 8 collective: 10.90 ms per step from 0.9 against
+        11.12-11.16 beside the merge (profiles/r6/tail_points.log), so the default
+        threshold is off; ``ANA_DP_SERIAL_AR_US`` restores it.  The probe still times one
+        merge's all-reduce on this group (the max over ranks, identical everywhere) and
+        reports it (``allreduce_probe_ms``)."""
         from ..parallel.comm import time_all_reduce
 
         if getattr(merger, "world", 1) <= 1 and getattr(merger, "emulate", None) is not None:
@@ -187,8 +188,8 @@ class WindowPipeline:
             ms = time_all_reduce(buf, getattr(merger, "group", None))
             del buf
         self.allreduce_probe_ms = ms
-        thr = float(os.environ.get("ANA_DP_SERIAL_AR_US") or 40.0) / 1000.0
-        return ms > thr
+        thr = os.environ.get("ANA_DP_SERIAL_AR_US")
+        return thr is not None and ms > float(thr) / 1000.0
 
     @staticmethod
     def tail_point(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512, capped: bool = True) -> float:

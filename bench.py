@@ -304,8 +304,8 @@ def main(argv=None) -> int:
         if not cpu and _native().can_wait_value(dev.index or 0):
             args.telemetry_mode = "tail"
             tele_path = ("MFMA kernel on its own stream from %s of the rating's chunks (launch > "
-                         "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.5"))
-    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.5 if auto_mode else 0.9)) \
+                         "ANA_TELE_FUSE_MAX)" % (os.environ.get("ANA_TELE_TAIL_AT") or "0.2"))
+    tail_at = float(os.environ.get("ANA_TELE_TAIL_AT") or (0.2 if auto_mode else 0.9)) \
         if tele is not None and args.telemetry_mode == "tail" else 0.0
     pipe = WindowPipeline(rater, roster, K, merger=merger, signal_at=tail_at,
                           telemetry=tele is not None and args.telemetry_mode == "fused")
