@@ -174,11 +174,14 @@ class WindowPipeline:
         once one merge's all-reduce cost more than 40 us (profiles/r3/
         dp_prepass_placement_k8.log: the collective exposed in the tail placement ran under
         the prepass in the serial one).  With the one-held-chunk executor (round 6) the tail
-        wins even beside an emulated N = 8 collective: 10.90 ms per step from 0.9 against
-        11.12-11.16 beside the merge (profiles/r6/tail_points.log), so the default
-        threshold is off; ``ANA_DP_SERIAL_AR_US`` restores it.  The probe still times one
-        merge's all-reduce on this group (the max over ranks, identical everywhere) and
-        reports it (``allreduce_probe_ms``)."""
+        wins at one wave per SIMD even beside an emulated N = 8 collective: config 2
+        10.90-11.00 ms per step from 0.9 against 11.12-11.16 beside the merge
+        (profiles/r6/tail_points.log), so there the threshold is off; at two waves per SIMD
+        (512 workgroups: configs 3 and 5) serial stays faster (config 3 26.75-26.96 vs
+        27.26-27.33 ms from 0.7, config 5 15.69 vs 16.06 from 0.9, profiles/r6/
+        dp_placement.log).  ``ANA_DP_SERIAL_AR_US`` restores the threshold.  The probe still
+        times one merge's all-reduce on this group (the max over ranks, identical
+        everywhere) and reports it (``allreduce_probe_ms``)."""
         from ..parallel.comm import time_all_reduce
 
         if getattr(merger, "world", 1) <= 1 and getattr(merger, "emulate", None) is not None:
@@ -189,7 +192,9 @@ class WindowPipeline:
             del buf
         self.allreduce_probe_ms = ms
         thr = os.environ.get("ANA_DP_SERIAL_AR_US")
-        return thr is not None and ms > float(thr) / 1000.0
+        if thr is not None:
+            return ms > float(thr) / 1000.0
+        return self.grid >= 512
 
     @staticmethod
     def tail_point(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512, capped: bool = True) -> float:
