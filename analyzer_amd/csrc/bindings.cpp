@@ -882,20 +882,27 @@ void warm_rows(Tensor state, Tensor sink) {
 }
 
 // runtime/rerate.py window digest of the packed output rows (digest.hip); out [3 + 10K] fp64
-void records_digest(Tensor rows, int64_t K, Tensor scratch, Tensor out) {
+void records_digest(Tensor rows, int64_t K, Tensor scratch, Tensor out, const c10::optional<Tensor>& hist) {
   const auto dev = rows.device();
   check(rows, "rows", torch::kFloat32, dev);
   check(scratch, "scratch", torch::kFloat64, dev);
   check(out, "out", torch::kFloat64, dev);
   TORCH_CHECK(K >= 1 && K <= 5, "records_digest: K in 1..5");
-  TORCH_CHECK(rows.dim() == 2 && rows.size(1) >= 10 * K + 2 && rows.size(1) % 4 == 0,
-              "records_digest: rows must be the packed [M, W] output rows");
+  TORCH_CHECK(rows.dim() == 2 && rows.size(1) >= 10 * K + 2 && rows.size(1) % 4 == 0 &&
+                  256 % (rows.size(1) / 4) == 0,
+              "records_digest: rows must be the packed [M, W] output rows (W / 4 a divisor of 256)");
   TORCH_CHECK(out.numel() == 3 + 10 * K, "records_digest: out needs 3 + 10K doubles");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(rows.data_ptr()) % 16 == 0, "records_digest: rows must be 16-B aligned");
   TORCH_CHECK(dev.is_cuda(), "records_digest: device rows (the host path is runtime/rerate.py window_digest)");
   TORCH_CHECK((size_t)scratch.numel() >= ana::records_digest_scratch_doubles((int)K), "records_digest: scratch too small");
+  int64_t* h = nullptr;
+  if (hist.has_value()) {
+    check(*hist, "hist", torch::kInt64, dev);
+    TORCH_CHECK(hist->numel() == 256, "records_digest: hist must be int64[256]");
+    h = hist->data_ptr<int64_t>();
+  }
   check_hip(ana::launch_records_digest((int)K, rows.data_ptr<float>(), rows.size(0), rows.size(1),
-                                       scratch.data_ptr<double>(), out.data_ptr<double>(), stream_of(rows)),
+                                       scratch.data_ptr<double>(), out.data_ptr<double>(), h, stream_of(rows)),
             "records_digest");
 }
 
@@ -972,7 +979,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stream_write_value64", &stream_write_value64, "hipStreamWriteValue64(stream, ptr, value)");
   m.def("can_wait_value", &can_wait_value, "hipDeviceAttributeCanUseStreamWaitValue");
   m.def("reset_tags", &reset_tags, "zero the dataflow tags of a roster");
-  m.def("records_digest", &records_digest, "deterministic fp64 digest of a window's packed output rows");
+  m.def("records_digest", &records_digest, "deterministic fp64 digest of a window's packed output rows "
+        "(+ its status counts added to hist)", py::arg("rows"), py::arg("K"), py::arg("scratch"),
+        py::arg("out"), py::arg("hist") = py::none());
   m.def("records_digest_scratch", &records_digest_scratch, "scratch doubles of records_digest");
   m.def("emulate_allreduce", &emulate_allreduce,
         "DP pricing on one GPU: an all-reduce stand-in (buffer unchanged) on N CUs for >= us microseconds");

@@ -30,10 +30,11 @@ size_t schedule_workspace_bytes(int64_t nslots, int64_t num_players);
 // Deterministic per-window digest of the packed output rows [M, W] (digest.hip):
 // out[3 + 10K] fp64 = matches with records, participant records, the NaN-skipping
 // column sums of s_mu / s_sig / delta / m_mu / m_sig per slot, the quality sum.
-// scratch: records_digest_scratch_doubles(K) doubles.
+// scratch: records_digest_scratch_doubles(K) doubles.  hist (nullable) int64[256]:
+// the window's status counts are ADDED to it (the run's running status histogram).
 size_t records_digest_scratch_doubles(int K);
 int launch_records_digest(int K, const float* rows, int64_t M, int64_t W, double* scratch, double* out,
-                          hipStream_t s);
+                          int64_t* hist, hipStream_t s);
 
 // Stable LSD radix sort of (key, value) pairs on the low ``bits`` key bits
 // (radix_sort.hip).  Ping-pongs between the two buffer pairs; *result_in_alt

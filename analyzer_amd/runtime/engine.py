@@ -77,7 +77,7 @@ class WindowPipeline:
     """Rate consecutive windows against one roster, prepass overlapped."""
 
     def __init__(self, rater: BatchRater, roster: Roster, K: int, merger=None, signal_at: float = 0.0,
-                 telemetry: bool = False):
+                 telemetry: bool = False, depth: Optional[int] = None):
         self.rater = rater
         self.roster = roster
         self.K = int(K)
@@ -85,7 +85,6 @@ class WindowPipeline:
         self.device = roster.device
         self.cuda = self.device.type == "cuda"
         self._set = 0
-        self._free: List[Optional[torch.cuda.Event]] = [None, None]
         self.windows_rated = 0
         # tail overlap: signal word + number of the last enqueued rate launch
         self.ecfg = EngineConfig.from_env()
@@ -125,6 +124,14 @@ class WindowPipeline:
             self.defer_at = float(env) if env else DP_DEFER_AT
             if self.defer_at > 0 and self.tail == 0:
                 self.tail = self.defer_at
+        # windows prepared ahead of the one being rated (``depth``, ANA_PREPASS_DEPTH): the
+        # caller prepares window i + depth behind rate(i)'s tail; depth + 1 schedule buffer
+        # sets rotate.  Two lets the prepass of window i + 2 run beside the whole of rate(i+1)
+        # instead of only rate(i)'s tail (overlapped placements only)
+        d = depth if depth is not None else int(os.environ.get("ANA_PREPASS_DEPTH") or 0)
+        self.depth = self.prepass_depth(self.K, self.grid, self.serial, dp) if d <= 0 else \
+            (1 if self.serial or dp else int(d))
+        self._free: List[Optional[torch.cuda.Event]] = [None] * (self.depth + 1)
         self._signal = 0
         self._seq = 0
         self.side = self._side_stream() if self.cuda else None
@@ -154,6 +161,11 @@ class WindowPipeline:
                 self._signal = native().progress_signal(dev)
         if self._signal and self.defer_at > 0:
             merger.defer_gate = self._gate_next
+
+    @staticmethod
+    def prepass_depth(K: int, grid: int, serial: bool, dp: bool) -> int:
+        """Windows prepared ahead by default: 1 (see ``depth``)."""
+        return 1
 
     @staticmethod
     def serial_prepass(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512) -> bool:
@@ -302,7 +314,7 @@ class WindowPipeline:
             ready = torch.cuda.Event()
             ready.record(side)
         used = self._set
-        self._set ^= 1
+        self._set = (self._set + 1) % len(self._free)
         return Prepared(rec, sched, ready, used)
 
     def rate(self, prep: Prepared, out: Optional[RateResult] = None, check: bool = False,

@@ -37,6 +37,7 @@ import json
 import os
 import sys
 import time
+from collections import deque
 from dataclasses import asdict, dataclass
 from typing import Callable, Dict, Optional
 
@@ -97,14 +98,22 @@ def window_slice(spec: RerateSpec, g: int, rank: int, size: int):
 class _Digest:
     """Per-window digests on the device: one deterministic streaming pass over the
     packed output rows (csrc/digest.hip) -- 7 torch nansum passes and a bincount
-    before, 8.5 ms per 16M-match window (profiles/r6/rerate_attribution.log)."""
+    before, 8.5 ms per 16M-match window (profiles/r6/rerate_attribution.log).  With
+    ``hist`` (int64[256] on the rows' device) the pass also adds the window's status
+    counts to it, in place of a strided copy + bincount of the status bytes (the host
+    path counts with a bincount)."""
 
     def __init__(self):
         self._scratch = {}
 
-    def __call__(self, res: R.RateResult, K: int) -> torch.Tensor:
+    def device(self, res: R.RateResult) -> bool:
+        return res.packed is not None and res.packed.is_cuda
+
+    def __call__(self, res: R.RateResult, K: int, hist: Optional[torch.Tensor] = None) -> torch.Tensor:
         rows = res.packed
-        if rows is None or not rows.is_cuda:
+        if not self.device(res):
+            if hist is not None:
+                hist += torch.bincount(res.status.to(torch.int64), minlength=256)
             return window_digest(res)
         from ..ops.native import native
 
@@ -113,7 +122,7 @@ class _Digest:
             self._scratch[key] = torch.empty(native().records_digest_scratch(K), dtype=torch.float64,
                                              device=rows.device)
         out = torch.empty(3 + 10 * K, dtype=torch.float64, device=rows.device)
-        native().records_digest(rows, K, self._scratch[key], out)
+        native().records_digest(rows, K, self._scratch[key], out, hist)
         return out
 
 
@@ -190,24 +199,47 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
         lo, hi = window_slice(spec, g, rank, size)
         return make_stream(sspec, hi - lo, spec.players, K=K, base=lo, device=dev)
 
+    # ANA_RERATE_GEN=tail (default): the next window's records are generated in the rating's
+    # tail on the prepass stream (needs the tail-overlapped prepass, no DP merge); main: on
+    # the main stream between the ratings
+    gen_tail = (os.environ.get("ANA_RERATE_GEN", "tail") == "tail" and dev.type == "cuda" and merger is None
+                and pipe.side is not None and pipe.side != torch.cuda.current_stream(dev) and pipe.tail > 0)
     t0 = time.perf_counter()
     rated = 0
-    nxt = pipe.prepare(window_rec(start_window)) if start_window < total else None
+    D = pipe.depth  # windows prepared ahead (runtime/engine.py)
+    ahead = deque(pipe.prepare(window_rec(j)) for j in range(start_window, min(start_window + D, total)))
     for g in range(start_window, total):
-        cur = nxt
+        cur = ahead.popleft()
         M = cur.rec.shape[0]
         b = g & 1
         if outs[b] is None or outs[b].quality.shape[0] != M:
             outs[b] = R.RateResult.allocate(M, K, dev)
         elif sink is not None and sink.copied(outs[b]) is not None:
             torch.cuda.current_stream(dev).wait_event(sink.copied(outs[b]))
-        # window g+1 is generated before rate(g) is enqueued; its prepass waits for the tail
-        res, nxt = pipe.step(cur, window_rec(g + 1) if g + 1 < total else None, out=outs[b])
+        nw = g + D  # the window prepared behind this rating
+        if gen_tail and nw < total:
+            # window g+D is generated on the prepass stream in rate(g)'s tail, right before
+            # its prepass, instead of on the main stream in front of rate(g)
+            res = pipe.rate(cur, out=outs[b])
+            side = pipe.side
+            with torch.cuda.stream(side):
+                pipe.wait_tail(side)
+                rec_next = window_rec(nw)
+                made = torch.cuda.Event()
+                made.record(side)
+            rec_next.record_stream(torch.cuda.current_stream(dev))
+            ahead.append(pipe.prepare(rec_next, produced=made))
+        else:
+            # window g+D is generated before rate(g) is enqueued; its prepass waits for the tail
+            res, nxt = pipe.step(cur, window_rec(nw) if nw < total else None, out=outs[b])
+            if nxt is not None:
+                ahead.append(nxt)
         pipe.results_ready(res)  # the DP merge's deferred record correction of these rows
-        counts += torch.bincount(res.status.to(torch.int64), minlength=256)
         if records == "digest":
-            digests[g] = digest(res, K)
-        elif sink is not None:
+            digests[g] = digest(res, K, counts)  # + the status counts
+        else:
+            counts += torch.bincount(res.status.to(torch.int64), minlength=256)
+        if sink is not None:
             sink.push(window_slice(spec, g, rank, size)[0], res)
         rated += M
         if on_window is not None:

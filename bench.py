@@ -316,7 +316,8 @@ def main(argv=None) -> int:
         merger.defer else [out]
     rater.clear_sticky(dev)  # executor error flags, OR-ed over every launch of the run
     sync()
-    prepared = {0: pipe.prepare(windows[0])}
+    D = pipe.depth  # windows prepared ahead (runtime/engine.py)
+    prepared = {j: pipe.prepare(windows[j % n_windows]) for j in range(min(D, total_windows))}
 
     tstream = None
     ttail = None
@@ -337,9 +338,9 @@ def main(argv=None) -> int:
 
     def step(i):
         out = outs[i % len(outs)]
-        # rate window i, then the prepass of window i+1 on the side stream behind
+        # rate window i, then the prepass of window i+D on the side stream behind
         # its tail (every timed step carries exactly one prepass and one rating)
-        nxt = windows[(i + 1) % n_windows]
+        nxt = windows[(i + D) % n_windows]
         if ttail is not None:
             # the telemetry of window i beside the tail of its rating and the next
             # prepass; rating i + 1 waits for it (no co-run with a full executor)
@@ -353,7 +354,7 @@ def main(argv=None) -> int:
             pipe.wait_tail(ttail)
             with torch.cuda.stream(ttail):
                 aggregate(tele[i % n_windows], K, stats)
-            prepared[i + 1] = res_prep[1]
+            prepared[i + D] = res_prep[1]
             return
         if tstream is not None:
             # window i's telemetry co-runs with its rating; the step ends when both have
@@ -361,15 +362,15 @@ def main(argv=None) -> int:
             tstream.wait_stream(main)
             with torch.cuda.stream(tstream):
                 aggregate(tele[i % n_windows], K, stats)
-            _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out)
+            _, prepared[i + D] = pipe.step(prepared.pop(i), nxt, out=out)
             main.wait_stream(tstream)
         elif tele is None or args.telemetry_mode == "separate":
-            _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out)
+            _, prepared[i + D] = pipe.step(prepared.pop(i), nxt, out=out)
             if tele is not None:
                 aggregate(tele[i % n_windows], K, stats)
         else:
             t = tele[i % n_windows]
-            _, prepared[i + 1] = pipe.step(prepared.pop(i), nxt, out=out,
+            _, prepared[i + D] = pipe.step(prepared.pop(i), nxt, out=out,
                                            telemetry=(t.evoff, t.events, stats))
 
     per = sub  # loop units (windows) per step

@@ -22,11 +22,15 @@ def test_device_digest_matches_fp64_torch(gpu_device, K, M, P):
     res = R.BatchRater().rate(roster, rec, K)
     torch.cuda.synchronize()
     dig = _Digest()
-    a = dig(res, K)
+    hist = torch.full((256,), 5, dtype=torch.int64, device=gpu_device)
+    a = dig(res, K, hist)
     b = dig(res, K)
     ref = window_digest(res)
     assert a.shape == ref.shape
-    assert torch.equal(a, b)  # deterministic: fixed grid, no atomics
+    assert torch.equal(a, b)  # deterministic: fixed grid, fixed-order sums
+    # the status counts are added to the histogram: every match once
+    want = torch.bincount(res.status.to(torch.int64), minlength=256) + 5
+    assert torch.equal(hist, want)
     a, ref = a.cpu().numpy(), ref.cpu().numpy()
     assert a[0] == ref[0] and a[1] == ref[1]  # counts are exact
     np.testing.assert_allclose(a[2:], ref[2:], rtol=1e-12, atol=1e-6)
