@@ -183,6 +183,9 @@ class BatchRater:
         # inline (fused) telemetry up to this many matches per launch, the MFMA kernel after
         # the rating above (scripts/tele_batch.py, profiles/r3/tele_fused_vs_separate_by_batch.log)
         self.tele_fuse_max = int(ecfg.tele_fuse_max)
+        # ANA_RATE_CHUNK (tuning): cap on the matches per ticket of a window launch (8-64;
+        # default per team size, chunk_len)
+        self.chunk_cap = int(os.environ.get("ANA_RATE_CHUNK") or 0)
         self._vst: Dict[str, torch.Tensor] = {}
         self._ws: Dict[Tuple[str, str], torch.Tensor] = {}
 
@@ -209,31 +212,39 @@ class BatchRater:
         return self.has_telemetry(telemetry) and (self.knobs[5] >= 0 or M <= self.tele_fuse_max)
 
     def launch_blocks(self, K: int = 3, roster_bytes: int = 0) -> int:
-        """Workgroups of a window launch: 256 (one wave per SIMD) for teams of <= 3 over a
-        roster that fits the 256-MB Infinity Cache, else 512.  Measured per workload on
-        MI355X (profiles/r5/executor_grid.log, 256 vs 512): 3v3 over 1M players 6.56 vs
-        6.65 ms per 10M window, config 2 step 7.95 vs 8.01, config 4 8.85 vs 9.35, skewed
-        windows -4.5 / -6 %; 5v5 (config 3) 20.3-20.5 vs 20.1 and 10M players (config 5,
-        1.28-GB roster: the gathers miss to HBM and need the waves) 13.05 vs 11.73."""
+        """Workgroups of a window launch: 256 (one wave per SIMD) over a roster that fits
+        the 256-MB Infinity Cache, else 512.  Measured per workload on MI355X
+        (profiles/r5/executor_grid.log, 256 vs 512): 3v3 over 1M players 6.56 vs 6.65 ms
+        per 10M window, config 2 step 7.95 vs 8.01, config 4 8.85 vs 9.35, skewed windows
+        -4.5 / -6 %; 10M players (config 5, 1.28-GB roster: the gathers miss to HBM and
+        need the waves) 13.05 vs 11.73.  4v4 and 5v5 took 512 until the one-held-chunk
+        executor: since then 256 wins for them too -- 4v4 (10M window) 9.29-9.56 vs
+        10.77-10.80 ms per step, config 3 with 32-match chunks 14.36-14.48 vs 15.43-15.51
+        (profiles/r6/wide_teams_grid_chunk.log)."""
         if self.fixed_blocks:
             return self.fixed_blocks
-        return 256 if K <= 3 and roster_bytes <= (256 << 20) else 512
+        return 256 if roster_bytes <= (256 << 20) else 512
 
-    def chunk_len(self, M: int, telemetry: bool = False, blocks: Optional[int] = None) -> int:
-        """Matches per executor ticket: 64 (one per lane) for windows, shorter
-        (8-32, a power of two) when 64-match chunks would leave the full grid
+    def chunk_len(self, M: int, telemetry: bool = False, blocks: Optional[int] = None, K: int = 3) -> int:
+        """Matches per executor ticket: 64 (one per lane) for windows -- 32 for 5v5 --,
+        shorter (8-32, a power of two) when such chunks would leave the full grid
         (``4 * self.blocks`` waves) short of work.  A wave rates 64/G matches per
         iteration, so a 500-match micro-batch in 64-match chunks runs 8 waves x 8
-        dependent iterations; in 8-match chunks it runs 63 waves x 1."""
+        dependent iterations; in 8-match chunks it runs 63 waves x 1.  5v5 windows are
+        ~3,000 dependency levels of ~4k matches: a wave holding 32 claims closer to the
+        frontier (config 3 18.5-18.9 -> 15.4-15.5 ms per step at 512 workgroups; 16:
+        22.8; 3v3 and 4v4 lose with 32: config 2 8.45, config 5 13.96, 4v4 9.74-9.93 vs
+        9.29-9.56 ms, profiles/r6/wide_teams_grid_chunk.log).  ``ANA_RATE_CHUNK`` caps it."""
         if telemetry:
             return 64
+        cap = self.chunk_cap if self.chunk_cap > 0 else (32 if K >= 5 else 64)
         need = -(-M // (4 * (blocks or self.blocks)))  # matches per wave at the full grid
         cl = 8
         while cl < need and cl < 64:
             cl *= 2
-        return cl
+        return max(8, min(cl, cap))
 
-    def grid_blocks(self, M: int, telemetry: bool = False, blocks: Optional[int] = None) -> int:
+    def grid_blocks(self, M: int, telemetry: bool = False, blocks: Optional[int] = None, K: int = 3) -> int:
         """Persistent-grid size for a window of M matches: ``blocks`` (launch_blocks),
         but no more than one wave per chunk (``chunk_len``) -- a micro-batch of 500
         matches needs 63 waves, not 2048 (the extra workgroups only cost launch and exit
@@ -241,7 +252,7 @@ class BatchRater:
         if telemetry:
             return self.blocks
         b = blocks or self.blocks
-        chunks = -(-M // self.chunk_len(M, blocks=b))
+        chunks = -(-M // self.chunk_len(M, blocks=b, K=K))
         return max(1, min(b, -(-chunks // 4)))
 
     # ------------------------------------------------------------- buffers
@@ -357,11 +368,11 @@ class BatchRater:
         native().rate(rec, K, link, deps, roster.state, roster.attrs, fp, out.quality, out.status,
                       out.s_mu, out.s_sig, out.delta, out.m_mu, out.m_sig, ctrl, self.vst(dev),
                       float(cfg.beta) ** 2, float(cfg.tau) ** 2, float(cfg.unknown_player_sigma),
-                      record, self.grid_blocks(M, tiles, blocks), epoch,
+                      record, self.grid_blocks(M, tiles, blocks, K), epoch,
                       self.host_fp64, *telemetry,
                       *(progress if progress is not None and dev.type == "cuda" else (0, 0, 0)),
                       epoch_dev.data_ptr() if epoch_dev is not None and dev.type == "cuda" else 0,
-                      self.chunk_len(M, tiles, blocks), ctrl_ready, self.knobs)
+                      self.chunk_len(M, tiles, blocks, K), ctrl_ready, self.knobs)
         if after is not None:
             # same stream, after the rating; malformed events count into ctrl[13] as in
             # the fused launch (zeroed by this launch, read by telemetry_errors)

@@ -61,6 +61,9 @@ DP_TAIL_AT = 0.9  # tail-overlap start of the next prepass between DP merges (3v
 SPARE_TAIL_AT = 0.55  # ... of a window launch at one wave per SIMD (config 2, one held chunk: 0.45-0.65
 #                       6.87-6.90 ms vs 7.10 at 0.75, profiles/r6/tail_points.log; 0.75 with four held chunks)
 FULL_TAIL_AT = 0.1  # ... of a 1v1-3v3 launch at two waves per SIMD (config 5: 0-0.7 swept)
+WIDE_TAIL_AT = 0.5  # ... of a 5v5 launch at one wave per SIMD (config 3: 14.36-14.48 ms from 0.3-0.5,
+#                     14.44-14.64 from 0.7, 14.85-15.04 from 0.85, serial 15.22-15.47,
+#                     profiles/r6/wide_teams_grid_chunk.log)
 DP_DEFER_AT = 0.8  # split DP merge: the deferred prefix exchange + record correction of window w
 #                    start once rating w+1 claimed this fraction of its chunks (ANA_DP_DEFER_AT)
 
@@ -170,12 +173,14 @@ class WindowPipeline:
     @staticmethod
     def serial_prepass(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512) -> bool:
         """Prepass on the main stream?  ``ANA_PREPASS_SERIAL`` if set, else serial for 4v4 and
-        5v5 at two waves per SIMD (``grid`` 512), where a sort workgroup does not fit beside
-        the executor's waves -- 1v1-3v3 launches are compiled to leave it room
-        (csrc/dataflow.hip ANA_EXEC_WPE); under DP merges (``dp``) the windows are short and
-        the placement follows the collective's cost (probe_placement).  5v5 was overlapped
-        from 0.7 until round 6; with the two-chunk 5v5 executor the serial prepass is
-        faster (config 3 19.23-19.27 vs 19.66-19.73 ms, profiles/r6/config3_held_chunks.log)."""
+        5v5 at two waves per SIMD (``grid`` 512: a roster past the Infinity Cache), where a
+        sort workgroup does not fit beside the executor's waves -- 1v1-3v3 launches are
+        compiled to leave it room (csrc/dataflow.hip ANA_EXEC_WPE); under DP merges (``dp``)
+        the windows are short and the placement follows the collective's cost
+        (probe_placement).  At 512 workgroups the serial prepass was faster for config 3
+        (19.23-19.27 vs 19.66-19.73 ms, profiles/r6/config3_held_chunks.log); at one wave
+        per SIMD (its default since the 32-match 5v5 chunks) the tail overlap is
+        (14.36-14.48 vs 15.22-15.47 ms, profiles/r6/wide_teams_grid_chunk.log)."""
         if ecfg.prepass_serial is not None:
             return ecfg.prepass_serial
         return K >= 4 and not dp and grid >= 512
@@ -211,13 +216,16 @@ class WindowPipeline:
     @staticmethod
     def tail_point(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512, capped: bool = True) -> float:
         """Where the overlapped prepass starts: ``ANA_PREPASS_AT`` if set, else 0.7,
-        DP_TAIL_AT for 1v1-4v4 windows between merges (measured: config 2 with 8 merges
+        WIDE_TAIL_AT for 5v5 windows at one wave per SIMD, DP_TAIL_AT for 1v1-4v4 windows
+        between merges (measured: config 2 with 8 merges
         per step, profiles/r3/dp_prepass_placement_k8.log), SPARE_TAIL_AT for 1v1-4v4
         windows at one wave per SIMD, FULL_TAIL_AT for 1v1-3v3 windows at two when the
         launch takes the 128-VGPR build (``capped``: no fused telemetry, no timing build --
         the uncapped build leaves a sort workgroup no room, so its prepass starts at 0.7)."""
-        if ecfg.prepass_at_set or K >= 5:
+        if ecfg.prepass_at_set:
             return ecfg.prepass_at
+        if K >= 5:
+            return WIDE_TAIL_AT if grid < 512 and not dp else ecfg.prepass_at
         if dp:
             return DP_TAIL_AT
         if grid < 512:
@@ -340,7 +348,7 @@ class WindowPipeline:
             self._seq += 1
             M = int(prep.rec.shape[0])
             blocks = self.rater.launch_blocks(self.K, self.roster.state.numel() * self.roster.state.element_size())
-            cl = self.rater.chunk_len(M, self.rater.tiles(telemetry, M), blocks)
+            cl = self.rater.chunk_len(M, self.rater.tiles(telemetry, M), blocks, self.K)
             at = int(self.tail * ((M + cl - 1) // cl))
             progress = (self._signal, self._seq, at)
         if self.warm and self.cuda:

@@ -160,6 +160,33 @@ def test_device_repeat_launch_deterministic(gpu_device):
     assert torch.equal(outs[0][1].view(torch.int32), outs[1][1].view(torch.int32))
 
 
+@pytest.mark.parametrize("K", [4, 5])
+def test_chunk_length_bit_identical(gpu_device, K):
+    """4v4 / 5v5 windows at their default grid and chunk (5v5: 32-match tickets,
+    ops/rate.py chunk_len) give the bits of 64- and 16-match tickets at 512 workgroups:
+    the ticket size changes only when a match runs."""
+    P, M = 100000, 400000
+    rs = RosterSpec(num_players=P, seed=21)
+    rec = make_stream(StreamSpec(team_size=K, seed=22), M, P, K=K, device=gpu_device)
+    outs = []
+    for blocks, cap in ((None, 0), (512, 64), (512, 16)):
+        ro = make_roster(rs, device=gpu_device)
+        rater = R.BatchRater(blocks=blocks)
+        rater.chunk_cap = cap
+        if blocks is None:
+            assert rater.launch_blocks(K, ro.state.numel() * ro.state.element_size()) == 256
+            assert rater.chunk_len(M, blocks=256, K=K) == (32 if K == 5 else 64)
+        res = rater.rate(ro, rec, K)
+        assert int(rater.error_flags(gpu_device).sum()) == 0
+        outs.append((ro.state.cpu(), res.s_mu.cpu(), res.status.cpu(), res.m_sig.cpu()))
+    a = outs[0]
+    for b in outs[1:]:
+        assert torch.equal(a[0][:, 0::2].contiguous().view(torch.int32), b[0][:, 0::2].contiguous().view(torch.int32))
+        assert torch.equal(a[1].view(torch.int32), b[1].view(torch.int32))
+        assert torch.equal(a[2], b[2])
+        assert torch.equal(a[3].view(torch.int32), b[3].view(torch.int32))
+
+
 @pytest.mark.parametrize("K", [2, 3])
 def test_grid_and_register_builds_bit_identical(gpu_device, K):
     """The launch grid picks the build: at two waves per SIMD (> 256 workgroups) plain

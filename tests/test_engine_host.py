@@ -134,6 +134,10 @@ def test_grid_blocks_scale_with_the_window():
     assert br.chunk_len(64 * 2048 * 2) == 64 and br.grid_blocks(64 * 2048 * 2) == 512
     assert br.grid_blocks(10_000_000) == 512
     assert br.grid_blocks(500, telemetry=True) == 512
+    # 5v5 windows take 32-match chunks (ANA_RATE_CHUNK caps any team size)
+    assert br.chunk_len(10_000_000, K=5) == 32 and br.chunk_len(10_000_000, K=4) == 64
+    assert br.grid_blocks(64 * 2048, K=5) == 512 and br.grid_blocks(32 * 2048, K=5) == 512
+    assert br.chunk_len(500, K=5) == 8 and br.chunk_len(500, telemetry=True, K=5) == 64
 
 
 @pytest.mark.parametrize("skew", [1, 2, 3])
@@ -178,7 +182,11 @@ def test_prepass_placement_knob():
 
     br = BatchRater()
     assert br.launch_blocks(3, 128 << 20) == 256 and br.launch_blocks(3, 1280 << 20) == 512
-    assert br.launch_blocks(5, 128 << 20) == 512 and BatchRater(blocks=384).launch_blocks(3, 0) == 384
+    assert br.launch_blocks(5, 128 << 20) == 256 and br.launch_blocks(4, 1280 << 20) == 512
+    assert BatchRater(blocks=384).launch_blocks(3, 0) == 384
+    # 4v4 / 5v5 over a cached roster: one wave per SIMD, the prepass overlapped (5v5 from 0.5)
+    assert not WindowPipeline.serial_prepass(5, auto, grid=256) and WindowPipeline.tail_point(5, auto, grid=256) == 0.5
+    assert not WindowPipeline.serial_prepass(4, auto, grid=256) and WindowPipeline.tail_point(4, auto, grid=256) == 0.55
     assert not auto.roster_warm and EngineConfig.from_env({"ANA_ROSTER_WARM": "1"}).roster_warm
 
 
