@@ -57,7 +57,7 @@ from ..ops.rate import BatchRater, RateResult, Roster, Schedule
 from ..utils.trace import trace_range
 
 CHUNK = 64  # matches per executor ticket of a window (csrc/dataflow.hip kChunk; BatchRater.chunk_len)
-DP_TAIL_AT = 0.9  # tail-overlap start of the next prepass between DP merges (3v3; see tail_point)
+DP_TAIL_AT = 0.9  # tail-overlap start of the next prepass between DP merges (see tail_point)
 SPARE_TAIL_AT = 0.55  # ... of a window launch at one wave per SIMD (config 2, one held chunk: 0.45-0.65
 #                       6.87-6.90 ms vs 7.10 at 0.75, profiles/r6/tail_points.log; 0.75 with four held chunks)
 FULL_TAIL_AT = 0.1  # ... of a 1v1-3v3 launch at two waves per SIMD (config 5: 0-0.7 swept)
@@ -216,17 +216,19 @@ class WindowPipeline:
     @staticmethod
     def tail_point(K: int, ecfg: EngineConfig, dp: bool = False, grid: int = 512, capped: bool = True) -> float:
         """Where the overlapped prepass starts: ``ANA_PREPASS_AT`` if set, else 0.7,
-        WIDE_TAIL_AT for 5v5 windows at one wave per SIMD, DP_TAIL_AT for 1v1-4v4 windows
-        between merges (measured: config 2 with 8 merges
+        WIDE_TAIL_AT for 5v5 windows at one wave per SIMD, DP_TAIL_AT for windows between
+        merges (measured: config 2 with 8 merges
         per step, profiles/r3/dp_prepass_placement_k8.log), SPARE_TAIL_AT for 1v1-4v4
         windows at one wave per SIMD, FULL_TAIL_AT for 1v1-3v3 windows at two when the
         launch takes the 128-VGPR build (``capped``: no fused telemetry, no timing build --
         the uncapped build leaves a sort workgroup no room, so its prepass starts at 0.7)."""
         if ecfg.prepass_at_set:
             return ecfg.prepass_at
-        if K >= 5:
-            return WIDE_TAIL_AT if grid < 512 and not dp else ecfg.prepass_at
+        if K >= 5 and not dp:
+            return WIDE_TAIL_AT if grid < 512 else ecfg.prepass_at
         if dp:
+            # (5v5 between 16 merges per step, emulated N = 8: 22.97-23.00 ms from 0.9, 23.69-23.75
+            # from 0.7, 24.45 from 0.5, 23.24-23.39 beside the merge, profiles/r6/dp_placement.log)
             return DP_TAIL_AT
         if grid < 512:
             return SPARE_TAIL_AT

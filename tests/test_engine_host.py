@@ -172,7 +172,7 @@ def test_prepass_placement_knob():
     assert auto.prepass_at == 0.7 and EngineConfig.from_env({"ANA_PREPASS_AT": "0"}).prepass_at == 0.0
     # DP merges: short windows between merges overlap the next prepass with the tail, from 0.9 (3v3)
     assert not WindowPipeline.serial_prepass(3, auto, dp=True) and WindowPipeline.serial_prepass(3, on, dp=True)
-    assert WindowPipeline.tail_point(3, auto, dp=True) == 0.9 and WindowPipeline.tail_point(5, auto, dp=True) == 0.7
+    assert WindowPipeline.tail_point(3, auto, dp=True) == 0.9 and WindowPipeline.tail_point(5, auto, dp=True) == 0.9
     assert WindowPipeline.tail_point(3, EngineConfig.from_env({"ANA_PREPASS_AT": "0.5"}), dp=True) == 0.5
     assert WindowPipeline.tail_point(4, auto) == 0.7
     # one wave per SIMD (256 workgroups: <= 3v3 over a cached roster): the tail overlap from 0.55
