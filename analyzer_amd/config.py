@@ -179,7 +179,7 @@ class EngineConfig:
                                       its rows come from the Infinity Cache (runtime/engine.py); auto =
                                       on between DP merges (short windows: k = 8 forced merges 9.30 vs
                                       9.53 ms), off for whole windows (8.02 either way)
-    ANA_MERGE_BUCKET_MB     16        sweep-merge bucket size (parallel/sweep.py)
+    ANA_MERGE_BUCKET_MB     64        sweep-merge bucket size (parallel/sweep.py)
     ANA_DP_SERIAL_AR_US     40        DP with N > 1 ranks: the next prepass runs beside the merge when one
                                       merge-sized all-reduce (timed when the pipeline is built, max over
                                       ranks) takes longer than this, else in the rating's tail
@@ -217,7 +217,7 @@ class EngineConfig:
     prepass_exclusive: bool = False  # with prepass_cus: the executor gets the other CUs
     prepass_serial: Optional[bool] = None  # None = auto (WindowPipeline.serial_prepass)
     roster_warm: Optional[bool] = None  # None = auto (WindowPipeline)
-    merge_bucket_mb: float = 16.0
+    merge_bucket_mb: float = 64.0
     comm_dtype: str = ""  # "" = by sweeps (runtime/rerate.py default_comm_dtype)
     sweeps: int = 1
     dist_backend: str = "nccl"
@@ -261,7 +261,7 @@ class EngineConfig:
             prepass_exclusive=env.get("ANA_PREPASS_EXCLUSIVE", "0") not in ("", "0", "false"),
             prepass_serial=_tristate(env.get("ANA_PREPASS_SERIAL")),
             roster_warm=_tristate(env.get("ANA_ROSTER_WARM")),
-            merge_bucket_mb=float(_env(env, "ANA_MERGE_BUCKET_MB") or 16),
+            merge_bucket_mb=float(_env(env, "ANA_MERGE_BUCKET_MB") or 64),
             comm_dtype=_env(env, "COMM_DTYPE") or "",
             sweeps=int(_env(env, "SWEEPS") or 1),
             dist_backend=_env(env, "ANA_DIST_BACKEND") or "nccl",

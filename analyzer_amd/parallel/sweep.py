@@ -14,12 +14,14 @@ ONE dense all-reduce of natural-parameter messages (csrc/sweep.hip):
 all-reduce of bucket b (asynchronous, on the collective's own stream) runs
 while the main stream computes the messages of bucket b+1 and decodes bucket
 b-1, so on xGMI only the first bucket's message kernel and the last bucket's
-decode stay exposed.  Buckets default to 16 MB of messages (ANA_MERGE_BUCKET_MB;
-0 = one bucket): a 1M-player roster (64 MB) becomes four all-reduces, each big
-enough to run the xGMI links at bandwidth, so the message kernel of bucket b+1
-and the decode of bucket b-1 (~0.1 ms each per 16 MB) hide behind the
-collective; a 10M-player re-rate roster (640 MB) becomes forty.  Every stage
-is per player, so bucketing is exact.
+decode stay exposed.  Buckets default to 64 MB of messages (ANA_MERGE_BUCKET_MB;
+0 = one bucket): the 1M-player operands (32 B per player with fp16 / bf16
+messages) stay one all-reduce, a 10M-player re-rate roster (320 MB) becomes five,
+each big enough to run the xGMI links at bandwidth, so the message kernel of
+bucket b+1 and the decode of bucket b-1 hide behind the collective.  Emulated
+N = 2 (profiles/r6/dp_bucketed_merge.log): config 5 13.02-13.04 ms per step at
+64 MB, 13.14-13.16 at 16 MB, 13.44-13.45 whole; config 2 7.57-7.60 either way.
+Every stage is per player, so bucketing is exact.
 
 **Causal re-sweeps (``sweeps`` > 1).**  Rank r's shard is the r-th time slice
 of the global window (bench.py, runtime/rerate.py), so under the reference's
@@ -175,6 +177,13 @@ class SweepMerger:
         self._corr_done = None    # event: the last deferred correction finished
         self._pd_done = None      # event: its delta table is written (the start it read is free)
         self._split_pending = None  # the correction waiting for the next merge (defer_mode "next")
+        # the corrected merge (merge_corrected) pipelined over the row buckets (messages of
+        # bucket b+1 and the decode of bucket b-1 beside bucket b's collective):
+        # ANA_DP_CORR_BUCKETS=1.  Off by default: emulated N = 8, config 2, 11.09 ms per step
+        # with 16-MB buckets and 11.58 with 8-MB ones against 10.83-10.86 whole; config 5
+        # 15.91-15.94 vs 15.67 (profiles/r6/dp_bucketed_merge.log) -- the overlapped
+        # kernels slow the collective's stand-in and each other by more than they hide
+        self.corr_buckets = os.environ.get("ANA_DP_CORR_BUCKETS", "0") not in ("", "0", "false")
         # ANA_DP_DEFER: "next" (default) -- window w's correction runs beside window w+1's
         # collective; "tail" -- behind the decode, gated on the next rating's tail; "now" --
         # behind the decode at once
@@ -192,9 +201,10 @@ class SweepMerger:
             mb = EngineConfig.from_env().merge_bucket_mb
             row_bytes = 16 * 4 if not self.scaled else 14 * torch.finfo(COMM_DTYPES[comm_dtype]).bits // 8 + 4
             bucket_rows = int(mb * (1 << 20)) // row_bytes if mb > 0 else self.P
-        if self.world <= 1:
+        if self.world <= 1 and self.emulate is None:
             # one rank (force): no collective to overlap, so one bucket -- two launches
-            # per merge instead of two per 16 MB
+            # per merge instead of two per bucket (the emulated collective is bucketed like
+            # the real one)
             bucket_rows = self.P
         self.bucket_rows = max(1, min(int(bucket_rows), max(self.P, 1)))
         self.windows = 0
@@ -614,63 +624,81 @@ class SweepMerger:
         """``merge`` with the causal record correction of this window's records
         (``rec``, RateResult ``out``): messages -> ONE collective giving the sum and
         this rank's exclusive prefix (comm.scan_and_sum) -> the decode, which also turns
-        the prefix into the increment table -> the records pass.  Not bucketed: the
-        records name any player, so the whole prefix is needed before the pass.
+        the prefix into the increment table -> the records pass.  The records name any
+        player, so the pass needs the whole table; the messages, the collective and the
+        decode are row-wise and pipeline over the row buckets (``corr_buckets``): bucket
+        b+1's messages and bucket b-1's decode run beside bucket b's collective.
 
         Deferred (``defer``, default): the records pass of this window is enqueued by
-        the NEXT merge right after its collective is launched, so it runs while the
-        collective is in flight (RCCL on its own stream; the emulated stand-in on 32 CUs)
+        the NEXT merge right after its collectives are launched, so it runs while they
+        are in flight (RCCL on its own stream; the emulated stand-in on 32 CUs)
         instead of on the critical path; ``flush_correction`` runs a pending pass."""
         K = (int(rec.shape[1]) - 2) // 2
         self._ev("begin")
-        if self.msg is not None:
-            self.messages_packed(roster)
-            operand = self.msg
-        else:
-            self.messages(roster)
-            operand = self.buf
+        packed = self.msg is not None
+        buckets = self.buckets() if (packed and self.corr_buckets) else [(0, self.P)]
+        launched = []
+        for lo, hi in buckets:
+            if packed:
+                self.messages_packed(roster, lo, hi)
+            else:
+                self.messages(roster)
+            launched.append((lo, hi, self._launch_scan(lo, hi, packed)))
         self._ev("messages")
-        if self.world > 1:
-            if self._coll is None and self.device.type == "cuda":
-                self._coll = torch.cuda.Stream(self.device)
-            # (force: a world_size override above the group's real size runs the exchanges
-            # anyway -- the one-rank RCCL test of this path)
-            fin = scan_and_sum_start(operand, group=self.group, stream=self._coll,
-                                     extra=self.cnt if self.msg is not None else None,
-                                     force=world(self.group)[1] < self.world)
-        else:
-            prefix0 = self._prefix_zero(operand)
-            fin = lambda: (prefix0, operand)  # noqa: E731
-            if self.emulate is not None and self.device.type == "cuda":  # 1.5x the all-reduce's volume
-                n, bw, lat = self.emulate
-                self.emulate = (n, bw / 1.5, lat)
-                efin = self._launch_reduce(0, self.P, self.msg is not None)
-                self.emulate = (n, bw, lat)
-                fin = lambda: (efin(), (prefix0, operand))[1]  # noqa: E731
-        self.flush_correction()  # the previous window's records, beside the collective
+        self.flush_correction()  # the previous window's records, beside the collectives
         self._ev("correct")
-        prefix, total = fin()
-        if total is not operand:
-            operand.copy_(total)
-        self._ev("allreduce")
         if overlap is not None:
             overlap()
         self._ev("overlap")
-        if self.msg is not None:  # the decode also turns the scaled prefix into raw increments
-            if self.delta is None:
-                self.delta = torch.empty((self.P, 16), dtype=torch.float32, device=self.device)
-            self.decode_packed(roster, into=self.start, prefix=prefix, delta=self.delta)
-            delta = self.delta
-        else:                     # raw fp32 messages: the prefix IS the increment table
-            self.decode(roster, into=self.start)
-            delta = prefix
-        self._ev("apply")
+        if packed and self.delta is None:
+            self.delta = torch.empty((self.P, 16), dtype=torch.float32, device=self.device)
+        delta = self.delta
+        for lo, hi, fin in launched:
+            prefix, total = fin()
+            self._ev("allreduce")
+            if packed:  # the decode also turns the scaled prefix into raw increments
+                if total is not self.msg[lo:hi] and total.data_ptr() != self.msg[lo:hi].data_ptr():
+                    self.msg[lo:hi].copy_(total)
+                native().sweep_apply_packed(self.start[lo:hi], self.msg[lo:hi], self.cnt[lo:hi],
+                                            roster.attrs[lo:hi], roster.state[lo:hi], self.start[lo:hi],
+                                            self.vst, float(self.cfg.unknown_player_sigma), self.clamps,
+                                            prefix, delta[lo:hi])
+                roster.epoch = roster.epoch if roster.epoch is not None else 0
+            else:                 # raw fp32 messages: the prefix IS the increment table
+                if total is not self.buf:
+                    self.buf.copy_(total)
+                self.decode(roster, into=self.start)
+                delta = prefix
+            self._ev("apply")
         self._pending = (rec, K, out.packed, delta)
         if not self.defer:
             self.flush_correction()
             self._ev("correct")
         self._synced = True
         self.windows += 1
+
+    def _launch_scan(self, lo: int, hi: int, packed: bool):
+        """Start the scan-and-sum collective of rows [lo, hi) (comm.scan_and_sum_start on
+        the collective stream); returns ``finish() -> (prefix, total)`` of those rows.  One
+        rank (force): the prefix is zero and the total the operand -- with ``emulate`` the
+        stand-in prices the N-rank exchange, 1.5x an all-reduce's volume."""
+        operand = self.msg[lo:hi] if packed else self.buf
+        if self.world > 1:
+            if self._coll is None and self.device.type == "cuda":
+                self._coll = torch.cuda.Stream(self.device)
+            # (force: a world_size override above the group's real size runs the exchanges
+            # anyway -- the one-rank RCCL test of this path)
+            return scan_and_sum_start(operand, group=self.group, stream=self._coll,
+                                      extra=self.cnt[lo:hi] if packed else None,
+                                      force=world(self.group)[1] < self.world)
+        prefix0 = self._prefix_zero(self.msg)[lo:hi] if packed else self._prefix_zero(self.buf)
+        if self.emulate is not None and self.device.type == "cuda":
+            n, bw, lat = self.emulate
+            self.emulate = (n, bw / 1.5, lat)
+            efin = self._launch_reduce(lo, hi, packed)
+            self.emulate = (n, bw, lat)
+            return lambda: (efin(), (prefix0, operand))[1]
+        return lambda: (prefix0, operand)
 
     def flush_correction(self) -> None:
         """Run the deferred record correction now (stream-ordered), if one is pending."""

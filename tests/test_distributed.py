@@ -523,11 +523,15 @@ def _corrected_ring(rank, size, P, M, K, seed, windows, mode):
     from analyzer_amd.runtime.engine import WindowPipeline
 
     os.environ["ANA_DP_SPLIT"] = "1" if mode == "split" else "0"
-    os.environ["ANA_DP_CORRECT_DEFER"] = "1" if mode == "defer" else "0"
+    os.environ["ANA_DP_CORRECT_DEFER"] = "1" if mode in ("defer", "bucketed") else "0"
+    os.environ["ANA_DP_CORR_BUCKETS"] = "1" if mode == "bucketed" else "0"
     roster = make_roster(RosterSpec(num_players=P, seed=seed, p_rated=0.3))
     spec = StreamSpec(team_size=K, seed=seed + 1)
     recs = [make_stream(spec, M, P, K=K, base=(w * size + rank) * M) for w in range(windows)]
-    merger = SweepMerger(P, "cpu", comm_dtype="bf16", correct_records=True)
+    # "bucketed": the scan merge pipelined over 4 row buckets (a ragged last one)
+    merger = SweepMerger(P, "cpu", comm_dtype="bf16", correct_records=True,
+                         bucket_rows=P // 4 + 1 if mode == "bucketed" else None)
+    assert len(merger.buckets()) == (4 if mode == "bucketed" else 1)
     assert merger.split() == (mode == "split"), (mode, merger.split())
     pipe = WindowPipeline(BatchRater(), roster, K, merger=merger)
     outs = [RateResult.allocate(M, K, "cpu") for _ in range(2)]
@@ -540,17 +544,19 @@ def _corrected_ring(rank, size, P, M, K, seed, windows, mode):
 
 
 def test_deferred_record_correction_matches_inline(tmp_path):
-    """The record correction deferred into the next merge (beside its collective), and
-    the round-6 split merge (all-to-all / owner reduce / all-gather of the sum, the prefix
-    returned and the records corrected after the decode), write exactly the records and
-    the roster the in-line pass writes, once finish() has run."""
+    """The record correction deferred into the next merge (beside its collective), the
+    same merge pipelined over row buckets, and the round-6 split merge (all-to-all /
+    owner reduce / all-gather of the sum, the prefix returned and the records corrected
+    after the decode), write exactly the records and the roster the in-line pass writes,
+    once finish() has run."""
     P, M, K, seed, size, windows = 300, 700, 3, 41, 2, 3
     a = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, "defer")
     b = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, "inline")
     c = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, "split")
+    d = run_ranks(_corrected_ring, size, tmp_path, P, M, K, seed, windows, "bucketed")
     for r in range(size):
-        assert a[r]["pending"] and not b[r]["pending"]
-        for o in (a[r], c[r]):
+        assert a[r]["pending"] and not b[r]["pending"] and d[r]["pending"]
+        for o in (a[r], c[r], d[r]):
             assert torch.equal(o["state"].view(torch.int32), b[r]["state"].view(torch.int32))
             for x, y in zip(o["rows"], b[r]["rows"]):
                 assert torch.equal(x.view(torch.int32), y.view(torch.int32))

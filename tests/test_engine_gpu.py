@@ -778,7 +778,9 @@ def _rccl_single_rank(rank, size, P, M, K, seed):
     # the corrected merge (bench N >= 4): the scan collective (byte rows: bf16 messages +
     # int32 touch fields) on a side stream, the records pass deferred into the next merge
     rc = roster.clone()
-    mc = SweepMerger(P, dev, world_size=2, comm_dtype="bf16", correct_records=True)
+    mc = SweepMerger(P, dev, world_size=2, comm_dtype="bf16", correct_records=True, bucket_rows=P // 3 + 1)
+    mc.corr_buckets = True
+    assert len(mc.buckets()) == 3  # the scan collective per row bucket, on the side stream
     mc.start.copy_(merger.start)
     mc._synced = True
     mc.begin(rc)
