@@ -192,7 +192,7 @@ class EngineConfig:
     ANA_TRACE               0         roctx ranges + Chrome trace (utils/trace.py)
     ANA_CHECK_ROUNDS        0         exact DP race detector: rounds share no player (parallel/exact_dp.py)
     ANA_RATE_IDLE           0         executor: max s_sleep rounds of an idle wave (<= 0: none)
-    ANA_RATE_LOCAL          0         executor: LDS hand-off of successors the producing wave holds (1 = on)
+    ANA_RATE_LOCAL          1         executor: LDS hand-off of successors the producing wave holds (0 = off; 1v1-3v3)
     ANA_RATE_DIAG           0         executor timing build: per-phase clocks in ctrl[20..47] (ops/rate.diag)
     ANA_RATE_TIGHT          -1        executor: 2K lanes per match instead of the next power of two (-1 auto)
     ANA_TELE_FUSED_TAIL     0         fused telemetry only after the executor's chunks are drained
@@ -230,7 +230,7 @@ class EngineConfig:
     # per SIMD with idle waves re-polling at once, the global counter path is as fast on a
     # serial chain and faster everywhere else (config 2 -0.03 ms, config 3 -0.13, quadratic /
     # cubic skew -3.8 / -3.3 %; config 5 +0.04, noise; profiles/r5/local_handoff_off.log)
-    rate_local: int = 0
+    rate_local: int = 1
     rate_diag: int = 0
     rate_tight: int = -1
     tele_fused_tail: int = 0
@@ -270,7 +270,7 @@ class EngineConfig:
             trace=(env.get("ANA_TRACE") or "0") not in ("", "0"),
             check_rounds=(env.get("ANA_CHECK_ROUNDS") or "0") not in ("", "0"),
             rate_idle=int(_env(env, "ANA_RATE_IDLE") or 0),
-            rate_local=int(_env(env, "ANA_RATE_LOCAL") or 0),
+            rate_local=int(_env(env, "ANA_RATE_LOCAL") or 1),
             rate_diag=int(_env(env, "ANA_RATE_DIAG") or 0),
             rate_tight=int(_env(env, "ANA_RATE_TIGHT") or -1),
             tele_fused_tail=int(_env(env, "ANA_TELE_FUSED_TAIL") or 0),

@@ -61,8 +61,18 @@
 
 namespace ana {
 
-// The LDS local hand-off (ANA_RATE_LOCAL) exists in the diagnostic library only.
-constexpr bool kLocalHandoff = ANA_DIAG_BUILD != 0;
+// The LDS local hand-off (ANA_RATE_LOCAL, on by default): compiled into the 1v1-3v3
+// executors (and every executor of the diagnostic library).  Off from round 5 with four
+// held chunks per wave (profiles/r5/local_handoff_off.log); with one held chunk (round 6)
+// it pays for 3v3 (in-call A/B of the libraries, profiles/r6/local_handoff_on.log): serial
+// hop 1.96-1.97 -> 1.85-1.87 us, cubic skew 1180 -> 1170 ms per 10M window, config 2
+// 6.88 -> 6.83 ms per step, config 4 7.43 -> 7.32, config 5 10.93 -> 10.79, config 2 between
+// emulated N = 8 merges 10.86-10.89 -> 10.33-10.34; quadratic skew 128.9 -> 131.4 ms; 5v5
+// gained nothing (14.48 vs 14.54 with it), so its executor keeps it compiled out
+#ifndef ANA_LOCAL_HANDOFF
+#define ANA_LOCAL_HANDOFF 1
+#endif
+constexpr bool kLocalHandoff = ANA_LOCAL_HANDOFF != 0;
 
 
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight (1v1-4v4)
@@ -121,6 +131,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
   constexpr int kH = K >= 5 ? ANA_HELD5 : kHeld;
+  constexpr bool kLH = kLocalHandoff && (K <= 3 || ANA_DIAG_BUILD != 0);  // LDS local hand-off compiled in
   constexpr bool TILES = TELE == 1;  // K8 tiles taken by idle / dedicated waves
   constexpr bool INL = TELE == 2;    // K8 inline: each group folds its match's events
   static_assert(G >= S && G <= 64, "a group holds one match");
@@ -131,11 +142,10 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   typedef uint32_t hvec __attribute__((ext_vector_type(kH <= 2 ? 2 : 4)));
   // local hand-off counters: increments of each held match's completion count
   // by publishes of THIS wave (never also added to the global counter); [lane][h]
-  // so a lane reads them in one ds_read_b64/b128.  Measured slower than the global
-  // counters since round 5 (profiles/r5/local_handoff_off.log): compiled into the
-  // diagnostic library only (kLocalHandoff), the production executor has no LDS
-  // array, no per-iteration read of it and no held-chunk scan in notify
-  __shared__ hvec lloc[kWavesPerBlock][kLocalHandoff ? kChunk : 1];
+  // so a lane reads them in one ds_read_b64/b128.  Without kLH (4v4 / 5v5 in the
+  // production library) the executor has no LDS array, no per-iteration read of it
+  // and no held-chunk scan in notify
+  __shared__ hvec lloc[kWavesPerBlock][kLH ? kChunk : 1];
   // this iteration's pick per group, written by the lane holding the match:
   // {match index, slot << 8 | lane in chunk, meta0, meta1, player ids...}
   constexpr int SPT = (4 + S + 3) / 4 * 4;  // inline telemetry words: {offset lo, hi, count, 0}
@@ -174,7 +184,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   // (ctrl[3] counts retired chunks), so long dependency chains never trip it
   uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_progress = 0;
-  const bool local_ok = kLocalHandoff && prm.local_handoff != 0;
+  const bool local_ok = kLH && prm.local_handoff != 0;
   // hand-off statistics (wave-uniform counts, added to ctrl[26..27] at exit); stale
   // reads retried (ctrl[14])
   uint32_t n_local = 0, n_global = 0, n_stale = 0;
@@ -311,7 +321,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
     uint64_t ready[kH];
     {
       hvec lv = {};
-      if constexpr (kLocalHandoff) lv = lloc[wv][lane];
+      if constexpr (kLH) lv = lloc[wv][lane];
 #pragma unroll
       for (int h = 0; h < kH; ++h)
         ready[h] = __ballot(dval[h] != kNone && dval[h] + lv[h] == need[h]) & pend[h];
@@ -530,7 +540,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
       if (succ == kNoMatch) return;
       int lh = -1;
       int32_t lcb = 0;
-      if (kLocalHandoff && local_ok) {
+      if (kLH && local_ok) {
 #pragma unroll
         for (int h = 0; h < kH; ++h)
           if (cbase[h] >= 0 && (int32_t)succ >= cbase[h] && (int32_t)succ < cbase[h] + cl) {
@@ -538,7 +548,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
             lcb = cbase[h];
           }
       }
-      if (kLocalHandoff && lh >= 0) {  // held by this wave: release it through LDS, next iteration
+      if (kLH && lh >= 0) {  // held by this wave: release it through LDS, next iteration
         atomicAdd(reinterpret_cast<uint32_t*>(&lloc[wv][(int32_t)succ - lcb]) + lh, 1u);
       } else {
         __hip_atomic_fetch_add((gu32*)(deps + succ), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -809,7 +819,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
           hoff[h] = stoff;
           hcnt[h] = stcnt;
         }
-      if constexpr (kLocalHandoff) reinterpret_cast<uint32_t*>(&lloc[wv][lane])[staging] = 0u;
+      if constexpr (kLH) reinterpret_cast<uint32_t*>(&lloc[wv][lane])[staging] = 0u;
       // no state, no dependencies: its output row is written after this iteration's
       // rating (early_row), so the rating's waits never include these stores
       if (mm < M && est != kRated && !tonly) {

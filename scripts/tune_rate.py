@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--idle", default="8", help="ANA_RATE_IDLE values (max idle sleep rounds)")
     ap.add_argument("--tight", default="-1", help="ANA_RATE_TIGHT values (2K lanes per match; -1 auto)")
-    ap.add_argument("--local", default="0", help="ANA_RATE_LOCAL values (LDS local hand-off; 0 = the default)")
+    ap.add_argument("--local", default="1", help="ANA_RATE_LOCAL values (LDS local hand-off; 1 = the default)")
     ap.add_argument("--diag", default="0", help="ANA_RATE_DIAG values (timing build)")
     ap.add_argument("--skew", type=int, default=1)
     ap.add_argument("--rated", type=float, default=1.0,
