@@ -1,26 +1,22 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/r6t; mkdir -p $O
-B="python3 bench.py --steps 20 --warmup 3"
-for r in 1 2 3; do
-  for at in 0.45 0.55 0.65 0.75; do
-    ANA_PREPASS_AT=$at timeout -k 10 300 $B > $O/c2_at${at}_$r.log 2>&1 || exit 1
-  done
-  ANA_RATE_BLOCKS=512 ANA_PREPASS_AT=0.3 timeout -k 10 300 $B > $O/c2_b512_at0.3_$r.log 2>&1 || exit 1
-  for at in 0.3 0.4 0.5; do
-    ANA_TELE_TAIL_AT=$at timeout -k 10 300 python3 bench.py --config 4 --steps 10 --warmup 2 > $O/c4_at${at}_$r.log 2>&1 || exit 1
-  done
-  timeout -k 10 300 python3 bench.py --config 3 --steps 8 --warmup 2 > $O/c3_serial_$r.log 2>&1 || exit 1
-  ANA_PREPASS_SERIAL=0 timeout -k 10 300 python3 bench.py --config 3 --steps 8 --warmup 2 > $O/c3_tail0.7_$r.log 2>&1 || exit 1
+export PYTHONPATH=$GRAFT_REPO_ROOT
+O=gpurun_out/r6t2; mkdir -p $O
+b() { local name=$1; shift
+  timeout -k 10 400 env "$@" > $O/$name.log 2>&1 || { echo "FAIL $name"; tail -5 $O/$name.log; exit 1; }
+}
+for nb in 2:300 4:300 8:300 8:150 8:600; do
+  n=${nb%%:*}
+  b e${n}_${nb#*:} python3 bench.py --steps 10 --warmup 2 --force-merge --merges-per-step $n --emulate-allreduce $nb
 done
-python3 - <<'PY'
-import glob, re, collections
-rows = collections.defaultdict(list)
-for f in sorted(glob.glob("gpurun_out/r6t/*.log")):
-    m = re.search(r'"ms_per_step": ([0-9.]+)', open(f).read())
-    key = re.sub(r"_\d\.log$", "", f.split("/")[-1])
-    rows[key].append(float(m.group(1)) if m else None)
-for k, v in sorted(rows.items()):
-    print("%-22s %s" % (k, " ".join("%.3f" % x for x in v)))
-PY
+for n in 2 4 8; do
+  b c5e$n python3 bench.py --config 5 --steps 6 --warmup 2 --force-merge --merges-per-step 1 --emulate-allreduce $n:300
+done
+b k8plain python3 bench.py --steps 10 --warmup 2 --force-merge --merges-per-step 8
+b c2 python3 bench.py --steps 20 --warmup 3
+b c5 python3 bench.py --config 5 --steps 10 --warmup 2
+b c4 python3 bench.py --config 4 --steps 10 --warmup 2
+b worker env DATABASE_URI=columnar:// ENGINE=native BATCHSIZE=500 IDLE_TIMEOUT=0.01 python3 worker.py --synthetic 200000
+tail -3 $O/worker.log
+for f in $O/*.log; do n=$(basename $f .log); echo "$n $(grep -o '"ms_per_step": [0-9.]*' $f | tail -1)"; done | sort
