@@ -11,12 +11,11 @@
 //    number of its distinct players with an earlier occurrence, which the wave
 //    counts from the links when it stages the chunk.
 //  * 8 sharded tickets (MICROARCH "dequeue") hand out chunks of 64
-//    consecutive matches.  A wave holds up to 4 chunks (256 matches; records
-//    cached in LDS), so ~1M matches wait in flight GPU-wide: per-player
-//    dependency levels of a random stream spread over hundreds of thousands of
-//    matches, and a narrower window starves the machine.  Waiting costs nothing
-//    per match: the wave polls its chunks' counters with one coalesced 4-B sc1
-//    load per lane.
+//    consecutive matches (32 for 5v5, ops/rate.py chunk_len).  A wave holds one
+//    chunk (ANA_HELD; four until round 6), its records in registers, so 64k
+//    matches wait in flight at one wave per SIMD -- several dependency levels of a
+//    random stream.  Waiting costs nothing per match: the wave polls its chunk's
+//    counters with one coalesced 4-B sc1 load per lane.
 //  * The oldest ready matches go to the wave's lane groups (G lanes = one
 //    match, one roster slot per lane).  A group gathers its players' 16-B
 //    granules (sc1 buffer loads), seeds, rates both tracks (rate_core.h),
@@ -29,8 +28,8 @@
 //  * Software pipeline, one memory round trip per iteration: this iteration's
 //    granule/link/attribute loads, the next iteration's counter polls and the
 //    next chunk ticket retire in ONE vmcnt(0) wait.
-//  * Local hand-off: when the successor of a published player lies in a chunk
-//    the SAME wave holds, the producer bumps that match's counter in LDS
+//  * Local hand-off (1v1-3v3): when the successor of a published player lies in
+//    the chunk the SAME wave holds, the producer bumps that match's counter in LDS
 //    instead of the global one.  Readiness = polled global count + LDS count,
 //    so the successor is assigned in the very next iteration -- no poll round
 //    trip -- which is what a hot player's chain (consecutive matches of one
