@@ -28,7 +28,7 @@
 //  * Software pipeline, one memory round trip per iteration: this iteration's
 //    granule/link/attribute loads, the next iteration's counter polls and the
 //    next chunk ticket retire in ONE vmcnt(0) wait.
-//  * Local hand-off (1v1-3v3): when the successor of a published player lies in
+//  * Local hand-off (1v1-4v4): when the successor of a published player lies in
 //    the chunk the SAME wave holds, the producer bumps that match's counter in LDS
 //    instead of the global one.  Readiness = polled global count + LDS count,
 //    so the successor is assigned in the very next iteration -- no poll round
@@ -60,7 +60,7 @@
 
 namespace ana {
 
-// The LDS local hand-off (ANA_RATE_LOCAL, on by default): compiled into the 1v1-3v3
+// The LDS local hand-off (ANA_RATE_LOCAL, on by default): compiled into the 1v1-4v4
 // executors (and every executor of the diagnostic library).  Off from round 5 with four
 // held chunks per wave (profiles/r5/local_handoff_off.log); with one held chunk (round 6)
 // it pays for 3v3 (in-call A/B of the libraries, profiles/r6/local_handoff_on.log): serial
@@ -72,6 +72,9 @@ namespace ana {
 #define ANA_LOCAL_HANDOFF 1
 #endif
 constexpr bool kLocalHandoff = ANA_LOCAL_HANDOFF != 0;
+#ifndef ANA_LOCAL_HANDOFF_MAXK
+#define ANA_LOCAL_HANDOFF_MAXK 4  // the widest team the production hand-off is compiled for (4v4: 9.56-9.58 -> 9.50-9.54 ms)
+#endif
 
 
 constexpr int kHeld = ANA_HELD;  // chunks a wave keeps in flight (1v1-4v4)
@@ -130,7 +133,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   constexpr int S = 2 * K;
   constexpr int R = S + 2;
   constexpr int kH = K >= 5 ? ANA_HELD5 : kHeld;
-  constexpr bool kLH = kLocalHandoff && (K <= 3 || ANA_DIAG_BUILD != 0);  // LDS local hand-off compiled in
+  constexpr bool kLH = kLocalHandoff && (K <= ANA_LOCAL_HANDOFF_MAXK || ANA_DIAG_BUILD != 0);  // LDS local hand-off compiled in
   constexpr bool TILES = TELE == 1;  // K8 tiles taken by idle / dedicated waves
   constexpr bool INL = TELE == 2;    // K8 inline: each group folds its match's events
   static_assert(G >= S && G <= 64, "a group holds one match");
@@ -141,7 +144,7 @@ rate_dataflow_kernel(const int32_t* __restrict__ rec, const uint32_t* __restrict
   typedef uint32_t hvec __attribute__((ext_vector_type(kH <= 2 ? 2 : 4)));
   // local hand-off counters: increments of each held match's completion count
   // by publishes of THIS wave (never also added to the global counter); [lane][h]
-  // so a lane reads them in one ds_read_b64/b128.  Without kLH (4v4 / 5v5 in the
+  // so a lane reads them in one ds_read_b64/b128.  Without kLH (5v5 in the
   // production library) the executor has no LDS array, no per-iteration read of it
   // and no held-chunk scan in notify
   __shared__ hvec lloc[kWavesPerBlock][kLH ? kChunk : 1];

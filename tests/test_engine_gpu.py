@@ -247,15 +247,15 @@ def _handoff_run(K, P, M, skew, device, expect_local):
 
 
 @pytest.mark.parametrize("K,P,M,skew", [(3, 16, 4000, 1), (3, 100000, 1000000, 1), (5, 2000, 200000, 1),
-                                        (3, 100000, 300000, 3)])
+                                        (3, 100000, 300000, 3), (4, 50000, 300000, 3)])
 def test_local_handoff_and_timing_build_bit_identical(gpu_device, monkeypatch, K, P, M, skew):
     """The timing build (ANA_RATE_DIAG) and the LDS local hand-off (ANA_RATE_LOCAL) change
     only WHEN a match runs, never its result.  The production library compiles the hand-off
-    into the 1v1-3v3 executors only (csrc/dataflow.hip kLH): there hot chains take it, for
+    into the 1v1-4v4 executors only (csrc/dataflow.hip kLH): there hot chains take it, for
     5v5 setting it changes nothing and no hand-off goes local."""
     monkeypatch.setenv("ANA_RATE_LOCAL", "0")
     monkeypatch.setenv("ANA_RATE_DIAG", "0")
-    _handoff_run(K, P, M, skew, gpu_device, expect_local=K <= 3)
+    _handoff_run(K, P, M, skew, gpu_device, expect_local=K <= 4)
 
 
 def test_local_handoff_in_diagnostic_library(gpu_device):
