@@ -38,6 +38,7 @@ import queue
 import struct
 import tempfile
 import threading
+import time
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
@@ -300,6 +301,8 @@ class AsyncCheckpointer:
         self._writer: Optional[threading.Thread] = None
         self.written = 0
         self.bytes = 0
+        self.write_s: List[float] = []  # seconds per committed checkpoint (write + fsync + rename)
+        self.flush_s = 0.0              # seconds the callers waited in flush()
 
     def _buffers(self, roster: Roster) -> None:
         if self._host:
@@ -326,7 +329,9 @@ class AsyncCheckpointer:
                 if done is not None:
                     done.synchronize()
                 link = self._attrs_file if self.static_attrs else None
+                t0 = time.perf_counter()
                 _write(path, hb, attrs, meta, self.fsync, link_attrs=link)
+                self.write_s.append(time.perf_counter() - t0)
                 if self.static_attrs:
                     self._attrs_file = os.path.join(path, ATTRS)
                 self.written += 1
@@ -336,6 +341,14 @@ class AsyncCheckpointer:
             finally:
                 self._free[i].set()
                 self._queue.task_done()
+
+    def prepare(self, roster: Roster) -> None:
+        """Allocate the staging and pinned host buffers (and, with static attributes, take
+        their one host copy) now -- a run calls it before its first window, so page-locking
+        ~1 GB of host memory does not land inside the run's first checkpoint."""
+        self._buffers(roster)
+        if self.static_attrs and self._attrs_host is None:
+            self._attrs_host = roster.attrs.detach().to("cpu", copy=True).contiguous()
 
     def submit(self, path: str, roster: Roster, meta: Dict[str, Any]) -> None:
         self._buffers(roster)
@@ -380,7 +393,9 @@ class AsyncCheckpointer:
 
     def flush(self) -> None:
         """Wait until every submitted checkpoint is committed (renamed into place)."""
+        t0 = time.perf_counter()
         self._queue.join()
+        self.flush_s += time.perf_counter() - t0
         self._raise()
 
     def close(self) -> None:
@@ -420,13 +435,25 @@ class CheckpointManager:
     def due(self, windows_done: int) -> bool:
         return bool(self.directory) and windows_done > 0 and windows_done % self.every == 0
 
+    def _use_async(self, roster: Roster) -> bool:
+        return roster.state.device.type == "cuda" and \
+            os.environ.get("ANA_CKPT_ASYNC", "1") not in ("", "0", "false")
+
+    def prepare(self, roster: Roster) -> None:
+        """Set up the asynchronous writer's buffers ahead of the first save (no-op without a
+        directory or on the host path)."""
+        if not self.directory or not self._use_async(roster):
+            return
+        if self._async is None:
+            self._async = AsyncCheckpointer(roster.state.device, roster.num_players, fsync=self.fsync,
+                                            static_attrs=self.static_attrs)
+        self._async.prepare(roster)
+
     def maybe_save(self, windows_done: int, roster: Roster, meta: Dict[str, Any]) -> bool:
         if not self.due(windows_done):
             return False
         meta = dict(meta, windows_done=windows_done)
-        use_async = roster.state.device.type == "cuda" and \
-            os.environ.get("ANA_CKPT_ASYNC", "1") not in ("", "0", "false")
-        if use_async:
+        if self._use_async(roster):
             if self._async is None:
                 self._async = AsyncCheckpointer(roster.state.device, roster.num_players, fsync=self.fsync,
                                                 static_attrs=self.static_attrs)
@@ -439,6 +466,15 @@ class CheckpointManager:
     def flush(self) -> None:
         if self._async is not None:
             self._async.flush()
+
+    def stats(self) -> Dict[str, float]:
+        """Asynchronous writer timing: checkpoints committed, mean / max seconds per commit
+        and the seconds callers waited in flush() (empty without the writer)."""
+        a = self._async
+        if a is None or not a.write_s:
+            return {}
+        return {"checkpoints": float(len(a.write_s)), "write_s_mean": sum(a.write_s) / len(a.write_s),
+                "write_s_max": max(a.write_s), "flush_wait_s": a.flush_s}
 
     def latest(self, device="cpu") -> Optional[Tuple[Roster, Dict[str, Any]]]:
         """The newest complete checkpoint: ``latest``, or ``latest.old`` when a

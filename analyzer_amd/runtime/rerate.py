@@ -204,6 +204,10 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
     # the main stream between the ratings
     gen_tail = (os.environ.get("ANA_RERATE_GEN", "tail") == "tail" and dev.type == "cuda" and merger is None
                 and pipe.side is not None and pipe.side != torch.cuda.current_stream(dev) and pipe.tail > 0)
+    # the checkpoint writer's pinned buffers are set up before the run, like the roster
+    # (ANA_CKPT_PREPARE=0: at the first save)
+    if rank == 0 and os.environ.get("ANA_CKPT_PREPARE", "1") not in ("", "0", "false"):
+        ck.prepare(roster)
     t0 = time.perf_counter()
     rated = 0
     D = pipe.depth  # windows prepared ahead (runtime/engine.py)
@@ -286,6 +290,8 @@ def run(spec: RerateSpec, device=None, checkpoint_dir: Optional[str] = None,
     summed["windows"] = float(total - start_window)
     summed["resumed_from_window"] = float(start_window)
     summed["matches_per_s"] = summed["matches"] / summed["seconds"] if summed["seconds"] > 0 else 0.0
+    if rank == 0:
+        summed.update({"checkpoint_" + k: v for k, v in ck.stats().items()})
     if records == "digest":
         summed["window_digests"] = {g: digests[g].cpu().tolist() for g in sorted(digests)}
     return summed, roster

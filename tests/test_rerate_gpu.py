@@ -53,3 +53,23 @@ def test_async_checkpoint_roundtrip_on_device(gpu_device, tmp_path):
     assert torch.equal(base(got.state), base(want))
     assert torch.equal(got.attrs.nan_to_num(-7), roster.attrs.nan_to_num(-7))
     assert float(got.state.view(-1, 8, 4)[:, :, 1::2].abs().max()) == 0.0  # tags are not saved
+
+
+def test_prepared_checkpoint_buffers(gpu_device, tmp_path):
+    """CheckpointManager.prepare allocates the pinned buffers (and the static attributes'
+    host copy) before the first save; the saves then write what a lazily prepared writer
+    writes."""
+    roster = make_roster(RosterSpec(num_players=50_000, seed=19, p_rated=0.5), device=gpu_device)
+    out = {}
+    for tag, prep in (("lazy", False), ("prepared", True)):
+        mgr = checkpoint.CheckpointManager(str(tmp_path / tag), every=1, static_attrs=True)
+        if prep:
+            mgr.prepare(roster)
+            assert mgr._async is not None and mgr._async._host
+        assert mgr.maybe_save(1, roster, {"x": 1})
+        mgr.flush()
+        assert mgr.stats()["checkpoints"] == 1.0
+        out[tag] = mgr.latest(gpu_device)[0]
+    a, b = out["lazy"], out["prepared"]
+    assert torch.equal(a.state.nan_to_num(-7), b.state.nan_to_num(-7))
+    assert torch.equal(a.attrs.nan_to_num(-7), b.attrs.nan_to_num(-7))
